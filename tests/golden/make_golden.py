@@ -1,0 +1,316 @@
+"""Generate the golden parity fixtures by running the REFERENCE (dcrecommend) on CPU.
+
+Run in the build container only (the reference never travels to the GPU box):
+
+    PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+Every fixture is data (inputs + the reference's outputs); no reference source is stored.
+Which reference code produced what:
+
+* model_*.npz   -- dcrecommend/dcue/dcue.py:21-108 (DCUENet fwd), nn/dcue.py:167-170 (hinge loss),
+                   torch autograd backward, torch.optim.Adam as built at nn/dcue.py:143-147.
+* inbatch_*.npz -- the in-batch sampler spec of nn/dcue.py:698-709 (commented out in the reference;
+                   the draws below follow that text literally), plus a forward/backward of the
+                   reference model on the duplicated [pos; neg] batch it builds.
+* catalogue.npz -- DCUEDataset._user_nonitem_songids (datasets/dcuedataset.py:207-220) under both
+                   RNG protocols (random_seed set -> reseed per sample :167-168; global stream).
+* batches.npz   -- DCUEDataset.get_batches (datasets/dcuedataset.py:189-201).
+* scheduler.npz -- CyclicLRWithRestarts (optim/cyclic_scheduler.py:49-215) driven the way
+                   DCUE.fit/_train_epoch drive it (nn/dcue.py:338-341, 209-210).
+* train5.npz    -- five DCUE train steps (nn/dcue.py:202-210) with Adam + scheduler.
+* metrics.npz   -- DCUE.score's split-weighted AUC / mAP arithmetic (nn/dcue.py:399-449) and
+                   score_song's (nn/dcue.py:463-476), on fixed score vectors.
+"""
+import os
+import sys
+
+import numpy as np
+import pandas as pd
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = os.environ.get("DCUE_REFERENCE", "/root/reference")
+if REF not in sys.path:
+    sys.path.insert(0, REF)
+
+from dcrecommend.dcue.dcue import DCUENet  # noqa: E402  (reference)
+from dcrecommend.nn.dcue import DCUE  # noqa: E402  (reference)
+from dcrecommend.datasets.dcuedataset import DCUEDataset  # noqa: E402  (reference)
+from dcrecommend.optim.cyclic_scheduler import CyclicLRWithRestarts  # noqa: E402  (reference)
+
+torch.set_num_threads(8)
+
+
+def _spectros(gen, *shape):
+    """Synthetic spectrograms, rounded to fp16-representable values."""
+    return torch.randn(*shape, generator=gen).half().float()
+
+
+def _state(model):
+    return {k: v.detach().clone() for k, v in model.state_dict().items()}
+
+
+def _save(name, **arrays):
+    path = os.path.join(HERE, name)
+    out = {}
+    for k, v in arrays.items():
+        if isinstance(v, torch.Tensor):
+            v = v.detach().cpu().numpy()
+        out[k] = np.asarray(v)
+    np.savez_compressed(path, **out)
+    print("wrote", path, sum(a.nbytes for a in out.values()) // 1024, "KiB raw")
+
+
+def model_fixture(name, H, d, n_users, B, N, lr=1e-3, store_init=True, store_steps=True, seed=0):
+    """fwd (train) -> hinge -> bwd -> Adam(lr) step -> Adam(lr, wd=1e-4) step -> eval fwd."""
+    torch.manual_seed(seed)
+    net = DCUENet({"feature_dim": d, "conv_hidden": H, "user_embdim": 300,
+                   "user_count": n_users, "model_type": "truedcuemel1dbn"})
+    init = _state(net)
+    gen = torch.Generator().manual_seed(seed + 1)
+    u = torch.randint(0, n_users, (B,), generator=gen)
+    pos = _spectros(gen, B, 128, 131)
+    neg = _spectros(gen, B, N, 128, 131)
+    trainer = DCUE(feature_dim=d, conv_hidden=H, batch_size=B, margin=0.2)
+
+    net.train()
+    net.zero_grad()
+    scores, uf, pf, nf = net(u, pos, neg)
+    loss = trainer._loss_func(scores)
+    loss.backward()
+    grads = {"grad." + n: p.grad.detach().clone() for n, p in net.named_parameters()}
+    after_fwd = _state(net)  # running stats updated by the train-mode forward
+
+    opt = torch.optim.Adam(net.parameters(), lr, (0.9, 0.99), 1e-8, 0)
+    opt.step()
+    step1 = {"step1." + k: v for k, v in _state(net).items()}
+    # second step, same grads, weight decay on (exercises Adam's grad += wd * p)
+    for g in opt.param_groups:
+        g["weight_decay"] = 1e-4
+    opt.step()
+    step2 = {"step2." + k: v for k, v in _state(net).items()}
+
+    net.eval()
+    with torch.no_grad():
+        e_scores, e_uf, e_pf, e_nf = net(u, pos, neg)
+
+    payload = dict(H=H, d=d, n_users=n_users, B=B, N=N, lr=lr, seed=seed,
+                   u=u, pos=pos.half(), neg=neg.half(),
+                   scores=scores, uf=uf, pf=pf, nf=nf, loss=loss,
+                   eval_scores=e_scores, eval_uf=e_uf, eval_pf=e_pf, eval_nf=e_nf)
+    payload.update(grads)
+    payload.update({"fwd." + k: v for k, v in after_fwd.items() if "running" in k or "num_batches" in k})
+    if store_steps:
+        payload.update(step1)
+        payload.update(step2)
+    if store_init:
+        payload.update({"init." + k: v for k, v in init.items()})
+    else:
+        payload.update({"initsum." + k: v.double().sum() for k, v in init.items()})
+        payload.update({"initsq." + k: (v.double() ** 2).sum() for k, v in init.items()})
+    _save(name, **payload)
+
+
+def inbatch_draws(B, N, seed):
+    """nn/dcue.py:698-709 text: for i<B, j<N: rand_idx = np.random.choice([0..i-1, i+1..B-1])."""
+    np.random.seed(seed)
+    r = np.zeros((B, N), dtype=np.int64)
+    for i in range(B):
+        indexes = [x for x in range(0, i)] + [x for x in range(i + 1, B)]
+        for j in range(N):
+            r[i, j] = np.random.choice(indexes)
+    return r
+
+
+def inbatch_fixtures():
+    seeds = [0, 5, 99]
+    draws = {"seed%d" % s: inbatch_draws(64, 20, s) for s in seeds}
+    draws.update({"small_seed3": inbatch_draws(8, 5, 3)})
+    _save("inbatch_draws.npz", **draws)
+
+    # model-level: negatives are copies of in-batch positives (the reference conv runs on the
+    # duplicated [pos; neg] stack, so BN statistics count each copy).
+    H, d, n_users, B, N = 32, 32, 10, 8, 5
+    torch.manual_seed(0)
+    net = DCUENet({"feature_dim": d, "conv_hidden": H, "user_embdim": 300,
+                   "user_count": n_users, "model_type": "truedcuemel1dbn"})
+    gen = torch.Generator().manual_seed(11)
+    u = torch.randint(0, n_users, (B,), generator=gen)
+    pos = _spectros(gen, B, 128, 131)
+    r = torch.from_numpy(draws["small_seed3"])
+    neg = pos[r.reshape(-1)].reshape(B, N, 128, 131).clone()
+    trainer = DCUE(feature_dim=d, conv_hidden=H, batch_size=B, margin=0.2)
+    net.train()
+    net.zero_grad()
+    scores, uf, pf, nf = net(u, pos, neg)
+    loss = trainer._loss_func(scores)
+    loss.backward()
+    payload = dict(H=H, d=d, n_users=n_users, B=B, N=N, u=u, pos=pos.half(), r=r,
+                   scores=scores, uf=uf, pf=pf, nf=nf, loss=loss)
+    payload.update({"grad." + n: p.grad for n, p in net.named_parameters()})
+    payload.update({"fwd." + k: v for k, v in _state(net).items() if "running" in k})
+    _save("inbatch_model.npz", **payload)
+
+
+def _synthetic_triplets(n_users, n_tracks, n_pairs, seed):
+    rs = np.random.RandomState(seed)
+    pairs = set()
+    while len(pairs) < n_pairs:
+        pairs.add((int(rs.randint(n_users)), int(rs.randint(n_tracks))))
+    pairs = sorted(pairs)
+    users = ["u%05d" % p[0] for p in pairs]
+    songs = ["S%07d" % p[1] for p in pairs]
+    score = rs.randint(1, 10, size=len(pairs))
+    order = rs.permutation(len(pairs))
+    return pd.DataFrame({"user_id": np.array(users)[order], "song_id": np.array(songs)[order],
+                         "score": score[order]})
+
+
+def catalogue_fixture():
+    n_users, n_tracks, n_pairs, N = 40, 60, 600, 7
+    trip = _synthetic_triplets(n_users, n_tracks, n_pairs, 0)
+    raw_users = trip["user_id"].to_numpy().astype(str)
+    raw_songs = trip["song_id"].to_numpy().astype(str)
+    raw_score = trip["score"].to_numpy()
+    meta = pd.DataFrame({"song_id": sorted(set(raw_songs)), "data_mel": ""})
+    ds = DCUEDataset(trip.copy(), meta, neg_samples=N, split="train")
+    split_items = np.array(sorted(ds.uniq_song_idxs), dtype=np.int64)
+    # the CSR over all interactions, as item indices per user index
+    users_seq = np.random.RandomState(42).randint(0, len(ds.user_index), size=50)
+    userids = [ds.userindex2userid[int(i)] for i in users_seq]
+
+    def codes(songs):
+        return np.array([ds.item_index[s] for s in songs], dtype=np.int64)
+
+    # (1) random_seed=S protocol: the RNG is reseeded before every sample (dcuedataset.py:167-168)
+    seeded = []
+    for uid in userids:
+        np.random.seed(1234)
+        seeded.append(codes(ds._user_nonitem_songids(uid)))
+    # (2) global-stream protocol: one np.random.seed then draws in sampler order
+    np.random.seed(77)
+    stream = [codes(ds._user_nonitem_songids(uid)) for uid in userids]
+    _save("catalogue.npz", raw_users=raw_users, raw_songs=raw_songs, raw_score=raw_score,
+          n_items=ds.n_items, n_users=ds.n_users, N=N,
+          user_categories=np.array(list(ds.user_index.keys())).astype(str),
+          song_categories=np.array(list(ds.item_index.keys())).astype(str),
+          split_items=split_items, users_seq=users_seq,
+          seeded=np.stack(seeded), stream=np.stack(stream), train_len=len(ds),
+          train_users=np.array([ds.user_index[x] for x in ds.triplets["user_id"]], dtype=np.int64),
+          train_songs=np.array([ds.item_index[x] for x in ds.triplets["song_id"]], dtype=np.int64))
+
+
+class _Len:
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+
+def batches_fixture():
+    out = {}
+    for n, seed in [(95, 0), (100, 1), (1003, 2), (7, 3)]:
+        np.random.seed(seed)
+        chunks = DCUEDataset.get_batches(_Len(n), k=10)
+        out["n%d_lens" % n] = np.array([len(c) for c in chunks], dtype=np.int64)
+        out["n%d_flat" % n] = np.array([x for c in chunks for x in c], dtype=np.int64)
+    _save("batches.npz", **out)
+
+
+def scheduler_fixture():
+    out = {}
+    for tag, (B, n_train, period, t_mult, base_wd) in {
+            "a": (64, 6400, 2, 2, 0.0), "b": (32, 1000, 3, 1.5, 1e-3)}.items():
+        p = torch.nn.Parameter(torch.zeros(1))
+        opt = torch.optim.Adam([p], 1e-3, (0.9, 0.99), 1e-8, base_wd)
+        epoch_size = int(int(np.ceil(n_train / 10)) // B) * B  # nn/dcue.py:302-303
+        sch = CyclicLRWithRestarts(opt, B, epoch_size=epoch_size, restart_period=period,
+                                   t_mult=t_mult, policy="cosine")
+        chunk = int(np.ceil(n_train / 10))
+        nb = chunk // B  # DataLoader(drop_last=True) over one get_batches chunk
+        lrs, wds = [], []
+        for sub in range(20):
+            sch.step()
+            for _ in range(nb):
+                lrs.append(opt.param_groups[0]["lr"])
+                wds.append(opt.param_groups[0]["weight_decay"])
+                sch.batch_step()
+        # overrun: the reference raises StopIteration once the increments run out
+        sch.step()
+        raised = 0
+        try:
+            for _ in range(nb + 5):
+                sch.batch_step()
+        except StopIteration:
+            raised = 1
+        out[tag + "_cfg"] = np.array([B, n_train, period, t_mult, base_wd, epoch_size, nb], dtype=np.float64)
+        out[tag + "_lr"] = np.array(lrs)
+        out[tag + "_wd"] = np.array(wds)
+        out[tag + "_raised"] = np.array(raised)
+    _save("scheduler.npz", **out)
+
+
+def train5_fixture():
+    H, d, n_users, B, N = 32, 32, 12, 4, 3
+    torch.manual_seed(0)
+    trainer = DCUE(feature_dim=d, conv_hidden=H, batch_size=B, margin=0.2, lr=1e-3,
+                   restart_period=2, t_mult=2)
+    trainer.n_users = n_users
+    trainer.epoch_size = 5 * B
+    trainer.USE_CUDA = False
+    trainer._init_nn()
+    gen = torch.Generator().manual_seed(5)
+    us, poss, negs, losses, lrs = [], [], [], [], []
+    trainer.model.train()
+    trainer.scheduler.step()
+    for _ in range(5):
+        u = torch.randint(0, n_users, (B,), generator=gen)
+        pos = _spectros(gen, B, 128, 131)
+        neg = _spectros(gen, B, N, 128, 131)
+        lrs.append(trainer.optimizer.param_groups[0]["lr"])
+        trainer.model.zero_grad()
+        preds, _, _, _ = trainer.model(u, pos, neg)
+        loss = trainer._loss_func(preds)
+        loss.backward()
+        trainer.optimizer.step()
+        trainer.scheduler.batch_step()
+        us.append(u)
+        poss.append(pos.half())
+        negs.append(neg.half())
+        losses.append(loss.item())
+    payload = dict(H=H, d=d, n_users=n_users, B=B, N=N, u=torch.stack(us), pos=torch.stack(poss),
+                   neg=torch.stack(negs), loss=np.array(losses), lr=np.array(lrs))
+    payload.update({"final." + k: v for k, v in _state(trainer.model).items()})
+    _save("train5.npz", **payload)
+
+
+def metrics_fixture():
+    """The AUC/mAP arithmetic of DCUE.score / score_song on fixed vectors (sklearn underneath)."""
+    from sklearn.metrics import roc_auc_score, average_precision_score
+    rs = np.random.RandomState(3)
+    cases = []
+    for n in [5, 17, 40]:
+        sp = np.round(rs.rand(n), 2)  # rounding creates ties (sklearn tie semantics)
+        tp = (rs.rand(n) < 0.3).astype(np.int64)
+        st = np.round(rs.rand(n + 3), 2)
+        tt = (rs.rand(n + 3) < 0.5).astype(np.int64)
+        cases.append((sp, tp, st, tt))
+    out = {}
+    for c, (sp, tp, st, tt) in enumerate(cases):
+        out["c%d_sp" % c], out["c%d_tp" % c], out["c%d_st" % c], out["c%d_tt" % c] = sp, tp, st, tt
+        out["c%d_auc" % c] = roc_auc_score(tp, sp) if 0 < tp.sum() < len(tp) else np.nan
+        out["c%d_ap" % c] = average_precision_score(tp, sp)
+    _save("metrics.npz", **out)
+
+
+if __name__ == "__main__":
+    model_fixture("model_tiny.npz", H=32, d=32, n_users=10, B=4, N=3)
+    model_fixture("model_h128.npz", H=128, d=128, n_users=10, B=2, N=2, store_init=False,
+                  store_steps=False)
+    inbatch_fixtures()
+    catalogue_fixture()
+    batches_fixture()
+    scheduler_fixture()
+    train5_fixture()
+    metrics_fixture()
