@@ -1,0 +1,510 @@
+// libdcue_hip C ABI: layouts, workspace carving and the per-step kernel schedule.
+//
+// The schedule mirrors the reference step (nn/dcue.py:202-210):
+//   forward   bn0 stats -> [conv_l (BN_{l-1} fused in its load) -> BN_l stats] x5 -> fc ->
+//             user tower -> cosine scores + hinge loss                (dcue/dcue.py:70-108)
+//   backward  score grads -> item grads -> fc -> [BN_l bwd sums -> wgrad_l, dgrad_l] l=5..2 ->
+//             BN1 -> wgrad_1 (+ bn0 grads without conv1 dgrad) -> user tower -> embedding rows
+//   adam      dense params + user table, then weight repack
+#include <math.h>
+#include <string.h>
+
+#include "dcue_internal.h"
+
+using namespace dcue;
+
+namespace {
+
+constexpr int kSeg = DCUE_N_DENSE_SEGMENTS;
+
+bool pow2_32_256(int v) { return v == 32 || v == 64 || v == 128 || v == 256; }
+
+int check_dims(const dcue_dims* d) {
+  if (!d) return DCUE_ERR_INVALID;
+  if (d->conv_hidden <= 0 || d->feature_dim <= 0 || d->user_embdim <= 0 || d->n_users < 0)
+    return DCUE_ERR_INVALID;
+  if (!pow2_32_256(d->conv_hidden) || !pow2_32_256(d->feature_dim) || d->user_embdim > 1024)
+    return DCUE_ERR_UNSUPPORTED;
+  return DCUE_OK;
+}
+
+long al4(long v) { return (v + 3) & ~3L; }
+
+void param_sizes(const dcue_dims* d, long* sz) {
+  const long H = d->conv_hidden, D = d->feature_dim, E = d->user_embdim;
+  const long cin[5] = {kMels, H, H, H, H}, cout[5] = {H, H, H, H, D};
+  int s = 0;
+  sz[s++] = kMels;  // bn0.weight
+  sz[s++] = kMels;  // bn0.bias
+  for (int l = 1; l <= 5; ++l) {
+    sz[s++] = cout[l - 1] * cin[l - 1] * layer_geom(l).ks;  // conv.layer{l}.weight
+    sz[s++] = cout[l - 1];                                  // conv.layer{l}.bias
+    sz[s++] = cout[l - 1];                                  // conv.bn{l}.weight
+    sz[s++] = cout[l - 1];                                  // conv.bn{l}.bias
+  }
+  sz[s++] = D * D;  // conv.fc.weight
+  sz[s++] = D;      // conv.fc.bias
+  sz[s++] = E * E;  // user_embd.linear1.weight
+  sz[s++] = E;
+  sz[s++] = D * E;  // user_embd.linear2.weight
+  sz[s++] = D;
+}
+
+void param_offsets(const dcue_dims* d, int64_t* off) {
+  long sz[kSeg];
+  param_sizes(d, sz);
+  long o = 0;
+  for (int s = 0; s < kSeg; ++s) {
+    off[s] = o;
+    o = al4(o + sz[s]);
+  }
+  off[kSeg] = o;
+}
+
+int bn_channels(const dcue_dims* d, int l) {
+  return l == 0 ? kMels : l == 5 ? d->feature_dim : d->conv_hidden;
+}
+
+void bn_offsets(const dcue_dims* d, int64_t* off) {
+  long o = 0;
+  for (int l = 0; l < DCUE_N_BN; ++l) {
+    off[2 * l] = o;
+    o = al4(o + bn_channels(d, l));
+    off[2 * l + 1] = o;
+    o = al4(o + bn_channels(d, l));
+  }
+  off[2 * DCUE_N_BN] = o;
+}
+
+long wpack_floats(const dcue_dims* d) {
+  const long H = d->conv_hidden, D = d->feature_dim;
+  long n = 0;
+  for (int l = 1; l <= 5; ++l) {
+    const long cin = l == 1 ? kMels : H, cout = l == 5 ? D : H;
+    const long e = cin * cout * layer_geom(l).ks;
+    n += l == 1 ? e : 2 * e;
+  }
+  return n;
+}
+
+long wpack_offset(const dcue_dims* d, int l, bool bwd) {
+  const long H = d->conv_hidden, D = d->feature_dim;
+  long n = 0;
+  for (int k = 1; k <= 5; ++k) {
+    const long cin = k == 1 ? kMels : H, cout = k == 5 ? D : H;
+    const long e = cin * cout * layer_geom(k).ks;
+    if (k == l) return bwd ? n + e : n;
+    n += k == 1 ? e : 2 * e;
+  }
+  return n;
+}
+
+// pointers into the caller's workspace
+struct Ws {
+  float* counts;
+  float *mean[6], *invstd[6], *a[6], *sD[6], *sDx[6];
+  float* partials;
+  float* y[6];
+  uint8_t* idx[6];
+  float *f, *uf, *emb_g, *h1;
+  float *cosv, *norms, *row_loss, *scores, *loss, *dhinge;
+  float *du, *dfcopy, *df;
+  float* g[6];
+  float *dh1, *de;
+  float *wpart, *bpart, *G, *S;
+};
+
+size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
+  Arena ar{(char*)base, 0, 0};
+  const int H = d->conv_hidden, D = d->feature_dim, E = d->user_embdim;
+  const int Cmax = H > kMels ? H : kMels;
+  w->counts = ar.take<float>(M);
+  for (int l = 0; l < 6; ++l) {
+    const int C = bn_channels(d, l);
+    w->mean[l] = ar.take<float>(C);
+    w->invstd[l] = ar.take<float>(C);
+    w->a[l] = ar.take<float>(C);
+    w->sD[l] = ar.take<float>(C);
+    w->sDx[l] = ar.take<float>(C);
+  }
+  long pmax = 1024L * 2 * kMels;
+  for (int l = 1; l <= 5; ++l) {
+    const long p = (long)conv_fwd_grid(l, M) * 2 * (l == 5 ? D : H);
+    if (p > pmax) pmax = p;
+  }
+  if (512L * 2 * Cmax > pmax) pmax = 512L * 2 * Cmax;
+  w->partials = ar.take<float>(pmax);
+  w->y[0] = nullptr;
+  w->idx[0] = nullptr;
+  for (int l = 1; l <= 5; ++l) {
+    const long n = (long)M * layer_geom(l).lp * (l == 5 ? D : H);
+    w->y[l] = ar.take<float>(n);
+    w->idx[l] = ar.take<uint8_t>(n);
+  }
+  w->f = ar.take<float>((long)M * D);
+  w->uf = ar.take<float>((long)B * D);
+  w->emb_g = ar.take<float>((long)B * E);
+  w->h1 = ar.take<float>((long)B * E);
+  w->cosv = ar.take<float>((long)B * (N + 1));
+  w->norms = ar.take<float>((long)B * (N + 2));
+  w->row_loss = ar.take<float>(B);
+  w->scores = ar.take<float>((long)B * (N > 0 ? N : 1));
+  w->loss = ar.take<float>(4);
+  w->dhinge = ar.take<float>((long)B * (N > 0 ? N : 1));
+  w->du = ar.take<float>((long)B * D);
+  w->dfcopy = ar.take<float>((long)B * (N + 1) * D);
+  w->df = ar.take<float>((long)M * D);
+  w->g[0] = nullptr;
+  for (int l = 1; l <= 5; ++l) w->g[l] = ar.take<float>((long)M * layer_geom(l).lp * (l == 5 ? D : H));
+  w->dh1 = ar.take<float>((long)B * E);
+  w->de = ar.take<float>((long)B * E);
+  long wp = 0, bp = 0;
+  for (int l = 1; l <= 5; ++l) {
+    const int cin = l == 1 ? kMels : H, cout = l == 5 ? D : H;
+    const long nch = wgrad_nchunk(l, M, cout, cin);
+    const long e = nch * cout * cin * layer_geom(l).ks;
+    if (e > wp) wp = e;
+    if (nch * 5 * cout > bp) bp = nch * 5 * cout;
+  }
+  w->wpart = ar.take<float>(wp);
+  w->bpart = ar.take<float>(bp);
+  w->G = ar.take<float>((long)H * 4 * kMels);
+  w->S = ar.take<float>(4L * H);
+  return ar.used + 256;
+}
+
+struct Ctx {
+  const dcue_model* m;
+  int64_t poff[kSeg + 1];
+  int64_t boff[2 * DCUE_N_BN + 1];
+  int H, D, E;
+  const float* P(int seg) const { return m->params + poff[seg]; }
+  float* Gd(int seg) const { return m->grads + poff[seg]; }
+  float* rmean(int l) const { return m->bn_stats + boff[2 * l]; }
+  float* rvar(int l) const { return m->bn_stats + boff[2 * l + 1]; }
+};
+// segment indices
+int seg_bn_w(int l) { return l == 0 ? 0 : 4 + 4 * (l - 1); }
+int seg_bn_b(int l) { return l == 0 ? 1 : 5 + 4 * (l - 1); }
+int seg_conv_w(int l) { return 2 + 4 * (l - 1); }
+int seg_conv_b(int l) { return 3 + 4 * (l - 1); }
+constexpr int SEG_FC_W = 22, SEG_FC_B = 23, SEG_L1_W = 24, SEG_L1_B = 25, SEG_L2_W = 26, SEG_L2_B = 27;
+
+int init_ctx(Ctx* c, const dcue_model* m) {
+  int st = check_dims(&m->dims);
+  if (st) return st;
+  if (!m->params || !m->bn_stats || !m->bn_batches || !m->wpack) return DCUE_ERR_INVALID;
+  c->m = m;
+  param_offsets(&m->dims, c->poff);
+  bn_offsets(&m->dims, c->boff);
+  c->H = m->dims.conv_hidden;
+  c->D = m->dims.feature_dim;
+  c->E = m->dims.user_embdim;
+  return DCUE_OK;
+}
+
+#define TRY(x)                 \
+  do {                         \
+    int _st = (x);             \
+    if (_st) return _st;       \
+  } while (0)
+
+// Item tower forward. train: batch statistics (weighted by counts) + running-stat update.
+int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t* item_track, int M,
+                 double copies, bool train, const float* counts, hipStream_t s) {
+  const dcue_model* m = c.m;
+  const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
+  int nparts = 0;
+  if (train) TRY(launch_input_stats(src, t->data, item_track, counts, M, w.partials, &nparts, s));
+  TRY(launch_bn_finalize(w.partials, nparts, kMels, copies * kFrames, c.P(seg_bn_w(0)), c.rmean(0),
+                         c.rvar(0), m->bn_batches + 0, train, w.mean[0], w.invstd[0], w.a[0], s));
+  for (int l = 1; l <= 5; ++l) {
+    RowsArgs a = {};
+    a.src = l == 1 ? t->data : (const void*)w.y[l - 1];
+    a.item_track = item_track;
+    a.in_mean = w.mean[l - 1];
+    a.in_a = w.a[l - 1];
+    a.in_beta = c.P(seg_bn_b(l - 1));
+    a.counts = counts;
+    a.wpack = m->wpack + wpack_offset(&m->dims, l, false);
+    a.bias = c.P(seg_conv_b(l));
+    a.out = w.y[l];
+    a.out_idx = w.idx[l];
+    a.partials = train ? w.partials : nullptr;
+    a.M = M;
+    a.nout = l == 5 ? c.D : c.H;
+    TRY(launch_conv_fwd(l, l == 1 ? kMels : c.H, l == 1 ? src : SRC_ACT, a, s));
+    const int C = a.nout;
+    TRY(launch_bn_finalize(w.partials, conv_fwd_grid(l, M), C, copies * layer_geom(l).lp,
+                           c.P(seg_bn_w(l)), c.rmean(l), c.rvar(l), m->bn_batches + l, train,
+                           w.mean[l], w.invstd[l], w.a[l], s));
+  }
+  // fc on BN5(y5): f = bn5(y5) W^T + b
+  GemmArgs g = {};
+  g.M = M; g.N = c.D; g.K = c.D;
+  g.A = w.y[5]; g.sam = c.D; g.sak = 1;
+  g.tmean = w.mean[5]; g.ta = w.a[5]; g.tbeta = c.P(seg_bn_b(5));
+  g.B = c.P(SEG_FC_W); g.sbk = 1; g.sbn = c.D;
+  g.bias = c.P(SEG_FC_B);
+  g.C = w.f; g.scm = c.D; g.scn = 1;
+  return launch_gemm(2, g, s);
+}
+
+int user_forward(const Ctx& c, const Ws& w, const int64_t* users, int B, hipStream_t s) {
+  const dcue_model* m = c.m;
+  TRY(launch_gather_rows(m->emb, users, B, c.E, w.emb_g, s));
+  GemmArgs g = {};
+  g.M = B; g.N = c.E; g.K = c.E;
+  g.A = w.emb_g; g.sam = c.E; g.sak = 1;
+  g.B = c.P(SEG_L1_W); g.sbk = 1; g.sbn = c.E;
+  g.bias = c.P(SEG_L1_B);
+  g.C = w.h1; g.scm = c.E; g.scn = 1;
+  TRY(launch_gemm(1, g, s));
+  g = GemmArgs{};
+  g.M = B; g.N = c.D; g.K = c.E;
+  g.A = w.h1; g.sam = c.E; g.sak = 1;
+  g.B = c.P(SEG_L2_W); g.sbk = 1; g.sbn = c.E;
+  g.bias = c.P(SEG_L2_B);
+  g.C = w.uf; g.scm = c.D; g.scn = 1;
+  return launch_gemm(1, g, s);
+}
+
+int check_batch(const dcue_batch* b) {
+  if (!b || !b->users || !b->item_track || b->n_rows <= 0 || b->n_neg < 0 || b->n_items <= 0)
+    return DCUE_ERR_INVALID;
+  if (b->layout == DCUE_LAYOUT_CATALOGUE) {
+    if ((long)b->n_items != (long)b->n_rows * (1 + b->n_neg)) return DCUE_ERR_INVALID;
+  } else if (b->layout == DCUE_LAYOUT_GATHER) {
+    if (b->n_neg > 0 && !b->neg_item) return DCUE_ERR_INVALID;
+    if (b->n_items < b->n_rows) return DCUE_ERR_INVALID;
+  } else {
+    return DCUE_ERR_INVALID;
+  }
+  return DCUE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dcue_abi_version(void) { return DCUE_ABI_VERSION; }
+
+int dcue_param_layout(const dcue_dims* dims, int64_t* offsets_host) {
+  TRY(check_dims(dims));
+  if (!offsets_host) return DCUE_ERR_INVALID;
+  param_offsets(dims, offsets_host);
+  return DCUE_OK;
+}
+
+int dcue_bn_layout(const dcue_dims* dims, int64_t* offsets_host) {
+  TRY(check_dims(dims));
+  if (!offsets_host) return DCUE_ERR_INVALID;
+  bn_offsets(dims, offsets_host);
+  return DCUE_OK;
+}
+
+int dcue_wpack_floats(const dcue_dims* dims, int64_t* n) {
+  TRY(check_dims(dims));
+  if (!n) return DCUE_ERR_INVALID;
+  *n = wpack_floats(dims);
+  return DCUE_OK;
+}
+
+int dcue_workspace_bytes(const dcue_dims* dims, int32_t max_rows, int32_t max_neg,
+                         int32_t max_items, size_t* bytes) {
+  TRY(check_dims(dims));
+  if (!bytes || max_rows <= 0 || max_neg < 0 || max_items <= 0) return DCUE_ERR_INVALID;
+  Ws w;
+  *bytes = carve(dims, max_rows, max_neg, max_items, nullptr, &w);
+  return DCUE_OK;
+}
+
+int dcue_pack_weights(const dcue_model* m, void* stream) {
+  Ctx c;
+  TRY(init_ctx(&c, m));
+  return launch_pack(m, c.poff, (hipStream_t)stream);
+}
+
+int dcue_forward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws,
+                 size_t ws_bytes, int32_t train, float margin, float* scores, float* user_feat,
+                 float* item_feat, float* loss, void* stream) {
+  Ctx c;
+  TRY(init_ctx(&c, m));
+  TRY(check_batch(b));
+  if (!t || !t->data || !ws || !m->emb) return DCUE_ERR_INVALID;
+  Ws w;
+  if (carve(&m->dims, b->n_rows, b->n_neg, b->n_items, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
+  carve(&m->dims, b->n_rows, b->n_neg, b->n_items, ws, &w);
+  hipStream_t s = (hipStream_t)stream;
+  const double copies = (double)b->n_rows * (1 + b->n_neg);
+  TRY(launch_item_counts(b, w.counts, s));
+  TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, s));
+  TRY(user_forward(c, w, b->users, b->n_rows, s));
+  TRY(launch_score_fwd(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.row_loss, w.loss,
+                       w.dhinge, s));
+  const int B = b->n_rows, N = b->n_neg, M = b->n_items;
+  if (scores && N > 0) DCUE_HIP_CHECK(hipMemcpyAsync(scores, w.scores, sizeof(float) * B * N, hipMemcpyDeviceToDevice, s));
+  if (user_feat) DCUE_HIP_CHECK(hipMemcpyAsync(user_feat, w.uf, sizeof(float) * B * c.D, hipMemcpyDeviceToDevice, s));
+  if (item_feat) DCUE_HIP_CHECK(hipMemcpyAsync(item_feat, w.f, sizeof(float) * (size_t)M * c.D, hipMemcpyDeviceToDevice, s));
+  if (loss) DCUE_HIP_CHECK(hipMemcpyAsync(loss, w.loss, sizeof(float), hipMemcpyDeviceToDevice, s));
+  return DCUE_OK;
+}
+
+int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws,
+                        size_t ws_bytes, const float* dscores, float emb_grad_scale, void* stream) {
+  Ctx c;
+  TRY(init_ctx(&c, m));
+  TRY(check_batch(b));
+  if (!t || !t->data || !ws || !m->grads || !m->emb_grad || !m->emb_slot) return DCUE_ERR_INVALID;
+  Ws w;
+  if (carve(&m->dims, b->n_rows, b->n_neg, b->n_items, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
+  carve(&m->dims, b->n_rows, b->n_neg, b->n_items, ws, &w);
+  hipStream_t s = (hipStream_t)stream;
+  const int B = b->n_rows, N = b->n_neg, M = b->n_items;
+  const int H = c.H, D = c.D, E = c.E;
+  const double copies = (double)B * (1 + N);
+  const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
+
+  TRY(launch_score_bwd(w.uf, w.f, b, D, dscores ? dscores : w.dhinge, w.cosv, w.norms, w.du,
+                       w.dfcopy, s));
+  TRY(launch_item_grad(w.dfcopy, b, D, w.df, s));
+
+  // fc: dW[n][k] = sum_m df[m][n] z[m][k] (z = bn5(y5)); db = sum df; g5 = df W
+  {
+    GemmArgs g = {};
+    g.M = D; g.N = D; g.K = M;
+    g.A = w.y[5]; g.sam = 1; g.sak = D;  // A(k, m) = y5[m][k], BN5 affine on the row index
+    g.tmean = w.mean[5]; g.ta = w.a[5]; g.tbeta = c.P(seg_bn_b(5));
+    g.B = w.df; g.sbk = D; g.sbn = 1;
+    g.C = c.Gd(SEG_FC_W); g.scm = 1; g.scn = D;
+    TRY(launch_gemm(3, g, s));
+    TRY(launch_colsum(w.df, M, D, c.Gd(SEG_FC_B), s));
+    g = GemmArgs{};
+    g.M = M; g.N = D; g.K = D;
+    g.A = w.df; g.sam = D; g.sak = 1;
+    g.B = c.P(SEG_FC_W); g.sbk = D; g.sbn = 1;
+    g.C = w.g[5]; g.scm = D; g.scn = 1;
+    TRY(launch_gemm(0, g, s));
+  }
+  // conv layers 5..1
+  for (int l = 5; l >= 1; --l) {
+    const LayerGeom gm = layer_geom(l);
+    const int C = l == 5 ? D : H;
+    const int cin = l == 1 ? kMels : H;
+    int nparts = 0;
+    TRY(launch_bwd_partials(w.g[l], w.y[l], w.mean[l], w.invstd[l], (long)M * gm.lp, C, w.partials,
+                            &nparts, s));
+    TRY(launch_bwd_finalize(w.partials, nparts, C, w.sD[l], w.sDx[l], c.Gd(seg_bn_w(l)),
+                            c.Gd(seg_bn_b(l)), s));
+    const float invN = (float)(1.0 / (copies * gm.lp));
+    WgradArgs wa = {};
+    wa.xsrc = l == 1 ? t->data : (const void*)w.y[l - 1];
+    wa.item_track = b->item_track;
+    wa.x_mean = w.mean[l - 1];
+    wa.x_a = l == 1 ? w.invstd[0] : w.a[l - 1];
+    wa.x_beta = l == 1 ? nullptr : c.P(seg_bn_b(l - 1));
+    wa.g_l = w.g[l]; wa.y_l = w.y[l]; wa.idx_l = w.idx[l];
+    wa.mean_l = w.mean[l]; wa.invstd_l = w.invstd[l]; wa.a_l = w.a[l];
+    wa.sD = w.sD[l]; wa.sDx = w.sDx[l]; wa.invN = invN; wa.counts = w.counts;
+    wa.M = M; wa.cout = C; wa.cin = cin;
+    wa.wpart = w.wpart; wa.bpart = w.bpart;
+    const int nch = wgrad_nchunk(l, M, C, cin);
+    TRY(launch_conv_wgrad(l, l == 1 ? src : SRC_ACT, wa, nch, s));
+    TRY(launch_wgrad_reduce(l, w.wpart, w.bpart, nch, C, cin, c.Gd(seg_conv_w(l)),
+                            c.Gd(seg_conv_b(l)), w.G, w.S, s));
+    if (l == 1) {
+      TRY(launch_bn0_grads(w.G, w.S, c.P(seg_conv_w(1)), c.P(seg_bn_w(0)), c.P(seg_bn_b(0)), H,
+                           c.Gd(seg_conv_w(1)), c.Gd(seg_bn_w(0)), c.Gd(seg_bn_b(0)), s));
+    } else {
+      RowsArgs ra = {};
+      ra.src = w.g[l]; ra.y_l = w.y[l]; ra.idx_l = w.idx[l];
+      ra.mean_l = w.mean[l]; ra.invstd_l = w.invstd[l]; ra.a_l = w.a[l];
+      ra.sD = w.sD[l]; ra.sDx = w.sDx[l]; ra.invN = invN; ra.counts = w.counts;
+      ra.wpack = m->wpack + wpack_offset(&m->dims, l, true);
+      ra.out = w.g[l - 1];
+      ra.M = M;
+      ra.nout = H;
+      TRY(launch_conv_dgrad(l, C, ra, s));
+    }
+  }
+  // user tower
+  {
+    GemmArgs g = {};
+    // dW2[n][k] = sum_b du[b][n] relu(h1)[b][k]   (as C[k][n], A(k,b) = relu(h1[b][k]))
+    g.M = E; g.N = D; g.K = B;
+    g.A = w.h1; g.sam = 1; g.sak = E;
+    g.B = w.du; g.sbk = D; g.sbn = 1;
+    g.C = c.Gd(SEG_L2_W); g.scm = 1; g.scn = E;
+    TRY(launch_gemm(1, g, s));
+    TRY(launch_colsum(w.du, B, D, c.Gd(SEG_L2_B), s));
+    // dh1 = (du W2) * (h1 > 0)
+    g = GemmArgs{};
+    g.M = B; g.N = E; g.K = D;
+    g.A = w.du; g.sam = D; g.sak = 1;
+    g.B = c.P(SEG_L2_W); g.sbk = E; g.sbn = 1;
+    g.C = w.dh1; g.scm = E; g.scn = 1;
+    g.cmask = w.h1;
+    TRY(launch_gemm(0, g, s));
+    // dW1[n][k] = sum_b dh1[b][n] relu(e)[b][k]
+    g = GemmArgs{};
+    g.M = E; g.N = E; g.K = B;
+    g.A = w.emb_g; g.sam = 1; g.sak = E;
+    g.B = w.dh1; g.sbk = E; g.sbn = 1;
+    g.C = c.Gd(SEG_L1_W); g.scm = 1; g.scn = E;
+    TRY(launch_gemm(1, g, s));
+    TRY(launch_colsum(w.dh1, B, E, c.Gd(SEG_L1_B), s));
+    // de = (dh1 W1) * (e > 0)
+    g = GemmArgs{};
+    g.M = B; g.N = E; g.K = E;
+    g.A = w.dh1; g.sam = E; g.sak = 1;
+    g.B = c.P(SEG_L1_W); g.sbk = E; g.sbn = 1;
+    g.C = w.de; g.scm = E; g.scn = 1;
+    g.cmask = w.emb_g;
+    TRY(launch_gemm(0, g, s));
+    TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, s));
+  }
+  return DCUE_OK;
+}
+
+int dcue_adam_step(const dcue_model* m, const dcue_adam_args* a, void* stream) {
+  Ctx c;
+  TRY(init_ctx(&c, m));
+  if (!a || !m->grads || !m->exp_avg || !m->exp_avg_sq || a->step < 1) return DCUE_ERR_INVALID;
+  if (a->update_embedding && (!m->emb || !m->emb_exp_avg || !m->emb_exp_avg_sq || !m->emb_slot || !m->emb_grad))
+    return DCUE_ERR_INVALID;
+  TRY(launch_adam(m, a, c.poff, (hipStream_t)stream));
+  return launch_pack(m, c.poff, (hipStream_t)stream);
+}
+
+int dcue_item_tower_eval(const dcue_model* m, const dcue_tracks* t, const int32_t* item_track,
+                         int32_t n_items, void* ws, size_t ws_bytes, float* item_feat,
+                         void* stream) {
+  Ctx c;
+  TRY(init_ctx(&c, m));
+  if (!t || !t->data || !item_track || !ws || !item_feat || n_items <= 0) return DCUE_ERR_INVALID;
+  Ws w;
+  if (carve(&m->dims, 1, 0, n_items, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
+  carve(&m->dims, 1, 0, n_items, ws, &w);
+  hipStream_t s = (hipStream_t)stream;
+  TRY(item_forward(c, w, t, item_track, n_items, (double)n_items, false, nullptr, s));
+  DCUE_HIP_CHECK(hipMemcpyAsync(item_feat, w.f, sizeof(float) * (size_t)n_items * c.D,
+                                hipMemcpyDeviceToDevice, s));
+  return DCUE_OK;
+}
+
+int dcue_user_tower(const dcue_model* m, const int64_t* users, int32_t n, void* ws, size_t ws_bytes,
+                    float* user_feat, void* stream) {
+  Ctx c;
+  TRY(init_ctx(&c, m));
+  if (!users || !ws || !user_feat || n <= 0 || !m->emb) return DCUE_ERR_INVALID;
+  Ws w;
+  if (carve(&m->dims, n, 0, 1, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
+  carve(&m->dims, n, 0, 1, ws, &w);
+  hipStream_t s = (hipStream_t)stream;
+  TRY(user_forward(c, w, users, n, s));
+  DCUE_HIP_CHECK(hipMemcpyAsync(user_feat, w.uf, sizeof(float) * (size_t)n * c.D,
+                                hipMemcpyDeviceToDevice, s));
+  return DCUE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,593 @@
+// Item-tower convolutions on f32-input MFMA (v_mfma_f32_16x16x4_f32), gfx950.
+//
+// Reference ops replaced (dcrecommend/dcue/audiomodels/truedcuemel1dbn.py):
+//   forward  bn_{l-1} -> Conv1d_l -> MaxPool1d -> ReLU   (:77-99), with BN_l batch statistics
+//   backward Conv1d weight/bias grads, input grads, MaxPool1d/ReLU/BatchNorm backward (autograd of
+//            the same ops, nn/dcue.py:208)
+//
+// Data layout in HBM (all fp32 unless noted):
+//   tracks   [n_tracks][131][128] fp16|fp32      frame-major rows of mel bins (one 256/512-B row per frame)
+//   y_l      [M][Lp_l][C_l]   ReLU(maxpool(conv_l)) = input of BN_l;  idx_l same shape, uint8 argmax
+//   g_l      [M][Lp_l][C_l]   dL/d(BN_l output), summed over an item's copies
+//   wpack    [ks][cin/4][cout][4] forward B operand; [ks][cout/4][cin][4] (taps reversed) dgrad B
+// Rows of the GEMM are (item, position) pairs packed densely over items; a workgroup owns 16*TW rows
+// and all 128 output channels of its column block (4 waves x 32). Its A operand is an LDS slab of
+// the input positions those rows touch (taps + zero halos), built once with the neighbouring
+// elementwise op fused into the load, then read with ds_read_b128 (4 consecutive K per lane; the
+// four MFMA k-steps of a 16-deep K chunk take one component each).
+#include "dcue_internal.h"
+
+namespace dcue {
+
+template <int SRC, int KC, int LIN, int POOLL, int LPL>
+__device__ __forceinline__ float4 slab_value(const RowsArgs& a, long i, int p, int c4) {
+  const int c = 4 * c4;
+  float x[4];
+  if constexpr (SRC == SRC_TRACK_F16 || SRC == SRC_TRACK_F32) {
+    const long trk = a.item_track[i];
+    const long off = (trk * kFrames + p) * kMels + c;
+    if constexpr (SRC == SRC_TRACK_F16) {
+      const uint2 raw = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.src) + off);
+      const __half2 h0 = *reinterpret_cast<const __half2*>(&raw.x);
+      const __half2 h1 = *reinterpret_cast<const __half2*>(&raw.y);
+      x[0] = __low2float(h0); x[1] = __high2float(h0); x[2] = __low2float(h1); x[3] = __high2float(h1);
+    } else {
+      const float4 v = ld4(reinterpret_cast<const float*>(a.src) + off);
+      x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+    }
+  } else if constexpr (SRC == SRC_ACT) {
+    const float4 v = ld4(reinterpret_cast<const float*>(a.src) + ((i * LIN + p) * KC + c));
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  }
+  if constexpr (SRC != SRC_DZ) {
+    const float4 mu = ld4(a.in_mean + c), sc = ld4(a.in_a + c);
+    const float4 be = a.in_beta ? ld4(a.in_beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    return make_float4((x[0] - mu.x) * sc.x + be.x, (x[1] - mu.y) * sc.y + be.y,
+                       (x[2] - mu.z) * sc.z + be.z, (x[3] - mu.w) * sc.w + be.w);
+  } else {
+    // conv position p of layer l -> pool window w, offset j; gradient reaches p only if it was the
+    // window's argmax and the window's ReLU was active (threshold_backward on the ReLU output).
+    const int w = p / POOLL, j = p - w * POOLL;
+    const long base = (i * LPL + w) * KC + c;
+    const float4 g = ld4(reinterpret_cast<const float*>(a.src) + base);
+    const float4 y = ld4(a.y_l + base);
+    const uint32_t id = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
+    const float cnt = a.counts ? a.counts[i] : 1.f;
+    const float kD = cnt * a.invN;
+    const float gv[4] = {g.x, g.y, g.z, g.w}, yv[4] = {y.x, y.y, y.z, y.w};
+    float r[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int cc = c + s;
+      const float xh = (yv[s] - a.mean_l[cc]) * a.invstd_l[cc];
+      const float dx = a.a_l[cc] * (gv[s] - kD * a.sD[cc] - kD * xh * a.sDx[cc]);
+      const int arg = (id >> (8 * s)) & 0xff;
+      r[s] = (arg == j && yv[s] > 0.f) ? dx : 0.f;
+    }
+    return make_float4(r[0], r[1], r[2], r[3]);
+  }
+}
+
+// MODE 0 = forward (pool+relu+stats epilogue), 1 = dgrad (plain store).
+// Slab position p of item i is valid for 0 <= p < LIN; rows are (i, t), t < R; tap k of row t reads
+// slab position t + k - PADL.
+template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,
+          int POOLL>
+__global__ __launch_bounds__(256) void k_conv_rows(RowsArgs a) {
+  constexpr int RX = R + KS - 1;
+  constexpr int ROWS = TW * 16;
+  constexpr int MAXI = (ROWS + R - 1) / R + 1;
+  constexpr int PITCH = KC + 8;  // == 8 (mod 64) dwords: conflict-free ds_read_b128 over 16 rows
+  constexpr int C4 = KC / 4;
+  constexpr int NSTEP = KS * (KC / 16);
+  extern __shared__ __attribute__((aligned(16))) float slab[];
+
+  const int M = a.M;
+  const long total = (long)M * R;
+  const long gr0 = (long)blockIdx.x * ROWS;
+  const long gr1 = min(gr0 + ROWS, total);
+  const long i0 = gr0 / R, i1 = (gr1 - 1) / R;
+  const long elo = i0 * RX + (gr0 - i0 * R);
+  const int nslab = (int)(i1 * RX + (gr1 - 1 - i1 * R) + KS - elo);
+  (void)MAXI;
+
+  for (int e = threadIdx.x; e < nslab * C4; e += 256) {
+    const int sr = e / C4, c4 = e - sr * C4;
+    const long E = elo + sr;
+    const long i = E / RX;
+    const int p = (int)(E - i * RX) - PADL;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < M && p >= 0 && p < LIN) v = slab_value<SRC, KC, LIN, POOLL, LPL>(a, i, p, c4);
+    st4(&slab[sr * PITCH + 4 * c4], v);
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int nout = a.nout;
+  const int ocol0 = blockIdx.y * 128 + wave * 32;
+  if (ocol0 >= nout) return;  // no barrier follows
+
+  int sbase[TW];
+#pragma unroll
+  for (int r = 0; r < TW; ++r) {
+    long gr = gr0 + 16 * r + l16;
+    if (gr >= total) gr = gr0;
+    const long i = gr / R;
+    sbase[r] = (int)(i * RX + (gr - i * R) - elo) * PITCH + 4 * g;
+  }
+
+  f32x4 acc[TW][2];
+#pragma unroll
+  for (int r = 0; r < TW; ++r) acc[r][0] = acc[r][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const float* wp = a.wpack + ((size_t)g * nout + ocol0 + l16) * 4;
+  const size_t wstep = (size_t)16 * nout;
+  float4 b0 = ld4(wp), b1 = ld4(wp + 64);
+  for (int st = 0; st < NSTEP; ++st) {
+    float4 nb0 = b0, nb1 = b1;
+    if (st + 1 < NSTEP) {
+      nb0 = ld4(wp + (st + 1) * wstep);
+      nb1 = ld4(wp + (st + 1) * wstep + 64);
+    }
+    const int k = st / (KC / 16);
+    const int c0 = (st - k * (KC / 16)) * 16;
+    const int aoff = k * PITCH + c0;
+    float4 av[TW];
+#pragma unroll
+    for (int r = 0; r < TW; ++r) av[r] = *reinterpret_cast<const float4*>(&slab[sbase[r] + aoff]);
+#pragma unroll
+    for (int r = 0; r < TW; ++r) {
+      acc[r][0] = mfma4(av[r].x, b0.x, acc[r][0]);
+      acc[r][1] = mfma4(av[r].x, b1.x, acc[r][1]);
+    }
+#pragma unroll
+    for (int r = 0; r < TW; ++r) {
+      acc[r][0] = mfma4(av[r].y, b0.y, acc[r][0]);
+      acc[r][1] = mfma4(av[r].y, b1.y, acc[r][1]);
+    }
+#pragma unroll
+    for (int r = 0; r < TW; ++r) {
+      acc[r][0] = mfma4(av[r].z, b0.z, acc[r][0]);
+      acc[r][1] = mfma4(av[r].z, b1.z, acc[r][1]);
+    }
+#pragma unroll
+    for (int r = 0; r < TW; ++r) {
+      acc[r][0] = mfma4(av[r].w, b0.w, acc[r][0]);
+      acc[r][1] = mfma4(av[r].w, b1.w, acc[r][1]);
+    }
+    b0 = nb0;
+    b1 = nb1;
+  }
+
+  if constexpr (MODE == 1) {
+#pragma unroll
+    for (int r = 0; r < TW; ++r) {
+      const long grb = gr0 + 16 * r + 4 * g;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const int o = ocol0 + 16 * ct + l16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (grb + j < total) a.out[(grb + j) * nout + o] = acc[r][ct][j];
+      }
+    }
+  } else {
+    constexpr int LP = R / POOL;
+    float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const int o = ocol0 + 16 * ct + l16;
+      const float bias = a.bias[o];
+#pragma unroll
+      for (int r = 0; r < TW; ++r) {
+        const long grb = gr0 + 16 * r + 4 * g;
+#pragma unroll
+        for (int win = 0; win < 4 / POOL; ++win) {
+          const long row = grb + win * POOL;  // first conv row of this pool window
+          if (row < total) {
+            const long i = row / R;
+            const int w = (int)(row - i * R) / POOL;
+            float best = acc[r][ct][win * POOL] + bias;
+            int arg = 0;
+#pragma unroll
+            for (int j = 1; j < POOL; ++j) {
+              const float v = acc[r][ct][win * POOL + j] + bias;
+              if (v > best) { best = v; arg = j; }  // first maximum wins (max_pool1d)
+            }
+            const float y = best > 0.f ? best : 0.f;
+            const long oidx = (i * LP + w) * nout + o;
+            a.out[oidx] = y;
+            a.out_idx[oidx] = (uint8_t)arg;
+            const float cnt = a.counts ? a.counts[i] : 1.f;
+            ssum[ct] += cnt * y;
+            ssq[ct] += cnt * y * y;
+          }
+        }
+      }
+    }
+    if (a.partials) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        float s = ssum[ct], q = ssq[ct];
+        s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+        q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+        if (g == 0) {
+          const int o = ocol0 + 16 * ct + l16;
+          a.partials[((long)blockIdx.x * 2 + 0) * nout + o] = s;
+          a.partials[((long)blockIdx.x * 2 + 1) * nout + o] = q;
+        }
+      }
+    }
+  }
+}
+
+template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,
+          int POOLL>
+static int run_rows(const RowsArgs& a, hipStream_t s) {
+  constexpr int ROWS = TW * 16;
+  constexpr int MAXI = (ROWS + R - 1) / R + 1;
+  constexpr int SLAB = ROWS + MAXI * (KS - 1);
+  constexpr size_t LDS = (size_t)SLAB * (KC + 8) * sizeof(float);
+  static_assert(LDS <= 160 * 1024, "slab exceeds LDS");
+  auto kern = k_conv_rows<MODE, SRC, KC, KS, PADL, LIN, R, POOL, TW, LPL, POOLL>;
+  static bool attr = false;
+  if (!attr) {
+    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)LDS));
+    attr = true;
+  }
+  const long total = (long)a.M * R;
+  dim3 grid((unsigned)((total + ROWS - 1) / ROWS), (unsigned)((a.nout + 127) / 128));
+  hipLaunchKernelGGL(kern, grid, dim3(256), LDS, s, a);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+// Row tiles per workgroup, per layer (forward). Chosen so the slab stays <= ~100 KB.
+static constexpr int fwd_tw(int layer) { return layer == 1 ? 8 : layer == 2 ? 8 : layer == 5 ? 8 : 4; }
+
+int conv_fwd_grid(int layer, int M) {
+  const LayerGeom gm = layer_geom(layer);
+  const long R = (long)gm.lp * gm.pool;
+  const long rows = fwd_tw(layer) * 16;
+  return (int)(((long)M * R + rows - 1) / rows);
+}
+
+template <int L, int KC, int SRC>
+static int fwd_layer(const RowsArgs& a, hipStream_t s) {
+  constexpr LayerGeom gm = layer_geom(L);
+  return run_rows<0, SRC, KC, gm.ks, gm.pad, gm.lin, gm.lp * gm.pool, gm.pool, fwd_tw(L), 1, 1>(a, s);
+}
+
+template <int L>
+static int fwd_kc(int kc, int src, const RowsArgs& a, hipStream_t s) {
+  if constexpr (L == 1) {
+    if (kc != kMels) return DCUE_ERR_INVALID;
+    return src == SRC_TRACK_F16 ? fwd_layer<1, 128, SRC_TRACK_F16>(a, s)
+                                : fwd_layer<1, 128, SRC_TRACK_F32>(a, s);
+  } else {
+    switch (kc) {
+      case 32: return fwd_layer<L, 32, SRC_ACT>(a, s);
+      case 64: return fwd_layer<L, 64, SRC_ACT>(a, s);
+      case 128: return fwd_layer<L, 128, SRC_ACT>(a, s);
+      case 256: return fwd_layer<L, 256, SRC_ACT>(a, s);
+      default: return DCUE_ERR_UNSUPPORTED;
+    }
+  }
+}
+
+int launch_conv_fwd(int layer, int kc, int src, const RowsArgs& a, hipStream_t s) {
+  switch (layer) {
+    case 1: return fwd_kc<1>(kc, src, a, s);
+    case 2: return fwd_kc<2>(kc, src, a, s);
+    case 3: return fwd_kc<3>(kc, src, a, s);
+    case 4: return fwd_kc<4>(kc, src, a, s);
+    case 5: return fwd_kc<5>(kc, src, a, s);
+    default: return DCUE_ERR_INVALID;
+  }
+}
+
+// dgrad of layer L: rows = (item, input position t' < Lin_L), slab = layer-L conv positions
+// [0, Lp*pool) carrying dz, taps reversed (PADL = ks-1-pad).
+template <int L, int KC>
+static int dgrad_layer(const RowsArgs& a, hipStream_t s) {
+  constexpr LayerGeom gm = layer_geom(L);
+  return run_rows<1, SRC_DZ, KC, gm.ks, gm.ks - 1 - gm.pad, gm.lp * gm.pool, gm.lin, 1, 4, gm.lp,
+                  gm.pool>(a, s);
+}
+
+template <int L>
+static int dgrad_kc(int kc, const RowsArgs& a, hipStream_t s) {
+  switch (kc) {
+    case 32: return dgrad_layer<L, 32>(a, s);
+    case 64: return dgrad_layer<L, 64>(a, s);
+    case 128: return dgrad_layer<L, 128>(a, s);
+    case 256: return dgrad_layer<L, 256>(a, s);
+    default: return DCUE_ERR_UNSUPPORTED;
+  }
+}
+
+int launch_conv_dgrad(int layer, int kc, const RowsArgs& a, hipStream_t s) {
+  switch (layer) {
+    case 2: return dgrad_kc<2>(kc, a, s);
+    case 3: return dgrad_kc<3>(kc, a, s);
+    case 4: return dgrad_kc<4>(kc, a, s);
+    case 5: return dgrad_kc<5>(kc, a, s);
+    default: return DCUE_ERR_INVALID;
+  }
+}
+
+// ------------------------------------------------------------------------------------ wgrad
+// dW[o][k*cin+c] = sum over conv rows (i,t) of dz[i][t][o] * x[i][t+k-pad][c]: a GEMM whose K is
+// the row dimension. Workgroup = 128 (o) x 128 (kc) output block x one chunk of rows; the chunk is
+// streamed through LDS RCH rows at a time (dz and x tiles, both built by fused elementwise loads);
+// each wave owns a 64x64 block (4x4 MFMA tiles). Partial blocks per chunk are summed by
+// k_wgrad_reduce in a fixed order (deterministic). EDGES (layer 1) also accumulates the per-output
+// sums of dz at the first/last two positions: with them the reduce recovers, per tap, the sum of dz
+// over positions whose input is not zero padding -- what bn0's beta gradient and the bn0 affine
+// split of dW1 need ("bn0 without conv1 dgrad").
+template <int SRCX, int KS, int PAD, int LIN, int R, int POOL, int LP, int RCH, bool EDGES>
+__global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
+  constexpr int PW = 128 + 16;  // == 16 (mod 32): ds_read_b32 rows r and r+1 on disjoint banks
+  constexpr int NB = EDGES ? 5 : 1;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* dzs = lds;
+  float* xs = lds + RCH * PW;
+  __shared__ float bsum[8][NB][128];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int wo = wave >> 1, wk = wave & 1;
+  const int cout = a.cout, cin = a.cin, kcn = KS * cin;
+  const int obase = blockIdx.y * 128, kcbase = blockIdx.x * 128;
+  const long total = (long)a.M * R;
+  const long r_begin = (long)blockIdx.z * a.rows_per_chunk;
+  const long r_end = min(r_begin + a.rows_per_chunk, total);
+  const bool do_bias = blockIdx.x == 0;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 bacc[NB];
+#pragma unroll
+  for (int e = 0; e < NB; ++e) bacc[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  const int q = tid & 31, slot = tid >> 5;  // fill mapping: 4-channel quad, row slot (8 slots)
+  for (long rb = r_begin; rb < r_end; rb += RCH) {
+    for (int rr = slot; rr < RCH; rr += 8) {
+      const long row = rb + rr;
+      float4 dz = make_float4(0.f, 0.f, 0.f, 0.f), xv = dz;
+      const int o = obase + 4 * q;
+      const int kc = kcbase + 4 * q;
+      if (row < r_end) {
+        const long i = row / R;
+        const int t = (int)(row - i * R);
+        if (o < cout) {
+          const int w = t / POOL, j = t - w * POOL;
+          const long base = (i * LP + w) * cout + o;
+          const float4 gg = ld4(a.g_l + base), yy = ld4(a.y_l + base);
+          const uint32_t id = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
+          const float kD = (a.counts ? a.counts[i] : 1.f) * a.invN;
+          const float gv[4] = {gg.x, gg.y, gg.z, gg.w}, yv[4] = {yy.x, yy.y, yy.z, yy.w};
+          float r4[4];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const int oc = o + s;
+            const float xh = (yv[s] - a.mean_l[oc]) * a.invstd_l[oc];
+            const float dx = a.a_l[oc] * (gv[s] - kD * a.sD[oc] - kD * xh * a.sDx[oc]);
+            r4[s] = (((id >> (8 * s)) & 0xff) == (uint32_t)j && yv[s] > 0.f) ? dx : 0.f;
+          }
+          dz = make_float4(r4[0], r4[1], r4[2], r4[3]);
+          if (do_bias) {
+            bacc[0].x += dz.x; bacc[0].y += dz.y; bacc[0].z += dz.z; bacc[0].w += dz.w;
+            if constexpr (EDGES) {  // static indices only: keeps bacc[] in registers
+              const int e = t == 0 ? 1 : t == 1 ? 2 : t == R - 2 ? 3 : t == R - 1 ? 4 : 0;
+#pragma unroll
+              for (int k = 1; k < NB; ++k) {
+                const float f = e == k ? 1.f : 0.f;
+                bacc[k].x += f * dz.x; bacc[k].y += f * dz.y; bacc[k].z += f * dz.z; bacc[k].w += f * dz.w;
+              }
+            }
+          }
+        }
+        if (kc < kcn) {
+          const int k = kc / cin, c = kc - k * cin;
+          const int p = t + k - PAD;
+          if (p >= 0 && p < LIN) {
+            float x[4];
+            if constexpr (SRCX == SRC_TRACK_F16 || SRCX == SRC_TRACK_F32) {
+              const long off = ((long)a.item_track[i] * kFrames + p) * kMels + c;
+              if constexpr (SRCX == SRC_TRACK_F16) {
+                const uint2 raw = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.xsrc) + off);
+                const __half2 h0 = *reinterpret_cast<const __half2*>(&raw.x);
+                const __half2 h1 = *reinterpret_cast<const __half2*>(&raw.y);
+                x[0] = __low2float(h0); x[1] = __high2float(h0); x[2] = __low2float(h1); x[3] = __high2float(h1);
+              } else {
+                const float4 v = ld4(reinterpret_cast<const float*>(a.xsrc) + off);
+                x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+              }
+            } else {
+              const float4 v = ld4(reinterpret_cast<const float*>(a.xsrc) + ((i * LIN + p) * cin + c));
+              x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+            }
+            const float4 mu = ld4(a.x_mean + c), sc = ld4(a.x_a + c);
+            const float4 be = a.x_beta ? ld4(a.x_beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+            xv = make_float4((x[0] - mu.x) * sc.x + be.x, (x[1] - mu.y) * sc.y + be.y,
+                             (x[2] - mu.z) * sc.z + be.z, (x[3] - mu.w) * sc.w + be.w);
+          }
+        }
+      }
+      st4(&dzs[rr * PW + 4 * q], dz);
+      st4(&xs[rr * PW + 4 * q], xv);
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int r0 = 0; r0 < RCH; r0 += 4) {
+      float av[4], bv[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) av[m] = dzs[(r0 + g) * PW + 64 * wo + 16 * m + l16];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) bv[n] = xs[(r0 + g) * PW + 64 * wk + 16 * n + l16];
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = mfma4(av[m], bv[n], acc[m][n]);
+    }
+    __syncthreads();
+  }
+
+  // partial block -> wpart[z][o][kc]; D lane map: o = 4g + reg, kc = l16
+  float* wp = a.wpart + (size_t)blockIdx.z * cout * kcn;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int kc = kcbase + 64 * wk + 16 * n + l16;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int o = obase + 64 * wo + 16 * m + 4 * g + j;
+        if (o < cout && kc < kcn) wp[(size_t)o * kcn + kc] = acc[m][n][j];
+      }
+    }
+  if (do_bias) {
+#pragma unroll
+    for (int e = 0; e < NB; ++e) st4(&bsum[slot][e][4 * q], bacc[e]);
+    __syncthreads();
+    if (tid < 128 && obase + tid < cout) {
+#pragma unroll
+      for (int e = 0; e < NB; ++e) {
+        float v = 0.f;
+#pragma unroll
+        for (int sl = 0; sl < 8; ++sl) v += bsum[sl][e][tid];
+        a.bpart[((size_t)blockIdx.z * NB + e) * cout + obase + tid] = v;
+      }
+    }
+  }
+}
+
+static constexpr int kWgradRch = 64;
+
+int wgrad_nchunk(int layer, int M, int cout, int cin) {
+  const LayerGeom gm = layer_geom(layer);
+  const long rows = (long)M * gm.lp * gm.pool;
+  const int blocks = ((gm.ks * cin + 127) / 128) * ((cout + 127) / 128);
+  long n = (512 + blocks - 1) / blocks;
+  const long maxn = (rows + kWgradRch - 1) / kWgradRch;
+  if (n > maxn) n = maxn;
+  if (n < 1) n = 1;
+  return (int)n;
+}
+
+template <int L, int SRCX>
+static int wgrad_layer(const WgradArgs& a0, int nchunk, hipStream_t s) {
+  constexpr LayerGeom gm = layer_geom(L);
+  constexpr int R = gm.lp * gm.pool;
+  constexpr bool EDGES = L == 1;
+  constexpr size_t LDS = (size_t)2 * kWgradRch * (128 + 16) * sizeof(float);
+  auto kern = k_conv_wgrad<SRCX, gm.ks, gm.pad, gm.lin, R, gm.pool, gm.lp, kWgradRch, EDGES>;
+  static bool attr = false;
+  if (!attr) {
+    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)LDS));
+    attr = true;
+  }
+  WgradArgs a = a0;
+  const long rows = (long)a.M * R;
+  long rpc = (rows + nchunk - 1) / nchunk;
+  rpc = (rpc + kWgradRch - 1) / kWgradRch * kWgradRch;
+  a.rows_per_chunk = (int)rpc;
+  dim3 grid((unsigned)((gm.ks * a.cin + 127) / 128), (unsigned)((a.cout + 127) / 128), (unsigned)nchunk);
+  hipLaunchKernelGGL(kern, grid, dim3(256), LDS, s, a);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+int launch_conv_wgrad(int layer, int src, const WgradArgs& a, int nchunk, hipStream_t s) {
+  switch (layer) {
+    case 1: return src == SRC_TRACK_F16 ? wgrad_layer<1, SRC_TRACK_F16>(a, nchunk, s)
+                                        : wgrad_layer<1, SRC_TRACK_F32>(a, nchunk, s);
+    case 2: return wgrad_layer<2, SRC_ACT>(a, nchunk, s);
+    case 3: return wgrad_layer<3, SRC_ACT>(a, nchunk, s);
+    case 4: return wgrad_layer<4, SRC_ACT>(a, nchunk, s);
+    case 5: return wgrad_layer<5, SRC_ACT>(a, nchunk, s);
+    default: return DCUE_ERR_INVALID;
+  }
+}
+
+// Sum partial blocks over chunks (fixed order) and write reference layout dW[o][c][k], db[o].
+// Layer 1 writes G[o][k*cin+c] (the xhat0 contraction) and S[k][o] instead (see k_bn0_grads).
+__global__ void k_wgrad_reduce(const float* __restrict__ wpart, const float* __restrict__ bpart,
+                               int nchunk, int cout, int cin, int ks, int nb, float* dW, float* db,
+                               float* G, float* S) {
+  const long kcn = (long)ks * cin;
+  const long nw = (long)cout * kcn;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < nw) {
+    float v = 0.f;
+    for (int z = 0; z < nchunk; ++z) v += wpart[(size_t)z * nw + idx];
+    const long o = idx / kcn, kc = idx - o * kcn;
+    const long k = kc / cin, c = kc - k * cin;
+    if (G) G[idx] = v;
+    else dW[(o * cin + c) * ks + k] = v;
+  } else if (idx < nw + cout) {
+    const int o = (int)(idx - nw);
+    float e[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < nchunk; ++z)
+      for (int j = 0; j < nb; ++j) e[j] += bpart[((size_t)z * nb + j) * cout + o];
+    db[o] = e[0];
+    if (S) {  // layer 1: tap k of row t reads input t+k-2; zero padding at t+k-2 < 0 or > 130
+      S[0 * cout + o] = e[0] - e[1] - e[2];
+      S[1 * cout + o] = e[0] - e[1];
+      S[2 * cout + o] = e[0] - e[4];
+      S[3 * cout + o] = e[0] - e[3] - e[4];
+    }
+  }
+}
+
+int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int nchunk, int cout,
+                        int cin, float* dW, float* db, float* G_tmp, float* S_tmp, hipStream_t s) {
+  const LayerGeom gm = layer_geom(layer);
+  const long n = (long)cout * gm.ks * cin + cout;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, wpart,
+                     bpart, nchunk, cout, cin, gm.ks, layer == 1 ? 5 : 1, dW, db,
+                     layer == 1 ? G_tmp : nullptr, layer == 1 ? S_tmp : nullptr);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+// bn0 gradients without conv1's input gradient: with xhat0 the normalised input and
+// G[o][k*128+c] = sum dz1 * xhat0_pad, S[k][o] = sum of dz1 over rows whose tap-k input is real,
+//   dW1[o][c][k] = gamma0[c] G + beta0[c] S,   dgamma0[c] = sum_{o,k} W1 G,   dbeta0[c] = sum_{o,k} W1 S.
+__global__ void k_bn0_grads(const float* __restrict__ G, const float* __restrict__ S,
+                            const float* __restrict__ W1, const float* gamma0, const float* beta0,
+                            int H, float* dW1, float* dgamma0, float* dbeta0) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= kMels) return;
+  const float ga = gamma0[c], be = beta0[c];
+  float dg = 0.f, db = 0.f;
+  for (int o = 0; o < H; ++o)
+    for (int k = 0; k < 4; ++k) {
+      const float gv = G[(size_t)o * 4 * kMels + k * kMels + c];
+      const float sv = S[k * H + o];
+      const float w = W1[((size_t)o * kMels + c) * 4 + k];
+      dg += w * gv;
+      db += w * sv;
+      dW1[((size_t)o * kMels + c) * 4 + k] = ga * gv + be * sv;
+    }
+  dgamma0[c] = dg;
+  dbeta0[c] = db;
+}
+
+int launch_bn0_grads(const float* G, const float* S, const float* W1, const float* gamma0,
+                     const float* beta0, int H, float* dW1, float* dgamma0, float* dbeta0,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(k_bn0_grads, dim3(2), dim3(64), 0, s, G, S, W1, gamma0, beta0, H, dW1, dgamma0,
+                     dbeta0);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+}  // namespace dcue

@@ -1,0 +1,65 @@
+// Shared device/host helpers for libdcue_hip (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+#include "dcue.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define DCUE_HIP_CHECK(expr)                              \
+  do {                                                    \
+    if ((expr) != hipSuccess) return DCUE_ERR_HIP;        \
+  } while (0)
+#define DCUE_LAUNCH_CHECK() DCUE_HIP_CHECK(hipGetLastError())
+
+namespace dcue {
+
+constexpr int kMels = DCUE_N_MELS;     // 128, truedcuemel1dbn.py:24
+constexpr int kFrames = DCUE_N_FRAMES; // 131, datasets/dcuedataset.py:235
+constexpr int kWave = 64;
+
+// Per-layer geometry of the default item tower (truedcuemel1dbn.py:25-61).
+//   conv positions Lconv = Lin + 2*pad - ks + 1, pooled Lp = floor(Lconv / pool); only the
+//   R = Lp*pool conv rows that land in a pool window are computed (the reference drops the rest).
+struct LayerGeom {
+  int ks, pad, pool, lin, lp;
+};
+__host__ __device__ constexpr LayerGeom layer_geom(int l) {
+  return l == 1 ? LayerGeom{4, 2, 4, 131, 33}
+       : l == 2 ? LayerGeom{4, 2, 4, 33, 8}
+       : l == 3 ? LayerGeom{4, 2, 4, 8, 2}
+       : l == 4 ? LayerGeom{2, 1, 2, 2, 1}
+                : LayerGeom{1, 0, 1, 1, 1};
+}
+
+// v_mfma_f32_16x16x4_f32: A lane l = A[l&15][l>>4], B lane l = B[l>>4][l&15],
+// D lane l, reg r = D[4*(l>>4)+r][l&15]. Exact f32 products, k-ordered f32 accumulation.
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// bump allocator over a caller-owned workspace (host side)
+struct Arena {
+  char* base;
+  size_t cap, used;
+  template <typename T>
+  T* take(size_t n) {
+    size_t off = (used + 255) & ~size_t(255);
+    used = off + n * sizeof(T);
+    return base ? reinterpret_cast<T*>(base + off) : nullptr;
+  }
+};
+
+}  // namespace dcue

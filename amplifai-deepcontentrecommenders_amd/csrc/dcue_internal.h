@@ -1,0 +1,112 @@
+// Internal launch interfaces shared by the libdcue_hip translation units.
+#pragma once
+
+#include "dcue_common.h"
+
+namespace dcue {
+
+// -------------------------------------------------------------- conv as row-GEMM (fwd / dgrad)
+// One kernel shape serves the forward conv of every layer and the input-gradient (dgrad) of
+// layers 2..5: rows = (item, position) pairs, columns = output channels, K = taps x slab channels.
+// The A operand is an LDS "slab" of input positions (with zero halos) built from its source with
+// the neighbouring elementwise op fused into the load (BatchNorm apply in forward; BatchNorm
+// backward + ReLU mask + max-pool routing in dgrad).
+enum SlabSrc { SRC_TRACK_F16 = 0, SRC_TRACK_F32 = 1, SRC_ACT = 2, SRC_DZ = 3 };
+
+struct RowsArgs {
+  const void* src;            // tracks [n_tracks][131][128] | y_{l-1} [M][Lin][KC] | g_l [M][Lp_l][KC]
+  const int32_t* item_track;  // tracks only
+  const float* in_mean;       // forward BN apply: (x - mean) * a + beta
+  const float* in_a;
+  const float* in_beta;
+  const float* y_l;           // dgrad: layer-l ReLU output (pre-BN) [M][Lp_l][KC]
+  const uint8_t* idx_l;       // dgrad: layer-l max-pool argmax [M][Lp_l][KC]
+  const float* mean_l;
+  const float* invstd_l;
+  const float* a_l;           // gamma_l * invstd_l
+  const float* sD;            // sum of g_l per channel
+  const float* sDx;           // sum of g_l * xhat_l per channel
+  float invN;                 // 1 / (copies * positions)
+  const float* counts;        // [M] copies per item (nullable -> 1)
+  const float* wpack;         // [KS][KC/4][nout][4]
+  const float* bias;          // forward [nout]
+  float* out;                 // forward y_l [M][Lp][nout]; dgrad g_{l-1} [M][R][nout]
+  uint8_t* out_idx;           // forward argmax [M][Lp][nout]
+  float* partials;            // forward BN stats partials [grid.x][2][nout] (null: eval)
+  int M;
+  int nout;
+};
+
+struct WgradArgs {
+  const void* xsrc;           // layer input: tracks (l=1) or y_{l-1} [M][Lin][cin]
+  const int32_t* item_track;
+  const float* x_mean;        // x = (src - mean) * a + beta ; l=1 uses xhat0 (a = invstd0, beta = 0)
+  const float* x_a;
+  const float* x_beta;        // nullable
+  const float* g_l;           // dz construction, as RowsArgs
+  const float* y_l;
+  const uint8_t* idx_l;
+  const float* mean_l;
+  const float* invstd_l;
+  const float* a_l;
+  const float* sD;
+  const float* sDx;
+  float invN;
+  const float* counts;
+  int M, cout, cin;
+  int rows_per_chunk;
+  float* wpart;               // [nchunk][cout][KS*cin]  (kc = k*cin + c)
+  float* bpart;               // [nchunk][NB][cout]
+};
+
+int launch_conv_fwd(int layer, int kc, int src, const RowsArgs& a, hipStream_t s);
+int launch_conv_dgrad(int layer, int kc, const RowsArgs& a, hipStream_t s);
+int conv_fwd_grid(int layer, int M);  // grid.x of the forward launch (partials rows)
+int launch_conv_wgrad(int layer, int src, const WgradArgs& a, int nchunk, hipStream_t s);
+int wgrad_nchunk(int layer, int M, int cout, int cin);
+int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int nchunk, int cout,
+                        int cin, float* dW, float* db, float* G_tmp, float* S_tmp, hipStream_t s);
+int launch_bn0_grads(const float* G, const float* S, const float* W1, const float* gamma0,
+                     const float* beta0, int H, float* dW1, float* dgamma0, float* dbeta0,
+                     hipStream_t s);
+
+// ------------------------------------------------------------------------------- dense ops
+struct GemmArgs {
+  int M, N, K;
+  const float* A; long sam, sak; const int64_t* arow;  // A(m,k) = A[row(m)*sam + k*sak]
+  const float* B; long sbk, sbn;                       // B(k,n) = B[k*sbk + n*sbn]
+  const float* tmean; const float* ta; const float* tbeta;  // A transform 2: (x-mean[k])*a[k]+beta[k]
+  const float* bias;                                   // [N] nullable
+  float* C; long scm, scn;                             // C(m,n)
+  const float* cmask;                                  // nullable: C(m,n) *= (cmask(m,n) > 0)
+};
+// A transform: 0 none, 1 relu, 2 BN affine per k (column), 3 BN affine per m (row)
+int launch_gemm(int ta, const GemmArgs& g, hipStream_t s);
+
+int launch_input_stats(int src, const void* tracks, const int32_t* item_track, const float* counts,
+                       int M, float* partials, int* nparts, hipStream_t s);
+int launch_bn_finalize(const float* partials, int nparts, int C, double count, const float* gamma,
+                       float* rmean, float* rvar, int64_t* nbt, int train, float* mean,
+                       float* invstd, float* a, hipStream_t s);
+int launch_bwd_partials(const float* g, const float* y, const float* mean, const float* invstd,
+                        long rows, int C, float* partials, int* nparts, hipStream_t s);
+int launch_bwd_finalize(const float* partials, int nparts, int C, float* sD, float* sDx,
+                        float* dgamma, float* dbeta, hipStream_t s);
+int launch_colsum(const float* A, int M, int N, float* out, hipStream_t s);
+
+int launch_item_counts(const dcue_batch* b, float* counts, hipStream_t s);
+int launch_score_fwd(const float* uf, const float* f, const dcue_batch* b, int d, float margin,
+                     float* scores, float* cosv, float* norms, float* row_loss, float* loss,
+                     float* dhinge, hipStream_t s);
+int launch_score_bwd(const float* uf, const float* f, const dcue_batch* b, int d,
+                     const float* dscores, const float* cosv, const float* norms, float* du,
+                     float* dfcopy, hipStream_t s);
+int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df, hipStream_t s);
+int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float scale,
+                    float* emb_grad, int32_t* slot, hipStream_t s);
+int launch_adam(const dcue_model* m, const dcue_adam_args* a, const int64_t* poff, hipStream_t s);
+int launch_pack(const dcue_model* m, const int64_t* poff, hipStream_t s);
+int launch_gather_rows(const float* table, const int64_t* rows, int n, int E, float* out,
+                       hipStream_t s);
+
+}  // namespace dcue

@@ -1,0 +1,181 @@
+/*
+ * dcue.h -- C ABI of libdcue_hip.so, the MI355X (gfx950) DCUE training-step library.
+ *
+ * The reference (estebandito22/Amplifai-DeepContentRecommenders) is pure Python/PyTorch; its
+ * "operator interface" for the hot path is the torch module/trainer API listed per entry point
+ * below. These entry points are what a ctypes binding of that interface calls.
+ *
+ * Conventions
+ *  - Every pointer is a DEVICE pointer unless the name ends in _host. The caller (PyTorch's caching
+ *    allocator in the shipped binding) owns every buffer; the library allocates nothing.
+ *  - Every call is asynchronous on `stream` (a hipStream_t passed as void*) and returns a
+ *    dcue_status; argument errors are detected on the host before anything is launched.
+ *  - Float math is fp32 throughout (f32-input MFMA, exact f32 products); spectrogram tables may be
+ *    stored as fp16 (lossless for fp16-representable inputs) or fp32.
+ *  - Layouts: spectrogram table [n_tracks][n_frames=131][n_mels=128] (frame-major rows of mel bins);
+ *    dense parameters are ONE flat fp32 buffer in reference parameter order and reference tensor
+ *    layouts (offsets from dcue_param_layout); the user-embedding table is a separate
+ *    [n_users][user_embdim] buffer (sharded by user across ranks).
+ */
+#ifndef DCUE_H_
+#define DCUE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCUE_ABI_VERSION 1
+#define DCUE_N_MELS 128
+#define DCUE_N_FRAMES 131
+#define DCUE_N_BN 6
+/* dense parameter segments, reference order (DCUENet.named_parameters(), minus the embedding) */
+#define DCUE_N_DENSE_SEGMENTS 28
+
+typedef enum {
+  DCUE_OK = 0,
+  DCUE_ERR_INVALID = 1,     /* bad argument (null pointer, size out of range) */
+  DCUE_ERR_UNSUPPORTED = 2, /* valid for the reference, not (yet) for this build (e.g. d % 32 != 0) */
+  DCUE_ERR_HIP = 3,         /* a HIP launch failed */
+  DCUE_ERR_WORKSPACE = 4    /* workspace too small */
+} dcue_status;
+
+typedef struct dcue_dims {
+  int32_t conv_hidden; /* H: nn/dcue.py:45 conv_hidden (multiple of 32, <= 256) */
+  int32_t feature_dim; /* d: feature_dim (multiple of 32, <= 256) */
+  int32_t user_embdim; /* E: u_embdim (<= 1024) */
+  int32_t reserved;
+  int64_t n_users;     /* rows of the (local shard of the) user table */
+} dcue_dims;
+
+/* Model state. Replaces DCUENet's parameters/buffers (dcue/dcue.py:21-68) + torch.optim.Adam state. */
+typedef struct dcue_model {
+  dcue_dims dims;
+  float* params;       /* flat dense params, dcue_param_layout offsets */
+  float* grads;        /* same layout */
+  float* exp_avg;      /* Adam first moment, same layout */
+  float* exp_avg_sq;   /* Adam second moment, same layout */
+  float* emb;          /* [n_users][E] user_embd.embeddings.weight */
+  float* emb_exp_avg;
+  float* emb_exp_avg_sq;
+  float* emb_grad;     /* [max_rows][E] compact rows of the embedding gradient (one per distinct user) */
+  int32_t* emb_slot;   /* [n_users] slot of each user row in emb_grad, -1 = no gradient this step */
+  float* bn_stats;     /* running_mean/var per BN layer, dcue_bn_layout offsets */
+  int64_t* bn_batches; /* [6] num_batches_tracked */
+  float* wpack;        /* packed conv weights (dcue_wpack_floats), refreshed by dcue_pack_weights */
+} dcue_model;
+
+/* One training batch, already resident in HBM.
+ * Items are the spectrograms the item tower runs on. Catalogue mode (datasets/dcuedataset.py:242-250):
+ * M = B*(1+N) items, item b = positive of row b, item B+b*N+j = negative j of row b. In-batch mode
+ * (nn/dcue.py:698-709): M = B, negative (b,j) is a copy of positive neg_item[b][j]; the library runs
+ * the tower once per distinct item and weights BatchNorm statistics by each item's copy count, which
+ * is exactly the reference's computation on the duplicated [pos; neg] stack. */
+#define DCUE_LAYOUT_CATALOGUE 0 /* M = B*(1+N), item b = positive b, item B+b*N+j = negative (b,j) */
+#define DCUE_LAYOUT_GATHER 1    /* positives are items 0..B-1, negative (b,j) = item neg_item[b][j] */
+
+typedef struct dcue_batch {
+  int32_t n_rows;            /* B */
+  int32_t n_neg;             /* N */
+  int32_t n_items;           /* M */
+  int32_t layout;            /* DCUE_LAYOUT_* */
+  const int64_t* users;      /* [B] local user rows */
+  const int32_t* item_track; /* [M] track row of each item */
+  const int32_t* neg_item;   /* [B][N] item of each negative copy (GATHER layout; ignored otherwise) */
+} dcue_batch;
+
+typedef struct dcue_tracks {
+  const void* data;  /* [n_tracks][131][128] */
+  int64_t n_tracks;
+  int32_t dtype;     /* 0 = fp16, 1 = fp32 */
+  int32_t reserved;
+} dcue_tracks;
+
+typedef struct dcue_adam_args {
+  float lr, beta1, beta2, eps, weight_decay; /* param_group values set by CyclicLRWithRestarts */
+  int32_t step;                              /* Adam step count AFTER increment (1 on first step) */
+  int32_t update_embedding;                  /* 0: skip the user table (frozen) */
+} dcue_adam_args;
+
+/* ---------------------------------------------------------------------------------- layout */
+int dcue_abi_version(void);
+/* offsets[DCUE_N_DENSE_SEGMENTS+1] (floats) of each dense parameter in `params` */
+int dcue_param_layout(const dcue_dims* dims, int64_t* offsets_host);
+/* offsets[2*DCUE_N_BN+1]: running_mean(l), running_var(l) for l = 0..5 */
+int dcue_bn_layout(const dcue_dims* dims, int64_t* offsets_host);
+int dcue_wpack_floats(const dcue_dims* dims, int64_t* n_floats_host);
+int dcue_workspace_bytes(const dcue_dims* dims, int32_t max_rows, int32_t max_neg,
+                         int32_t max_items, size_t* bytes_host);
+
+/* ------------------------------------------------------------------------- hot-path entries */
+/* Refresh wpack from params (after any host-side write of conv weights and after every Adam step). */
+int dcue_pack_weights(const dcue_model* m, void* stream);
+
+/* Forward: DCUENet.forward(u, pos, neg) (dcue/dcue.py:70-108) + hinge loss (nn/dcue.py:167-170).
+ * train != 0: model.train() semantics -- BatchNorm batch statistics over all copies, running stats
+ * and num_batches_tracked updated, activations kept in `ws` for dcue_train_backward.
+ * train == 0: model.eval() semantics (running statistics, nothing updated).
+ * Outputs (each nullable): scores[B][N], user feats [B][d], item feats [M][d], loss[1] (mean over
+ * rows of the summed hinge). */
+int dcue_forward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws,
+                 size_t ws_bytes, int32_t train, float margin, float* scores, float* user_feat,
+                 float* item_feat, float* loss, void* stream);
+
+/* Backward of the last train-mode dcue_forward on the same ws: loss.backward() (nn/dcue.py:208).
+ * dscores == NULL: gradient of the hinge loss; else dL/dscores [B][N] from the caller.
+ * Writes m->grads (dense, overwritten) and the compact embedding gradient (emb_grad/emb_slot),
+ * scaled by emb_grad_scale (1/world_size under user-sharded data parallelism). */
+int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws,
+                        size_t ws_bytes, const float* dscores, float emb_grad_scale, void* stream);
+
+/* optimizer.step() (nn/dcue.py:209, torch.optim.Adam semantics): dense params + every user row
+ * (rows without a gradient this step still decay their moments and move, as the reference's dense
+ * embedding gradient does), then clears emb_slot and refreshes wpack. */
+int dcue_adam_step(const dcue_model* m, const dcue_adam_args* a, void* stream);
+
+/* Eval-mode item tower (running BN stats): DCUENet.conv(X) under model.eval() (nn/dcue.py:663). */
+int dcue_item_tower_eval(const dcue_model* m, const dcue_tracks* t, const int32_t* item_track,
+                         int32_t n_items, void* ws, size_t ws_bytes, float* item_feat, void* stream);
+/* Eval user tower: DCUENet.user_embd(idx) (nn/dcue.py:638). */
+int dcue_user_tower(const dcue_model* m, const int64_t* users, int32_t n, void* ws, size_t ws_bytes,
+                    float* user_feat, void* stream);
+
+/* Layout conversion of caller-provided spectrograms: [M][128][131] (the reference's per-track tensor,
+ * datasets/dcuedataset.py:234-235) -> [M][131][128] track rows (the table layout). */
+int dcue_transpose_spectrograms(const float* ncl, int32_t M, float* out, void* stream);
+/* Catalogue batch assembly (datasets/dcuedataset.py:242-250 + dcue/dcue.py:90 concat order):
+ * item_track = [pos_items[0..B); neg_items[b][j] at B + b*N + j]. */
+int dcue_build_catalogue_batch(const int64_t* pos_items, const int64_t* neg_items, int32_t B,
+                               int32_t N, int32_t* item_track, void* stream);
+
+/* ------------------------------------------------------------------------------ samplers */
+/* MT19937 state (numpy legacy RandomState): 624 words + position, in device memory. */
+typedef struct dcue_mt_state {
+  uint32_t key[624];
+  int32_t pos;
+  int32_t pad[3];
+} dcue_mt_state;
+
+/* np.random.seed(seed) into a device state (init_genrand). */
+int dcue_mt_seed(dcue_mt_state* state, uint32_t seed, void* stream);
+/* n tempered 32-bit outputs, advancing the state (genrand_int32). */
+int dcue_mt_draw(dcue_mt_state* state, uint32_t* out, int32_t n, void* stream);
+/* In-batch negatives (nn/dcue.py:698-709): neg[b][j] = masked draw over the B-1 other rows, from
+ * one global stream, row-major. Bit-exact with numpy for the same state. */
+int dcue_sample_inbatch(dcue_mt_state* state, int32_t B, int32_t N, int32_t* neg, void* stream);
+/* Catalogue negatives (datasets/dcuedataset.py:207-220): for each sample the user's non-items in
+ * the split (split_items sorted; user_split_rank = CSR over users of the ranks, inside split_items,
+ * of the user's split items, sorted), N draws with replacement. reseed != 0: every sample draws from
+ * a fresh stream seeded with `seed` (random_seed mode); else all samples share `state` in order.
+ * Writes item ids (values of split_items). */
+int dcue_sample_catalogue(dcue_mt_state* state, int32_t reseed, uint32_t seed,
+                          const int64_t* split_items, int64_t n_split, const int64_t* user_indptr,
+                          const int32_t* user_split_rank, const int64_t* users, int32_t n_samples,
+                          int32_t N, int64_t* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DCUE_H_ */

@@ -1,0 +1,86 @@
+"""CPU-side checks of the HIP library and the host mirror: the C ABI loads, exports every symbol
+include/dcue.h declares, reports the reference layouts; DCUENet builds the reference's parameters."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "dcue.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^int\s+(dcue_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_library_exports_header_symbols():
+    from dcrecommend import _native as nat
+    lib = nat.lib()
+    names = _declared()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), n
+    assert lib.dcue_abi_version() == 1
+
+
+def test_binding_covers_header():
+    from dcrecommend import _native as nat
+    assert set(_declared()) == set(nat._SIGS), set(_declared()) ^ set(nat._SIGS)
+
+
+def test_layouts_match_reference_shapes(golden):
+    from dcrecommend import _native as nat
+    g = golden("model_tiny.npz")
+    H, d = int(g["H"]), int(g["d"])
+    dims = nat.make_dims(H, d, 300, int(g["n_users"]))
+    off = nat.param_layout(dims)
+    for s, name in enumerate(nat.DENSE_NAMES):
+        n = g["init." + name].size
+        assert off[s] % 4 == 0
+        assert off[s + 1] - off[s] >= n, name
+        assert off[s + 1] - off[s] < n + 4, name
+    boff = nat.bn_layout(dims)
+    assert boff[1] - boff[0] >= 128 and boff[-1] > 0
+    assert nat.wpack_floats(dims) == 128 * H * 4 + 2 * (2 * H * H * 4 + H * H * 2 + d * H)
+    assert nat.workspace_bytes(dims, 4, 3, 16) > 0
+
+
+def test_unsupported_dims_rejected():
+    from dcrecommend import _native as nat
+    with pytest.raises(RuntimeError, match="UNSUPPORTED"):
+        nat.param_layout(nat.make_dims(128, 100, 300, 10))
+
+
+def test_dcuenet_init_matches_reference(golden):
+    from dcrecommend.dcue.dcue import DCUENet
+    g = golden("model_tiny.npz")
+    torch.manual_seed(int(g["seed"]))
+    net = DCUENet({"feature_dim": int(g["d"]), "conv_hidden": int(g["H"]), "user_embdim": 300,
+                   "user_count": int(g["n_users"]), "model_type": "truedcuemel1dbn"})
+    sd = net.state_dict()
+    keys = [k[len("init."):] for k in g.files if k.startswith("init.")]
+    assert set(sd) == set(keys)
+    for k in keys:
+        assert np.array_equal(sd[k].numpy(), g["init." + k]), k
+
+
+def test_dcuenet_model_type_errors():
+    from dcrecommend.dcue.dcue import DCUENet
+    args = {"feature_dim": 32, "conv_hidden": 32, "user_embdim": 300, "user_count": 4}
+    with pytest.raises(ValueError):
+        DCUENet(dict(args, model_type="nope"))
+    with pytest.raises(NotImplementedError):
+        DCUENet(dict(args, model_type="truedcuemel1dres"))
+
+
+def test_cpu_model_refuses_compute():
+    from dcrecommend.dcue.dcue import DCUENet
+    net = DCUENet({"feature_dim": 32, "conv_hidden": 32, "user_embdim": 300, "user_count": 4,
+                   "model_type": "truedcuemel1dbn"})
+    with pytest.raises(RuntimeError, match="GPU"):
+        net(torch.zeros(2, dtype=torch.long), torch.zeros(2, 128, 131), torch.zeros(2, 1, 128, 131))
