@@ -469,11 +469,15 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
 int dcue_adam_step(const dcue_model* m, const dcue_adam_args* a, void* stream) {
   Ctx c;
   TRY(init_ctx(&c, m));
-  if (!a || !m->grads || !m->exp_avg || !m->exp_avg_sq || a->step < 1) return DCUE_ERR_INVALID;
-  if (a->update_embedding && (!m->emb || !m->emb_exp_avg || !m->emb_exp_avg_sq || !m->emb_slot || !m->emb_grad))
+  if (!a || a->step < 1 || (a->parts & ~(DCUE_ADAM_DENSE | DCUE_ADAM_EMBEDDING))) return DCUE_ERR_INVALID;
+  const int parts = a->parts ? a->parts : (DCUE_ADAM_DENSE | DCUE_ADAM_EMBEDDING);
+  if ((parts & DCUE_ADAM_DENSE) && (!m->grads || !m->exp_avg || !m->exp_avg_sq)) return DCUE_ERR_INVALID;
+  if ((parts & DCUE_ADAM_EMBEDDING) &&
+      (!m->emb || !m->emb_exp_avg || !m->emb_exp_avg_sq || !m->emb_slot || !m->emb_grad))
     return DCUE_ERR_INVALID;
   TRY(launch_adam(m, a, c.poff, (hipStream_t)stream));
-  return launch_pack(m, c.poff, (hipStream_t)stream);
+  if (parts & DCUE_ADAM_DENSE) return launch_pack(m, c.poff, (hipStream_t)stream);
+  return DCUE_OK;
 }
 
 int dcue_item_tower_eval(const dcue_model* m, const dcue_tracks* t, const int32_t* item_track,

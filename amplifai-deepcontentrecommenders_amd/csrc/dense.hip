@@ -587,11 +587,14 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
   sc.bc2_sqrt = (float)sqrt(bc2);
   sc.eps = a->eps;
   sc.wd = a->weight_decay;
+  const int parts = a->parts ? a->parts : (DCUE_ADAM_DENSE | DCUE_ADAM_EMBEDDING);
   const long n = poff[DCUE_N_DENSE_SEGMENTS];
-  hipLaunchKernelGGL(k_adam_dense, dim3(512), dim3(256), 0, s, md->params, md->grads, md->exp_avg,
-                     md->exp_avg_sq, n, sc);
-  DCUE_LAUNCH_CHECK();
-  if (a->update_embedding && md->dims.n_users > 0) {
+  if (parts & DCUE_ADAM_DENSE) {
+    hipLaunchKernelGGL(k_adam_dense, dim3(512), dim3(256), 0, s, md->params, md->grads, md->exp_avg,
+                       md->exp_avg_sq, n, sc);
+    DCUE_LAUNCH_CHECK();
+  }
+  if ((parts & DCUE_ADAM_EMBEDDING) && md->dims.n_users > 0) {
     long blocks = (md->dims.n_users + 3) / 4;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(k_adam_embed, dim3((unsigned)blocks), dim3(256), 0, s, md->emb,

@@ -56,7 +56,11 @@ class Tracks(ctypes.Structure):
 class AdamArgs(ctypes.Structure):
     _fields_ = [("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
                 ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float), ("step", ctypes.c_int32),
-                ("update_embedding", ctypes.c_int32)]
+                ("parts", ctypes.c_int32)]
+
+
+ADAM_DENSE = 1
+ADAM_EMBEDDING = 2
 
 
 MT_STATE_BYTES = 624 * 4 + 16

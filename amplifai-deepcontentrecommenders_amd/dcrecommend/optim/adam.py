@@ -56,7 +56,7 @@ class NativeAdam(torch.optim.Optimizer):
         st = self._adam_state()
         self.step_count += 1
         args = nat.AdamArgs(float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]),
-                            float(g["weight_decay"]), self.step_count, 1)
+                            float(g["weight_decay"]), self.step_count, 0)
         model = self.net._model_struct(st)
         if not model.emb_grad:
             # no backward ran yet (e.g. a resumed optimizer): every row takes the zero-gradient step

@@ -93,10 +93,13 @@ typedef struct dcue_tracks {
   int32_t reserved;
 } dcue_tracks;
 
+#define DCUE_ADAM_DENSE 1     /* flat dense params, then the conv-weight repack */
+#define DCUE_ADAM_EMBEDDING 2 /* the user table */
+
 typedef struct dcue_adam_args {
   float lr, beta1, beta2, eps, weight_decay; /* param_group values set by CyclicLRWithRestarts */
   int32_t step;                              /* Adam step count AFTER increment (1 on first step) */
-  int32_t update_embedding;                  /* 0: skip the user table (frozen) */
+  int32_t parts;                             /* DCUE_ADAM_* mask; 0 = both */
 } dcue_adam_args;
 
 /* ---------------------------------------------------------------------------------- layout */
