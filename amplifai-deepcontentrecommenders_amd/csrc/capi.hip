@@ -76,27 +76,9 @@ void bn_offsets(const dcue_dims* d, int64_t* off) {
   off[2 * DCUE_N_BN] = o;
 }
 
-long wpack_floats(const dcue_dims* d) {
-  const long H = d->conv_hidden, D = d->feature_dim;
-  long n = 0;
-  for (int l = 1; l <= 5; ++l) {
-    const long cin = l == 1 ? kMels : H, cout = l == 5 ? D : H;
-    const long e = cin * cout * layer_geom(l).ks;
-    n += l == 1 ? e : 2 * e;
-  }
-  return n;
-}
-
 long wpack_offset(const dcue_dims* d, int l, bool bwd) {
-  const long H = d->conv_hidden, D = d->feature_dim;
-  long n = 0;
-  for (int k = 1; k <= 5; ++k) {
-    const long cin = k == 1 ? kMels : H, cout = k == 5 ? D : H;
-    const long e = cin * cout * layer_geom(k).ks;
-    if (k == l) return bwd ? n + e : n;
-    n += k == 1 ? e : 2 * e;
-  }
-  return n;
+  const WpackLayout wl = wpack_layout(d);
+  return bwd ? wl.conv_bwd[l] : wl.conv_fwd[l];
 }
 
 // pointers into the caller's workspace
@@ -106,8 +88,8 @@ struct Ws {
   float* partials;
   float* y[6];
   uint8_t* idx[6];
-  float *f, *uf, *emb_g, *h1;
-  float *cosv, *norms, *row_loss, *scores, *loss, *dhinge;
+  float *f, *uf, *h1;
+  float *cosv, *norms, *hinge, *scores, *loss, *dhinge;
   float *du, *dfcopy, *df;
   float* g[6];
   float *dh1, *de;
@@ -129,7 +111,7 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   }
   long pmax = 1024L * 2 * kMels;
   for (int l = 1; l <= 5; ++l) {
-    const long p = (long)conv_fwd_grid(l, M) * 2 * (l == 5 ? D : H);
+    const long p = (long)conv_fwd_grid(l, l == 1 ? kMels : H, M) * 2 * (l == 5 ? D : H);
     if (p > pmax) pmax = p;
   }
   if (512L * 2 * Cmax > pmax) pmax = 512L * 2 * Cmax;
@@ -143,11 +125,10 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   }
   w->f = ar.take<float>((long)M * D);
   w->uf = ar.take<float>((long)B * D);
-  w->emb_g = ar.take<float>((long)B * E);
   w->h1 = ar.take<float>((long)B * E);
   w->cosv = ar.take<float>((long)B * (N + 1));
   w->norms = ar.take<float>((long)B * (N + 2));
-  w->row_loss = ar.take<float>(B);
+  w->hinge = ar.take<float>((long)B * (N > 0 ? N : 1));
   w->scores = ar.take<float>((long)B * (N > 0 ? N : 1));
   w->loss = ar.take<float>(4);
   w->dhinge = ar.take<float>((long)B * (N > 0 ? N : 1));
@@ -211,7 +192,7 @@ int init_ctx(Ctx* c, const dcue_model* m) {
 
 // Item tower forward. train: batch statistics (weighted by counts) + running-stat update.
 int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t* item_track, int M,
-                 double copies, bool train, const float* counts, hipStream_t s) {
+                 double copies, bool train, const float* counts, float* f_out, hipStream_t s) {
   const dcue_model* m = c.m;
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
   int nparts = 0;
@@ -235,38 +216,38 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     a.nout = l == 5 ? c.D : c.H;
     TRY(launch_conv_fwd(l, l == 1 ? kMels : c.H, l == 1 ? src : SRC_ACT, a, s));
     const int C = a.nout;
-    TRY(launch_bn_finalize(w.partials, conv_fwd_grid(l, M), C, copies * layer_geom(l).lp,
+    TRY(launch_bn_finalize(w.partials, conv_fwd_grid(l, l == 1 ? kMels : c.H, M), C, copies * layer_geom(l).lp,
                            c.P(seg_bn_w(l)), c.rmean(l), c.rvar(l), m->bn_batches + l, train,
                            w.mean[l], w.invstd[l], w.a[l], s));
   }
-  // fc on BN5(y5): f = bn5(y5) W^T + b
-  GemmArgs g = {};
+  // fc on BN5(y5): f = bn5(y5) W^T + b   (truedcuemel1dbn.py:65,101)
+  TGemmArgs g = {};
   g.M = M; g.N = c.D; g.K = c.D;
   g.A = w.y[5]; g.sam = c.D; g.sak = 1;
-  g.tmean = w.mean[5]; g.ta = w.a[5]; g.tbeta = c.P(seg_bn_b(5));
+  g.amean = w.mean[5]; g.aa = w.a[5]; g.abeta = c.P(seg_bn_b(5));
   g.B = c.P(SEG_FC_W); g.sbk = 1; g.sbn = c.D;
   g.bias = c.P(SEG_FC_B);
-  g.C = w.f; g.scm = c.D; g.scn = 1;
-  return launch_gemm(2, g, s);
+  g.C = f_out ? f_out : w.f; g.scm = c.D; g.scn = 1;
+  return launch_tgemm(2, 0, g, s);
 }
 
-int user_forward(const Ctx& c, const Ws& w, const int64_t* users, int B, hipStream_t s) {
+// user tower (userembedding.py:33-44): h1 = relu(E[u]) W1^T + b1; uf = relu(h1) W2^T + b2
+int user_forward(const Ctx& c, const Ws& w, const int64_t* users, int B, float* uf_out, hipStream_t s) {
   const dcue_model* m = c.m;
-  TRY(launch_gather_rows(m->emb, users, B, c.E, w.emb_g, s));
-  GemmArgs g = {};
+  TGemmArgs g = {};
   g.M = B; g.N = c.E; g.K = c.E;
-  g.A = w.emb_g; g.sam = c.E; g.sak = 1;
+  g.A = m->emb; g.sam = c.E; g.sak = 1; g.arow = users;
   g.B = c.P(SEG_L1_W); g.sbk = 1; g.sbn = c.E;
   g.bias = c.P(SEG_L1_B);
   g.C = w.h1; g.scm = c.E; g.scn = 1;
-  TRY(launch_gemm(1, g, s));
-  g = GemmArgs{};
+  TRY(launch_tgemm(1, 0, g, s));
+  g = TGemmArgs{};
   g.M = B; g.N = c.D; g.K = c.E;
   g.A = w.h1; g.sam = c.E; g.sak = 1;
   g.B = c.P(SEG_L2_W); g.sbk = 1; g.sbn = c.E;
   g.bias = c.P(SEG_L2_B);
-  g.C = w.uf; g.scm = c.D; g.scn = 1;
-  return launch_gemm(1, g, s);
+  g.C = uf_out ? uf_out : w.uf; g.scm = c.D; g.scn = 1;
+  return launch_tgemm(1, 0, g, s);
 }
 
 int check_batch(const dcue_batch* b) {
@@ -306,7 +287,7 @@ int dcue_bn_layout(const dcue_dims* dims, int64_t* offsets_host) {
 int dcue_wpack_floats(const dcue_dims* dims, int64_t* n) {
   TRY(check_dims(dims));
   if (!n) return DCUE_ERR_INVALID;
-  *n = wpack_floats(dims);
+  *n = wpack_layout(dims).total;
   return DCUE_OK;
 }
 
@@ -316,6 +297,19 @@ int dcue_workspace_bytes(const dcue_dims* dims, int32_t max_rows, int32_t max_ne
   if (!bytes || max_rows <= 0 || max_neg < 0 || max_items <= 0) return DCUE_ERR_INVALID;
   Ws w;
   *bytes = carve(dims, max_rows, max_neg, max_items, nullptr, &w);
+  return DCUE_OK;
+}
+
+int dcue_workspace_outputs(const dcue_dims* dims, int32_t B, int32_t N, int32_t M,
+                           size_t* offsets_host) {
+  TRY(check_dims(dims));
+  if (!offsets_host || B <= 0 || N < 0 || M <= 0) return DCUE_ERR_INVALID;
+  Ws w;
+  carve(dims, B, N, M, nullptr, &w);
+  offsets_host[0] = (size_t)w.scores;
+  offsets_host[1] = (size_t)w.uf;
+  offsets_host[2] = (size_t)w.f;
+  offsets_host[3] = (size_t)w.loss;
   return DCUE_OK;
 }
 
@@ -338,10 +332,12 @@ int dcue_forward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   hipStream_t s = (hipStream_t)stream;
   const double copies = (double)b->n_rows * (1 + b->n_neg);
   TRY(launch_item_counts(b, w.counts, s));
-  TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, s));
-  TRY(user_forward(c, w, b->users, b->n_rows, s));
-  TRY(launch_score_fwd(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.row_loss, w.loss,
+  TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s));
+  TRY(user_forward(c, w, b->users, b->n_rows, nullptr, s));
+  TRY(launch_score_fwd(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.hinge, w.loss,
                        w.dhinge, s));
+  // the outputs live in the workspace (dcue_workspace_outputs gives their offsets); copies are
+  // made only for callers that ask for their own buffers
   const int B = b->n_rows, N = b->n_neg, M = b->n_items;
   if (scores && N > 0) DCUE_HIP_CHECK(hipMemcpyAsync(scores, w.scores, sizeof(float) * B * N, hipMemcpyDeviceToDevice, s));
   if (user_feat) DCUE_HIP_CHECK(hipMemcpyAsync(user_feat, w.uf, sizeof(float) * B * c.D, hipMemcpyDeviceToDevice, s));
@@ -368,23 +364,22 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
   TRY(launch_score_bwd(w.uf, w.f, b, D, dscores ? dscores : w.dhinge, w.cosv, w.norms, w.du,
                        w.dfcopy, s));
   TRY(launch_item_grad(w.dfcopy, b, D, w.df, s));
-
-  // fc: dW[n][k] = sum_m df[m][n] z[m][k] (z = bn5(y5)); db = sum df; g5 = df W
+  // fc: dW[n][k] = sum_m df[m][n] bn5(y5)[m][k], db = sum_m df (row sums of A); g5 = df W
   {
-    GemmArgs g = {};
+    TGemmArgs g = {};
     g.M = D; g.N = D; g.K = M;
-    g.A = w.y[5]; g.sam = 1; g.sak = D;  // A(k, m) = y5[m][k], BN5 affine on the row index
-    g.tmean = w.mean[5]; g.ta = w.a[5]; g.tbeta = c.P(seg_bn_b(5));
-    g.B = w.df; g.sbk = D; g.sbn = 1;
-    g.C = c.Gd(SEG_FC_W); g.scm = 1; g.scn = D;
-    TRY(launch_gemm(3, g, s));
-    TRY(launch_colsum(w.df, M, D, c.Gd(SEG_FC_B), s));
-    g = GemmArgs{};
+    g.A = w.df; g.sam = 1; g.sak = D;
+    g.B = w.y[5]; g.sbk = D; g.sbn = 1;
+    g.bmean = w.mean[5]; g.ba = w.a[5]; g.bbeta = c.P(seg_bn_b(5));
+    g.C = c.Gd(SEG_FC_W); g.scm = D; g.scn = 1;
+    g.rowsum = c.Gd(SEG_FC_B);
+    TRY(launch_tgemm(0, 2, g, s));
+    g = TGemmArgs{};
     g.M = M; g.N = D; g.K = D;
     g.A = w.df; g.sam = D; g.sak = 1;
     g.B = c.P(SEG_FC_W); g.sbk = D; g.sbn = 1;
     g.C = w.g[5]; g.scm = D; g.scn = 1;
-    TRY(launch_gemm(0, g, s));
+    TRY(launch_tgemm(0, 0, g, s));
   }
   // conv layers 5..1
   for (int l = 5; l >= 1; --l) {
@@ -427,42 +422,42 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
       TRY(launch_conv_dgrad(l, C, ra, s));
     }
   }
-  // user tower
+  // user tower (userembedding.py:33-44 backward), then the compact embedding rows
   {
-    GemmArgs g = {};
-    // dW2[n][k] = sum_b du[b][n] relu(h1)[b][k]   (as C[k][n], A(k,b) = relu(h1[b][k]))
-    g.M = E; g.N = D; g.K = B;
-    g.A = w.h1; g.sam = 1; g.sak = E;
-    g.B = w.du; g.sbk = D; g.sbn = 1;
-    g.C = c.Gd(SEG_L2_W); g.scm = 1; g.scn = E;
-    TRY(launch_gemm(1, g, s));
-    TRY(launch_colsum(w.du, B, D, c.Gd(SEG_L2_B), s));
+    TGemmArgs g = {};
+    // dW2[n][k] = sum_b du[b][n] relu(h1)[b][k]; db2[n] = sum_b du[b][n]
+    g.M = D; g.N = E; g.K = B;
+    g.A = w.du; g.sam = 1; g.sak = D;
+    g.B = w.h1; g.sbk = E; g.sbn = 1;
+    g.C = c.Gd(SEG_L2_W); g.scm = E; g.scn = 1;
+    g.rowsum = c.Gd(SEG_L2_B);
+    TRY(launch_tgemm(0, 1, g, s));
     // dh1 = (du W2) * (h1 > 0)
-    g = GemmArgs{};
+    g = TGemmArgs{};
     g.M = B; g.N = E; g.K = D;
     g.A = w.du; g.sam = D; g.sak = 1;
     g.B = c.P(SEG_L2_W); g.sbk = E; g.sbn = 1;
     g.C = w.dh1; g.scm = E; g.scn = 1;
-    g.cmask = w.h1;
-    TRY(launch_gemm(0, g, s));
-    // dW1[n][k] = sum_b dh1[b][n] relu(e)[b][k]
-    g = GemmArgs{};
+    g.cmask = w.h1; g.smm = E; g.smn = 1;
+    TRY(launch_tgemm(0, 0, g, s));
+    // dW1[n][k] = sum_b dh1[b][n] relu(E[u_b])[k]; db1[n] = sum_b dh1[b][n]
+    g = TGemmArgs{};
     g.M = E; g.N = E; g.K = B;
-    g.A = w.emb_g; g.sam = 1; g.sak = E;
-    g.B = w.dh1; g.sbk = E; g.sbn = 1;
-    g.C = c.Gd(SEG_L1_W); g.scm = 1; g.scn = E;
-    TRY(launch_gemm(1, g, s));
-    TRY(launch_colsum(w.dh1, B, E, c.Gd(SEG_L1_B), s));
-    // de = (dh1 W1) * (e > 0)
-    g = GemmArgs{};
+    g.A = w.dh1; g.sam = 1; g.sak = E;
+    g.B = m->emb; g.sbk = E; g.sbn = 1; g.brow = b->users;
+    g.C = c.Gd(SEG_L1_W); g.scm = E; g.scn = 1;
+    g.rowsum = c.Gd(SEG_L1_B);
+    TRY(launch_tgemm(0, 1, g, s));
+    // de = (dh1 W1) * (E[u_b] > 0)
+    g = TGemmArgs{};
     g.M = B; g.N = E; g.K = E;
     g.A = w.dh1; g.sam = E; g.sak = 1;
     g.B = c.P(SEG_L1_W); g.sbk = E; g.sbn = 1;
     g.C = w.de; g.scm = E; g.scn = 1;
-    g.cmask = w.emb_g;
-    TRY(launch_gemm(0, g, s));
-    TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, s));
+    g.cmask = m->emb; g.smm = E; g.smn = 1; g.cmrow = b->users;
+    TRY(launch_tgemm(0, 0, g, s));
   }
+  TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, s));
   return DCUE_OK;
 }
 
@@ -489,11 +484,8 @@ int dcue_item_tower_eval(const dcue_model* m, const dcue_tracks* t, const int32_
   Ws w;
   if (carve(&m->dims, 1, 0, n_items, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
   carve(&m->dims, 1, 0, n_items, ws, &w);
-  hipStream_t s = (hipStream_t)stream;
-  TRY(item_forward(c, w, t, item_track, n_items, (double)n_items, false, nullptr, s));
-  DCUE_HIP_CHECK(hipMemcpyAsync(item_feat, w.f, sizeof(float) * (size_t)n_items * c.D,
-                                hipMemcpyDeviceToDevice, s));
-  return DCUE_OK;
+  return item_forward(c, w, t, item_track, n_items, (double)n_items, false, nullptr, item_feat,
+                      (hipStream_t)stream);
 }
 
 int dcue_user_tower(const dcue_model* m, const int64_t* users, int32_t n, void* ws, size_t ws_bytes,
@@ -504,11 +496,7 @@ int dcue_user_tower(const dcue_model* m, const int64_t* users, int32_t n, void* 
   Ws w;
   if (carve(&m->dims, n, 0, 1, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
   carve(&m->dims, n, 0, 1, ws, &w);
-  hipStream_t s = (hipStream_t)stream;
-  TRY(user_forward(c, w, users, n, s));
-  DCUE_HIP_CHECK(hipMemcpyAsync(user_feat, w.uf, sizeof(float) * (size_t)n * c.D,
-                                hipMemcpyDeviceToDevice, s));
-  return DCUE_OK;
+  return user_forward(c, w, users, n, user_feat, (hipStream_t)stream);
 }
 
 }  // extern "C"

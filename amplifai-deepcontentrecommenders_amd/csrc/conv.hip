@@ -19,27 +19,50 @@
 
 namespace dcue {
 
-template <int SRC, int KC, int LIN, int POOLL, int LPL>
-__device__ __forceinline__ float4 slab_value(const RowsArgs& a, long i, int p, int c4) {
+// Slab fill in two halves so a thread keeps several loads in flight: slab_load issues the raw
+// global reads of one float4 slot (after the item's track row is known), slab_finish applies the
+// fused elementwise op. The loads are the latency of these small kernels, not the math.
+struct Raw {
+  float4 a, b;
+  uint32_t id;
+};
+
+template <int SRC, int KC, int LIN, int LPL, int POOLL>
+__device__ __forceinline__ Raw slab_load(const RowsArgs& a, long i, int p, int c4, long trk) {
   const int c = 4 * c4;
-  float x[4];
-  if constexpr (SRC == SRC_TRACK_F16 || SRC == SRC_TRACK_F32) {
-    const long trk = a.item_track[i];
-    const long off = (trk * kFrames + p) * kMels + c;
+  Raw r;
+  if constexpr (SRC == SRC_TRACK_F16) {
+    const uint2 raw = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.src) +
+                                                      ((trk * kFrames + p) * kMels + c));
+    r.a.x = __uint_as_float(raw.x);
+    r.a.y = __uint_as_float(raw.y);
+  } else if constexpr (SRC == SRC_TRACK_F32) {
+    r.a = ld4(reinterpret_cast<const float*>(a.src) + ((trk * kFrames + p) * kMels + c));
+  } else if constexpr (SRC == SRC_ACT) {
+    r.a = ld4(reinterpret_cast<const float*>(a.src) + ((i * LIN + p) * KC + c));
+  } else {
+    const int w = p / POOLL;
+    const long base = (i * LPL + w) * KC + c;
+    r.a = ld4(reinterpret_cast<const float*>(a.src) + base);
+    r.b = ld4(a.y_l + base);
+    r.id = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
+  }
+  return r;
+}
+
+template <int SRC, int POOLL>
+__device__ __forceinline__ float4 slab_finish(const RowsArgs& a, long i, int p, int c4, const Raw& r) {
+  const int c = 4 * c4;
+  if constexpr (SRC != SRC_DZ) {
+    float x[4];
     if constexpr (SRC == SRC_TRACK_F16) {
-      const uint2 raw = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.src) + off);
-      const __half2 h0 = *reinterpret_cast<const __half2*>(&raw.x);
-      const __half2 h1 = *reinterpret_cast<const __half2*>(&raw.y);
+      const uint32_t lo = __float_as_uint(r.a.x), hi = __float_as_uint(r.a.y);
+      const __half2 h0 = *reinterpret_cast<const __half2*>(&lo);
+      const __half2 h1 = *reinterpret_cast<const __half2*>(&hi);
       x[0] = __low2float(h0); x[1] = __high2float(h0); x[2] = __low2float(h1); x[3] = __high2float(h1);
     } else {
-      const float4 v = ld4(reinterpret_cast<const float*>(a.src) + off);
-      x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+      x[0] = r.a.x; x[1] = r.a.y; x[2] = r.a.z; x[3] = r.a.w;
     }
-  } else if constexpr (SRC == SRC_ACT) {
-    const float4 v = ld4(reinterpret_cast<const float*>(a.src) + ((i * LIN + p) * KC + c));
-    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
-  }
-  if constexpr (SRC != SRC_DZ) {
     const float4 mu = ld4(a.in_mean + c), sc = ld4(a.in_a + c);
     const float4 be = a.in_beta ? ld4(a.in_beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     return make_float4((x[0] - mu.x) * sc.x + be.x, (x[1] - mu.y) * sc.y + be.y,
@@ -47,24 +70,19 @@ __device__ __forceinline__ float4 slab_value(const RowsArgs& a, long i, int p, i
   } else {
     // conv position p of layer l -> pool window w, offset j; gradient reaches p only if it was the
     // window's argmax and the window's ReLU was active (threshold_backward on the ReLU output).
-    const int w = p / POOLL, j = p - w * POOLL;
-    const long base = (i * LPL + w) * KC + c;
-    const float4 g = ld4(reinterpret_cast<const float*>(a.src) + base);
-    const float4 y = ld4(a.y_l + base);
-    const uint32_t id = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
-    const float cnt = a.counts ? a.counts[i] : 1.f;
-    const float kD = cnt * a.invN;
-    const float gv[4] = {g.x, g.y, g.z, g.w}, yv[4] = {y.x, y.y, y.z, y.w};
-    float r[4];
+    const int j = p % POOLL;
+    const float kD = (a.counts ? a.counts[i] : 1.f) * a.invN;
+    const float gv[4] = {r.a.x, r.a.y, r.a.z, r.a.w}, yv[4] = {r.b.x, r.b.y, r.b.z, r.b.w};
+    float o[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int cc = c + s;
       const float xh = (yv[s] - a.mean_l[cc]) * a.invstd_l[cc];
       const float dx = a.a_l[cc] * (gv[s] - kD * a.sD[cc] - kD * xh * a.sDx[cc]);
-      const int arg = (id >> (8 * s)) & 0xff;
-      r[s] = (arg == j && yv[s] > 0.f) ? dx : 0.f;
+      const int arg = (r.id >> (8 * s)) & 0xff;
+      o[s] = (arg == j && yv[s] > 0.f) ? dx : 0.f;
     }
-    return make_float4(r[0], r[1], r[2], r[3]);
+    return make_float4(o[0], o[1], o[2], o[3]);
   }
 }
 
@@ -91,14 +109,43 @@ __global__ __launch_bounds__(256) void k_conv_rows(RowsArgs a) {
   const int nslab = (int)(i1 * RX + (gr1 - 1 - i1 * R) + KS - elo);
   (void)MAXI;
 
-  for (int e = threadIdx.x; e < nslab * C4; e += 256) {
-    const int sr = e / C4, c4 = e - sr * C4;
-    const long E = elo + sr;
-    const long i = E / RX;
-    const int p = (int)(E - i * RX) - PADL;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < M && p >= 0 && p < LIN) v = slab_value<SRC, KC, LIN, POOLL, LPL>(a, i, p, c4);
-    st4(&slab[sr * PITCH + 4 * c4], v);
+  {
+    constexpr int FB = SRC == SRC_DZ ? 4 : 8;  // slab slots (float4) in flight per thread
+    const int nfill = nslab * C4;
+    for (int base = threadIdx.x; base < nfill; base += 256 * FB) {
+      long ii[FB], trk[FB];
+      int pp[FB];
+      bool ok[FB];
+      Raw raw[FB];
+#pragma unroll
+      for (int j = 0; j < FB; ++j) {
+        const int e = base + 256 * j;
+        const int sr = e / C4;
+        const long E = elo + sr;
+        ii[j] = E / RX;
+        pp[j] = (int)(E - ii[j] * RX) - PADL;
+        ok[j] = e < nfill && ii[j] < M && pp[j] >= 0 && pp[j] < LIN;
+        trk[j] = 0;
+      }
+      if constexpr (SRC == SRC_TRACK_F16 || SRC == SRC_TRACK_F32) {
+#pragma unroll
+        for (int j = 0; j < FB; ++j)
+          if (ok[j]) trk[j] = a.item_track[ii[j]];
+      }
+#pragma unroll
+      for (int j = 0; j < FB; ++j)
+        if (ok[j]) raw[j] = slab_load<SRC, KC, LIN, LPL, POOLL>(a, ii[j], pp[j], (base + 256 * j) % C4, trk[j]);
+#pragma unroll
+      for (int j = 0; j < FB; ++j) {
+        const int e = base + 256 * j;
+        if (e < nfill) {
+          const int sr = e / C4, c4 = e - sr * C4;
+          const float4 v = ok[j] ? slab_finish<SRC, POOLL>(a, ii[j], pp[j], c4, raw[j])
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+          st4(&slab[sr * PITCH + 4 * c4], v);
+        }
+      }
+    }
   }
   __syncthreads();
 
@@ -244,20 +291,49 @@ static int run_rows(const RowsArgs& a, hipStream_t s) {
   return DCUE_OK;
 }
 
-// Row tiles per workgroup, per layer (forward). Chosen so the slab stays <= ~100 KB.
-static constexpr int fwd_tw(int layer) { return layer == 1 ? 8 : layer == 2 ? 8 : layer == 5 ? 8 : 4; }
+// Row tiles per workgroup: the largest of 8/4/2/1 that still gives >= 256 workgroups (one per CU),
+// so small batches (in-batch negatives: M = B) spread over the chip instead of queueing behind a
+// few long-running workgroups.
+static int choose_tw(long rows) {
+  for (int tw : {8, 4, 2})
+    if ((rows + 16 * tw - 1) / (16 * tw) >= 256) return tw;
+  return 1;
+}
 
-int conv_fwd_grid(int layer, int M) {
+
+template <int L, int KC, int SRC, int TW>
+static int fwd_layer_tw(const RowsArgs& a, hipStream_t s) {
+  constexpr LayerGeom gm = layer_geom(L);
+  return run_rows<0, SRC, KC, gm.ks, gm.pad, gm.lin, gm.lp * gm.pool, gm.pool, TW, 1, 1>(a, s);
+}
+
+// LDS bytes of a slab for R rows per item, KS taps, KC channels and TW row tiles
+constexpr size_t slab_bytes(int R, int KS, int KC, int TW) {
+  return (size_t)(TW * 16 + ((TW * 16 + R - 1) / R + 1) * (KS - 1)) * (KC + 8) * sizeof(float);
+}
+constexpr int max_tw(int R, int KS, int KC) {
+  return slab_bytes(R, KS, KC, 8) <= 160 * 1024 ? 8
+       : slab_bytes(R, KS, KC, 4) <= 160 * 1024 ? 4
+       : slab_bytes(R, KS, KC, 2) <= 160 * 1024 ? 2 : 1;
+}
+
+int conv_fwd_grid(int layer, int kc, int M) {
   const LayerGeom gm = layer_geom(layer);
-  const long R = (long)gm.lp * gm.pool;
-  const long rows = fwd_tw(layer) * 16;
-  return (int)(((long)M * R + rows - 1) / rows);
+  const long rows = (long)M * gm.lp * gm.pool;
+  const int tw = min(choose_tw(rows), max_tw(gm.lp * gm.pool, gm.ks, kc));
+  const long per = 16L * tw;
+  return (int)((rows + per - 1) / per);
 }
 
 template <int L, int KC, int SRC>
 static int fwd_layer(const RowsArgs& a, hipStream_t s) {
   constexpr LayerGeom gm = layer_geom(L);
-  return run_rows<0, SRC, KC, gm.ks, gm.pad, gm.lin, gm.lp * gm.pool, gm.pool, fwd_tw(L), 1, 1>(a, s);
+  constexpr int TWMAX = max_tw(gm.lp * gm.pool, gm.ks, KC);
+  const int tw = min(choose_tw((long)a.M * gm.lp * gm.pool), TWMAX);
+  if constexpr (TWMAX >= 8) if (tw == 8) return fwd_layer_tw<L, KC, SRC, 8>(a, s);
+  if constexpr (TWMAX >= 4) if (tw == 4) return fwd_layer_tw<L, KC, SRC, 4>(a, s);
+  if constexpr (TWMAX >= 2) if (tw == 2) return fwd_layer_tw<L, KC, SRC, 2>(a, s);
+  return fwd_layer_tw<L, KC, SRC, 1>(a, s);
 }
 
 template <int L>
@@ -290,11 +366,22 @@ int launch_conv_fwd(int layer, int kc, int src, const RowsArgs& a, hipStream_t s
 
 // dgrad of layer L: rows = (item, input position t' < Lin_L), slab = layer-L conv positions
 // [0, Lp*pool) carrying dz, taps reversed (PADL = ks-1-pad).
+template <int L, int KC, int TW>
+static int dgrad_layer_tw(const RowsArgs& a, hipStream_t s) {
+  constexpr LayerGeom gm = layer_geom(L);
+  return run_rows<1, SRC_DZ, KC, gm.ks, gm.ks - 1 - gm.pad, gm.lp * gm.pool, gm.lin, 1, TW, gm.lp,
+                  gm.pool>(a, s);
+}
+
 template <int L, int KC>
 static int dgrad_layer(const RowsArgs& a, hipStream_t s) {
   constexpr LayerGeom gm = layer_geom(L);
-  return run_rows<1, SRC_DZ, KC, gm.ks, gm.ks - 1 - gm.pad, gm.lp * gm.pool, gm.lin, 1, 4, gm.lp,
-                  gm.pool>(a, s);
+  constexpr int TWMAX = max_tw(gm.lin, gm.ks, KC);
+  const int tw = min(choose_tw((long)a.M * gm.lin), TWMAX);
+  if constexpr (TWMAX >= 8) if (tw == 8) return dgrad_layer_tw<L, KC, 8>(a, s);
+  if constexpr (TWMAX >= 4) if (tw == 4) return dgrad_layer_tw<L, KC, 4>(a, s);
+  if constexpr (TWMAX >= 2) if (tw == 2) return dgrad_layer_tw<L, KC, 2>(a, s);
+  return dgrad_layer_tw<L, KC, 1>(a, s);
 }
 
 template <int L>
@@ -357,28 +444,71 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
 
   const int q = tid & 31, slot = tid >> 5;  // fill mapping: 4-channel quad, row slot (8 slots)
   for (long rb = r_begin; rb < r_end; rb += RCH) {
-    for (int rr = slot; rr < RCH; rr += 8) {
-      const long row = rb + rr;
-      float4 dz = make_float4(0.f, 0.f, 0.f, 0.f), xv = dz;
-      const int o = obase + 4 * q;
-      const int kc = kcbase + 4 * q;
-      if (row < r_end) {
-        const long i = row / R;
-        const int t = (int)(row - i * R);
-        if (o < cout) {
-          const int w = t / POOL, j = t - w * POOL;
-          const long base = (i * LP + w) * cout + o;
-          const float4 gg = ld4(a.g_l + base), yy = ld4(a.y_l + base);
-          const uint32_t id = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
-          const float kD = (a.counts ? a.counts[i] : 1.f) * a.invN;
-          const float gv[4] = {gg.x, gg.y, gg.z, gg.w}, yv[4] = {yy.x, yy.y, yy.z, yy.w};
+    // fill: this thread's 8 rows of the chunk in two batches of 4, all loads of a batch in flight
+    constexpr int FB = 4;
+    const int o = obase + 4 * q;
+    const int kc = kcbase + 4 * q;
+    const int kx = kc / cin, cx = kc - kx * cin;
+#pragma unroll
+    for (int rf = 0; rf < RCH / 8; rf += FB) {
+      long ii[FB], trk[FB];
+      int tt[FB];
+      bool zok[FB], xok[FB];
+      float4 gg[FB], yy[FB], xr[FB];
+      uint32_t id[FB];
+#pragma unroll
+      for (int j = 0; j < FB; ++j) {
+        const long row = rb + slot + 8 * (rf + j);
+        ii[j] = row / R;
+        tt[j] = (int)(row - ii[j] * R);
+        zok[j] = row < r_end && o < cout;
+        const int p = tt[j] + kx - PAD;
+        xok[j] = row < r_end && kc < kcn && p >= 0 && p < LIN;
+        trk[j] = 0;
+      }
+      if constexpr (SRCX == SRC_TRACK_F16 || SRCX == SRC_TRACK_F32) {
+#pragma unroll
+        for (int j = 0; j < FB; ++j)
+          if (xok[j]) trk[j] = a.item_track[ii[j]];
+      }
+#pragma unroll
+      for (int j = 0; j < FB; ++j) {
+        if (zok[j]) {
+          const long base = (ii[j] * LP + tt[j] / POOL) * cout + o;
+          gg[j] = ld4(a.g_l + base);
+          yy[j] = ld4(a.y_l + base);
+          id[j] = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
+        }
+        if (xok[j]) {
+          const int p = tt[j] + kx - PAD;
+          if constexpr (SRCX == SRC_TRACK_F16) {
+            const uint2 raw = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.xsrc) +
+                                                              ((trk[j] * kFrames + p) * kMels + cx));
+            xr[j].x = __uint_as_float(raw.x);
+            xr[j].y = __uint_as_float(raw.y);
+          } else if constexpr (SRCX == SRC_TRACK_F32) {
+            xr[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + ((trk[j] * kFrames + p) * kMels + cx));
+          } else {
+            xr[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + ((ii[j] * LIN + p) * cin + cx));
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < FB; ++j) {
+        const int rr = slot + 8 * (rf + j);
+        float4 dz = make_float4(0.f, 0.f, 0.f, 0.f), xv = dz;
+        if (zok[j]) {
+          const int t = tt[j], jp = t % POOL;
+          const float kD = (a.counts ? a.counts[ii[j]] : 1.f) * a.invN;
+          const float gv[4] = {gg[j].x, gg[j].y, gg[j].z, gg[j].w};
+          const float yv[4] = {yy[j].x, yy[j].y, yy[j].z, yy[j].w};
           float r4[4];
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
             const int oc = o + s;
             const float xh = (yv[s] - a.mean_l[oc]) * a.invstd_l[oc];
             const float dx = a.a_l[oc] * (gv[s] - kD * a.sD[oc] - kD * xh * a.sDx[oc]);
-            r4[s] = (((id >> (8 * s)) & 0xff) == (uint32_t)j && yv[s] > 0.f) ? dx : 0.f;
+            r4[s] = (((id[j] >> (8 * s)) & 0xff) == (uint32_t)jp && yv[s] > 0.f) ? dx : 0.f;
           }
           dz = make_float4(r4[0], r4[1], r4[2], r4[3]);
           if (do_bias) {
@@ -393,35 +523,24 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
             }
           }
         }
-        if (kc < kcn) {
-          const int k = kc / cin, c = kc - k * cin;
-          const int p = t + k - PAD;
-          if (p >= 0 && p < LIN) {
-            float x[4];
-            if constexpr (SRCX == SRC_TRACK_F16 || SRCX == SRC_TRACK_F32) {
-              const long off = ((long)a.item_track[i] * kFrames + p) * kMels + c;
-              if constexpr (SRCX == SRC_TRACK_F16) {
-                const uint2 raw = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.xsrc) + off);
-                const __half2 h0 = *reinterpret_cast<const __half2*>(&raw.x);
-                const __half2 h1 = *reinterpret_cast<const __half2*>(&raw.y);
-                x[0] = __low2float(h0); x[1] = __high2float(h0); x[2] = __low2float(h1); x[3] = __high2float(h1);
-              } else {
-                const float4 v = ld4(reinterpret_cast<const float*>(a.xsrc) + off);
-                x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
-              }
-            } else {
-              const float4 v = ld4(reinterpret_cast<const float*>(a.xsrc) + ((i * LIN + p) * cin + c));
-              x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
-            }
-            const float4 mu = ld4(a.x_mean + c), sc = ld4(a.x_a + c);
-            const float4 be = a.x_beta ? ld4(a.x_beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-            xv = make_float4((x[0] - mu.x) * sc.x + be.x, (x[1] - mu.y) * sc.y + be.y,
-                             (x[2] - mu.z) * sc.z + be.z, (x[3] - mu.w) * sc.w + be.w);
+        if (xok[j]) {
+          float x[4];
+          if constexpr (SRCX == SRC_TRACK_F16) {
+            const uint32_t lo = __float_as_uint(xr[j].x), hi = __float_as_uint(xr[j].y);
+            const __half2 h0 = *reinterpret_cast<const __half2*>(&lo);
+            const __half2 h1 = *reinterpret_cast<const __half2*>(&hi);
+            x[0] = __low2float(h0); x[1] = __high2float(h0); x[2] = __low2float(h1); x[3] = __high2float(h1);
+          } else {
+            x[0] = xr[j].x; x[1] = xr[j].y; x[2] = xr[j].z; x[3] = xr[j].w;
           }
+          const float4 mu = ld4(a.x_mean + cx), sc = ld4(a.x_a + cx);
+          const float4 be = a.x_beta ? ld4(a.x_beta + cx) : make_float4(0.f, 0.f, 0.f, 0.f);
+          xv = make_float4((x[0] - mu.x) * sc.x + be.x, (x[1] - mu.y) * sc.y + be.y,
+                           (x[2] - mu.z) * sc.z + be.z, (x[3] - mu.w) * sc.w + be.w);
         }
+        st4(&dzs[rr * PW + 4 * q], dz);
+        st4(&xs[rr * PW + 4 * q], xv);
       }
-      st4(&dzs[rr * PW + 4 * q], dz);
-      st4(&xs[rr * PW + 4 * q], xv);
     }
     __syncthreads();
 #pragma unroll 4
@@ -476,7 +595,10 @@ int wgrad_nchunk(int layer, int M, int cout, int cin) {
   const int blocks = ((gm.ks * cin + 127) / 128) * ((cout + 127) / 128);
   long n = (512 + blocks - 1) / blocks;
   const long maxn = (rows + kWgradRch - 1) / kWgradRch;
+  // partial blocks cost a write + a read of cout*ks*cin floats each: keep them <= 16 MB
+  const long cap = (4L << 20) / ((long)cout * gm.ks * cin);
   if (n > maxn) n = maxn;
+  if (n > cap) n = cap;
   if (n < 1) n = 1;
   return (int)n;
 }
@@ -517,32 +639,70 @@ int launch_conv_wgrad(int layer, int src, const WgradArgs& a, int nchunk, hipStr
   }
 }
 
-// Sum partial blocks over chunks (fixed order) and write reference layout dW[o][c][k], db[o].
-// Layer 1 writes G[o][k*cin+c] (the xhat0 contraction) and S[k][o] instead (see k_bn0_grads).
-__global__ void k_wgrad_reduce(const float* __restrict__ wpart, const float* __restrict__ bpart,
-                               int nchunk, int cout, int cin, int ks, int nb, float* dW, float* db,
-                               float* G, float* S) {
+// Sum partial blocks over chunks and write reference layout dW[o][c][k], db[o]. A workgroup owns
+// 256 output elements (64 float4 columns) x 4 chunk groups; each thread streams its group's chunks
+// with 16-B loads, the four group sums are added in a fixed order (deterministic). Layer 1 writes
+// G[o][k*cin+c] (the xhat0 contraction) and S[k][o] instead (see k_bn0_grads).
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ wpart,
+                                                      const float* __restrict__ bpart, int nchunk,
+                                                      int cout, int cin, int ks, int nb, float* dW,
+                                                      float* db, float* G, float* S) {
+  __shared__ float4 red[4][64];
   const long kcn = (long)ks * cin;
-  const long nw = (long)cout * kcn;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx < nw) {
-    float v = 0.f;
-    for (int z = 0; z < nchunk; ++z) v += wpart[(size_t)z * nw + idx];
-    const long o = idx / kcn, kc = idx - o * kcn;
-    const long k = kc / cin, c = kc - k * cin;
-    if (G) G[idx] = v;
-    else dW[(o * cin + c) * ks + k] = v;
-  } else if (idx < nw + cout) {
-    const int o = (int)(idx - nw);
+  const long nw = (long)cout * kcn;  // multiple of 4 (cin % 32 == 0)
+  const long nwblk = (nw + 255) / 256;
+  if ((long)blockIdx.x < nwblk) {
+    const int col = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const long e4 = (long)blockIdx.x * 256 + 4 * col;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e4 < nw) {
+#pragma unroll 4
+      for (int z = grp; z < nchunk; z += 4) {
+        const float4 v = ld4(wpart + (size_t)z * nw + e4);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    }
+    red[grp][col] = acc;
+    __syncthreads();
+    if (grp == 0 && e4 < nw) {
+      const float4 a = red[0][col], b = red[1][col], c = red[2][col], d = red[3][col];
+      const float v[4] = {(a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y),
+                          (a.z + b.z) + (c.z + d.z), (a.w + b.w) + (c.w + d.w)};
+      if (G) {
+        st4(G + e4, make_float4(v[0], v[1], v[2], v[3]));
+      } else {
+        const long o = e4 / kcn, kc = e4 - o * kcn;
+        const long k = kc / cin, c0 = kc - k * cin;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dW[(o * cin + c0 + j) * ks + k] = v[j];
+      }
+    }
+    return;
+  }
+  // bias (+ layer-1 edge) sums: 64 outputs x 4 chunk groups per workgroup, fixed combine order
+  {
+    __shared__ float rb[4][5][64];
+    const int col = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const int o = (int)((blockIdx.x - nwblk) * 64 + col);
     float e[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int z = 0; z < nchunk; ++z)
-      for (int j = 0; j < nb; ++j) e[j] += bpart[((size_t)z * nb + j) * cout + o];
-    db[o] = e[0];
-    if (S) {  // layer 1: tap k of row t reads input t+k-2; zero padding at t+k-2 < 0 or > 130
-      S[0 * cout + o] = e[0] - e[1] - e[2];
-      S[1 * cout + o] = e[0] - e[1];
-      S[2 * cout + o] = e[0] - e[4];
-      S[3 * cout + o] = e[0] - e[3] - e[4];
+    if (o < cout)
+      for (int z = grp; z < nchunk; z += 4)
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+          if (j < nb) e[j] += bpart[((size_t)z * nb + j) * cout + o];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) rb[grp][j][col] = e[j];
+    __syncthreads();
+    if (grp == 0 && o < cout) {
+#pragma unroll
+      for (int j = 0; j < 5; ++j) e[j] = (rb[0][j][col] + rb[1][j][col]) + (rb[2][j][col] + rb[3][j][col]);
+      db[o] = e[0];
+      if (S) {  // layer 1: tap k of row t reads input t+k-2; zero padding at t+k-2 < 0 or > 130
+        S[0 * cout + o] = e[0] - e[1] - e[2];
+        S[1 * cout + o] = e[0] - e[1];
+        S[2 * cout + o] = e[0] - e[4];
+        S[3 * cout + o] = e[0] - e[3] - e[4];
+      }
     }
   }
 }
@@ -550,8 +710,8 @@ __global__ void k_wgrad_reduce(const float* __restrict__ wpart, const float* __r
 int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int nchunk, int cout,
                         int cin, float* dW, float* db, float* G_tmp, float* S_tmp, hipStream_t s) {
   const LayerGeom gm = layer_geom(layer);
-  const long n = (long)cout * gm.ks * cin + cout;
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, wpart,
+  const long nblk = ((long)cout * gm.ks * cin + 255) / 256 + (cout + 63) / 64;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)nblk), dim3(256), 0, s, wpart,
                      bpart, nchunk, cout, cin, gm.ks, layer == 1 ? 5 : 1, dW, db,
                      layer == 1 ? G_tmp : nullptr, layer == 1 ? S_tmp : nullptr);
   DCUE_LAUNCH_CHECK();
@@ -561,30 +721,43 @@ int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int n
 // bn0 gradients without conv1's input gradient: with xhat0 the normalised input and
 // G[o][k*128+c] = sum dz1 * xhat0_pad, S[k][o] = sum of dz1 over rows whose tap-k input is real,
 //   dW1[o][c][k] = gamma0[c] G + beta0[c] S,   dgamma0[c] = sum_{o,k} W1 G,   dbeta0[c] = sum_{o,k} W1 S.
-__global__ void k_bn0_grads(const float* __restrict__ G, const float* __restrict__ S,
-                            const float* __restrict__ W1, const float* gamma0, const float* beta0,
-                            int H, float* dW1, float* dgamma0, float* dbeta0) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= kMels) return;
+__global__ __launch_bounds__(256) void k_bn0_grads(const float* __restrict__ G, const float* __restrict__ S,
+                                                   const float* __restrict__ W1, const float* gamma0,
+                                                   const float* beta0, int H, float* dW1,
+                                                   float* dgamma0, float* dbeta0) {
+  __shared__ float rg[256], rb[256];
+  const int c = blockIdx.x, t = threadIdx.x;
   const float ga = gamma0[c], be = beta0[c];
   float dg = 0.f, db = 0.f;
-  for (int o = 0; o < H; ++o)
-    for (int k = 0; k < 4; ++k) {
-      const float gv = G[(size_t)o * 4 * kMels + k * kMels + c];
-      const float sv = S[k * H + o];
-      const float w = W1[((size_t)o * kMels + c) * 4 + k];
-      dg += w * gv;
-      db += w * sv;
-      dW1[((size_t)o * kMels + c) * 4 + k] = ga * gv + be * sv;
+  for (int e = t; e < 4 * H; e += blockDim.x) {  // e = o*4 + k: dW1[o][c][k] layout
+    const int o = e >> 2, k = e & 3;
+    const float gv = G[(size_t)o * 4 * kMels + k * kMels + c];
+    const float sv = S[k * H + o];
+    const float w = W1[((size_t)o * kMels + c) * 4 + k];
+    dg += w * gv;
+    db += w * sv;
+    dW1[((size_t)o * kMels + c) * 4 + k] = ga * gv + be * sv;
+  }
+  rg[t] = dg;
+  rb[t] = db;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) {
+      rg[t] += rg[t + off];
+      rb[t] += rb[t + off];
     }
-  dgamma0[c] = dg;
-  dbeta0[c] = db;
+    __syncthreads();
+  }
+  if (t == 0) {
+    dgamma0[c] = rg[0];
+    dbeta0[c] = rb[0];
+  }
 }
 
 int launch_bn0_grads(const float* G, const float* S, const float* W1, const float* gamma0,
                      const float* beta0, int H, float* dW1, float* dgamma0, float* dbeta0,
                      hipStream_t s) {
-  hipLaunchKernelGGL(k_bn0_grads, dim3(2), dim3(64), 0, s, G, S, W1, gamma0, beta0, H, dW1, dgamma0,
+  hipLaunchKernelGGL(k_bn0_grads, dim3(kMels), dim3(256), 0, s, G, S, W1, gamma0, beta0, H, dW1, dgamma0,
                      dbeta0);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;

@@ -58,7 +58,8 @@ struct Arena {
   T* take(size_t n) {
     size_t off = (used + 255) & ~size_t(255);
     used = off + n * sizeof(T);
-    return base ? reinterpret_cast<T*>(base + off) : nullptr;
+    // base == nullptr: the returned "pointer" is the byte offset (sizing / layout queries)
+    return reinterpret_cast<T*>(reinterpret_cast<uintptr_t>(base) + off);
   }
 };
 

@@ -61,7 +61,7 @@ struct WgradArgs {
 
 int launch_conv_fwd(int layer, int kc, int src, const RowsArgs& a, hipStream_t s);
 int launch_conv_dgrad(int layer, int kc, const RowsArgs& a, hipStream_t s);
-int conv_fwd_grid(int layer, int M);  // grid.x of the forward launch (partials rows)
+int conv_fwd_grid(int layer, int kc, int M);  // grid.x of the forward launch (partials rows)
 int launch_conv_wgrad(int layer, int src, const WgradArgs& a, int nchunk, hipStream_t s);
 int wgrad_nchunk(int layer, int M, int cout, int cin);
 int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int nchunk, int cout,
@@ -70,19 +70,7 @@ int launch_bn0_grads(const float* G, const float* S, const float* W1, const floa
                      const float* beta0, int H, float* dW1, float* dgamma0, float* dbeta0,
                      hipStream_t s);
 
-// ------------------------------------------------------------------------------- dense ops
-struct GemmArgs {
-  int M, N, K;
-  const float* A; long sam, sak; const int64_t* arow;  // A(m,k) = A[row(m)*sam + k*sak]
-  const float* B; long sbk, sbn;                       // B(k,n) = B[k*sbk + n*sbn]
-  const float* tmean; const float* ta; const float* tbeta;  // A transform 2: (x-mean[k])*a[k]+beta[k]
-  const float* bias;                                   // [N] nullable
-  float* C; long scm, scn;                             // C(m,n)
-  const float* cmask;                                  // nullable: C(m,n) *= (cmask(m,n) > 0)
-};
-// A transform: 0 none, 1 relu, 2 BN affine per k (column), 3 BN affine per m (row)
-int launch_gemm(int ta, const GemmArgs& g, hipStream_t s);
-
+// ------------------------------------------------------------------------------- BatchNorm
 int launch_input_stats(int src, const void* tracks, const int32_t* item_track, const float* counts,
                        int M, float* partials, int* nparts, hipStream_t s);
 int launch_bn_finalize(const float* partials, int nparts, int C, double count, const float* gamma,
@@ -92,11 +80,50 @@ int launch_bwd_partials(const float* g, const float* y, const float* mean, const
                         long rows, int C, float* partials, int* nparts, hipStream_t s);
 int launch_bwd_finalize(const float* partials, int nparts, int C, float* sD, float* sDx,
                         float* dgamma, float* dbeta, hipStream_t s);
-int launch_colsum(const float* A, int M, int N, float* out, hipStream_t s);
 
+// ------------------------------------------------------------------ packed weight layout
+// wpack = conv B operands (forward per layer, dgrad per layer >= 2). Dense weights are read in place.
+struct WpackLayout {
+  long conv_fwd[6], conv_bwd[6];
+  long total;
+};
+inline WpackLayout wpack_layout(const dcue_dims* dm) {
+  WpackLayout w = {};
+  const long H = dm->conv_hidden, D = dm->feature_dim;
+  long n = 0;
+  for (int l = 1; l <= 5; ++l) {
+    const long cin = l == 1 ? kMels : H, cout = l == 5 ? D : H;
+    const long e = cin * cout * layer_geom(l).ks;
+    w.conv_fwd[l] = n;
+    n += e;
+    w.conv_bwd[l] = l >= 2 ? n : -1;
+    if (l >= 2) n += e;
+  }
+  w.total = n;
+  return w;
+}
+
+// --------------------------------------------------------------------- batch, tail, towers
+// copies per item (BatchNorm weights); in-batch negatives are found by wave ballots over neg_item
 int launch_item_counts(const dcue_batch* b, float* counts, hipStream_t s);
+
+// small GEMM: C(m,n) = sum_k TA(A(m,k)) TB(B(k,n)) (+bias[n]) (*[cmask > 0]); TA: 0 none, 1 relu,
+// 2 affine per k; TB: 0 none, 1 relu, 2 affine per n (affine = BatchNorm apply (x-mean)*a+beta)
+struct TGemmArgs {
+  int M, N, K;
+  const float* A; long sam, sak; const int64_t* arow;
+  const float* B; long sbk, sbn; const int64_t* brow;
+  const float *amean, *aa, *abeta;
+  const float *bmean, *ba, *bbeta;
+  const float* bias;
+  float* C; long scm, scn;
+  const float* cmask; long smm, smn; const int64_t* cmrow;
+  float* rowsum;  // nullable: sum_k TA(A(m,k)) per row m
+};
+int launch_tgemm(int ta, int tb, const TGemmArgs& g, hipStream_t s);
+
 int launch_score_fwd(const float* uf, const float* f, const dcue_batch* b, int d, float margin,
-                     float* scores, float* cosv, float* norms, float* row_loss, float* loss,
+                     float* scores, float* cosv, float* norms, float* hinge, float* loss,
                      float* dhinge, hipStream_t s);
 int launch_score_bwd(const float* uf, const float* f, const dcue_batch* b, int d,
                      const float* dscores, const float* cosv, const float* norms, float* du,
@@ -106,7 +133,5 @@ int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float s
                     float* emb_grad, int32_t* slot, hipStream_t s);
 int launch_adam(const dcue_model* m, const dcue_adam_args* a, const int64_t* poff, hipStream_t s);
 int launch_pack(const dcue_model* m, const int64_t* poff, hipStream_t s);
-int launch_gather_rows(const float* table, const int64_t* rows, int n, int E, float* out,
-                       hipStream_t s);
 
 }  // namespace dcue

@@ -1,0 +1,451 @@
+// Everything after the conv stack: small GEMMs (fc projection, user tower) on MFMA, cosine scoring
+// + hinge loss, copy bookkeeping of in-batch negatives, embedding-row gradients -- gfx950.
+//
+// Reference ops replaced:
+//   fc Linear(d,d) on BN5 output                           truedcuemel1dbn.py:65,101
+//   UserEmbeddings: gather, relu, linear, relu, linear      userembedding.py:33-44
+//   nn.CosineSimilarity(dim=1) scoring, pos - neg           dcue/dcue.py:68,94-106
+//   hinge loss mean_b sum_n max(0, margin - s)              nn/dcue.py:167-170
+//   in-batch copies pos[rand] -> neg[i][j]                  nn/dcue.py:698-709
+// These are tiny (B=64 rows, d<=256, E<=1024): the kernels are shaped for latency -- one wave per
+// 16x16 output tile, per batch row or per item -- with fixed summation orders throughout (bitwise
+// reproducible run to run).
+#include "dcue_internal.h"
+
+namespace dcue {
+
+// ------------------------------------------------------------------------ batch bookkeeping
+// copies of each item (BatchNorm weights): catalogue = 1 each; gather = its positive (items < B)
+// plus the negatives that reference it. One wave per item, 64 references per ballot.
+__global__ __launch_bounds__(256) void k_item_counts(dcue_batch b, float* counts) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= b.n_items) return;
+  if (b.layout == DCUE_LAYOUT_CATALOGUE) {
+    if (lane == 0) counts[i] = 1.f;
+    return;
+  }
+  const int nneg = b.n_rows * b.n_neg;
+  int cnt = i < b.n_rows ? 1 : 0;
+  for (int e0 = 0; e0 < nneg; e0 += 64) {
+    const int e = e0 + lane;
+    cnt += __popcll(__ballot(e < nneg && b.neg_item[e] == i));
+  }
+  if (lane == 0) counts[i] = (float)cnt;
+}
+
+int launch_item_counts(const dcue_batch* b, float* counts, hipStream_t s) {
+  hipLaunchKernelGGL(k_item_counts, dim3((b->n_items + 3) / 4), dim3(256), 0, s, *b, counts);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+// ------------------------------------------------------------ small GEMMs on f32-input MFMA
+// C(m,n) = sum_k TA(A(m,k)) TB(B(k,n)) (+ bias[n]) (* [cmask(m,n) > 0]) on v_mfma_f32_16x16x4_f32.
+// A workgroup owns a 16 (m) x 64 (n) output block; K is staged through LDS 128 at a time with every
+// load of a stage issued at once (these operands are <= 1.2 MB and L2/MALL resident: the cost is
+// load latency, so the chain of dependent load rounds is kept to ceil(K/128)). Each wave computes
+// one 16x16 tile from the k-major LDS images (conflict-free ds_read_b32). Optional row gathers
+// (arow: A rows, brow: B rows along K, cmrow: mask rows) and per-row sums of TA(A) (bias grads).
+constexpr int kTgKC = 128;
+// AKF: A is k-contiguous (sak == 1); BNF: B is n-contiguous (sbn == 1) -- picks the staging thread
+// map that keeps global reads coalesced. All staging addresses are clamped in-range and loaded
+// unconditionally (no per-element branch), row gathers resolved before the data loads.
+template <int TA, int TB, int AKF, int BNF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_tgemm(TGemmArgs g) {
+  __shared__ float As[kTgKC][16];
+  __shared__ float Bs[kTgKC][80];
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int m0 = blockIdx.x * 16, nb0 = blockIdx.y * 64, n0 = nb0 + 16 * wave;
+  const int l16 = lane & 15, kq = lane >> 4;
+  const int n = n0 + l16;
+  const bool nok = n < g.N;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float rsum = 0.f;
+  constexpr int NA = 16 * kTgKC / 256, NB = 64 * kTgKC / 256;  // staged elements per thread
+  constexpr int NAR = AKF ? NA : 1;
+  // A rows (fixed over K): AKF -> rows (t>>7)+2j, k = t&127; else row t&15, k = (t>>4)+16j
+  // Rows m >= M / columns n >= N are clamped onto real data and never stored; only the K tail of
+  // the A image is zeroed (a zero A column annihilates whatever finite B value sits beside it).
+  long abase[NAR];
+#pragma unroll
+  for (int j = 0; j < NAR; ++j) {
+    const int mc = min(m0 + (AKF ? (t >> 7) + 2 * j : (t & 15)), g.M - 1);
+    abase[j] = (g.arow ? g.arow[mc] : mc) * g.sam;
+  }
+  // B columns: BNF -> column t&63 (fixed), k = (t>>6)+4j; else columns (t>>7)+2j, k = t&127 (fixed)
+  const long bcol0 = (long)min(nb0 + (BNF ? (t & 63) : (t >> 7)), g.N - 1) * g.sbn;
+  for (int k0 = 0; k0 < g.K; k0 += kTgKC) {
+    float ra[NA], rb[NB];
+    long brk[BNF ? NB : 1];
+#pragma unroll
+    for (int j = 0; j < (BNF ? NB : 1); ++j) {
+      const int k = min(k0 + (BNF ? (t >> 6) + 4 * j : (t & 127)), g.K - 1);
+      brk[j] = (long)(g.brow ? g.brow[k] : k) * g.sbk;
+    }
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {  // every load of the stage issued before any is used
+      const int k = min(k0 + (AKF ? (t & 127) : (t >> 4) + 16 * j), g.K - 1);
+      ra[j] = g.A[abase[AKF ? j : 0] + (long)k * g.sak];
+    }
+    if constexpr (BNF) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) rb[j] = g.B[brk[j] + bcol0];
+    } else {
+      const float* bp = g.B + brk[0];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int nc = min(nb0 + (t >> 7) + 2 * j, g.N - 1);
+        rb[j] = bp[(long)nc * g.sbn];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const int kk = AKF ? (t & 127) : (t >> 4) + 16 * j, mm = AKF ? (t >> 7) + 2 * j : (t & 15);
+      const int k = k0 + kk;
+      float a = ra[j];
+      if constexpr (TA == 1) a = a > 0.f ? a : 0.f;
+      if constexpr (TA == 2) a = (a - g.amean[min(k, g.K - 1)]) * g.aa[min(k, g.K - 1)] + g.abeta[min(k, g.K - 1)];
+      As[kk][mm] = k < g.K ? a : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int kk = BNF ? (t >> 6) + 4 * j : (t & 127), nn = BNF ? (t & 63) : (t >> 7) + 2 * j;
+      const int nc = min(nb0 + nn, g.N - 1);
+      float b = rb[j];
+      if constexpr (TB == 1) b = b > 0.f ? b : 0.f;
+      if constexpr (TB == 2) b = (b - g.bmean[nc]) * g.ba[nc] + g.bbeta[nc];
+      Bs[kk][nn] = b;
+    }
+    __syncthreads();
+    const int kn = min(kTgKC, g.K - k0);
+    for (int kk = 0; kk < kn; kk += 4) {
+      const float a = As[kk + kq][l16];
+      acc = mfma4(a, Bs[kk + kq][16 * wave + l16], acc);
+      rsum += a;
+    }
+    __syncthreads();
+  }
+  const int m = m0 + l16;
+  const bool mok = m < g.M;
+  if (g.rowsum && n0 == 0) {  // sum_k TA(A(m,k)) for the tile's rows: lanes with equal l16
+    rsum += __shfl_xor(rsum, 16, 64);
+    rsum += __shfl_xor(rsum, 32, 64);
+    if (kq == 0 && mok) g.rowsum[m] = rsum;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int mm = m0 + 4 * kq + j;
+    if (mm < g.M && nok) {
+      float v = acc[j] + (g.bias ? g.bias[n] : 0.f);
+      if (g.cmask && !(g.cmask[(g.cmrow ? g.cmrow[mm] : mm) * g.smm + (long)n * g.smn] > 0.f)) v = 0.f;
+      g.C[(long)mm * g.scm + (long)n * g.scn] = v;
+    }
+  }
+}
+
+int launch_tgemm(int ta, int tb, const TGemmArgs& g, hipStream_t s) {
+  if (g.M <= 0 || g.N <= 0) return DCUE_OK;
+  const dim3 grid((unsigned)((g.M + 15) / 16), (unsigned)((g.N + 63) / 64));
+  const int akf = g.sak == 1, bnf = g.sbn == 1;
+  const int key = ((ta * 3 + tb) * 2 + akf) * 2 + bnf;
+#define DCUE_TG(TA_, TB_, AK_, BN_)                                                            \
+  case ((TA_ * 3 + TB_) * 2 + AK_) * 2 + BN_:                                                  \
+    hipLaunchKernelGGL((k_tgemm<TA_, TB_, AK_, BN_>), grid, dim3(256), 0, s, g);               \
+    break;
+  switch (key) {
+    DCUE_TG(0, 0, 0, 0) DCUE_TG(0, 0, 0, 1) DCUE_TG(0, 0, 1, 0) DCUE_TG(0, 0, 1, 1)
+    DCUE_TG(0, 1, 0, 0) DCUE_TG(0, 1, 0, 1) DCUE_TG(0, 1, 1, 0) DCUE_TG(0, 1, 1, 1)
+    DCUE_TG(0, 2, 0, 0) DCUE_TG(0, 2, 0, 1) DCUE_TG(0, 2, 1, 0) DCUE_TG(0, 2, 1, 1)
+    DCUE_TG(1, 0, 0, 0) DCUE_TG(1, 0, 0, 1) DCUE_TG(1, 0, 1, 0) DCUE_TG(1, 0, 1, 1)
+    DCUE_TG(2, 0, 0, 0) DCUE_TG(2, 0, 0, 1) DCUE_TG(2, 0, 1, 0) DCUE_TG(2, 0, 1, 1)
+    default: return DCUE_ERR_INVALID;
+  }
+#undef DCUE_TG
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+// ------------------------------------------------------------------- scores and hinge loss
+__device__ __forceinline__ int copy_item(const dcue_batch& b, int row, int c) {
+  if (c == 0) return row;
+  if (b.layout == DCUE_LAYOUT_CATALOGUE) return b.n_rows + row * b.n_neg + (c - 1);
+  return b.neg_item[(long)row * b.n_neg + (c - 1)];
+}
+
+// One workgroup (4 waves) per row; wave w scores copies w, w+4, ...:
+// torch cosine_similarity = sum((x/max(|x|,eps)) * (y/max(|y|,eps))) -- normalise, then dot.
+// cosv[b][c] (c=0 positive), norms[b][0]=|u|, norms[b][1+c]=|f_c|; scores = pos - neg;
+// hinge[b][j] = max(0, margin - s); dhinge = d(mean_b sum_j hinge)/ds (torch.max splits ties 1/2).
+__global__ __launch_bounds__(256) void k_score_fwd(const float* __restrict__ uf,
+                                                   const float* __restrict__ f, dcue_batch b, int d,
+                                                   float margin, float* scores, float* cosv,
+                                                   float* norms, float* hinge, float* dhinge) {
+  __shared__ float cs[1025];
+  const int row = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int N = b.n_neg, per = (d + 63) / 64;
+  const float eps = 1e-8f;
+  float u[4];
+  float su = 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = lane + 64 * e;
+    u[e] = (e < per && k < d) ? uf[(long)row * d + k] : 0.f;
+    su += u[e] * u[e];
+  }
+  const float nu = sqrtf(wave_sum(su));
+  const float du = fmaxf(nu, eps);
+  if (wave == 0 && lane == 0) norms[(long)row * (N + 2)] = nu;
+  for (int c = wave; c <= N; c += 4) {
+    const long item = copy_item(b, row, c);
+    float v[4], sf = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = lane + 64 * e;
+      v[e] = (e < per && k < d) ? f[item * d + k] : 0.f;
+      sf += v[e] * v[e];
+    }
+    const float nf = sqrtf(wave_sum(sf));
+    const float dfn = fmaxf(nf, eps);
+    float dot = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dot += (u[e] / du) * (v[e] / dfn);
+    const float cv = wave_sum(dot);
+    if (lane == 0) {
+      norms[(long)row * (N + 2) + 1 + c] = nf;
+      cosv[(long)row * (N + 1) + c] = cv;
+      cs[c] = cv;
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < N; j += blockDim.x) {
+    const float sc = cs[0] - cs[1 + j];
+    const float h = margin - sc;
+    scores[(long)row * N + j] = sc;
+    hinge[(long)row * N + j] = h > 0.f ? h : 0.f;
+    dhinge[(long)row * N + j] = h > 0.f ? -1.f / (float)b.n_rows : (h == 0.f ? -0.5f / (float)b.n_rows : 0.f);
+  }
+}
+
+// loss = mean over rows of the row's summed hinge (row sums in j order, rows in order)
+__global__ __launch_bounds__(256) void k_loss_mean(const float* hinge, int B, int N, float* loss) {
+  __shared__ float rs[1024];
+  for (int r = threadIdx.x; r < B; r += blockDim.x) {
+    float s = 0.f;
+    for (int j = 0; j < N; ++j) s += hinge[(long)r * N + j];
+    rs[r] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int r = 0; r < B; ++r) s += rs[r];
+    *loss = s / (float)B;
+  }
+}
+
+int launch_score_fwd(const float* uf, const float* f, const dcue_batch* b, int d, float margin,
+                     float* scores, float* cosv, float* norms, float* hinge, float* loss,
+                     float* dhinge, hipStream_t s) {
+  if (d > 256 || b->n_neg > 1024 || b->n_rows > 1024) return DCUE_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(k_score_fwd, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, margin, scores, cosv,
+                     norms, hinge, dhinge);
+  DCUE_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_loss_mean, dim3(1), dim3(256), 0, s, hinge, b->n_rows, b->n_neg, loss);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+// dL/dscores -> dL/du (waves' partial sums combined in wave order) and dL/df per copy.
+// d cos/dx = (yhat - cos*xhat)/|x| (non-degenerate norms).
+__global__ __launch_bounds__(256) void k_score_bwd(const float* __restrict__ uf,
+                                                   const float* __restrict__ f, dcue_batch b, int d,
+                                                   const float* dscores, const float* cosv,
+                                                   const float* norms, float* dU, float* dfcopy) {
+  __shared__ float gus[4][256];
+  const int row = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int N = b.n_neg, per = (d + 63) / 64;
+  const float eps = 1e-8f;
+  const float nu = fmaxf(norms[(long)row * (N + 2)], eps);
+  float u[4], gu[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = lane + 64 * e;
+    u[e] = (e < per && k < d) ? uf[(long)row * d + k] / nu : 0.f;
+    gu[e] = 0.f;
+  }
+  float dpos = 0.f;  // scores = pos_cos - neg_cos: the positive collects every score's gradient
+  for (int j = 0; j < N; ++j) dpos += dscores[(long)row * N + j];
+  for (int c = wave; c <= N; c += 4) {
+    const long item = copy_item(b, row, c);
+    const float dc = c == 0 ? dpos : -dscores[(long)row * N + c - 1];
+    const float cv = cosv[(long)row * (N + 1) + c];
+    const float nf = fmaxf(norms[(long)row * (N + 2) + 1 + c], eps);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = lane + 64 * e;
+      if (e < per && k < d) {
+        const float fh = f[item * d + k] / nf;
+        gu[e] += dc * (fh - cv * u[e]) / nu;
+        dfcopy[((long)row * (N + 1) + c) * d + k] = dc * (u[e] - cv * fh) / nf;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = lane + 64 * e;
+    if (e < per && k < d) gus[wave][k] = gu[e];
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < d; k += blockDim.x)
+    dU[(long)row * d + k] = ((gus[0][k] + gus[1][k]) + gus[2][k]) + gus[3][k];
+}
+
+int launch_score_bwd(const float* uf, const float* f, const dcue_batch* b, int d,
+                     const float* dscores, const float* cosv, const float* norms, float* du,
+                     float* dfcopy, hipStream_t s) {
+  hipLaunchKernelGGL(k_score_bwd, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, dscores, cosv, norms,
+                     du, dfcopy);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+// df[i] = sum over item i's copies, in (positive, (b,j) row-major) order; one wave per item.
+__global__ __launch_bounds__(256) void k_item_grad(const float* __restrict__ dfcopy, dcue_batch b, int d,
+                                                   float* df) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= b.n_items) return;
+  const int N = b.n_neg, B = b.n_rows, per = (d + 63) / 64;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  auto add_copy = [&](long c) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = lane + 64 * e;
+      if (e < per && k < d) acc[e] += dfcopy[c * d + k];
+    }
+  };
+  if (b.layout == DCUE_LAYOUT_CATALOGUE) {
+    add_copy(i < B ? (long)i * (N + 1) : (long)((i - B) / N) * (N + 1) + 1 + (i - B) % N);
+  } else {
+    // pass 1: ballots over neg_item append the item's copies, in order, to a per-wave LDS list;
+    // pass 2 drains the list 8 rows at a time (8 loads in flight, then the adds in list order)
+    constexpr int kCap = 256;
+    __shared__ int list[4][kCap];
+    int* my = list[threadIdx.x >> 6];
+    int len = 0;
+    if (i < B) my[len++] = i * (N + 1);
+    auto drain = [&]() {
+      for (int q0 = 0; q0 < len; q0 += 8) {
+        float v[8][4];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int k = lane + 64 * e;
+            v[q][e] = (q0 + q < len && e < per && k < d) ? dfcopy[(long)my[q0 + q] * d + k] : 0.f;
+          }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (q0 + q < len)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[e] += v[q][e];
+      }
+      len = 0;
+    };
+    const int nneg = B * N;
+    for (int e0 = 0; e0 < nneg; e0 += 64) {
+      const int e = e0 + lane;
+      const bool hit = e < nneg && b.neg_item[e] == i;
+      const unsigned long long bal = __ballot(hit);
+      const int cnt = __popcll(bal);
+      if (len + cnt > kCap) drain();
+      if (hit) {
+        const int row = e / N;
+        my[len + __popcll(bal & ((1ull << lane) - 1ull))] = row * (N + 1) + 1 + (e - row * N);
+      }
+      len += cnt;
+    }
+    drain();
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = lane + 64 * e;
+    if (e < per && k < d) df[(long)i * d + k] = acc[e];
+  }
+}
+
+int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df, hipStream_t s) {
+  if (d > 256) return DCUE_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(k_item_grad, dim3((b->n_items + 3) / 4), dim3(256), 0, s, dfcopy, *b, d, df);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+// Compact embedding gradient: one slot per distinct user (its first row), rows summed in order.
+__global__ void k_emb_grad(const float* __restrict__ de, const int64_t* users, int B, int E,
+                           float scale, float* emb_grad, int32_t* slot) {
+  const int b = blockIdx.x;
+  const int64_t u = users[b];
+  for (int r = 0; r < b; ++r)
+    if (users[r] == u) return;
+  for (int k = threadIdx.x; k < E; k += blockDim.x) {
+    float v = 0.f;
+    for (int r = b; r < B; ++r)
+      if (users[r] == u) v += de[(long)r * E + k];
+    emb_grad[(long)b * E + k] = v * scale;
+  }
+  if (threadIdx.x == 0) slot[u] = b;
+}
+
+int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float scale,
+                    float* emb_grad, int32_t* slot, hipStream_t s) {
+  hipLaunchKernelGGL(k_emb_grad, dim3(B), dim3(256), 0, s, de, users, B, E, scale, emb_grad, slot);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+// ------------------------------------------------------------------------- layout helpers
+// [M][128][T=131] (the reference's per-track tensor layout, NCL) -> [M][131][128] track rows.
+// 32x32 tiles through LDS so both the read and the write are coalesced.
+__global__ __launch_bounds__(256) void k_transpose_ncl(const float* __restrict__ in, int M, float* out) {
+  __shared__ float tile[32][33];
+  const int m = blockIdx.z;
+  const int c0 = blockIdx.y * 32, t0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int r = ty; r < 32; r += 8) {
+    const int c = c0 + r, t = t0 + tx;
+    tile[r][tx] = (c < kMels && t < kFrames) ? in[((long)m * kMels + c) * kFrames + t] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int t = t0 + r, c = c0 + tx;
+    if (c < kMels && t < kFrames) out[((long)m * kFrames + t) * kMels + c] = tile[tx][r];
+  }
+}
+
+__global__ void k_build_catalogue(const int64_t* pos, const int64_t* neg, int B, int N, int32_t* item_track) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long tot = (long)B * (1 + N);
+  if (e >= tot) return;
+  item_track[e] = (int32_t)(e < B ? pos[e] : neg[e - B]);
+}
+
+}  // namespace dcue
+
+extern "C" int dcue_transpose_spectrograms(const float* ncl, int32_t M, float* out, void* stream) {
+  if (!ncl || !out || M <= 0) return DCUE_ERR_INVALID;
+  dim3 grid((dcue::kFrames + 31) / 32, dcue::kMels / 32, (unsigned)M);
+  hipLaunchKernelGGL(dcue::k_transpose_ncl, grid, dim3(256), 0, (hipStream_t)stream, ncl, M, out);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+extern "C" int dcue_build_catalogue_batch(const int64_t* pos_items, const int64_t* neg_items, int32_t B,
+                                          int32_t N, int32_t* item_track, void* stream) {
+  if (!pos_items || (N > 0 && !neg_items) || !item_track || B <= 0 || N < 0) return DCUE_ERR_INVALID;
+  const long tot = (long)B * (1 + N);
+  hipLaunchKernelGGL(dcue::k_build_catalogue, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, pos_items, neg_items, B, N, item_track);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}

@@ -73,6 +73,8 @@ _SIGS = {
     "dcue_wpack_floats": ([ctypes.POINTER(Dims), _P], ctypes.c_int),
     "dcue_workspace_bytes": ([ctypes.POINTER(Dims), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                               ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "dcue_workspace_outputs": ([ctypes.POINTER(Dims), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "dcue_pack_weights": ([ctypes.POINTER(Model), _P], ctypes.c_int),
     "dcue_forward": ([ctypes.POINTER(Model), ctypes.POINTER(Batch), ctypes.POINTER(Tracks), _P,
                       ctypes.c_size_t, ctypes.c_int32, ctypes.c_float, _P, _P, _P, _P, _P], ctypes.c_int),
@@ -151,6 +153,13 @@ def wpack_floats(dims):
     n = ctypes.c_int64()
     check(lib().dcue_wpack_floats(ctypes.byref(dims), ctypes.cast(ctypes.byref(n), _P)), "dcue_wpack_floats")
     return n.value
+
+
+def workspace_outputs(dims, B, N, M):
+    """Byte offsets of (scores, user feats, item feats, loss) inside a (B, N, M) workspace."""
+    off = (ctypes.c_size_t * 4)()
+    check(lib().dcue_workspace_outputs(ctypes.byref(dims), B, N, M, off), "dcue_workspace_outputs")
+    return list(off)
 
 
 def workspace_bytes(dims, max_rows, max_neg, max_items):

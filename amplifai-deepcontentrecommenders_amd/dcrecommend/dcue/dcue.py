@@ -224,27 +224,33 @@ class DCUENet(nn.Module):
         return out
 
     def native_forward(self, users, tracks, item_track, n_neg, layout, neg_item=None, train=True,
-                       margin=0.2):
-        """Forward over an HBM-resident track table. Returns (scores, user_feat, item_feat, loss)."""
+                       margin=0.2, copy_outputs=True):
+        """Forward over an HBM-resident track table. Returns (scores, user_feat, item_feat, loss).
+
+        copy_outputs=False returns views into the workspace (no copy; overwritten by the next call)."""
         fl = self._require_device()
         B = users.shape[0]
         M = item_track.shape[0]
         ws = self._workspace(B, n_neg, M)
-        dev = fl["P"].device
-        scores = torch.empty((B, n_neg), dtype=torch.float32, device=dev)
-        uf = torch.empty((B, self.feature_dim), dtype=torch.float32, device=dev)
-        f = torch.empty((M, self.feature_dim), dtype=torch.float32, device=dev)
-        loss = torch.empty((), dtype=torch.float32, device=dev)
         batch = nat.Batch(B, n_neg, M, layout, users.data_ptr(), item_track.data_ptr(),
                           neg_item.data_ptr() if neg_item is not None else None)
         tr = nat.Tracks(tracks.data_ptr(), tracks.shape[0], 0 if tracks.dtype == torch.float16 else 1, 0)
         model = self._model_struct()
         nat.check(nat.lib().dcue_forward(ctypes.byref(model), ctypes.byref(batch), ctypes.byref(tr),
                                          nat.ptr(ws), ws.numel(), int(bool(train)), float(margin),
-                                         nat.ptr(scores), nat.ptr(uf), nat.ptr(f), nat.ptr(loss),
-                                         nat.stream_handle()), "dcue_forward")
+                                         None, None, None, None, nat.stream_handle()), "dcue_forward")
         self._last = (users, tracks, item_track, n_neg, layout, neg_item)
-        return scores, uf, f, loss
+        key = (B, n_neg, M)
+        if fl.get("out_key") != key:
+            fl["out_off"], fl["out_key"] = nat.workspace_outputs(fl["dims"], B, n_neg, M), key
+        off = fl["out_off"]
+        d = self.feature_dim
+
+        def view(o, n, shape):
+            return ws[o:o + 4 * n].view(torch.float32).view(shape)
+        outs = (view(off[0], B * n_neg, (B, n_neg)), view(off[1], B * d, (B, d)),
+                view(off[2], M * d, (M, d)), view(off[3], 1, ()))
+        return tuple(o.clone() for o in outs) if copy_outputs else outs
 
     def native_backward(self, dscores=None, emb_grad_scale=1.0):
         """Backward of the last train-mode native_forward: writes the flat grads + compact

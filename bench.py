@@ -140,7 +140,7 @@ def main():
         nat.check(nat.lib().dcue_sample_inbatch(nat.ptr(mt), B, N, nat.ptr(neg_item), nat.stream_handle()),
                   "sample_inbatch")
         net.native_forward(users_b[s], tracks, items_b[s], N, nat.LAYOUT_GATHER, neg_item, train=True,
-                           margin=0.2)
+                           margin=0.2, copy_outputs=False)
         net.native_backward(None, emb_grad_scale=1.0 / world)
         if world > 1:
             dist.all_reduce(G)

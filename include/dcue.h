@@ -111,6 +111,11 @@ int dcue_bn_layout(const dcue_dims* dims, int64_t* offsets_host);
 int dcue_wpack_floats(const dcue_dims* dims, int64_t* n_floats_host);
 int dcue_workspace_bytes(const dcue_dims* dims, int32_t max_rows, int32_t max_neg,
                          int32_t max_items, size_t* bytes_host);
+/* Byte offsets inside a workspace carved for (B, N, M) of the forward outputs a train/eval
+ * dcue_forward leaves there: [0] scores [B][N], [1] user feats [B][d], [2] item feats [M][d],
+ * [3] loss (one float). Valid until the next call on the same workspace. */
+int dcue_workspace_outputs(const dcue_dims* dims, int32_t B, int32_t N, int32_t M,
+                           size_t* offsets_host);
 
 /* ------------------------------------------------------------------------- hot-path entries */
 /* Refresh wpack from params (after any host-side write of conv weights and after every Adam step). */
