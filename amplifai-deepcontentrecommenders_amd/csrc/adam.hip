@@ -8,15 +8,21 @@ namespace dcue {
 //   g += wd*p (wd != 0);  m.lerp_(g, 1-b1);  v = v*b2 + (1-b2)*g*g;
 //   p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
 struct AdamScalars {
-  float lr_bc1, one_m_b1, b2, one_m_b2, bc2_sqrt, eps, wd;
+  float lr_bc1, one_m_b1, b2, one_m_b2, bc2_sqrt, eps, wd, pad;
 };
+static_assert(sizeof(AdamScalars) == 32, "history entry is [8] floats");
 
+// Every operation rounded on its own (fp contraction off: no fma fusion) so that the dense sweep,
+// the deferred replay and the touched-row step produce identical bits whatever code the compiler
+// schedules around them; the order follows torch's CPU kernels: lerp (w < 0.5) m + w*(g-m);
+// mul_(b2).addcmul_(g, g, 1-b2); denom = sqrt(v)/bc2_sqrt + eps; addcdiv_(m, denom, -lr/bc1).
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamScalars& s) {
-  if (s.wd != 0.f) g = g + s.wd * p;
-  m = m + s.one_m_b1 * (g - m);
-  v = v * s.b2 + s.one_m_b2 * (g * g);
-  const float denom = sqrtf(v) / s.bc2_sqrt + s.eps;
-  p = p - s.lr_bc1 * (m / denom);
+#pragma clang fp contract(off)
+  if (s.wd != 0.f) g = __fadd_rn(g, __fmul_rn(s.wd, p));
+  m = __fadd_rn(m, __fmul_rn(s.one_m_b1, __fsub_rn(g, m)));
+  v = __fadd_rn(__fmul_rn(v, s.b2), __fmul_rn(__fmul_rn(s.one_m_b2, g), g));
+  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), s.bc2_sqrt), s.eps);
+  p = __fadd_rn(p, __fmul_rn(-s.lr_bc1, __fdiv_rn(m, denom)));
 }
 
 __global__ __launch_bounds__(256) void k_adam_dense(float* __restrict__ p, const float* __restrict__ g,
@@ -67,6 +73,166 @@ __global__ __launch_bounds__(256) void k_adam_embed(float* __restrict__ p, float
   }
 }
 
+// ------------------------------------------------------------- deferred user-table Adam
+// The dense sweep's zero-gradient steps, replayed late with the recorded scalars of each step.
+// adam_elem is the same function (and `gz` a runtime 0.0f), so every replayed element goes through
+// the identical fp32 operation sequence as in k_adam_embed: results are bit-identical.
+__device__ __forceinline__ AdamScalars* log_hist(dcue_emb_log* hdr) {
+  return reinterpret_cast<AdamScalars*>(hdr + 1);
+}
+
+// Bring users' rows current to step_done (before a forward reads them). One workgroup per listed
+// user; a row listed twice is claimed by one workgroup (CAS on its clock; INT_MIN = in progress).
+__global__ __launch_bounds__(256) void k_emb_sync(float* __restrict__ p, float* __restrict__ m,
+                                                  float* __restrict__ v, dcue_emb_log* hdr,
+                                                  int32_t* emb_step, const int64_t* users, int E,
+                                                  float gz) {
+  __shared__ AdamScalars hs[DCUE_MAX_LOG_CAP];
+  __shared__ int s_from;
+  const int T = hdr->step_done, F = hdr->flush_step, cap = hdr->cap;
+  const int64_t u = users[blockIdx.x];
+  if (threadIdx.x == 0) {
+    int from = T;  // nothing to do
+    const int old = emb_step[u];
+    if (old != INT_MIN && max(old, F) < T && atomicCAS(&emb_step[u], old, INT_MIN) == old) from = max(old, F);
+    s_from = from;
+  }
+  __syncthreads();
+  const int from = s_from;
+  if (from >= T) return;
+  const AdamScalars* hist = log_hist(hdr);
+  for (int j = from + 1 + (int)threadIdx.x; j <= T; j += blockDim.x) hs[j % cap] = hist[j % cap];
+  __syncthreads();
+  float* pr = p + u * E;
+  float* mr = m + u * E;
+  float* vr = v + u * E;
+  for (int k = threadIdx.x; k < E; k += blockDim.x) {
+    float pp = pr[k], mm = mr[k], vv = vr[k];
+    for (int j = from + 1; j <= T; ++j) adam_elem(pp, gz, mm, vv, hs[j % cap]);
+    pr[k] = pp; mr[k] = mm; vr[k] = vv;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    emb_step[u] = T;
+  }
+}
+
+// Every row current to step_done. Lanes walk the outstanding steps in lockstep (LDS broadcast of
+// each step's scalars) and skip the steps their row already has.
+__global__ __launch_bounds__(256) void k_emb_flush(float* __restrict__ p, float* __restrict__ m,
+                                                   float* __restrict__ v, const dcue_emb_log* hdr,
+                                                   const int32_t* __restrict__ emb_step, long n_rows,
+                                                   int E, float gz) {
+  __shared__ AdamScalars hs[DCUE_MAX_LOG_CAP];
+  const int T = hdr->step_done, F = hdr->flush_step, cap = hdr->cap;
+  if (T <= F) return;
+  const AdamScalars* hist = log_hist(const_cast<dcue_emb_log*>(hdr));
+  for (int j = F + 1 + (int)threadIdx.x; j <= T; j += blockDim.x) hs[j - F - 1] = hist[j % cap];
+  __syncthreads();
+  const long stride = (long)gridDim.x * blockDim.x;
+  if ((E & 3) == 0) {
+    const int E4 = E >> 2;
+    const long n4 = n_rows * E4;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+      const int from = max(emb_step[i / E4], F);
+      float4 pp = ld4(p + 4 * i), mm = ld4(m + 4 * i), vv = ld4(v + 4 * i);
+      for (int j = F + 1; j <= T; ++j) {
+        if (j <= from) continue;
+        const AdamScalars s = hs[j - F - 1];
+        adam_elem(pp.x, gz, mm.x, vv.x, s);
+        adam_elem(pp.y, gz, mm.y, vv.y, s);
+        adam_elem(pp.z, gz, mm.z, vv.z, s);
+        adam_elem(pp.w, gz, mm.w, vv.w, s);
+      }
+      st4(p + 4 * i, pp); st4(m + 4 * i, mm); st4(v + 4 * i, vv);
+    }
+  } else {
+    const long n = n_rows * E;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      const int from = max(emb_step[i / E], F);
+      float pp = p[i], mm = m[i], vv = v[i];
+      for (int j = F + 1; j <= T; ++j)
+        if (j > from) adam_elem(pp, gz, mm, vv, hs[j - F - 1]);
+      p[i] = pp; m[i] = mm; v[i] = vv;
+    }
+  }
+}
+
+__global__ void k_emb_flush_done(dcue_emb_log* hdr) { hdr->flush_step = hdr->step_done; }
+
+// Step t for the rows that have a gradient (emb_rows from the backward); records step t's scalars.
+__global__ __launch_bounds__(256) void k_adam_touched(float* __restrict__ p, float* __restrict__ m,
+                                                      float* __restrict__ v,
+                                                      const float* __restrict__ gcompact,
+                                                      const int64_t* emb_rows, int32_t* emb_step,
+                                                      dcue_emb_log* hdr, int E, int t, AdamScalars s,
+                                                      float gz) {
+  __shared__ int s_from;
+  const int cap = hdr->cap, F = hdr->flush_step;
+  const int n = hdr->grad_step == t ? hdr->n_touched : 0;
+  const AdamScalars* hist = log_hist(hdr);
+  for (int b = blockIdx.x; b < n; b += gridDim.x) {
+    const int64_t u = emb_rows[b];
+    if (u < 0) continue;
+    if (threadIdx.x == 0) s_from = max(emb_step[u], F);
+    __syncthreads();
+    const int from = s_from;
+    float* pr = p + u * E;
+    float* mr = m + u * E;
+    float* vr = v + u * E;
+    const float* gr = gcompact + (long)b * E;
+    for (int k = threadIdx.x; k < E; k += blockDim.x) {
+      float pp = pr[k], mm = mr[k], vv = vr[k];
+      for (int j = from + 1; j < t; ++j) adam_elem(pp, gz, mm, vv, hist[j % cap]);  // normally none
+      adam_elem(pp, gr[k], mm, vv, s);
+      pr[k] = pp; mr[k] = mm; vr[k] = vv;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) emb_step[u] = t;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    log_hist(hdr)[t % cap] = s;
+    hdr->step_done = t;
+  }
+}
+
+__global__ void k_emb_log_init(dcue_emb_log* hdr, int cap, int step) {
+  hdr->step_done = step;
+  hdr->flush_step = step;
+  hdr->n_touched = 0;
+  hdr->grad_step = -1;
+  hdr->cap = cap;
+}
+
+int launch_emb_log_init(const dcue_model* md, int cap, int step, hipStream_t s) {
+  DCUE_HIP_CHECK(hipMemsetAsync(md->emb_step, 0, sizeof(int32_t) * md->dims.n_users, s));
+  hipLaunchKernelGGL(k_emb_log_init, dim3(1), dim3(1), 0, s, md->emb_log, cap, step);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+int launch_emb_sync(const dcue_model* md, const int64_t* users, int n, hipStream_t s) {
+  if (n <= 0) return DCUE_OK;
+  hipLaunchKernelGGL(k_emb_sync, dim3((unsigned)n), dim3(256), 0, s, md->emb, md->emb_exp_avg,
+                     md->emb_exp_avg_sq, md->emb_log, md->emb_step, users, md->dims.user_embdim, 0.f);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+int launch_emb_flush(const dcue_model* md, hipStream_t s) {
+  const long n = md->dims.n_users * (long)md->dims.user_embdim;
+  long blocks = (n / 4 + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 4096 ? 4096 : blocks);
+  hipLaunchKernelGGL(k_emb_flush, dim3((unsigned)blocks), dim3(256), 0, s, md->emb, md->emb_exp_avg,
+                     md->emb_exp_avg_sq, md->emb_log, md->emb_step, (long)md->dims.n_users,
+                     md->dims.user_embdim, 0.f);
+  DCUE_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_emb_flush_done, dim3(1), dim3(1), 0, s, md->emb_log);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
 int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* poff, hipStream_t s) {
   const double bc1 = 1.0 - pow((double)a->beta1, (double)a->step);
   const double bc2 = 1.0 - pow((double)a->beta2, (double)a->step);
@@ -78,6 +244,7 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
   sc.bc2_sqrt = (float)sqrt(bc2);
   sc.eps = a->eps;
   sc.wd = a->weight_decay;
+  sc.pad = 0.f;
   const int parts = a->parts ? a->parts : (DCUE_ADAM_DENSE | DCUE_ADAM_EMBEDDING);
   const long n = poff[DCUE_N_DENSE_SEGMENTS];
   if (parts & DCUE_ADAM_DENSE) {
@@ -85,7 +252,13 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
                        md->exp_avg_sq, n, sc);
     DCUE_LAUNCH_CHECK();
   }
-  if ((parts & DCUE_ADAM_EMBEDDING) && md->dims.n_users > 0) {
+  if ((parts & DCUE_ADAM_EMBEDDING) && md->emb_step) {
+    hipLaunchKernelGGL(k_adam_touched, dim3(256), dim3(256), 0, s, md->emb, md->emb_exp_avg,
+                       md->emb_exp_avg_sq, md->emb_grad, md->emb_rows, md->emb_step, md->emb_log,
+                       md->dims.user_embdim, a->step, sc, 0.f);
+    DCUE_LAUNCH_CHECK();
+    if (a->step % md->emb_log_cap == 0) return launch_emb_flush(md, s);
+  } else if ((parts & DCUE_ADAM_EMBEDDING) && md->dims.n_users > 0) {
     long blocks = (md->dims.n_users + 3) / 4;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(k_adam_embed, dim3((unsigned)blocks), dim3(256), 0, s, md->emb,

@@ -175,6 +175,10 @@ int init_ctx(Ctx* c, const dcue_model* m) {
   int st = check_dims(&m->dims);
   if (st) return st;
   if (!m->params || !m->bn_stats || !m->bn_batches || !m->wpack) return DCUE_ERR_INVALID;
+  // deferred user-table Adam needs its log, the moments it replays and a valid history capacity
+  if (m->emb_step && (!m->emb_log || !m->emb || !m->emb_exp_avg || !m->emb_exp_avg_sq ||
+                      m->emb_log_cap < 1 || m->emb_log_cap > DCUE_MAX_LOG_CAP))
+    return DCUE_ERR_INVALID;
   c->m = m;
   param_offsets(&m->dims, c->poff);
   bn_offsets(&m->dims, c->boff);
@@ -333,6 +337,7 @@ int dcue_forward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   const double copies = (double)b->n_rows * (1 + b->n_neg);
   TRY(launch_item_counts(b, w.counts, s));
   TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s));
+  if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, s));
   TRY(user_forward(c, w, b->users, b->n_rows, nullptr, s));
   TRY(launch_score_fwd(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.hinge, w.loss,
                        w.dhinge, s));
@@ -457,7 +462,8 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
     g.cmask = m->emb; g.smm = E; g.smn = 1; g.cmrow = b->users;
     TRY(launch_tgemm(0, 0, g, s));
   }
-  TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, s));
+  TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, m->emb_rows,
+                      m->emb_step ? m->emb_log : nullptr, s));
   return DCUE_OK;
 }
 
@@ -470,6 +476,7 @@ int dcue_adam_step(const dcue_model* m, const dcue_adam_args* a, void* stream) {
   if ((parts & DCUE_ADAM_EMBEDDING) &&
       (!m->emb || !m->emb_exp_avg || !m->emb_exp_avg_sq || !m->emb_slot || !m->emb_grad))
     return DCUE_ERR_INVALID;
+  if ((parts & DCUE_ADAM_EMBEDDING) && m->emb_step && !m->emb_rows) return DCUE_ERR_INVALID;
   TRY(launch_adam(m, a, c.poff, (hipStream_t)stream));
   if (parts & DCUE_ADAM_DENSE) return launch_pack(m, c.poff, (hipStream_t)stream);
   return DCUE_OK;
@@ -496,7 +503,38 @@ int dcue_user_tower(const dcue_model* m, const int64_t* users, int32_t n, void* 
   Ws w;
   if (carve(&m->dims, n, 0, 1, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
   carve(&m->dims, n, 0, 1, ws, &w);
+  if (m->emb_step) TRY(launch_emb_sync(m, users, n, (hipStream_t)stream));
   return user_forward(c, w, users, n, user_feat, (hipStream_t)stream);
+}
+
+int dcue_emb_log_bytes(int32_t cap, size_t* bytes_host) {
+  if (!bytes_host || cap < 1 || cap > DCUE_MAX_LOG_CAP) return DCUE_ERR_INVALID;
+  *bytes_host = sizeof(dcue_emb_log) + (size_t)cap * 8 * sizeof(float);
+  return DCUE_OK;
+}
+
+int dcue_emb_log_init(const dcue_model* m, int32_t cap, int32_t step, void* stream) {
+  Ctx c;
+  TRY(init_ctx(&c, m));
+  if (!m->emb_step || !m->emb_log || cap < 1 || cap > DCUE_MAX_LOG_CAP || cap != m->emb_log_cap ||
+      step < 0)
+    return DCUE_ERR_INVALID;
+  return launch_emb_log_init(m, cap, step, (hipStream_t)stream);
+}
+
+int dcue_embedding_sync(const dcue_model* m, const int64_t* users, int32_t n, void* stream) {
+  Ctx c;
+  TRY(init_ctx(&c, m));
+  if (!users || n < 0) return DCUE_ERR_INVALID;
+  if (!m->emb_step) return DCUE_OK;  // dense mode: rows are always current
+  return launch_emb_sync(m, users, n, (hipStream_t)stream);
+}
+
+int dcue_embedding_flush(const dcue_model* m, void* stream) {
+  Ctx c;
+  TRY(init_ctx(&c, m));
+  if (!m->emb_step) return DCUE_OK;
+  return launch_emb_flush(m, (hipStream_t)stream);
 }
 
 }  // extern "C"

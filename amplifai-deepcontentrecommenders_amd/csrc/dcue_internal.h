@@ -130,8 +130,12 @@ int launch_score_bwd(const float* uf, const float* f, const dcue_batch* b, int d
                      float* dfcopy, hipStream_t s);
 int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df, hipStream_t s);
 int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float scale,
-                    float* emb_grad, int32_t* slot, hipStream_t s);
+                    float* emb_grad, int32_t* slot, int64_t* emb_rows, dcue_emb_log* log,
+                    hipStream_t s);
 int launch_adam(const dcue_model* m, const dcue_adam_args* a, const int64_t* poff, hipStream_t s);
+int launch_emb_log_init(const dcue_model* m, int cap, int step, hipStream_t s);
+int launch_emb_sync(const dcue_model* m, const int64_t* users, int n, hipStream_t s);
+int launch_emb_flush(const dcue_model* m, hipStream_t s);
 int launch_pack(const dcue_model* m, const int64_t* poff, hipStream_t s);
 
 }  // namespace dcue

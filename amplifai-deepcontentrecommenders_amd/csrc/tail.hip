@@ -382,24 +382,40 @@ int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df,
 }
 
 // Compact embedding gradient: one slot per distinct user (its first row), rows summed in order.
+// Compact embedding gradient: row b = sum of de over the batch rows of user users[b], kept at the
+// user's first occurrence (emb_rows[b] = user, -1 at repeats). Deferred Adam also learns which step
+// the gradient is for (the step after the last one recorded).
 __global__ void k_emb_grad(const float* __restrict__ de, const int64_t* users, int B, int E,
-                           float scale, float* emb_grad, int32_t* slot) {
+                           float scale, float* emb_grad, int32_t* slot, int64_t* emb_rows,
+                           dcue_emb_log* log) {
   const int b = blockIdx.x;
   const int64_t u = users[b];
+  if (b == 0 && threadIdx.x == 0 && log) {
+    log->n_touched = B;
+    log->grad_step = log->step_done + 1;
+  }
   for (int r = 0; r < b; ++r)
-    if (users[r] == u) return;
+    if (users[r] == u) {
+      if (threadIdx.x == 0 && emb_rows) emb_rows[b] = -1;
+      return;
+    }
   for (int k = threadIdx.x; k < E; k += blockDim.x) {
     float v = 0.f;
     for (int r = b; r < B; ++r)
       if (users[r] == u) v += de[(long)r * E + k];
     emb_grad[(long)b * E + k] = v * scale;
   }
-  if (threadIdx.x == 0) slot[u] = b;
+  if (threadIdx.x == 0) {
+    slot[u] = b;
+    if (emb_rows) emb_rows[b] = u;
+  }
 }
 
 int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float scale,
-                    float* emb_grad, int32_t* slot, hipStream_t s) {
-  hipLaunchKernelGGL(k_emb_grad, dim3(B), dim3(256), 0, s, de, users, B, E, scale, emb_grad, slot);
+                    float* emb_grad, int32_t* slot, int64_t* emb_rows, dcue_emb_log* log,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(k_emb_grad, dim3(B), dim3(256), 0, s, de, users, B, E, scale, emb_grad, slot,
+                     emb_rows, log);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }

@@ -39,7 +39,8 @@ class Dims(ctypes.Structure):
 class Model(ctypes.Structure):
     _fields_ = [("dims", Dims)] + [(n, ctypes.c_void_p) for n in (
         "params", "grads", "exp_avg", "exp_avg_sq", "emb", "emb_exp_avg", "emb_exp_avg_sq",
-        "emb_grad", "emb_slot", "bn_stats", "bn_batches", "wpack")]
+        "emb_grad", "emb_slot", "bn_stats", "bn_batches", "wpack", "emb_rows", "emb_step", "emb_log")] + [
+        ("emb_log_cap", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class Batch(ctypes.Structure):
@@ -64,6 +65,8 @@ ADAM_EMBEDDING = 2
 
 
 MT_STATE_BYTES = 624 * 4 + 16
+MAX_LOG_CAP = 256
+ABI_VERSION = 2
 
 _P = ctypes.c_void_p
 _SIGS = {
@@ -92,6 +95,10 @@ _SIGS = {
     "dcue_sample_catalogue": ([_P, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int64, _P, _P, _P,
                                ctypes.c_int32, ctypes.c_int32, _P, _P], ctypes.c_int),
     "dcue_build_catalogue_batch": ([_P, _P, ctypes.c_int32, ctypes.c_int32, _P, _P], ctypes.c_int),
+    "dcue_emb_log_bytes": ([ctypes.c_int32, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "dcue_emb_log_init": ([ctypes.POINTER(Model), ctypes.c_int32, ctypes.c_int32, _P], ctypes.c_int),
+    "dcue_embedding_sync": ([ctypes.POINTER(Model), _P, ctypes.c_int32, _P], ctypes.c_int),
+    "dcue_embedding_flush": ([ctypes.POINTER(Model), _P], ctypes.c_int),
 }
 
 _lib = None
@@ -109,7 +116,7 @@ def lib():
             fn = getattr(handle, name)
             fn.argtypes = args
             fn.restype = res
-        if handle.dcue_abi_version() != 1:
+        if handle.dcue_abi_version() != ABI_VERSION:
             raise RuntimeError("libdcue_hip ABI mismatch")
         _lib = handle
     return _lib
@@ -160,6 +167,12 @@ def workspace_outputs(dims, B, N, M):
     off = (ctypes.c_size_t * 4)()
     check(lib().dcue_workspace_outputs(ctypes.byref(dims), B, N, M, off), "dcue_workspace_outputs")
     return list(off)
+
+
+def emb_log_bytes(cap):
+    n = ctypes.c_size_t()
+    check(lib().dcue_emb_log_bytes(cap, ctypes.byref(n)), "dcue_emb_log_bytes")
+    return n.value
 
 
 def workspace_bytes(dims, max_rows, max_neg, max_items):

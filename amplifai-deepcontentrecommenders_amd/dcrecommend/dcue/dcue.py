@@ -154,7 +154,8 @@ class DCUENet(nn.Module):
         slot = torch.full((max(self.user_count, 1),), -1, dtype=torch.int32, device=device)
         wpack = torch.empty(nat.wpack_floats(dims), dtype=torch.float32, device=device)
         self._flat = dict(dims=dims, poff=poff, boff=boff, P=P, G=G, stats=stats, nbt=nbt, slot=slot,
-                          wpack=wpack, emb_grad=torch.zeros(0, device=device), m=None, v=None,
+                          wpack=wpack, emb_grad=torch.zeros(0, device=device),
+                          emb_rows=torch.zeros(0, dtype=torch.int64, device=device), m=None, v=None,
                           em=None, ev=None)
         self._ws = None
         self._repack()
@@ -193,10 +194,34 @@ class DCUENet(nn.Module):
         m.emb_grad = fl["emb_grad"].data_ptr() if fl["emb_grad"].numel() else None
         m.emb_slot = fl["slot"].data_ptr()
         m.bn_stats, m.bn_batches, m.wpack = fl["stats"].data_ptr(), fl["nbt"].data_ptr(), fl["wpack"].data_ptr()
+        m.emb_rows = fl["emb_rows"].data_ptr() if fl["emb_rows"].numel() else None
+        opt = self._deferred_opt() if getattr(self, "_deferred_opt", None) is not None else None
+        if opt is not None and adam_state is None:
+            adam_state = opt._adam_state()  # the deferred user-table Adam replays inside forwards
         if adam_state is not None:
             m.exp_avg, m.exp_avg_sq = adam_state["m"].data_ptr(), adam_state["v"].data_ptr()
             m.emb_exp_avg, m.emb_exp_avg_sq = adam_state["em"].data_ptr(), adam_state["ev"].data_ptr()
+            if adam_state.get("emb_step") is not None:
+                m.emb_step, m.emb_log = adam_state["emb_step"].data_ptr(), adam_state["emb_log"].data_ptr()
+                m.emb_log_cap = adam_state["cap"]
         return m
+
+    def sync_user_table(self):
+        """Bring every user row current under a deferred-embedding NativeAdam (no-op otherwise):
+        afterwards the table and its moments equal the dense per-step sweep's bit for bit."""
+        opt = self._deferred_opt() if getattr(self, "_deferred_opt", None) is not None else None
+        if opt is not None:
+            opt.flush()
+
+    def state_dict(self, *args, **kwargs):
+        if self._flat is not None:
+            self.sync_user_table()
+        return super().state_dict(*args, **kwargs)
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        if self._flat is not None:
+            self.sync_user_table()  # pending deferred steps belong to the table being replaced
+        return super().load_state_dict(state_dict, strict=strict, assign=assign)
 
     def _workspace(self, B, N, M):
         key = (B, N, M)
@@ -208,6 +233,7 @@ class DCUENet(nn.Module):
         if self._flat["emb_grad"].numel() < B * self.user_embdim:
             self._flat["emb_grad"] = torch.zeros(B * self.user_embdim, dtype=torch.float32,
                                                  device=self._flat["P"].device)
+            self._flat["emb_rows"] = torch.full((B,), -1, dtype=torch.int64, device=self._flat["P"].device)
         return self._ws
 
     # -------------------------------------------------------------------------- native calls

@@ -39,6 +39,10 @@ def parse():
     ap.add_argument("--hidden", type=int, default=128)
     ap.add_argument("--user-embdim", type=int, default=300)
     ap.add_argument("--cpu-steps", type=int, default=6)
+    ap.add_argument("--dense-embedding-adam", action="store_true",
+                    help="step every user row every step (the literal sweep) instead of the deferred, "
+                         "bit-identical replay")
+    ap.add_argument("--flush-every", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -115,7 +119,9 @@ def main():
                    "user_embdim": args.user_embdim, "user_count": n_users_local,
                    "model_type": "truedcuemel1dbn"}).to(dev)
     net.train()
-    opt = NativeAdam(net.parameters(), 1e-5, (0.9, 0.99), 1e-8, 0)
+    defer = not args.dense_embedding_adam
+    opt = NativeAdam(net.parameters(), 1e-5, (0.9, 0.99), 1e-8, 0, defer_embedding=defer,
+                     flush_every=args.flush_every)
     epoch_size = (int(math.ceil(n_pairs / 10)) // B) * B
     sched = CyclicLRWithRestarts(opt, B, epoch_size=epoch_size, restart_period=30, t_mult=2, policy="cosine")
     sched.step()
@@ -162,12 +168,14 @@ def main():
 
     for s in range(args.warmup):
         step(s, None)
+    opt.flush()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k, k)
+    opt.flush()  # deferred user-table steps still pending are part of the timed work
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

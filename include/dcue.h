@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DCUE_ABI_VERSION 1
+#define DCUE_ABI_VERSION 2
 #define DCUE_N_MELS 128
 #define DCUE_N_FRAMES 131
 #define DCUE_N_BN 6
@@ -50,6 +50,24 @@ typedef struct dcue_dims {
   int64_t n_users;     /* rows of the (local shard of the) user table */
 } dcue_dims;
 
+/* Deferred user-table Adam (optional, selected by dcue_model.emb_step != NULL).
+ * The reference's dense embedding gradient makes torch.optim.Adam step EVERY user row each batch,
+ * with g = 0 (+ wd*p) for rows outside the batch (nn/dcue.py:143-147,209). Deferred mode performs
+ * exactly those steps, later: a row's zero-gradient steps are replayed with the same fp32
+ * operations and the same per-step scalars (kept in this log's history ring) right before the row
+ * is next read (dcue_forward / dcue_user_tower bring their users' rows current), for every row each
+ * `cap` steps, and on dcue_embedding_flush. After a flush the table and both moments are
+ * bit-identical to the dense sweep's; between flushes rows outside recent batches lag behind, so
+ * read the table directly only after a flush. The [cap][8] float history follows this header. */
+typedef struct dcue_emb_log {
+  int32_t step_done;   /* last Adam step recorded */
+  int32_t flush_step;  /* every row is current to at least this step */
+  int32_t n_touched;   /* emb_rows entries written by the last backward */
+  int32_t grad_step;   /* the Adam step the last backward's compact gradient belongs to */
+  int32_t cap;         /* history ring capacity in steps (= flush period) */
+  int32_t pad[3];
+} dcue_emb_log;
+
 /* Model state. Replaces DCUENet's parameters/buffers (dcue/dcue.py:21-68) + torch.optim.Adam state. */
 typedef struct dcue_model {
   dcue_dims dims;
@@ -65,7 +83,14 @@ typedef struct dcue_model {
   float* bn_stats;     /* running_mean/var per BN layer, dcue_bn_layout offsets */
   int64_t* bn_batches; /* [6] num_batches_tracked */
   float* wpack;        /* packed conv weights (dcue_wpack_floats), refreshed by dcue_pack_weights */
+  int64_t* emb_rows;   /* [max_rows] user row of each compact gradient row (-1: duplicate user) */
+  int32_t* emb_step;   /* deferred mode: [n_users] step each row is current to (NULL: dense sweep) */
+  dcue_emb_log* emb_log; /* deferred mode: header + history (dcue_emb_log_bytes) */
+  int32_t emb_log_cap;   /* deferred mode: the log's history capacity (1..DCUE_MAX_LOG_CAP) */
+  int32_t reserved;
 } dcue_model;
+
+#define DCUE_MAX_LOG_CAP 256
 
 /* One training batch, already resident in HBM.
  * Items are the spectrograms the item tower runs on. Catalogue mode (datasets/dcuedataset.py:242-250):
@@ -140,8 +165,18 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
 
 /* optimizer.step() (nn/dcue.py:209, torch.optim.Adam semantics): dense params + every user row
  * (rows without a gradient this step still decay their moments and move, as the reference's dense
- * embedding gradient does), then clears emb_slot and refreshes wpack. */
+ * embedding gradient does), then clears emb_slot and refreshes wpack. In deferred mode the user
+ * table part steps the batch's rows now and records the step for the others (dcue_emb_log); steps
+ * must then be consecutive (a->step == step_done + 1). */
 int dcue_adam_step(const dcue_model* m, const dcue_adam_args* a, void* stream);
+
+/* Deferred user-table Adam: log size for a `cap`-step history; (re)initialise the log and row
+ * clocks at Adam step `step` (table and moments current to it); bring `users`' rows current;
+ * bring every row current (the state then equals the dense sweep's bit for bit). */
+int dcue_emb_log_bytes(int32_t cap, size_t* bytes_host);
+int dcue_emb_log_init(const dcue_model* m, int32_t cap, int32_t step, void* stream);
+int dcue_embedding_sync(const dcue_model* m, const int64_t* users, int32_t n, void* stream);
+int dcue_embedding_flush(const dcue_model* m, void* stream);
 
 /* Eval-mode item tower (running BN stats): DCUENet.conv(X) under model.eval() (nn/dcue.py:663). */
 int dcue_item_tower_eval(const dcue_model* m, const dcue_tracks* t, const int32_t* item_track,

@@ -25,7 +25,36 @@ def test_library_exports_header_symbols():
     assert len(names) >= 15
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.dcue_abi_version() == 1
+    hdr = open(os.path.join(ROOT, "include", "dcue.h")).read()
+    assert lib.dcue_abi_version() == int(re.search(r"#define DCUE_ABI_VERSION (\d+)", hdr).group(1))
+    assert lib.dcue_abi_version() == nat.ABI_VERSION
+
+
+def test_ctypes_structs_match_header(tmp_path):
+    """sizeof/offsetof of every ABI struct, compiled from include/dcue.h, against the ctypes mirror."""
+    import ctypes
+    import subprocess
+    from dcrecommend import _native as nat
+    structs = {"dcue_dims": nat.Dims, "dcue_model": nat.Model, "dcue_batch": nat.Batch,
+               "dcue_tracks": nat.Tracks, "dcue_adam_args": nat.AdamArgs}
+    src = ["#include <stdio.h>", "#include <stddef.h>", '#include "dcue.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        src.append('printf("%s %%zu\\n", sizeof(%s));' % (cname, cname))
+        for fname, _ in py._fields_:
+            src.append('printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (cname, fname, cname, fname))
+    src.append('printf("dcue_emb_log %zu\\n", sizeof(dcue_emb_log));')
+    src.append('printf("dcue_mt_state %zu\\n", sizeof(dcue_mt_state));')
+    src.append("return 0; }")
+    (tmp_path / "probe.c").write_text("\n".join(src))
+    subprocess.check_call(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(tmp_path / "probe.c"),
+                           "-o", str(tmp_path / "probe")])
+    got = dict(l.split() for l in subprocess.check_output([str(tmp_path / "probe")]).decode().splitlines())
+    for cname, py in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert int(got["%s.%s" % (cname, fname)]) == getattr(py, fname).offset, (cname, fname)
+    assert int(got["dcue_mt_state"]) == nat.MT_STATE_BYTES
+    assert int(got["dcue_emb_log"]) == 32
 
 
 def test_binding_covers_header():
