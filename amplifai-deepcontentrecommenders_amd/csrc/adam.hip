@@ -224,10 +224,14 @@ int launch_emb_flush(const dcue_model* md, hipStream_t s) {
   const long n = md->dims.n_users * (long)md->dims.user_embdim;
   long blocks = (n / 4 + 255) / 256;
   blocks = blocks < 1 ? 1 : (blocks > 4096 ? 4096 : blocks);
+  TimerScope tsc;
+  int st = timer_begin(&tsc, DCUE_TIMED_EMB_FLUSH, s);
+  if (st) return st;
   hipLaunchKernelGGL(k_emb_flush, dim3((unsigned)blocks), dim3(256), 0, s, md->emb, md->emb_exp_avg,
                      md->emb_exp_avg_sq, md->emb_log, md->emb_step, (long)md->dims.n_users,
                      md->dims.user_embdim, 0.f);
   DCUE_LAUNCH_CHECK();
+  if ((st = timer_end(&tsc))) return st;
   hipLaunchKernelGGL(k_emb_flush_done, dim3(1), dim3(1), 0, s, md->emb_log);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
@@ -261,10 +265,14 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
   } else if ((parts & DCUE_ADAM_EMBEDDING) && md->dims.n_users > 0) {
     long blocks = (md->dims.n_users + 3) / 4;
     if (blocks > 8192) blocks = 8192;
+    TimerScope tsc;
+    int st = timer_begin(&tsc, DCUE_TIMED_ADAM_EMBED, s);
+    if (st) return st;
     hipLaunchKernelGGL(k_adam_embed, dim3((unsigned)blocks), dim3(256), 0, s, md->emb,
                        md->emb_exp_avg, md->emb_exp_avg_sq, md->emb_grad, md->emb_slot,
                        (long)md->dims.n_users, md->dims.user_embdim, sc);
     DCUE_LAUNCH_CHECK();
+    if ((st = timer_end(&tsc))) return st;
   }
   return DCUE_OK;
 }

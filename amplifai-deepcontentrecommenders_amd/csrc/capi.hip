@@ -13,6 +13,39 @@
 
 using namespace dcue;
 
+namespace dcue {
+// Side streams. A training step is a chain of small kernels, each far from filling 256 CUs; the
+// independent branches run concurrently: the user tower beside the item tower (forward and
+// backward), and each conv layer's weight gradient beside the dgrad chain of the layers below
+// (alternating between two streams, each with its own partial-sum buffers). Forks and joins are
+// event-ordered against the caller's stream, so the calls stay stream-ordered (and capturable).
+
+SidePool* side_pool() {
+  static SidePool pools[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  SidePool& p = pools[dev];
+  if (!p.st[0]) {
+    for (auto& s : p.st)
+      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    for (auto& e : p.ev)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  }
+  return &p;
+}
+
+// `to` waits for everything enqueued on `from` so far. An event is re-recorded only after the
+// wait on its previous record has been enqueued, so a small ring of events suffices.
+int stream_wait(SidePool* p, hipStream_t to, hipStream_t from) {
+  hipEvent_t e = p->ev[p->next];
+  p->next = (p->next + 1) % 32;
+  DCUE_HIP_CHECK(hipEventRecord(e, from));
+  DCUE_HIP_CHECK(hipStreamWaitEvent(to, e, 0));
+  return DCUE_OK;
+}
+
+}  // namespace dcue
+
 namespace {
 
 constexpr int kSeg = DCUE_N_DENSE_SEGMENTS;
@@ -93,7 +126,7 @@ struct Ws {
   float *du, *dfcopy, *df;
   float* g[6];
   float *dh1, *de;
-  float *wpart, *bpart, *G, *S;
+  float *wpart[2], *bpart[2], *G, *S;  // wgrad partials: one set per wgrad stream
 };
 
 size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
@@ -147,10 +180,12 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
     if (e > wp) wp = e;
     if (nch * 5 * cout > bp) bp = nch * 5 * cout;
   }
-  w->wpart = ar.take<float>(wp);
-  w->bpart = ar.take<float>(bp);
+  for (int i = 0; i < 2; ++i) {
+    w->wpart[i] = ar.take<float>(wp);
+    w->bpart[i] = ar.take<float>(bp);
+  }
   w->G = ar.take<float>((long)H * 4 * kMels);
-  w->S = ar.take<float>(4L * H);
+  w->S = ar.take<float>(9L * H);  // S[4][H] + the five layer-1 bias partial sums
   return ar.used + 256;
 }
 
@@ -218,7 +253,10 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     a.partials = train ? w.partials : nullptr;
     a.M = M;
     a.nout = l == 5 ? c.D : c.H;
+    TimerScope tsc;
+    TRY(timer_begin(&tsc, l == 1 ? DCUE_TIMED_CONV1_FWD : -1, s));
     TRY(launch_conv_fwd(l, l == 1 ? kMels : c.H, l == 1 ? src : SRC_ACT, a, s));
+    TRY(timer_end(&tsc));
     const int C = a.nout;
     TRY(launch_bn_finalize(w.partials, conv_fwd_grid(l, l == 1 ? kMels : c.H, M), C, copies * layer_geom(l).lp,
                            c.P(seg_bn_w(l)), c.rmean(l), c.rvar(l), m->bn_batches + l, train,
@@ -335,10 +373,15 @@ int dcue_forward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   carve(&m->dims, b->n_rows, b->n_neg, b->n_items, ws, &w);
   hipStream_t s = (hipStream_t)stream;
   const double copies = (double)b->n_rows * (1 + b->n_neg);
+  SidePool* sp = side_pool();
+  if (!sp) return DCUE_ERR_HIP;
+  hipStream_t su = sp->st[0];
+  TRY(stream_wait(sp, su, s));  // user tower beside the item tower
+  if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
+  TRY(user_forward(c, w, b->users, b->n_rows, nullptr, su));
   TRY(launch_item_counts(b, w.counts, s));
   TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s));
-  if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, s));
-  TRY(user_forward(c, w, b->users, b->n_rows, nullptr, s));
+  TRY(stream_wait(sp, s, su));
   TRY(launch_score_fwd(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.hinge, w.loss,
                        w.dhinge, s));
   // the outputs live in the workspace (dcue_workspace_outputs gives their offsets); copies are
@@ -368,6 +411,47 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
 
   TRY(launch_score_bwd(w.uf, w.f, b, D, dscores ? dscores : w.dhinge, w.cosv, w.norms, w.du,
                        w.dfcopy, s));
+  SidePool* sp = side_pool();
+  if (!sp) return DCUE_ERR_HIP;
+  hipStream_t su = sp->st[0], sw[2] = {sp->st[1], sp->st[2]};
+  TRY(stream_wait(sp, su, s));
+  // user tower (userembedding.py:33-44 backward), then the compact embedding rows
+  {
+    TGemmArgs g = {};
+    // dW2[n][k] = sum_b du[b][n] relu(h1)[b][k]; db2[n] = sum_b du[b][n]
+    g.M = D; g.N = E; g.K = B;
+    g.A = w.du; g.sam = 1; g.sak = D;
+    g.B = w.h1; g.sbk = E; g.sbn = 1;
+    g.C = c.Gd(SEG_L2_W); g.scm = E; g.scn = 1;
+    g.rowsum = c.Gd(SEG_L2_B);
+    TRY(launch_tgemm(0, 1, g, su));
+    // dh1 = (du W2) * (h1 > 0)
+    g = TGemmArgs{};
+    g.M = B; g.N = E; g.K = D;
+    g.A = w.du; g.sam = D; g.sak = 1;
+    g.B = c.P(SEG_L2_W); g.sbk = E; g.sbn = 1;
+    g.C = w.dh1; g.scm = E; g.scn = 1;
+    g.cmask = w.h1; g.smm = E; g.smn = 1;
+    TRY(launch_tgemm(0, 0, g, su));
+    // dW1[n][k] = sum_b dh1[b][n] relu(E[u_b])[k]; db1[n] = sum_b dh1[b][n]
+    g = TGemmArgs{};
+    g.M = E; g.N = E; g.K = B;
+    g.A = w.dh1; g.sam = 1; g.sak = E;
+    g.B = m->emb; g.sbk = E; g.sbn = 1; g.brow = b->users;
+    g.C = c.Gd(SEG_L1_W); g.scm = E; g.scn = 1;
+    g.rowsum = c.Gd(SEG_L1_B);
+    TRY(launch_tgemm(0, 1, g, su));
+    // de = (dh1 W1) * (E[u_b] > 0)
+    g = TGemmArgs{};
+    g.M = B; g.N = E; g.K = E;
+    g.A = w.dh1; g.sam = E; g.sak = 1;
+    g.B = c.P(SEG_L1_W); g.sbk = E; g.sbn = 1;
+    g.C = w.de; g.scm = E; g.scn = 1;
+    g.cmask = m->emb; g.smm = E; g.smn = 1; g.cmrow = b->users;
+    TRY(launch_tgemm(0, 0, g, su));
+  }
+  TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, m->emb_rows,
+                      m->emb_step ? m->emb_log : nullptr, su));
   TRY(launch_item_grad(w.dfcopy, b, D, w.df, s));
   // fc: dW[n][k] = sum_m df[m][n] bn5(y5)[m][k], db = sum_m df (row sums of A); g5 = df W
   {
@@ -397,6 +481,9 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
     TRY(launch_bwd_finalize(w.partials, nparts, C, w.sD[l], w.sDx[l], c.Gd(seg_bn_w(l)),
                             c.Gd(seg_bn_b(l)), s));
     const float invN = (float)(1.0 / (copies * gm.lp));
+    // weight gradient of layer l on a side stream (alternating, own partials); dgrad continues here
+    hipStream_t so = sw[l & 1];
+    TRY(stream_wait(sp, so, s));
     WgradArgs wa = {};
     wa.xsrc = l == 1 ? t->data : (const void*)w.y[l - 1];
     wa.item_track = b->item_track;
@@ -407,14 +494,17 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
     wa.mean_l = w.mean[l]; wa.invstd_l = w.invstd[l]; wa.a_l = w.a[l];
     wa.sD = w.sD[l]; wa.sDx = w.sDx[l]; wa.invN = invN; wa.counts = w.counts;
     wa.M = M; wa.cout = C; wa.cin = cin;
-    wa.wpart = w.wpart; wa.bpart = w.bpart;
+    wa.wpart = w.wpart[l & 1]; wa.bpart = w.bpart[l & 1];
     const int nch = wgrad_nchunk(l, M, C, cin);
-    TRY(launch_conv_wgrad(l, l == 1 ? src : SRC_ACT, wa, nch, s));
-    TRY(launch_wgrad_reduce(l, w.wpart, w.bpart, nch, C, cin, c.Gd(seg_conv_w(l)),
-                            c.Gd(seg_conv_b(l)), w.G, w.S, s));
+    TimerScope tsc;
+    TRY(timer_begin(&tsc, l == 1 ? DCUE_TIMED_CONV1_WGRAD : -1, so));
+    TRY(launch_conv_wgrad(l, l == 1 ? src : SRC_ACT, wa, nch, so));
+    TRY(timer_end(&tsc));
+    TRY(launch_wgrad_reduce(l, wa.wpart, wa.bpart, nch, C, cin, c.Gd(seg_conv_w(l)),
+                            c.Gd(seg_conv_b(l)), w.G, w.S, so));
     if (l == 1) {
       TRY(launch_bn0_grads(w.G, w.S, c.P(seg_conv_w(1)), c.P(seg_bn_w(0)), c.P(seg_bn_b(0)), H,
-                           c.Gd(seg_conv_w(1)), c.Gd(seg_bn_w(0)), c.Gd(seg_bn_b(0)), s));
+                           c.Gd(seg_conv_w(1)), c.Gd(seg_bn_w(0)), c.Gd(seg_bn_b(0)), so));
     } else {
       RowsArgs ra = {};
       ra.src = w.g[l]; ra.y_l = w.y[l]; ra.idx_l = w.idx[l];
@@ -427,43 +517,7 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
       TRY(launch_conv_dgrad(l, C, ra, s));
     }
   }
-  // user tower (userembedding.py:33-44 backward), then the compact embedding rows
-  {
-    TGemmArgs g = {};
-    // dW2[n][k] = sum_b du[b][n] relu(h1)[b][k]; db2[n] = sum_b du[b][n]
-    g.M = D; g.N = E; g.K = B;
-    g.A = w.du; g.sam = 1; g.sak = D;
-    g.B = w.h1; g.sbk = E; g.sbn = 1;
-    g.C = c.Gd(SEG_L2_W); g.scm = E; g.scn = 1;
-    g.rowsum = c.Gd(SEG_L2_B);
-    TRY(launch_tgemm(0, 1, g, s));
-    // dh1 = (du W2) * (h1 > 0)
-    g = TGemmArgs{};
-    g.M = B; g.N = E; g.K = D;
-    g.A = w.du; g.sam = D; g.sak = 1;
-    g.B = c.P(SEG_L2_W); g.sbk = E; g.sbn = 1;
-    g.C = w.dh1; g.scm = E; g.scn = 1;
-    g.cmask = w.h1; g.smm = E; g.smn = 1;
-    TRY(launch_tgemm(0, 0, g, s));
-    // dW1[n][k] = sum_b dh1[b][n] relu(E[u_b])[k]; db1[n] = sum_b dh1[b][n]
-    g = TGemmArgs{};
-    g.M = E; g.N = E; g.K = B;
-    g.A = w.dh1; g.sam = 1; g.sak = E;
-    g.B = m->emb; g.sbk = E; g.sbn = 1; g.brow = b->users;
-    g.C = c.Gd(SEG_L1_W); g.scm = E; g.scn = 1;
-    g.rowsum = c.Gd(SEG_L1_B);
-    TRY(launch_tgemm(0, 1, g, s));
-    // de = (dh1 W1) * (E[u_b] > 0)
-    g = TGemmArgs{};
-    g.M = B; g.N = E; g.K = E;
-    g.A = w.dh1; g.sam = E; g.sak = 1;
-    g.B = c.P(SEG_L1_W); g.sbk = E; g.sbn = 1;
-    g.C = w.de; g.scm = E; g.scn = 1;
-    g.cmask = m->emb; g.smm = E; g.smn = 1; g.cmrow = b->users;
-    TRY(launch_tgemm(0, 0, g, s));
-  }
-  TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, m->emb_rows,
-                      m->emb_step ? m->emb_log : nullptr, s));
+  for (hipStream_t x : {su, sw[0], sw[1]}) TRY(stream_wait(sp, s, x));
   return DCUE_OK;
 }
 

@@ -406,6 +406,8 @@ int launch_conv_dgrad(int layer, int kc, const RowsArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------ wgrad
+static constexpr int kWgradRch = 72;  // rows per chunk step (9 per thread)
+
 // dW[o][k*cin+c] = sum over conv rows (i,t) of dz[i][t][o] * x[i][t+k-pad][c]: a GEMM whose K is
 // the row dimension. Workgroup = 128 (o) x 128 (kc) output block x one chunk of rows; the chunk is
 // streamed through LDS RCH rows at a time (dz and x tiles, both built by fused elementwise loads);
@@ -418,6 +420,8 @@ template <int SRCX, int KS, int PAD, int LIN, int R, int POOL, int LP, int RCH, 
 __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
   constexpr int PW = 128 + 16;  // == 16 (mod 32): ds_read_b32 rows r and r+1 on disjoint banks
   constexpr int NB = EDGES ? 5 : 1;
+  constexpr int FR = RCH / 8;   // rows per thread per chunk step (8 row slots x 32 channel quads)
+  constexpr bool TRACK = SRCX == SRC_TRACK_F16 || SRCX == SRC_TRACK_F32;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* dzs = lds;
   float* xs = lds + RCH * PW;
@@ -442,109 +446,118 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
 #pragma unroll
   for (int e = 0; e < NB; ++e) bacc[e] = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  const int q = tid & 31, slot = tid >> 5;  // fill mapping: 4-channel quad, row slot (8 slots)
+  // this thread fills channel quad q (dz outputs o..o+3, x columns kc..kc+3) of row slots
+  // slot, slot+8, ...; everything per channel is loaded once, out of the row loop
+  const int q = tid & 31, slot = tid >> 5;
+  const int o = obase + 4 * q, kc = kcbase + 4 * q;
+  const bool o_ok = o < cout, kc_ok = kc < kcn;
+  const int oc = o_ok ? o : 0, kcc = kc_ok ? kc : 0;
+  const int kx = kcc / cin, cx = kcc - kx * cin;
+  const float4 mean4 = ld4(a.mean_l + oc), inv4 = ld4(a.invstd_l + oc), a4 = ld4(a.a_l + oc);
+  const float4 sD4 = ld4(a.sD + oc), sDx4 = ld4(a.sDx + oc);
+  const float4 xmu = ld4(a.x_mean + cx), xsc = ld4(a.x_a + cx);
+  const float4 xbe = a.x_beta ? ld4(a.x_beta + cx) : make_float4(0.f, 0.f, 0.f, 0.f);
+
+  // raw operands of one chunk step, loaded branch-free (clamped addresses, masks applied later)
+  float4 rg[FR], ry[FR], rx[FR];
+  uint32_t rid[FR];
+  float rcnt[FR];
+  auto issue = [&](long rb) {
+    long ii[FR];
+    int tt[FR], pc[FR];
+    int trk[FR];
+#pragma unroll
+    for (int j = 0; j < FR; ++j) {
+      long row = rb + slot + 8 * j;
+      row = row < r_end ? row : r_begin;
+      ii[j] = row / R;
+      tt[j] = (int)(row - ii[j] * R);
+      const int p = tt[j] + kx - PAD;
+      pc[j] = p < 0 ? 0 : (p >= LIN ? LIN - 1 : p);
+    }
+    if constexpr (TRACK) {
+#pragma unroll
+      for (int j = 0; j < FR; ++j) trk[j] = a.item_track[ii[j]];
+    }
+#pragma unroll
+    for (int j = 0; j < FR; ++j) {
+      const long base = (ii[j] * LP + tt[j] / POOL) * cout + oc;
+      rg[j] = ld4(a.g_l + base);
+      ry[j] = ld4(a.y_l + base);
+      rid[j] = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
+      rcnt[j] = a.counts ? a.counts[ii[j]] : 1.f;
+      if constexpr (SRCX == SRC_TRACK_F16) {
+        const uint2 raw = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.xsrc) +
+                                                          (((long)trk[j] * kFrames + pc[j]) * kMels + cx));
+        rx[j] = make_float4(__uint_as_float(raw.x), __uint_as_float(raw.y), 0.f, 0.f);
+      } else if constexpr (SRCX == SRC_TRACK_F32) {
+        rx[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + (((long)trk[j] * kFrames + pc[j]) * kMels + cx));
+      } else {
+        rx[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + ((ii[j] * LIN + pc[j]) * cin + cx));
+      }
+    }
+  };
+
+  issue(r_begin);
   for (long rb = r_begin; rb < r_end; rb += RCH) {
-    // fill: this thread's 8 rows of the chunk in two batches of 4, all loads of a batch in flight
-    constexpr int FB = 4;
-    const int o = obase + 4 * q;
-    const int kc = kcbase + 4 * q;
-    const int kx = kc / cin, cx = kc - kx * cin;
+    // dz (BN_l backward through relu + max-pool, as RowsArgs) and x (BN_{l-1} affine) -> LDS
 #pragma unroll
-    for (int rf = 0; rf < RCH / 8; rf += FB) {
-      long ii[FB], trk[FB];
-      int tt[FB];
-      bool zok[FB], xok[FB];
-      float4 gg[FB], yy[FB], xr[FB];
-      uint32_t id[FB];
+    for (int j = 0; j < FR; ++j) {
+      const long row = rb + slot + 8 * j;
+      const bool valid = row < r_end;
+      const long rowc = valid ? row : r_begin;
+      const long ii = rowc / R;
+      const int t = (int)(rowc - ii * R), jp = t % POOL;
+      const int p = t + kx - PAD;
+      float4 dz = make_float4(0.f, 0.f, 0.f, 0.f), xv = dz;
+      if (valid && o_ok) {
+        const float kD = rcnt[j] * a.invN;
+        const float gv[4] = {rg[j].x, rg[j].y, rg[j].z, rg[j].w};
+        const float yv[4] = {ry[j].x, ry[j].y, ry[j].z, ry[j].w};
+        const float mu[4] = {mean4.x, mean4.y, mean4.z, mean4.w}, iv[4] = {inv4.x, inv4.y, inv4.z, inv4.w};
+        const float av[4] = {a4.x, a4.y, a4.z, a4.w}, sd[4] = {sD4.x, sD4.y, sD4.z, sD4.w};
+        const float sdx[4] = {sDx4.x, sDx4.y, sDx4.z, sDx4.w};
+        float r4[4];
 #pragma unroll
-      for (int j = 0; j < FB; ++j) {
-        const long row = rb + slot + 8 * (rf + j);
-        ii[j] = row / R;
-        tt[j] = (int)(row - ii[j] * R);
-        zok[j] = row < r_end && o < cout;
-        const int p = tt[j] + kx - PAD;
-        xok[j] = row < r_end && kc < kcn && p >= 0 && p < LIN;
-        trk[j] = 0;
-      }
-      if constexpr (SRCX == SRC_TRACK_F16 || SRCX == SRC_TRACK_F32) {
-#pragma unroll
-        for (int j = 0; j < FB; ++j)
-          if (xok[j]) trk[j] = a.item_track[ii[j]];
-      }
-#pragma unroll
-      for (int j = 0; j < FB; ++j) {
-        if (zok[j]) {
-          const long base = (ii[j] * LP + tt[j] / POOL) * cout + o;
-          gg[j] = ld4(a.g_l + base);
-          yy[j] = ld4(a.y_l + base);
-          id[j] = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
+        for (int s = 0; s < 4; ++s) {
+          const float xh = (yv[s] - mu[s]) * iv[s];
+          const float dx = av[s] * (gv[s] - kD * sd[s] - kD * xh * sdx[s]);
+          r4[s] = (((rid[j] >> (8 * s)) & 0xff) == (uint32_t)jp && yv[s] > 0.f) ? dx : 0.f;
         }
-        if (xok[j]) {
-          const int p = tt[j] + kx - PAD;
-          if constexpr (SRCX == SRC_TRACK_F16) {
-            const uint2 raw = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.xsrc) +
-                                                              ((trk[j] * kFrames + p) * kMels + cx));
-            xr[j].x = __uint_as_float(raw.x);
-            xr[j].y = __uint_as_float(raw.y);
-          } else if constexpr (SRCX == SRC_TRACK_F32) {
-            xr[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + ((trk[j] * kFrames + p) * kMels + cx));
-          } else {
-            xr[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + ((ii[j] * LIN + p) * cin + cx));
-          }
-        }
-      }
+        dz = make_float4(r4[0], r4[1], r4[2], r4[3]);
+        if (do_bias) {
+          bacc[0].x += dz.x; bacc[0].y += dz.y; bacc[0].z += dz.z; bacc[0].w += dz.w;
+          if constexpr (EDGES) {  // static indices only: keeps bacc[] in registers
+            const int e = t == 0 ? 1 : t == 1 ? 2 : t == R - 2 ? 3 : t == R - 1 ? 4 : 0;
 #pragma unroll
-      for (int j = 0; j < FB; ++j) {
-        const int rr = slot + 8 * (rf + j);
-        float4 dz = make_float4(0.f, 0.f, 0.f, 0.f), xv = dz;
-        if (zok[j]) {
-          const int t = tt[j], jp = t % POOL;
-          const float kD = (a.counts ? a.counts[ii[j]] : 1.f) * a.invN;
-          const float gv[4] = {gg[j].x, gg[j].y, gg[j].z, gg[j].w};
-          const float yv[4] = {yy[j].x, yy[j].y, yy[j].z, yy[j].w};
-          float r4[4];
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            const int oc = o + s;
-            const float xh = (yv[s] - a.mean_l[oc]) * a.invstd_l[oc];
-            const float dx = a.a_l[oc] * (gv[s] - kD * a.sD[oc] - kD * xh * a.sDx[oc]);
-            r4[s] = (((id[j] >> (8 * s)) & 0xff) == (uint32_t)jp && yv[s] > 0.f) ? dx : 0.f;
-          }
-          dz = make_float4(r4[0], r4[1], r4[2], r4[3]);
-          if (do_bias) {
-            bacc[0].x += dz.x; bacc[0].y += dz.y; bacc[0].z += dz.z; bacc[0].w += dz.w;
-            if constexpr (EDGES) {  // static indices only: keeps bacc[] in registers
-              const int e = t == 0 ? 1 : t == 1 ? 2 : t == R - 2 ? 3 : t == R - 1 ? 4 : 0;
-#pragma unroll
-              for (int k = 1; k < NB; ++k) {
-                const float f = e == k ? 1.f : 0.f;
-                bacc[k].x += f * dz.x; bacc[k].y += f * dz.y; bacc[k].z += f * dz.z; bacc[k].w += f * dz.w;
-              }
+            for (int k = 1; k < NB; ++k) {
+              const float f = e == k ? 1.f : 0.f;
+              bacc[k].x += f * dz.x; bacc[k].y += f * dz.y; bacc[k].z += f * dz.z; bacc[k].w += f * dz.w;
             }
           }
         }
-        if (xok[j]) {
-          float x[4];
-          if constexpr (SRCX == SRC_TRACK_F16) {
-            const uint32_t lo = __float_as_uint(xr[j].x), hi = __float_as_uint(xr[j].y);
-            const __half2 h0 = *reinterpret_cast<const __half2*>(&lo);
-            const __half2 h1 = *reinterpret_cast<const __half2*>(&hi);
-            x[0] = __low2float(h0); x[1] = __high2float(h0); x[2] = __low2float(h1); x[3] = __high2float(h1);
-          } else {
-            x[0] = xr[j].x; x[1] = xr[j].y; x[2] = xr[j].z; x[3] = xr[j].w;
-          }
-          const float4 mu = ld4(a.x_mean + cx), sc = ld4(a.x_a + cx);
-          const float4 be = a.x_beta ? ld4(a.x_beta + cx) : make_float4(0.f, 0.f, 0.f, 0.f);
-          xv = make_float4((x[0] - mu.x) * sc.x + be.x, (x[1] - mu.y) * sc.y + be.y,
-                           (x[2] - mu.z) * sc.z + be.z, (x[3] - mu.w) * sc.w + be.w);
-        }
-        st4(&dzs[rr * PW + 4 * q], dz);
-        st4(&xs[rr * PW + 4 * q], xv);
       }
+      if (valid && kc_ok && p >= 0 && p < LIN) {
+        float x[4];
+        if constexpr (SRCX == SRC_TRACK_F16) {
+          const uint32_t lo = __float_as_uint(rx[j].x), hi = __float_as_uint(rx[j].y);
+          const __half2 h0 = *reinterpret_cast<const __half2*>(&lo);
+          const __half2 h1 = *reinterpret_cast<const __half2*>(&hi);
+          x[0] = __low2float(h0); x[1] = __high2float(h0); x[2] = __low2float(h1); x[3] = __high2float(h1);
+        } else {
+          x[0] = rx[j].x; x[1] = rx[j].y; x[2] = rx[j].z; x[3] = rx[j].w;
+        }
+        xv = make_float4((x[0] - xmu.x) * xsc.x + xbe.x, (x[1] - xmu.y) * xsc.y + xbe.y,
+                         (x[2] - xmu.z) * xsc.z + xbe.z, (x[3] - xmu.w) * xsc.w + xbe.w);
+      }
+      const int rr = slot + 8 * j;
+      st4(&dzs[rr * PW + 4 * q], dz);
+      st4(&xs[rr * PW + 4 * q], xv);
     }
     __syncthreads();
-#pragma unroll 4
-    for (int r0 = 0; r0 < RCH; r0 += 4) {
+    if (rb + RCH < r_end) issue(rb + RCH);  // next step's loads fly while the MFMAs run
+    const int nr = (int)min((long)RCH, (r_end - rb + 3) & ~3L);  // rows of this step, padded to 4
+    for (int r0 = 0; r0 < nr; r0 += 4) {
       float av[4], bv[4];
 #pragma unroll
       for (int m = 0; m < 4; ++m) av[m] = dzs[(r0 + g) * PW + 64 * wo + 16 * m + l16];
@@ -587,20 +600,17 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
   }
 }
 
-static constexpr int kWgradRch = 64;
-
 int wgrad_nchunk(int layer, int M, int cout, int cin) {
+  // one workgroup per CU (LDS-bound): at most 256 / tiles chunks, each of >= 64 rows; partial
+  // blocks cost a write + a read of cout*ks*cin floats per chunk
   const LayerGeom gm = layer_geom(layer);
   const long rows = (long)M * gm.lp * gm.pool;
-  const int blocks = ((gm.ks * cin + 127) / 128) * ((cout + 127) / 128);
-  long n = (512 + blocks - 1) / blocks;
-  const long maxn = (rows + kWgradRch - 1) / kWgradRch;
-  // partial blocks cost a write + a read of cout*ks*cin floats each: keep them <= 16 MB
-  const long cap = (4L << 20) / ((long)cout * gm.ks * cin);
-  if (n > maxn) n = maxn;
+  const long tiles = ((gm.ks * cin + 127) / 128) * ((cout + 127) / 128);
+  long n = 256 / tiles;
+  if (n > (rows + 63) / 64) n = (rows + 63) / 64;
+  const long cap = (8L << 20) / ((long)cout * gm.ks * cin);
   if (n > cap) n = cap;
-  if (n < 1) n = 1;
-  return (int)n;
+  return (int)(n < 1 ? 1 : n);
 }
 
 template <int L, int SRCX>
@@ -618,8 +628,7 @@ static int wgrad_layer(const WgradArgs& a0, int nchunk, hipStream_t s) {
   }
   WgradArgs a = a0;
   const long rows = (long)a.M * R;
-  long rpc = (rows + nchunk - 1) / nchunk;
-  rpc = (rpc + kWgradRch - 1) / kWgradRch * kWgradRch;
+  const long rpc = (rows + nchunk - 1) / nchunk;  // the last chunk may be short; rows past it are masked
   a.rows_per_chunk = (int)rpc;
   dim3 grid((unsigned)((gm.ks * a.cin + 127) / 128), (unsigned)((a.cout + 127) / 128), (unsigned)nchunk);
   hipLaunchKernelGGL(kern, grid, dim3(256), LDS, s, a);
@@ -640,37 +649,59 @@ int launch_conv_wgrad(int layer, int src, const WgradArgs& a, int nchunk, hipStr
 }
 
 // Sum partial blocks over chunks and write reference layout dW[o][c][k], db[o]. A workgroup owns
-// 256 output elements (64 float4 columns) x 4 chunk groups; each thread streams its group's chunks
-// with 16-B loads, the four group sums are added in a fixed order (deterministic). Layer 1 writes
-// G[o][k*cin+c] (the xhat0 contraction) and S[k][o] instead (see k_bn0_grads).
+// 32 float4 columns (128 outputs) x 8 chunk groups; each thread sums its group's chunks with every
+// load of a batch of 8 in flight (the chunk count is small, so this is one or two load rounds), and
+// the eight group sums are combined in a fixed order (deterministic). The bias (+ layer-1 edge)
+// sums use the same shape over the [chunk][nb][cout] bias partials. Layer 1 writes
+// G[o][k*cin+c] (the xhat0 contraction) and S[k][o] instead of dW1 (see k_bn0_grads).
+constexpr int kRedGroups = 8, kRedBatch = 8;
+
+__device__ __forceinline__ float4 sum_chunks(const float* __restrict__ base, size_t stride, int nchunk,
+                                             int grp) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int z0 = grp; z0 < nchunk; z0 += kRedGroups * kRedBatch) {
+    float4 v[kRedBatch];
+#pragma unroll
+    for (int i = 0; i < kRedBatch; ++i) {
+      const int z = z0 + kRedGroups * i;
+      v[i] = z < nchunk ? ld4(base + (size_t)z * stride) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < kRedBatch; ++i) {
+      acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w;
+    }
+  }
+  return acc;
+}
+
+__device__ __forceinline__ float4 combine_groups(float4 (*red)[32], int col) {
+  float4 r = red[0][col];
+#pragma unroll
+  for (int g = 1; g < kRedGroups; ++g) {
+    r.x += red[g][col].x; r.y += red[g][col].y; r.z += red[g][col].z; r.w += red[g][col].w;
+  }
+  return r;
+}
+
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ wpart,
                                                       const float* __restrict__ bpart, int nchunk,
                                                       int cout, int cin, int ks, int nb, float* dW,
                                                       float* db, float* G, float* S) {
-  __shared__ float4 red[4][64];
+  __shared__ float4 red[kRedGroups][32];
+  const int col = threadIdx.x & 31, grp = threadIdx.x >> 5;
   const long kcn = (long)ks * cin;
   const long nw = (long)cout * kcn;  // multiple of 4 (cin % 32 == 0)
-  const long nwblk = (nw + 255) / 256;
+  const long nwblk = (nw + 127) / 128;
   if ((long)blockIdx.x < nwblk) {
-    const int col = threadIdx.x & 63, grp = threadIdx.x >> 6;
-    const long e4 = (long)blockIdx.x * 256 + 4 * col;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (e4 < nw) {
-#pragma unroll 4
-      for (int z = grp; z < nchunk; z += 4) {
-        const float4 v = ld4(wpart + (size_t)z * nw + e4);
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-      }
-    }
-    red[grp][col] = acc;
+    const long e4 = (long)blockIdx.x * 128 + 4 * col;
+    red[grp][col] = e4 < nw ? sum_chunks(wpart + e4, (size_t)nw, nchunk, grp) : make_float4(0.f, 0.f, 0.f, 0.f);
     __syncthreads();
     if (grp == 0 && e4 < nw) {
-      const float4 a = red[0][col], b = red[1][col], c = red[2][col], d = red[3][col];
-      const float v[4] = {(a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y),
-                          (a.z + b.z) + (c.z + d.z), (a.w + b.w) + (c.w + d.w)};
+      const float4 r = combine_groups(red, col);
       if (G) {
-        st4(G + e4, make_float4(v[0], v[1], v[2], v[3]));
+        st4(G + e4, r);
       } else {
+        const float v[4] = {r.x, r.y, r.z, r.w};
         const long o = e4 / kcn, kc = e4 - o * kcn;
         const long k = kc / cin, c0 = kc - k * cin;
 #pragma unroll
@@ -679,42 +710,41 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
     }
     return;
   }
-  // bias (+ layer-1 edge) sums: 64 outputs x 4 chunk groups per workgroup, fixed combine order
-  {
-    __shared__ float rb[4][5][64];
-    const int col = threadIdx.x & 63, grp = threadIdx.x >> 6;
-    const int o = (int)((blockIdx.x - nwblk) * 64 + col);
-    float e[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    if (o < cout)
-      for (int z = grp; z < nchunk; z += 4)
-#pragma unroll
-        for (int j = 0; j < 5; ++j)
-          if (j < nb) e[j] += bpart[((size_t)z * nb + j) * cout + o];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) rb[grp][j][col] = e[j];
-    __syncthreads();
-    if (grp == 0 && o < cout) {
-#pragma unroll
-      for (int j = 0; j < 5; ++j) e[j] = (rb[0][j][col] + rb[1][j][col]) + (rb[2][j][col] + rb[3][j][col]);
-      db[o] = e[0];
-      if (S) {  // layer 1: tap k of row t reads input t+k-2; zero padding at t+k-2 < 0 or > 130
-        S[0 * cout + o] = e[0] - e[1] - e[2];
-        S[1 * cout + o] = e[0] - e[1];
-        S[2 * cout + o] = e[0] - e[4];
-        S[3 * cout + o] = e[0] - e[3] - e[4];
-      }
-    }
-  }
+  // bias (+ layer-1 edge) sums: bpart[z][j][o]; a workgroup owns 128 consecutive (j, o) entries
+  const long nbo = (long)nb * cout;  // multiple of 4
+  const long e4 = ((long)blockIdx.x - nwblk) * 128 + 4 * col;
+  red[grp][col] = e4 < nbo ? sum_chunks(bpart + e4, (size_t)nbo, nchunk, grp) : make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  if (grp == 0 && e4 < nbo) st4(G ? S + 4 * cout + e4 : db + e4, combine_groups(red, col));
+}
+
+// layer 1: the five bias-partial sums (db, and dz summed at t = 0, 1, R-2, R-1) -> db and S[k][o]:
+// tap k of conv row t reads input t+k-2, zero padding at t+k-2 < 0 or > 130
+__global__ void k_wgrad_edges(int cout, const float* e, float* db, float* S) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= cout) return;
+  const float e0 = e[o], e1 = e[cout + o], e2 = e[2 * cout + o], e3 = e[3 * cout + o], e4 = e[4 * cout + o];
+  db[o] = e0;
+  S[0 * cout + o] = e0 - e1 - e2;
+  S[1 * cout + o] = e0 - e1;
+  S[2 * cout + o] = e0 - e4;
+  S[3 * cout + o] = e0 - e3 - e4;
 }
 
 int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int nchunk, int cout,
                         int cin, float* dW, float* db, float* G_tmp, float* S_tmp, hipStream_t s) {
   const LayerGeom gm = layer_geom(layer);
-  const long nblk = ((long)cout * gm.ks * cin + 255) / 256 + (cout + 63) / 64;
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)nblk), dim3(256), 0, s, wpart,
-                     bpart, nchunk, cout, cin, gm.ks, layer == 1 ? 5 : 1, dW, db,
-                     layer == 1 ? G_tmp : nullptr, layer == 1 ? S_tmp : nullptr);
+  const int nb = layer == 1 ? 5 : 1;
+  const long nblk = ((long)cout * gm.ks * cin + 127) / 128 + ((long)nb * cout + 127) / 128;
+  // layer 1: the bias partial sums land in S_tmp[4*cout ..) and k_wgrad_edges finishes db and S
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)nblk), dim3(256), 0, s, wpart, bpart, nchunk, cout, cin,
+                     gm.ks, nb, dW, db, layer == 1 ? G_tmp : nullptr, layer == 1 ? S_tmp : nullptr);
   DCUE_LAUNCH_CHECK();
+  if (layer == 1) {
+    hipLaunchKernelGGL(k_wgrad_edges, dim3((cout + 127) / 128), dim3(128), 0, s, cout, S_tmp + 4 * cout, db,
+                       S_tmp);
+    DCUE_LAUNCH_CHECK();
+  }
   return DCUE_OK;
 }
 

@@ -10,9 +10,18 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-#define DCUE_HIP_CHECK(expr)                              \
-  do {                                                    \
-    if ((expr) != hipSuccess) return DCUE_ERR_HIP;        \
+namespace dcue {
+// records the failing HIP call for dcue_last_error() (timer.hip)
+void set_last_error(const char* expr, hipError_t e, const char* file, int line);
+}  // namespace dcue
+
+#define DCUE_HIP_CHECK(expr)                                      \
+  do {                                                            \
+    const hipError_t _dcue_e = (expr);                            \
+    if (_dcue_e != hipSuccess) {                                  \
+      dcue::set_last_error(#expr, _dcue_e, __FILE__, __LINE__);   \
+      return DCUE_ERR_HIP;                                        \
+    }                                                             \
   } while (0)
 #define DCUE_LAUNCH_CHECK() DCUE_HIP_CHECK(hipGetLastError())
 

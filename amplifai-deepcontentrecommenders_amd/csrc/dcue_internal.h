@@ -1,6 +1,8 @@
 // Internal launch interfaces shared by the libdcue_hip translation units.
 #pragma once
 
+#include <vector>
+
 #include "dcue_common.h"
 
 namespace dcue {
@@ -137,5 +139,35 @@ int launch_emb_log_init(const dcue_model* m, int cap, int step, hipStream_t s);
 int launch_emb_sync(const dcue_model* m, const int64_t* users, int n, hipStream_t s);
 int launch_emb_flush(const dcue_model* m, hipStream_t s);
 int launch_pack(const dcue_model* m, const int64_t* poff, hipStream_t s);
+
+// ----------------------------------------------------------------- live kernel timing (timer.hip)
+struct TimerScope {
+  int cls = -1;
+  hipStream_t s = nullptr;
+  hipEvent_t a = nullptr, b = nullptr;
+  bool capturing = false;
+  std::vector<hipGraphNode_t> preds;  // under capture: the stream's dependency set before the launch
+};
+// A timed launch seen under stream capture: the plan adds event-record nodes around `kernel`.
+struct CapturedTimer {
+  int cls;
+  std::vector<hipGraphNode_t> preds;
+  hipGraphNode_t kernel;
+};
+int timer_begin(TimerScope* sc, int cls, hipStream_t s);
+int timer_end(TimerScope* sc);
+hipEvent_t timer_event();
+void timer_release(hipEvent_t e);
+void timer_add_recorded(int cls, hipEvent_t a, hipEvent_t b);
+std::vector<CapturedTimer> timer_take_captured();
+
+// side streams (capi.hip): three per device, plus a ring of fork/join events
+struct SidePool {
+  hipStream_t st[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev[32] = {};
+  int next = 0;
+};
+SidePool* side_pool();
+int stream_wait(SidePool* p, hipStream_t to, hipStream_t from);
 
 }  // namespace dcue

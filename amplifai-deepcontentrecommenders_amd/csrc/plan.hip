@@ -1,0 +1,169 @@
+// Step plans (dcue_plan_*): one training step's sample + forward + backward bound once to its
+// buffers and issued by one host call.
+//
+// The reference's per-batch loop (nn/dcue.py:202-210) runs the same ~60 small kernels every step.
+// A plan binds model, batch, tracks and workspace at creation and replays the step either eagerly
+// (default: the kernels issued from C++ onto the caller's stream and the side streams, no Python
+// between them) or, with DCUE_PLAN_GRAPH, as a HIP graph captured once on a private stream.
+// Measured on MI355X / ROCm 7.2 the graph replay is the slower of the two: hipGraphLaunch costs
+// about as much host time as the individual launches and executes the captured side-stream
+// branches one after another on one queue, losing their overlap. Timed kernel classes
+// (dcue_timer_*) get event-record nodes added around their graph nodes, re-pointed at fresh events
+// on every replay.
+#include <vector>
+
+#include "dcue_internal.h"
+
+struct dcue_plan {
+  dcue_model model = {};
+  dcue_tracks tracks = {};
+  dcue_plan_config cfg = {};
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  dcue_batch batch = {};
+  struct TimerNodes {
+    int cls;
+    hipGraphNode_t a, b;
+  };
+  std::vector<TimerNodes> timers;
+  std::vector<hipEvent_t> placeholders;  // events the record nodes were built with
+};
+
+namespace {
+
+int capture(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
+            const dcue_plan_config* cfg, hipStream_t cs) {
+  int st = DCUE_OK;
+  if (cfg->flags & DCUE_PLAN_SAMPLE_INBATCH)
+    st = dcue_sample_inbatch(cfg->mt, b->n_rows, b->n_neg, const_cast<int32_t*>(b->neg_item), cs);
+  if (!st)
+    st = dcue_forward(m, b, t, ws, ws_bytes, 1, cfg->margin, nullptr, nullptr, nullptr, nullptr, cs);
+  if (!st) st = dcue_train_backward(m, b, t, ws, ws_bytes, nullptr, cfg->emb_grad_scale, cs);
+  return st;
+}
+
+}  // namespace
+
+extern "C" int dcue_plan_destroy(dcue_plan* p);
+
+extern "C" int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws,
+                                size_t ws_bytes, const dcue_plan_config* cfg, dcue_plan** plan_host) {
+  if (!m || !b || !t || !ws || !cfg || !plan_host) return DCUE_ERR_INVALID;
+  *plan_host = nullptr;
+  if (cfg->flags & ~(DCUE_PLAN_SAMPLE_INBATCH | DCUE_PLAN_GRAPH)) return DCUE_ERR_INVALID;
+  if ((cfg->flags & DCUE_PLAN_SAMPLE_INBATCH) &&
+      (!cfg->mt || b->layout != DCUE_LAYOUT_GATHER || !b->neg_item || b->n_neg <= 0))
+    return DCUE_ERR_INVALID;
+  if (!dcue::side_pool()) return DCUE_ERR_HIP;  // side streams exist before capture starts
+  if (!(cfg->flags & DCUE_PLAN_GRAPH)) {
+    // eager plan: validate once by issuing nothing but the checks the calls make themselves
+    dcue_plan* p = new dcue_plan;
+    p->model = *m;
+    p->batch = *b;
+    p->tracks = *t;
+    p->cfg = *cfg;
+    p->ws = ws;
+    p->ws_bytes = ws_bytes;
+    *plan_host = p;
+    return DCUE_OK;
+  }
+
+  hipStream_t cs = nullptr;
+  DCUE_HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  dcue::timer_take_captured();  // drop stale entries of an earlier failed capture
+  int st = DCUE_OK;
+  hipGraph_t graph = nullptr;
+  if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) {
+    st = DCUE_ERR_HIP;
+  } else {
+    st = capture(m, b, t, ws, ws_bytes, cfg, cs);
+    // end the capture whatever happened, so the stream is usable and nothing leaks
+    if (hipStreamEndCapture(cs, &graph) != hipSuccess && !st) st = DCUE_ERR_HIP;
+  }
+  std::vector<dcue::CapturedTimer> cap = dcue::timer_take_captured();
+  (void)hipStreamDestroy(cs);
+  if (st || !graph) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return st ? st : DCUE_ERR_HIP;
+  }
+
+  dcue_plan* p = new dcue_plan;
+  p->graph = graph;
+  p->batch = *b;
+  // timed kernels: a start record beside the kernel (same predecessors, ordered before it) and an
+  // end record after it; the events are placeholders, re-pointed at every launch
+  for (auto& c : cap) {
+    hipGraphNode_t na = nullptr, nb = nullptr;
+    hipEvent_t ea = dcue::timer_event(), eb = dcue::timer_event();
+    if (!ea || !eb ||
+        hipGraphAddEventRecordNode(&na, graph, c.preds.data(), c.preds.size(), ea) != hipSuccess ||
+        hipGraphAddDependencies(graph, &na, &c.kernel, 1) != hipSuccess ||
+        hipGraphAddEventRecordNode(&nb, graph, &c.kernel, 1, eb) != hipSuccess) {
+      dcue::set_last_error("plan timer nodes", hipErrorInvalidValue, __FILE__, __LINE__);
+      dcue::timer_release(ea);
+      dcue::timer_release(eb);
+      (void)hipGraphDestroy(graph);
+      delete p;
+      return DCUE_ERR_HIP;
+    }
+    p->timers.push_back(dcue_plan::TimerNodes{c.cls, na, nb});
+    p->placeholders.push_back(ea);
+    p->placeholders.push_back(eb);
+  }
+  const hipError_t ie = hipGraphInstantiate(&p->exec, graph, nullptr, nullptr, 0);
+  if (ie != hipSuccess) {
+    dcue::set_last_error("hipGraphInstantiate", ie, __FILE__, __LINE__);
+    p->exec = nullptr;
+    dcue_plan_destroy(p);
+    return DCUE_ERR_HIP;
+  }
+  *plan_host = p;
+  return DCUE_OK;
+}
+
+extern "C" int dcue_plan_launch(dcue_plan* p, const int64_t* users_src, const int32_t* item_track_src,
+                                void* stream) {
+  if (!p) return DCUE_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  const dcue_batch& b = p->batch;
+  if (users_src && users_src != b.users)
+    DCUE_HIP_CHECK(hipMemcpyAsync(const_cast<int64_t*>(b.users), users_src, sizeof(int64_t) * b.n_rows,
+                                  hipMemcpyDeviceToDevice, s));
+  if (item_track_src && item_track_src != b.item_track)
+    DCUE_HIP_CHECK(hipMemcpyAsync(const_cast<int32_t*>(b.item_track), item_track_src,
+                                  sizeof(int32_t) * b.n_items, hipMemcpyDeviceToDevice, s));
+  if (!p->exec) {  // eager replay
+    int st = DCUE_OK;
+    if (p->cfg.flags & DCUE_PLAN_SAMPLE_INBATCH)
+      st = dcue_sample_inbatch(p->cfg.mt, b.n_rows, b.n_neg, const_cast<int32_t*>(b.neg_item), s);
+    if (!st)
+      st = dcue_forward(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, 1, p->cfg.margin, nullptr, nullptr,
+                        nullptr, nullptr, s);
+    if (!st)
+      st = dcue_train_backward(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, nullptr,
+                               p->cfg.emb_grad_scale, s);
+    return st;
+  }
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> fresh;
+  for (auto& tn : p->timers) {
+    hipEvent_t a = dcue::timer_event(), e = dcue::timer_event();
+    if (!a || !e) return DCUE_ERR_HIP;
+    DCUE_HIP_CHECK(hipGraphExecEventRecordNodeSetEvent(p->exec, tn.a, a));
+    DCUE_HIP_CHECK(hipGraphExecEventRecordNodeSetEvent(p->exec, tn.b, e));
+    fresh.push_back({tn.cls, {a, e}});
+  }
+  DCUE_HIP_CHECK(hipGraphLaunch(p->exec, s));
+  for (auto& f : fresh) dcue::timer_add_recorded(f.first, f.second.first, f.second.second);
+  return DCUE_OK;
+}
+
+extern "C" int dcue_plan_destroy(dcue_plan* p) {
+  if (!p) return DCUE_OK;
+  if (p->exec) (void)hipGraphExecDestroy(p->exec);
+  if (p->graph) (void)hipGraphDestroy(p->graph);
+  for (hipEvent_t e : p->placeholders) dcue::timer_release(e);
+  delete p;
+  return DCUE_OK;
+}

@@ -1,0 +1,132 @@
+// Live kernel timing with HIP events (dcue_timer_*): the launch sites of the timed kernel classes
+// bracket the launch with an event pair on the stream the kernel runs on. Under stream capture the
+// launch's graph node and its predecessors are noted instead; the plan adds event-record nodes
+// around the kernel node and re-points them at fresh events on every launch (plan.hip), so each
+// replay is timed. Single host thread per process (the
+// library's usage model: one process per GPU).
+#include <stdio.h>
+
+#include <utility>
+#include <vector>
+
+#include "dcue_internal.h"
+
+namespace dcue {
+
+namespace {
+struct TimerState {
+  bool enabled[DCUE_N_TIMED] = {};
+  std::vector<hipEvent_t> pool;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> recorded[DCUE_N_TIMED];
+  std::vector<CapturedTimer> captured;
+};
+TimerState& ts() {
+  static TimerState s;
+  return s;
+}
+}  // namespace
+
+hipEvent_t timer_event() {
+  TimerState& t = ts();
+  if (!t.pool.empty()) {
+    hipEvent_t e = t.pool.back();
+    t.pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+void timer_add_recorded(int cls, hipEvent_t a, hipEvent_t b) { ts().recorded[cls].emplace_back(a, b); }
+
+int timer_begin(TimerScope* sc, int cls, hipStream_t s) {
+  sc->cls = cls;
+  sc->s = s;
+  sc->a = sc->b = nullptr;
+  sc->capturing = false;
+  sc->preds.clear();
+  if (cls < 0 || cls >= DCUE_N_TIMED || !ts().enabled[cls]) return DCUE_OK;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  const hipGraphNode_t* deps = nullptr;
+  size_t nd = 0;
+  DCUE_HIP_CHECK(hipStreamGetCaptureInfo_v2(s, &st, nullptr, nullptr, &deps, &nd));
+  if (st == hipStreamCaptureStatusActive) {  // the plan adds the record nodes after capture
+    sc->capturing = true;
+    sc->preds.assign(deps, deps + nd);
+    return DCUE_OK;
+  }
+  sc->a = timer_event();
+  sc->b = timer_event();
+  if (!sc->a || !sc->b) return DCUE_ERR_HIP;
+  DCUE_HIP_CHECK(hipEventRecord(sc->a, s));
+  return DCUE_OK;
+}
+
+int timer_end(TimerScope* sc) {
+  if (sc->capturing) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    const hipGraphNode_t* deps = nullptr;
+    size_t nd = 0;
+    DCUE_HIP_CHECK(hipStreamGetCaptureInfo_v2(sc->s, &st, nullptr, nullptr, &deps, &nd));
+    if (st == hipStreamCaptureStatusActive && nd == 1)
+      ts().captured.push_back(CapturedTimer{sc->cls, sc->preds, deps[0]});
+    return DCUE_OK;
+  }
+  if (!sc->a) return DCUE_OK;
+  DCUE_HIP_CHECK(hipEventRecord(sc->b, sc->s));
+  timer_add_recorded(sc->cls, sc->a, sc->b);
+  return DCUE_OK;
+}
+
+std::vector<CapturedTimer> timer_take_captured() {
+  std::vector<CapturedTimer> out;
+  out.swap(ts().captured);
+  return out;
+}
+
+void timer_release(hipEvent_t e) {
+  if (e) ts().pool.push_back(e);
+}
+
+namespace {
+char g_last_error[512] = "";
+}
+
+void set_last_error(const char* expr, hipError_t e, const char* file, int line) {
+  const char* base = file;
+  for (const char* q = file; *q; ++q)
+    if (*q == '/') base = q + 1;
+  snprintf(g_last_error, sizeof(g_last_error), "%s:%d: %s -> %s (%d)", base, line, expr,
+           hipGetErrorString(e), (int)e);
+}
+
+}  // namespace dcue
+
+extern "C" const char* dcue_last_error(void) { return dcue::g_last_error; }
+
+extern "C" int dcue_timer_enable(int32_t kernel, int32_t enable) {
+  if (kernel < 0 || kernel >= DCUE_N_TIMED) return DCUE_ERR_INVALID;
+  dcue::ts().enabled[kernel] = enable != 0;
+  return DCUE_OK;
+}
+
+extern "C" int dcue_timer_read(int32_t kernel, double* total_ms_host, int64_t* launches_host) {
+  if (kernel < 0 || kernel >= DCUE_N_TIMED || !total_ms_host || !launches_host) return DCUE_ERR_INVALID;
+  auto& rec = dcue::ts().recorded[kernel];
+  double total = 0.0;
+  int64_t n = 0;
+  for (auto& pr : rec) {
+    DCUE_HIP_CHECK(hipEventSynchronize(pr.second));
+    float ms = 0.f;
+    DCUE_HIP_CHECK(hipEventElapsedTime(&ms, pr.first, pr.second));
+    total += ms;
+    ++n;
+    dcue::timer_release(pr.first);
+    dcue::timer_release(pr.second);
+  }
+  rec.clear();
+  *total_ms_host = total;
+  *launches_host = n;
+  return DCUE_OK;
+}

@@ -63,6 +63,19 @@ class AdamArgs(ctypes.Structure):
 ADAM_DENSE = 1
 ADAM_EMBEDDING = 2
 
+PLAN_SAMPLE_INBATCH = 1
+PLAN_GRAPH = 2
+
+TIMED_CONV1_WGRAD = 0
+TIMED_CONV1_FWD = 1
+TIMED_EMB_FLUSH = 2
+TIMED_ADAM_EMBED = 3
+
+
+class PlanConfig(ctypes.Structure):
+    _fields_ = [("flags", ctypes.c_int32), ("margin", ctypes.c_float), ("emb_grad_scale", ctypes.c_float),
+                ("reserved", ctypes.c_int32), ("mt", ctypes.c_void_p)]
+
 
 MT_STATE_BYTES = 624 * 4 + 16
 MAX_LOG_CAP = 256
@@ -71,6 +84,7 @@ ABI_VERSION = 2
 _P = ctypes.c_void_p
 _SIGS = {
     "dcue_abi_version": ([], ctypes.c_int),
+    "dcue_last_error": ([], ctypes.c_char_p),
     "dcue_param_layout": ([ctypes.POINTER(Dims), _P], ctypes.c_int),
     "dcue_bn_layout": ([ctypes.POINTER(Dims), _P], ctypes.c_int),
     "dcue_wpack_floats": ([ctypes.POINTER(Dims), _P], ctypes.c_int),
@@ -99,6 +113,13 @@ _SIGS = {
     "dcue_emb_log_init": ([ctypes.POINTER(Model), ctypes.c_int32, ctypes.c_int32, _P], ctypes.c_int),
     "dcue_embedding_sync": ([ctypes.POINTER(Model), _P, ctypes.c_int32, _P], ctypes.c_int),
     "dcue_embedding_flush": ([ctypes.POINTER(Model), _P], ctypes.c_int),
+    "dcue_plan_create": ([ctypes.POINTER(Model), ctypes.POINTER(Batch), ctypes.POINTER(Tracks), _P, ctypes.c_size_t,
+                          ctypes.POINTER(PlanConfig), ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "dcue_plan_launch": ([_P, _P, _P, _P], ctypes.c_int),
+    "dcue_plan_destroy": ([_P], ctypes.c_int),
+    "dcue_timer_enable": ([ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
+    "dcue_timer_read": ([ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)],
+                        ctypes.c_int),
 }
 
 _lib = None
@@ -124,7 +145,10 @@ def lib():
 
 def check(status, what):
     if status != 0:
-        raise RuntimeError("%s failed: %s" % (what, STATUS.get(status, status)))
+        msg = "%s failed: %s" % (what, STATUS.get(status, status))
+        if status == 3:
+            msg += " [%s]" % lib().dcue_last_error().decode(errors="replace")
+        raise RuntimeError(msg)
 
 
 def ptr(t):
@@ -167,6 +191,17 @@ def workspace_outputs(dims, B, N, M):
     off = (ctypes.c_size_t * 4)()
     check(lib().dcue_workspace_outputs(ctypes.byref(dims), B, N, M, off), "dcue_workspace_outputs")
     return list(off)
+
+
+def timer_enable(kernel, enable=True):
+    check(lib().dcue_timer_enable(kernel, int(bool(enable))), "dcue_timer_enable")
+
+
+def timer_read(kernel):
+    """(total ms, launches) of the kernel class since the last read (waits for the events)."""
+    ms, n = ctypes.c_double(), ctypes.c_int64()
+    check(lib().dcue_timer_read(kernel, ctypes.byref(ms), ctypes.byref(n)), "dcue_timer_read")
+    return ms.value, n.value
 
 
 def emb_log_bytes(cap):

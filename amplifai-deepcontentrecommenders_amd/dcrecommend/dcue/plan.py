@@ -1,0 +1,96 @@
+"""Bound replay of the DCUE training step's sample + forward + backward (include/dcue.h dcue_plan_*).
+
+The reference trainer runs, per batch, `model(u, pos, neg)` -> `loss.backward()` (nn/dcue.py:202-208)
+after its in-batch sampler drew the negatives (nn/dcue.py:698-709). TrainPlan binds exactly that
+work -- the GPU MT19937 draw, dcue_forward(train) and dcue_train_backward -- to fixed batch buffers
+once and replays it with one host call per step: issued from C++ (default) or as a captured HIP
+graph (graph=True; slower on ROCm 7.2). The optimizer step (NativeAdam.step) and any
+gradient all-reduce stay outside, between replays.
+
+Build the optimizer (and with it any deferred user-table state) BEFORE the plan: the graph binds the
+buffers that exist at creation and refuses to run if the model or optimizer state was rebuilt.
+"""
+import ctypes
+
+import torch
+
+from dcrecommend import _native as nat
+
+
+class TrainPlan:
+
+    def __init__(self, net, tracks, n_rows, n_neg, mt_state=None, item_track=None, margin=0.2,
+                 emb_grad_scale=1.0, graph=False):
+        """tracks: HBM track table [n_tracks][131][128] (fp16/fp32). In-batch mode (mt_state given):
+        positives are items 0..B-1 of item_track, negatives drawn in-graph. Otherwise item_track holds
+        B*(1+N) items in catalogue order (datasets/dcuedataset.py:242-250)."""
+        fl = net._require_device()
+        dev = fl["P"].device
+        B, N = int(n_rows), int(n_neg)
+        self.inbatch = mt_state is not None
+        M = B if self.inbatch else B * (1 + N)
+        self.net, self.tracks = net, tracks
+        self.users = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.item_track = torch.zeros(M, dtype=torch.int32, device=dev)
+        if item_track is not None:
+            self.item_track.copy_(item_track)
+        self.neg_item = torch.zeros((B, N), dtype=torch.int32, device=dev) if self.inbatch else None
+        self.mt_state = mt_state
+        self.ws = net._workspace(B, N, M)
+        model = net._model_struct()  # creates the deferred optimizer state if it does not exist yet
+        opt = net._deferred_opt() if getattr(net, "_deferred_opt", None) is not None else None
+        self._bound = (fl, self.ws, fl["emb_grad"], opt._moments if opt is not None else None)
+        self._keep = (fl["emb_grad"], fl["emb_rows"])
+        batch = nat.Batch(B, N, M, nat.LAYOUT_GATHER if self.inbatch else nat.LAYOUT_CATALOGUE,
+                          self.users.data_ptr(), self.item_track.data_ptr(),
+                          self.neg_item.data_ptr() if self.inbatch else None)
+        tr = nat.Tracks(tracks.data_ptr(), tracks.shape[0], 0 if tracks.dtype == torch.float16 else 1, 0)
+        flags = (nat.PLAN_SAMPLE_INBATCH if self.inbatch else 0) | (nat.PLAN_GRAPH if graph else 0)
+        cfg = nat.PlanConfig(flags, float(margin),
+                             float(emb_grad_scale), 0, mt_state.data_ptr() if self.inbatch else None)
+        handle = ctypes.c_void_p()
+        nat.check(nat.lib().dcue_plan_create(ctypes.byref(model), ctypes.byref(batch), ctypes.byref(tr),
+                                             nat.ptr(self.ws), self.ws.numel(), ctypes.byref(cfg),
+                                             ctypes.byref(handle)), "dcue_plan_create")
+        self._handle = handle
+        self._lib = nat.lib()
+        # the replayed backward writes the flat gradient: expose the reference-shaped .grad views
+        named = dict(net.named_parameters())
+        for s, name in enumerate(nat.DENSE_NAMES):
+            p = named[name]
+            p.grad = fl["G"][fl["poff"][s]:fl["poff"][s] + p.numel()].view(p.shape)
+        net.user_embd.embeddings.weight.grad = None
+        net._grad_users = self.users
+
+    def _check_bound(self):
+        net = self.net
+        opt = net._deferred_opt() if getattr(net, "_deferred_opt", None) is not None else None
+        now = (net._flat, net._ws, net._flat["emb_grad"] if net._flat else None,
+               opt._moments if opt is not None else None)
+        if any(a is not b for a, b in zip(now, self._bound)):
+            raise RuntimeError("TrainPlan: the model's device buffers or the optimizer state were rebuilt "
+                               "after the plan was created; create a new plan")
+
+    def launch(self, users=None, item_track=None, stream=None):
+        """One training step's sample + forward + backward. users [B] int64 / item_track [M] int32
+        (device tensors, optional) are copied into the bound batch buffers first."""
+        if self._handle is None:
+            raise RuntimeError("TrainPlan was closed")
+        self._check_bound()
+        st = self._lib.dcue_plan_launch(self._handle, None if users is None else users.data_ptr(),
+                                        None if item_track is None else item_track.data_ptr(),
+                                        nat.stream_handle() if stream is None else stream)
+        if st != 0:
+            nat.check(st, "dcue_plan_launch")
+
+    def close(self):
+        if getattr(self, "_handle", None) is not None:
+            torch.cuda.synchronize()
+            self._lib.dcue_plan_destroy(self._handle)
+            self._handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -66,8 +66,10 @@ class NativeAdam(torch.optim.Optimizer):
     def _init_log(self, st):
         """Fresh deferred-Adam log: every row current at the present step count."""
         dev = st["m"].device
-        st["emb_step"] = torch.zeros(max(self.net.user_count, 1), dtype=torch.int32, device=dev)
-        st["emb_log"] = torch.zeros(nat.emb_log_bytes(self.flush_every), dtype=torch.uint8, device=dev)
+        # buffers are reused when present: plans (dcrecommend.dcue.plan) bind their addresses
+        if st.get("emb_step") is None:
+            st["emb_step"] = torch.zeros(max(self.net.user_count, 1), dtype=torch.int32, device=dev)
+            st["emb_log"] = torch.zeros(nat.emb_log_bytes(self.flush_every), dtype=torch.uint8, device=dev)
         st["cap"] = self.flush_every
         nat.check(nat.lib().dcue_emb_log_init(ctypes.byref(self.net._model_struct(st)), self.flush_every,
                                               self.step_count, nat.stream_handle()), "dcue_emb_log_init")
@@ -93,12 +95,17 @@ class NativeAdam(torch.optim.Optimizer):
         self.step_count += 1
         args = nat.AdamArgs(float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]),
                             float(g["weight_decay"]), self.step_count, 0)
-        model = self.net._model_struct(st)
-        if not model.emb_grad:
+        fl = self.net._flat
+        if fl["emb_grad"].numel() == 0:
             # no backward ran yet (e.g. a resumed optimizer): every row takes the zero-gradient step
             self.net._workspace(1, 0, 1)
-            model = self.net._model_struct(st)
-        nat.check(nat.lib().dcue_adam_step(ctypes.byref(model), ctypes.byref(args), nat.stream_handle()),
+        # the ctypes model struct is rebuilt only when a bound buffer changed (host cost per step)
+        key = (fl, fl["emb_grad"], st, self.net.user_embd.embeddings.weight.data_ptr())
+        cache = getattr(self, "_model_cache", None)
+        if cache is None or any(a is not b for a, b in zip(cache[0][:3], key[:3])) or cache[0][3] != key[3]:
+            cache = (key, self.net._model_struct(st))
+            self._model_cache = cache
+        nat.check(nat.lib().dcue_adam_step(ctypes.byref(cache[1]), ctypes.byref(args), nat.stream_handle()),
                   "dcue_adam_step")
         return loss
 

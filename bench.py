@@ -103,6 +103,7 @@ def main():
     from dcrecommend.dcue.dcue import DCUENet
     from dcrecommend.optim import NativeAdam
     from dcrecommend.optim.cyclic_scheduler import CyclicLRWithRestarts
+    from dcrecommend.dcue.plan import TrainPlan
 
     B, N = args.batch, args.neg
     # users are sharded across ranks (row u of rank r = global user u*world + r): each rank owns its
@@ -134,49 +135,39 @@ def main():
     items_b = pair_track[perm].to(torch.int32).contiguous()
     mt = torch.empty(nat.MT_STATE_BYTES, dtype=torch.uint8, device=dev)
     nat.check(nat.lib().dcue_mt_seed(nat.ptr(mt), 10 + rank, nat.stream_handle()), "mt_seed")
-    neg_item = torch.empty((B, N), dtype=torch.int32, device=dev)
     G = net._flat["G"]
-    adam_state = opt._adam_state()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    TIMED = nat.TIMED_CONV1_WGRAD  # the roofline kernel, timed live by HIP events in the library
 
     if args.mode == "catalogue":
         raise SystemExit("catalogue mode bench: use --mode inbatch (config 2); catalogue runs in tests")
 
-    def step(s, timed):
-        nat.check(nat.lib().dcue_sample_inbatch(nat.ptr(mt), B, N, nat.ptr(neg_item), nat.stream_handle()),
-                  "sample_inbatch")
-        net.native_forward(users_b[s], tracks, items_b[s], N, nat.LAYOUT_GATHER, neg_item, train=True,
-                           margin=0.2, copy_outputs=False)
-        net.native_backward(None, emb_grad_scale=1.0 / world)
+    # the step's sample + forward + backward replay as one HIP graph; Adam and the all-reduce between.
+    # The roofline kernel's timer is on before capture so the graph carries its event-record nodes.
+    nat.timer_enable(TIMED, True)
+    plan = TrainPlan(net, tracks, B, N, mt_state=mt, emb_grad_scale=1.0 / world)
+
+    def step(s):
+        plan.launch(users_b[s], items_b[s])
         if world > 1:
             dist.all_reduce(G)
             G.div_(world)
-        g = opt.param_groups[0]
-        opt.step_count += 1
-        model = net._model_struct(adam_state)
-        emb_args = nat.AdamArgs(float(g["lr"]), 0.9, 0.99, 1e-8, float(g["weight_decay"]), opt.step_count,
-                                nat.ADAM_EMBEDDING)
-        dense_args = nat.AdamArgs(float(g["lr"]), 0.9, 0.99, 1e-8, float(g["weight_decay"]), opt.step_count,
-                                  nat.ADAM_DENSE)
-        if timed is not None:
-            ev[timed][0].record()
-        nat.check(nat.lib().dcue_adam_step(ctypes_ref(model), ctypes_ref(emb_args), nat.stream_handle()), "adam")
-        if timed is not None:
-            ev[timed][1].record()
-        nat.check(nat.lib().dcue_adam_step(ctypes_ref(model), ctypes_ref(dense_args), nat.stream_handle()), "adam")
+        opt.step()
         sched.batch_step()
 
     for s in range(args.warmup):
-        step(s, None)
+        step(s)
     opt.flush()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    nat.timer_read(TIMED)  # drop the warm-up records
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(args.warmup + k, k)
+        step(args.warmup + k)
     opt.flush()  # deferred user-table steps still pending are part of the timed work
+    t_enq = time.perf_counter() - t0  # host time to enqueue the steps (diagnostic)
     torch.cuda.synchronize()
+    nat.timer_enable(TIMED, False)
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
@@ -186,19 +177,21 @@ def main():
         dt = float(t.item())
 
     rows = world * B * args.steps / dt
-    emb_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    E = args.user_embdim
-    # algorithmic bytes of one user-table Adam sweep: read p, m, v + write p, m, v for every row,
-    # the row's slot word, and the batch's compact gradient rows
-    emb_bytes = n_users_local * E * 4 * 6 + n_users_local * 4 + B * E * 4
-    achieved = emb_bytes / (emb_ms * 1e-3) / 1e9
+    wg_ms, wg_n = nat.timer_read(TIMED)
+    wg_ms = wg_ms / max(wg_n, 1)
+    # algorithmic FLOPs of one conv-1 weight-gradient launch: dW1[o][c][k] summed over every conv-1
+    # output row (item, position) of the batch's distinct items -- B items x 132 positions (131
+    # frames, kernel 4, padding 2) x 128 mel inputs x 4 taps x H outputs, 2 FLOP per product
+    wg_flops = 2.0 * args.hidden * 128 * 4 * (B * 132)
+    achieved = wg_flops / (wg_ms * 1e-3) / 1e12
     traffic = None
-    tf_path = os.path.join(ROOT, "profiles", "pmc_adam_embed.json")
+    tf_path = os.path.join(ROOT, "profiles", "pmc_conv1_wgrad.json")
     if os.path.exists(tf_path):
         try:
             traffic = json.load(open(tf_path)).get("hbm_bytes_per_launch")
         except (ValueError, OSError):
             traffic = None
+    E = args.user_embdim
 
     result = {
         "metric": "training triplets/sec (whole node) + AUC@val, DCUE d=128 at 1/2/4/8 MI355X",
@@ -208,6 +201,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
+        "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -221,9 +215,9 @@ def main():
                                   args.interactions, N),
                    "batch_per_gpu": B, "global_batch": B * world, "neg": N,
                    "parallelism": "dp%d (users sharded, dense grads all-reduced)" % world},
-        "roofline": {"kernel": "k_adam_embed (user-table Adam sweep)", "bound": "hbm",
-                     "achieved": achieved, "peak": 8000.0, "unit": "GB/s", "frac": achieved / 8000.0,
-                     "traffic": traffic, "avg_ms": emb_ms, "algorithmic_bytes": emb_bytes},
+        "roofline": {"kernel": "k_conv_wgrad layer 1 (f32 MFMA 16x16x4)", "bound": "mfma",
+                     "achieved": achieved, "peak": 157.3, "unit": "TFLOP/s", "frac": achieved / 157.3,
+                     "traffic": traffic, "avg_ms": wg_ms, "launches": wg_n, "algorithmic_flops": wg_flops},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, n_users_local)

@@ -129,6 +129,8 @@ typedef struct dcue_adam_args {
 
 /* ---------------------------------------------------------------------------------- layout */
 int dcue_abi_version(void);
+/* The HIP call behind the most recent DCUE_ERR_HIP (file:line, call, HIP error), "" if none. */
+const char* dcue_last_error(void);
 /* offsets[DCUE_N_DENSE_SEGMENTS+1] (floats) of each dense parameter in `params` */
 int dcue_param_layout(const dcue_dims* dims, int64_t* offsets_host);
 /* offsets[2*DCUE_N_BN+1]: running_mean(l), running_var(l) for l = 0..5 */
@@ -217,6 +219,44 @@ int dcue_sample_catalogue(dcue_mt_state* state, int32_t reseed, uint32_t seed,
                           const int64_t* split_items, int64_t n_split, const int64_t* user_indptr,
                           const int32_t* user_split_rank, const int64_t* users, int32_t n_samples,
                           int32_t N, int64_t* out, void* stream);
+
+/* -------------------------------------------------------------------------- step plans */
+/* A training-step plan: the step's kernels (optionally the in-batch negative draw, then the train
+ * forward and backward of dcue_forward/dcue_train_backward) bound once and issued by one host call
+ * per step. The model, batch, tracks and workspace buffers are bound at creation (their addresses
+ * must stay valid and unchanged); their CONTENTS are read at each launch, so the caller refreshes
+ * the batch buffers between launches (or passes sources to dcue_plan_launch, which copies them in
+ * stream order first). The optimizer step stays outside (its scalars change every step), as does
+ * any gradient all-reduce between the two. Replay is eager (issued from C++ onto the caller's
+ * stream + side streams) unless DCUE_PLAN_GRAPH asks for a captured HIP graph. */
+typedef struct dcue_plan dcue_plan;
+#define DCUE_PLAN_SAMPLE_INBATCH 1 /* step starts with dcue_sample_inbatch(mt, B, N, b->neg_item) */
+#define DCUE_PLAN_GRAPH 2          /* capture into a HIP graph and replay that */
+typedef struct dcue_plan_config {
+  int32_t flags;        /* DCUE_PLAN_* */
+  float margin;         /* hinge margin (nn/dcue.py:167-170) */
+  float emb_grad_scale; /* as dcue_train_backward */
+  int32_t reserved;
+  dcue_mt_state* mt;    /* sampler state (DCUE_PLAN_SAMPLE_INBATCH) */
+} dcue_plan_config;
+int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws,
+                     size_t ws_bytes, const dcue_plan_config* cfg, dcue_plan** plan_host);
+/* users_src / item_track_src (nullable): copied into the bound batch buffers before the replay. */
+int dcue_plan_launch(dcue_plan* plan, const int64_t* users_src, const int32_t* item_track_src,
+                     void* stream);
+int dcue_plan_destroy(dcue_plan* plan);
+
+/* ------------------------------------------------------------------- live kernel timing */
+/* While enabled, every launch of the kernel class (also inside plans created afterwards) is
+ * bracketed by HIP events on the stream it runs on; dcue_timer_read waits for the recorded pairs,
+ * returns their summed time and count, and resets. For bench rooflines. */
+#define DCUE_TIMED_CONV1_WGRAD 0 /* conv layer-1 weight gradient (the step's largest MFMA kernel) */
+#define DCUE_TIMED_CONV1_FWD 1   /* conv layer-1 forward */
+#define DCUE_TIMED_EMB_FLUSH 2   /* deferred user-table Adam: full-table flush */
+#define DCUE_TIMED_ADAM_EMBED 3  /* dense user-table Adam sweep */
+#define DCUE_N_TIMED 4
+int dcue_timer_enable(int32_t kernel, int32_t enable);
+int dcue_timer_read(int32_t kernel, double* total_ms_host, int64_t* launches_host);
 
 #ifdef __cplusplus
 }

@@ -15,7 +15,7 @@ HEADER = os.path.join(ROOT, "include", "dcue.h")
 
 def _declared():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^int\s+(dcue_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|const char\s*\*)\s*(dcue_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_library_exports_header_symbols():
