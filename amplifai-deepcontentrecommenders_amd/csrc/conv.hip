@@ -19,17 +19,40 @@
 
 namespace dcue {
 
-// Slab fill in two halves so a thread keeps several loads in flight: slab_load issues the raw
-// global reads of one float4 slot (after the item's track row is known), slab_finish applies the
-// fused elementwise op. The loads are the latency of these small kernels, not the math.
+// Slab fill: every thread owns one channel quad (256 % (KC/4) == 0), so the per-channel operands
+// of the fused elementwise op are loaded once; the raw global reads of a batch of slab slots are
+// issued branch-free (clamped addresses, masked afterwards) before any is used -- the loads are the
+// latency of these small kernels, not the math.
+struct ChanOps {        // per-channel constants of the fused op for one channel quad
+  float4 mu, sc, be;    // forward: (x - mu) * sc + be
+  float4 inv, sd, sdx;  // dgrad: BN_l backward (mu = mean_l, sc = a_l)
+};
+
+template <int SRC>
+__device__ __forceinline__ ChanOps chan_ops(const RowsArgs& a, int c) {
+  ChanOps k;
+  if constexpr (SRC != SRC_DZ) {
+    k.mu = ld4(a.in_mean + c);
+    k.sc = ld4(a.in_a + c);
+    k.be = a.in_beta ? ld4(a.in_beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  } else {
+    k.mu = ld4(a.mean_l + c);
+    k.sc = ld4(a.a_l + c);
+    k.inv = ld4(a.invstd_l + c);
+    k.sd = ld4(a.sD + c);
+    k.sdx = ld4(a.sDx + c);
+  }
+  return k;
+}
+
 struct Raw {
   float4 a, b;
   uint32_t id;
+  float cnt;
 };
 
 template <int SRC, int KC, int LIN, int LPL, int POOLL>
-__device__ __forceinline__ Raw slab_load(const RowsArgs& a, long i, int p, int c4, long trk) {
-  const int c = 4 * c4;
+__device__ __forceinline__ Raw slab_load(const RowsArgs& a, long i, int p, int c, long trk) {
   Raw r;
   if constexpr (SRC == SRC_TRACK_F16) {
     const uint2 raw = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.src) +
@@ -46,13 +69,13 @@ __device__ __forceinline__ Raw slab_load(const RowsArgs& a, long i, int p, int c
     r.a = ld4(reinterpret_cast<const float*>(a.src) + base);
     r.b = ld4(a.y_l + base);
     r.id = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
+    r.cnt = a.counts ? a.counts[i] : 1.f;
   }
   return r;
 }
 
 template <int SRC, int POOLL>
-__device__ __forceinline__ float4 slab_finish(const RowsArgs& a, long i, int p, int c4, const Raw& r) {
-  const int c = 4 * c4;
+__device__ __forceinline__ float4 slab_finish(const RowsArgs& a, const ChanOps& k, int p, const Raw& r) {
   if constexpr (SRC != SRC_DZ) {
     float x[4];
     if constexpr (SRC == SRC_TRACK_F16) {
@@ -63,22 +86,22 @@ __device__ __forceinline__ float4 slab_finish(const RowsArgs& a, long i, int p, 
     } else {
       x[0] = r.a.x; x[1] = r.a.y; x[2] = r.a.z; x[3] = r.a.w;
     }
-    const float4 mu = ld4(a.in_mean + c), sc = ld4(a.in_a + c);
-    const float4 be = a.in_beta ? ld4(a.in_beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    return make_float4((x[0] - mu.x) * sc.x + be.x, (x[1] - mu.y) * sc.y + be.y,
-                       (x[2] - mu.z) * sc.z + be.z, (x[3] - mu.w) * sc.w + be.w);
+    return make_float4((x[0] - k.mu.x) * k.sc.x + k.be.x, (x[1] - k.mu.y) * k.sc.y + k.be.y,
+                       (x[2] - k.mu.z) * k.sc.z + k.be.z, (x[3] - k.mu.w) * k.sc.w + k.be.w);
   } else {
     // conv position p of layer l -> pool window w, offset j; gradient reaches p only if it was the
     // window's argmax and the window's ReLU was active (threshold_backward on the ReLU output).
     const int j = p % POOLL;
-    const float kD = (a.counts ? a.counts[i] : 1.f) * a.invN;
+    const float kD = r.cnt * a.invN;
     const float gv[4] = {r.a.x, r.a.y, r.a.z, r.a.w}, yv[4] = {r.b.x, r.b.y, r.b.z, r.b.w};
+    const float mu[4] = {k.mu.x, k.mu.y, k.mu.z, k.mu.w}, iv[4] = {k.inv.x, k.inv.y, k.inv.z, k.inv.w};
+    const float av[4] = {k.sc.x, k.sc.y, k.sc.z, k.sc.w}, sd[4] = {k.sd.x, k.sd.y, k.sd.z, k.sd.w};
+    const float sdx[4] = {k.sdx.x, k.sdx.y, k.sdx.z, k.sdx.w};
     float o[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const int cc = c + s;
-      const float xh = (yv[s] - a.mean_l[cc]) * a.invstd_l[cc];
-      const float dx = a.a_l[cc] * (gv[s] - kD * a.sD[cc] - kD * xh * a.sDx[cc]);
+      const float xh = (yv[s] - mu[s]) * iv[s];
+      const float dx = av[s] * (gv[s] - kD * sd[s] - kD * xh * sdx[s]);
       const int arg = (r.id >> (8 * s)) & 0xff;
       o[s] = (arg == j && yv[s] > 0.f) ? dx : 0.f;
     }
@@ -91,7 +114,7 @@ __device__ __forceinline__ float4 slab_finish(const RowsArgs& a, long i, int p, 
 // slab position t + k - PADL.
 template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,
           int POOLL>
-__global__ __launch_bounds__(256) void k_conv_rows(RowsArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_conv_rows(RowsArgs a) {
   constexpr int RX = R + KS - 1;
   constexpr int ROWS = TW * 16;
   constexpr int MAXI = (ROWS + R - 1) / R + 1;
@@ -110,39 +133,41 @@ __global__ __launch_bounds__(256) void k_conv_rows(RowsArgs a) {
   (void)MAXI;
 
   {
+    static_assert(256 % C4 == 0, "a thread's slab slots share one channel quad");
     constexpr int FB = SRC == SRC_DZ ? 4 : 8;  // slab slots (float4) in flight per thread
     const int nfill = nslab * C4;
+    const int c = 4 * (threadIdx.x % C4);
+    const ChanOps kop = chan_ops<SRC>(a, c);
     for (int base = threadIdx.x; base < nfill; base += 256 * FB) {
-      long ii[FB], trk[FB];
+      long ii[FB];
       int pp[FB];
       bool ok[FB];
       Raw raw[FB];
 #pragma unroll
       for (int j = 0; j < FB; ++j) {
         const int e = base + 256 * j;
-        const int sr = e / C4;
-        const long E = elo + sr;
-        ii[j] = E / RX;
-        pp[j] = (int)(E - ii[j] * RX) - PADL;
-        ok[j] = e < nfill && ii[j] < M && pp[j] >= 0 && pp[j] < LIN;
-        trk[j] = 0;
+        const long E = elo + e / C4;
+        const long i = E / RX;
+        const int p = (int)(E - i * RX) - PADL;
+        ok[j] = e < nfill && i < M && p >= 0 && p < LIN;
+        ii[j] = ok[j] ? i : 0;  // masked slots load a real element and store zero
+        pp[j] = ok[j] ? p : 0;
       }
+      long trk[FB];
+#pragma unroll
+      for (int j = 0; j < FB; ++j) trk[j] = 0;
       if constexpr (SRC == SRC_TRACK_F16 || SRC == SRC_TRACK_F32) {
 #pragma unroll
-        for (int j = 0; j < FB; ++j)
-          if (ok[j]) trk[j] = a.item_track[ii[j]];
+        for (int j = 0; j < FB; ++j) trk[j] = a.item_track[ii[j]];
       }
 #pragma unroll
-      for (int j = 0; j < FB; ++j)
-        if (ok[j]) raw[j] = slab_load<SRC, KC, LIN, LPL, POOLL>(a, ii[j], pp[j], (base + 256 * j) % C4, trk[j]);
+      for (int j = 0; j < FB; ++j) raw[j] = slab_load<SRC, KC, LIN, LPL, POOLL>(a, ii[j], pp[j], c, trk[j]);
 #pragma unroll
       for (int j = 0; j < FB; ++j) {
         const int e = base + 256 * j;
         if (e < nfill) {
-          const int sr = e / C4, c4 = e - sr * C4;
-          const float4 v = ok[j] ? slab_finish<SRC, POOLL>(a, ii[j], pp[j], c4, raw[j])
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-          st4(&slab[sr * PITCH + 4 * c4], v);
+          const float4 v = slab_finish<SRC, POOLL>(a, kop, pp[j], raw[j]);
+          st4(&slab[(e / C4) * PITCH + c], ok[j] ? v : make_float4(0.f, 0.f, 0.f, 0.f));
         }
       }
     }
@@ -168,14 +193,18 @@ __global__ __launch_bounds__(256) void k_conv_rows(RowsArgs a) {
 #pragma unroll
   for (int r = 0; r < TW; ++r) acc[r][0] = acc[r][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // B operand (packed weights, L2-resident) streamed two k-steps ahead of the MFMAs
   const float* wp = a.wpack + ((size_t)g * nout + ocol0 + l16) * 4;
   const size_t wstep = (size_t)16 * nout;
   float4 b0 = ld4(wp), b1 = ld4(wp + 64);
+  float4 n0 = NSTEP > 1 ? ld4(wp + wstep) : b0, n1 = NSTEP > 1 ? ld4(wp + wstep + 64) : b1;
+  // fully unrolled: straight-line code lets the wait counters track the in-flight B loads exactly
+#pragma unroll
   for (int st = 0; st < NSTEP; ++st) {
-    float4 nb0 = b0, nb1 = b1;
-    if (st + 1 < NSTEP) {
-      nb0 = ld4(wp + (st + 1) * wstep);
-      nb1 = ld4(wp + (st + 1) * wstep + 64);
+    float4 f0 = n0, f1 = n1;
+    if (st + 2 < NSTEP) {
+      f0 = ld4(wp + (st + 2) * wstep);
+      f1 = ld4(wp + (st + 2) * wstep + 64);
     }
     const int k = st / (KC / 16);
     const int c0 = (st - k * (KC / 16)) * 16;
@@ -203,8 +232,10 @@ __global__ __launch_bounds__(256) void k_conv_rows(RowsArgs a) {
       acc[r][0] = mfma4(av[r].w, b0.w, acc[r][0]);
       acc[r][1] = mfma4(av[r].w, b1.w, acc[r][1]);
     }
-    b0 = nb0;
-    b1 = nb1;
+    b0 = n0;
+    b1 = n1;
+    n0 = f0;
+    n1 = f1;
   }
 
   if constexpr (MODE == 1) {
