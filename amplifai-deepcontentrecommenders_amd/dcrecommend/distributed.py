@@ -1,0 +1,50 @@
+"""Data-parallel layout of the DCUE step: one process per GPU, users sharded, dense grads all-reduced.
+
+SURVEY.md §8(e). The interaction set is sharded BY USER: global user u lives on rank u % W as local
+row u // W, so each rank owns its users' embedding rows and their Adam moments (the user table and
+its optimizer state never cross xGMI), and the per-rank user-table Adam work is 1/W. The track table
+is replicated. The one exchange per step is the all-reduce (sum, then / W) of the replicated dense
+gradient -- the flat buffer DCUENet keeps (393,276 fp32 at d=H=128) -- which together with
+emb_grad_scale = 1/W on the local rows reproduces DDP's mean-over-ranks gradient.
+"""
+import torch
+import torch.distributed as dist
+
+
+def local_user_count(n_users, rank, world):
+    """Rows of the user table rank `rank` owns: global users u with u % world == rank."""
+    return (n_users - rank + world - 1) // world if n_users > rank else 0
+
+
+def to_local_user(u, world):
+    return u // world
+
+
+def to_global_user(u_local, rank, world):
+    return u_local * world + rank
+
+
+def shard_interactions(user_idx, item_idx, rank, world):
+    """This rank's (local user, item) pairs of a global interaction list (tensors or arrays)."""
+    user_idx = torch.as_tensor(user_idx)
+    item_idx = torch.as_tensor(item_idx)
+    keep = (user_idx % world) == rank
+    return user_idx[keep] // world, item_idx[keep]
+
+
+def allreduce_mean_(grad, group=None):
+    """In-place mean of a replicated gradient over the ranks (RCCL on GPU, gloo in CPU tests)."""
+    world = dist.get_world_size(group)
+    if world > 1:
+        dist.all_reduce(grad, group=group)
+        grad.div_(world)
+    return grad
+
+
+def max_over_ranks(value, device, group=None):
+    """Max of a host scalar over the ranks (bench timing: the slowest rank defines the step)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())

@@ -100,6 +100,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from dcrecommend import _native as nat
+    from dcrecommend import distributed as D
     from dcrecommend.dcue.dcue import DCUENet
     from dcrecommend.optim import NativeAdam
     from dcrecommend.optim.cyclic_scheduler import CyclicLRWithRestarts
@@ -108,7 +109,7 @@ def main():
     B, N = args.batch, args.neg
     # users are sharded across ranks (row u of rank r = global user u*world + r): each rank owns its
     # users' embedding rows + Adam moments; the track table is replicated
-    n_users_local = (args.users + world - 1 - rank) // world
+    n_users_local = D.local_user_count(args.users, rank, world)
     tracks = synthetic_tracks(args.tracks, dev, seed=1234)
     gen = torch.Generator(device=dev).manual_seed(100 + rank)
     n_pairs = args.interactions // world
@@ -149,8 +150,7 @@ def main():
     def step(s):
         plan.launch(users_b[s], items_b[s])
         if world > 1:
-            dist.all_reduce(G)
-            G.div_(world)
+            D.allreduce_mean_(G)  # RCCL: the one exchange of the step (1.57 MB)
         opt.step()
         sched.batch_step()
 
@@ -171,10 +171,7 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = D.max_over_ranks(dt, dev)
 
     rows = world * B * args.steps / dt
     wg_ms, wg_n = nat.timer_read(TIMED)
