@@ -117,8 +117,10 @@ long wpack_offset(const dcue_dims* d, int l, bool bwd) {
 // pointers into the caller's workspace
 struct Ws {
   float* counts;
-  float *mean[6], *invstd[6], *a[6], *sD[6], *sDx[6];
-  float* partials;
+  float *mean[6], *invstd[6], *a[6];
+  // exact BN sums (bnacc.h), [6 layers][2 sums][Cmax][2 words]: forward stats, backward sums
+  unsigned long long *bnacc, *bnbacc;
+  int cmax;
   float* y[6];
   uint8_t* idx[6];
   float *f, *uf, *h1;
@@ -139,16 +141,10 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
     w->mean[l] = ar.take<float>(C);
     w->invstd[l] = ar.take<float>(C);
     w->a[l] = ar.take<float>(C);
-    w->sD[l] = ar.take<float>(C);
-    w->sDx[l] = ar.take<float>(C);
   }
-  long pmax = 1024L * 2 * kMels;
-  for (int l = 1; l <= 5; ++l) {
-    const long p = (long)conv_fwd_grid(l, l == 1 ? kMels : H, M) * 2 * (l == 5 ? D : H);
-    if (p > pmax) pmax = p;
-  }
-  if (512L * 2 * Cmax > pmax) pmax = 512L * 2 * Cmax;
-  w->partials = ar.take<float>(pmax);
+  w->cmax = Cmax > D ? Cmax : D;
+  w->bnacc = ar.take<unsigned long long>(2L * 6 * 2 * w->cmax * 2);
+  w->bnbacc = w->bnacc + 6L * 2 * w->cmax * 2;
   w->y[0] = nullptr;
   w->idx[0] = nullptr;
   for (int l = 1; l <= 5; ++l) {
@@ -187,6 +183,10 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   w->G = ar.take<float>((long)H * 4 * kMels);
   w->S = ar.take<float>(9L * H);  // S[4][H] + the five layer-1 bias partial sums
   return ar.used + 256;
+}
+
+inline unsigned long long* bn_acc(unsigned long long* base, int cmax, int l) {
+  return base + (size_t)l * 2 * cmax * 2;
 }
 
 struct Ctx {
@@ -229,15 +229,34 @@ int init_ctx(Ctx* c, const dcue_model* m) {
     if (_st) return _st;       \
   } while (0)
 
-// Item tower forward. train: batch statistics (weighted by counts) + running-stat update.
+// Item tower forward. train: batch statistics (weighted by counts, accumulated exactly by the
+// producing kernels) + running-stat update by each BN's first consumer; eval: running statistics.
 int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t* item_track, int M,
                  double copies, bool train, const float* counts, float* f_out, hipStream_t s) {
   const dcue_model* m = c.m;
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
-  int nparts = 0;
-  if (train) TRY(launch_input_stats(src, t->data, item_track, counts, M, w.partials, &nparts, s));
-  TRY(launch_bn_finalize(w.partials, nparts, kMels, copies * kFrames, c.P(seg_bn_w(0)), c.rmean(0),
-                         c.rvar(0), m->bn_batches + 0, train, w.mean[0], w.invstd[0], w.a[0], s));
+  // one BN's finalize/publish record for its first consumer (train) -- bnacc.h
+  auto bn_of = [&](int l) {
+    BnPublish p = {};
+    if (!train) return p;
+    p.acc = bn_acc(w.bnacc, w.cmax, l);
+    p.count = copies * (l == 0 ? kFrames : layer_geom(l).lp);
+    p.inv_count = 1.0 / p.count;
+    p.gamma = c.P(seg_bn_w(l));
+    p.beta = c.P(seg_bn_b(l));
+    p.mean = w.mean[l]; p.invstd = w.invstd[l]; p.a = w.a[l];
+    p.rmean = c.rmean(l); p.rvar = c.rvar(l); p.nbt = m->bn_batches + l;
+    p.C = bn_channels(&m->dims, l);
+    return p;
+  };
+  if (train) {
+    DCUE_HIP_CHECK(hipMemsetAsync(w.bnacc, 0, sizeof(unsigned long long) * 6 * 2 * w.cmax * 2, s));
+    TRY(launch_input_stats(src, t->data, item_track, counts, M, bn_acc(w.bnacc, w.cmax, 0), s));
+  } else {
+    for (int l = 0; l < 6; ++l)
+      TRY(launch_bn_eval(bn_channels(&m->dims, l), c.P(seg_bn_w(l)), c.rmean(l), c.rvar(l), w.mean[l],
+                         w.invstd[l], w.a[l], s));
+  }
   for (int l = 1; l <= 5; ++l) {
     RowsArgs a = {};
     a.src = l == 1 ? t->data : (const void*)w.y[l - 1];
@@ -245,28 +264,26 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     a.in_mean = w.mean[l - 1];
     a.in_a = w.a[l - 1];
     a.in_beta = c.P(seg_bn_b(l - 1));
+    a.in_bn = bn_of(l - 1);
     a.counts = counts;
     a.wpack = m->wpack + wpack_offset(&m->dims, l, false);
     a.bias = c.P(seg_conv_b(l));
     a.out = w.y[l];
     a.out_idx = w.idx[l];
-    a.partials = train ? w.partials : nullptr;
+    a.out_acc = train ? bn_acc(w.bnacc, w.cmax, l) : nullptr;
     a.M = M;
     a.nout = l == 5 ? c.D : c.H;
     TimerScope tsc;
     TRY(timer_begin(&tsc, l == 1 ? DCUE_TIMED_CONV1_FWD : -1, s));
     TRY(launch_conv_fwd(l, l == 1 ? kMels : c.H, l == 1 ? src : SRC_ACT, a, s));
     TRY(timer_end(&tsc));
-    const int C = a.nout;
-    TRY(launch_bn_finalize(w.partials, conv_fwd_grid(l, l == 1 ? kMels : c.H, M), C, copies * layer_geom(l).lp,
-                           c.P(seg_bn_w(l)), c.rmean(l), c.rvar(l), m->bn_batches + l, train,
-                           w.mean[l], w.invstd[l], w.a[l], s));
   }
   // fc on BN5(y5): f = bn5(y5) W^T + b   (truedcuemel1dbn.py:65,101)
   TGemmArgs g = {};
   g.M = M; g.N = c.D; g.K = c.D;
   g.A = w.y[5]; g.sam = c.D; g.sak = 1;
   g.amean = w.mean[5]; g.aa = w.a[5]; g.abeta = c.P(seg_bn_b(5));
+  g.abn = bn_of(5);
   g.B = c.P(SEG_FC_W); g.sbk = 1; g.sbn = c.D;
   g.bias = c.P(SEG_FC_B);
   g.C = f_out ? f_out : w.f; g.scm = c.D; g.scn = 1;
@@ -409,6 +426,7 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
   const double copies = (double)B * (1 + N);
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
 
+  DCUE_HIP_CHECK(hipMemsetAsync(w.bnbacc, 0, sizeof(unsigned long long) * 6 * 2 * w.cmax * 2, s));
   TRY(launch_score_bwd(w.uf, w.f, b, D, dscores ? dscores : w.dhinge, w.cosv, w.norms, w.du,
                        w.dfcopy, s));
   SidePool* sp = side_pool();
@@ -468,6 +486,8 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
     g.A = w.df; g.sam = D; g.sak = 1;
     g.B = c.P(SEG_FC_W); g.sbk = D; g.sbn = 1;
     g.C = w.g[5]; g.scm = D; g.scn = 1;
+    g.colacc = bn_acc(w.bnbacc, w.cmax, 5);  // BN5 backward sums of g5
+    g.xy = w.y[5]; g.xmean = w.mean[5]; g.xinvstd = w.invstd[5];
     TRY(launch_tgemm(0, 0, g, s));
   }
   // conv layers 5..1
@@ -475,11 +495,7 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
     const LayerGeom gm = layer_geom(l);
     const int C = l == 5 ? D : H;
     const int cin = l == 1 ? kMels : H;
-    int nparts = 0;
-    TRY(launch_bwd_partials(w.g[l], w.y[l], w.mean[l], w.invstd[l], (long)M * gm.lp, C, w.partials,
-                            &nparts, s));
-    TRY(launch_bwd_finalize(w.partials, nparts, C, w.sD[l], w.sDx[l], c.Gd(seg_bn_w(l)),
-                            c.Gd(seg_bn_b(l)), s));
+    unsigned long long* dzacc = bn_acc(w.bnbacc, w.cmax, l);  // complete: g_l's producer has run
     const float invN = (float)(1.0 / (copies * gm.lp));
     // weight gradient of layer l on a side stream (alternating, own partials); dgrad continues here
     hipStream_t so = sw[l & 1];
@@ -492,7 +508,8 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
     wa.x_beta = l == 1 ? nullptr : c.P(seg_bn_b(l - 1));
     wa.g_l = w.g[l]; wa.y_l = w.y[l]; wa.idx_l = w.idx[l];
     wa.mean_l = w.mean[l]; wa.invstd_l = w.invstd[l]; wa.a_l = w.a[l];
-    wa.sD = w.sD[l]; wa.sDx = w.sDx[l]; wa.invN = invN; wa.counts = w.counts;
+    wa.dz_acc = dzacc; wa.dgamma = c.Gd(seg_bn_w(l)); wa.dbeta = c.Gd(seg_bn_b(l));
+    wa.invN = invN; wa.counts = w.counts;
     wa.M = M; wa.cout = C; wa.cin = cin;
     wa.wpart = w.wpart[l & 1]; wa.bpart = w.bpart[l & 1];
     const int nch = wgrad_nchunk(l, M, C, cin);
@@ -509,9 +526,11 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
       RowsArgs ra = {};
       ra.src = w.g[l]; ra.y_l = w.y[l]; ra.idx_l = w.idx[l];
       ra.mean_l = w.mean[l]; ra.invstd_l = w.invstd[l]; ra.a_l = w.a[l];
-      ra.sD = w.sD[l]; ra.sDx = w.sDx[l]; ra.invN = invN; ra.counts = w.counts;
+      ra.dz_acc = dzacc; ra.invN = invN; ra.counts = w.counts;
       ra.wpack = m->wpack + wpack_offset(&m->dims, l, true);
       ra.out = w.g[l - 1];
+      ra.out_acc = bn_acc(w.bnbacc, w.cmax, l - 1);  // BN_{l-1} backward sums of g_{l-1}
+      ra.oy = w.y[l - 1]; ra.omean = w.mean[l - 1]; ra.oinvstd = w.invstd[l - 1];
       ra.M = M;
       ra.nout = H;
       TRY(launch_conv_dgrad(l, C, ra, s));

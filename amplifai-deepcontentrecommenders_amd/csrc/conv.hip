@@ -28,19 +28,53 @@ struct ChanOps {        // per-channel constants of the fused op for one channel
   float4 inv, sd, sdx;  // dgrad: BN_l backward (mu = mean_l, sc = a_l)
 };
 
+// BN_l backward sums of channel c from its accumulators: sum g (sD) and sum g*xhat (sDx)
+__device__ __forceinline__ float2 bwd_sums(const unsigned long long* acc, int C, int c) {
+  return make_float2((float)acc_sum(acc, C, 0, c), (float)acc_sum(acc, C, 1, c));
+}
+
+// Per-channel constants of the fused op, finalized once per channel per workgroup (thread t owns
+// channel t) into LDS, then read by quad: the fp64 finalize is one short chain per thread.
+struct ChanLds {
+  float v[5][256];
+};
+
 template <int SRC>
-__device__ __forceinline__ ChanOps chan_ops(const RowsArgs& a, int c) {
-  ChanOps k;
+__device__ __forceinline__ void chan_stage(const RowsArgs& a, int KC, ChanLds& L) {
+  const int t = threadIdx.x;
+  if (t >= KC) return;
   if constexpr (SRC != SRC_DZ) {
-    k.mu = ld4(a.in_mean + c);
-    k.sc = ld4(a.in_a + c);
-    k.be = a.in_beta ? ld4(a.in_beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.in_bn.acc) {  // train: the input BN's batch statistics, finalized here
+      const BnChan st = bn_chan_train(a.in_bn.acc, KC, t, a.in_bn.count, a.in_bn.inv_count);
+      L.v[0][t] = st.mean;
+      L.v[1][t] = a.in_bn.gamma[t] * st.invstd;
+    } else {
+      L.v[0][t] = a.in_mean[t];
+      L.v[1][t] = a.in_a[t];
+    }
+    L.v[2][t] = a.in_beta ? a.in_beta[t] : 0.f;
   } else {
-    k.mu = ld4(a.mean_l + c);
-    k.sc = ld4(a.a_l + c);
-    k.inv = ld4(a.invstd_l + c);
-    k.sd = ld4(a.sD + c);
-    k.sdx = ld4(a.sDx + c);
+    L.v[0][t] = a.mean_l[t];
+    L.v[1][t] = a.a_l[t];
+    L.v[2][t] = a.invstd_l[t];
+    const float2 sd = bwd_sums(a.dz_acc, KC, t);
+    L.v[3][t] = sd.x;
+    L.v[4][t] = sd.y;
+  }
+}
+
+template <int SRC>
+__device__ __forceinline__ ChanOps chan_ops(const ChanLds& L, int c) {
+  auto q = [&](int i) { return *reinterpret_cast<const float4*>(&L.v[i][c]); };
+  ChanOps k;
+  k.mu = q(0);
+  k.sc = q(1);
+  if constexpr (SRC != SRC_DZ) {
+    k.be = q(2);
+  } else {
+    k.inv = q(2);
+    k.sd = q(3);
+    k.sdx = q(4);
   }
   return k;
 }
@@ -137,7 +171,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     constexpr int FB = SRC == SRC_DZ ? 4 : 8;  // slab slots (float4) in flight per thread
     const int nfill = nslab * C4;
     const int c = 4 * (threadIdx.x % C4);
-    const ChanOps kop = chan_ops<SRC>(a, c);
+    __shared__ ChanLds chl;
+    chan_stage<SRC>(a, KC, chl);
+    if constexpr (SRC != SRC_DZ)
+      if (blockIdx.x == 0 && blockIdx.y == 0) bn_publish(a.in_bn, threadIdx.x);
+    __syncthreads();
+    const ChanOps kop = chan_ops<SRC>(chl, c);
     for (int base = threadIdx.x; base < nfill; base += 256 * FB) {
       long ii[FB];
       int pp[FB];
@@ -239,15 +278,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   }
 
   if constexpr (MODE == 1) {
+    // g_{l-1} rows, plus this tile's share of BN_{l-1}'s backward sums (sum g, sum g*xhat)
+    float sg[2] = {0.f, 0.f}, sgx[2] = {0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < TW; ++r) {
-      const long grb = gr0 + 16 * r + 4 * g;
+    for (int ct = 0; ct < 2; ++ct) {
+      const int o = ocol0 + 16 * ct + l16;
+      const float mu = a.out_acc ? a.omean[o] : 0.f, is = a.out_acc ? a.oinvstd[o] : 0.f;
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
-        const int o = ocol0 + 16 * ct + l16;
+      for (int r = 0; r < TW; ++r) {
+        const long grb = gr0 + 16 * r + 4 * g;
+        float yv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const long row = grb + j < total ? grb + j : gr0;
+          yv[j] = a.out_acc ? a.oy[row * nout + o] : 0.f;
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (grb + j < total) a.out[(grb + j) * nout + o] = acc[r][ct][j];
+          if (grb + j < total) {
+            const float gv = acc[r][ct][j];
+            a.out[(grb + j) * nout + o] = gv;
+            sg[ct] += gv;
+            sgx[ct] += gv * ((yv[j] - mu) * is);
+          }
+      }
+    }
+    if (a.out_acc) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        float s = sg[ct], q = sgx[ct];
+        s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+        q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+        if (g == 0) {
+          const int o = ocol0 + 16 * ct + l16;
+          acc128_add(acc_at(a.out_acc, nout, 0, o), s);
+          acc128_add(acc_at(a.out_acc, nout, 1, o), q);
+        }
       }
     }
   } else {
@@ -284,7 +350,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         }
       }
     }
-    if (a.partials) {
+    if (a.out_acc) {
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
         float s = ssum[ct], q = ssq[ct];
@@ -292,8 +358,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
         if (g == 0) {
           const int o = ocol0 + 16 * ct + l16;
-          a.partials[((long)blockIdx.x * 2 + 0) * nout + o] = s;
-          a.partials[((long)blockIdx.x * 2 + 1) * nout + o] = q;
+          acc128_add(acc_at(a.out_acc, nout, 0, o), s);
+          acc128_add(acc_at(a.out_acc, nout, 1, o), q);
         }
       }
     }
@@ -307,7 +373,7 @@ static int run_rows(const RowsArgs& a, hipStream_t s) {
   constexpr int MAXI = (ROWS + R - 1) / R + 1;
   constexpr int SLAB = ROWS + MAXI * (KS - 1);
   constexpr size_t LDS = (size_t)SLAB * (KC + 8) * sizeof(float);
-  static_assert(LDS <= 160 * 1024, "slab exceeds LDS");
+  static_assert(LDS + sizeof(ChanLds) <= 160 * 1024, "slab exceeds LDS");
   auto kern = k_conv_rows<MODE, SRC, KC, KS, PADL, LIN, R, POOL, TW, LPL, POOLL>;
   static bool attr = false;
   if (!attr) {
@@ -342,19 +408,13 @@ static int fwd_layer_tw(const RowsArgs& a, hipStream_t s) {
 constexpr size_t slab_bytes(int R, int KS, int KC, int TW) {
   return (size_t)(TW * 16 + ((TW * 16 + R - 1) / R + 1) * (KS - 1)) * (KC + 8) * sizeof(float);
 }
+constexpr size_t kSlabMax = 160 * 1024 - sizeof(ChanLds);
 constexpr int max_tw(int R, int KS, int KC) {
-  return slab_bytes(R, KS, KC, 8) <= 160 * 1024 ? 8
-       : slab_bytes(R, KS, KC, 4) <= 160 * 1024 ? 4
-       : slab_bytes(R, KS, KC, 2) <= 160 * 1024 ? 2 : 1;
+  return slab_bytes(R, KS, KC, 8) <= kSlabMax ? 8
+       : slab_bytes(R, KS, KC, 4) <= kSlabMax ? 4
+       : slab_bytes(R, KS, KC, 2) <= kSlabMax ? 2 : 1;
 }
 
-int conv_fwd_grid(int layer, int kc, int M) {
-  const LayerGeom gm = layer_geom(layer);
-  const long rows = (long)M * gm.lp * gm.pool;
-  const int tw = min(choose_tw(rows), max_tw(gm.lp * gm.pool, gm.ks, kc));
-  const long per = 16L * tw;
-  return (int)((rows + per - 1) / per);
-}
 
 template <int L, int KC, int SRC>
 static int fwd_layer(const RowsArgs& a, hipStream_t s) {
@@ -485,7 +545,22 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
   const int oc = o_ok ? o : 0, kcc = kc_ok ? kc : 0;
   const int kx = kcc / cin, cx = kcc - kx * cin;
   const float4 mean4 = ld4(a.mean_l + oc), inv4 = ld4(a.invstd_l + oc), a4 = ld4(a.a_l + oc);
-  const float4 sD4 = ld4(a.sD + oc), sDx4 = ld4(a.sDx + oc);
+  float4 sD4, sDx4;
+  {
+    float sd[4], sdx[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sd[s] = (float)acc_sum(a.dz_acc, cout, 0, oc + s);
+      sdx[s] = (float)acc_sum(a.dz_acc, cout, 1, oc + s);
+    }
+    sD4 = make_float4(sd[0], sd[1], sd[2], sd[3]);
+    sDx4 = make_float4(sdx[0], sdx[1], sdx[2], sdx[3]);
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && tid < cout) {
+    // BN_l = gamma * xhat + beta: dbeta = sum g, dgamma = sum g * xhat
+    a.dbeta[tid] = (float)acc_sum(a.dz_acc, cout, 0, tid);
+    a.dgamma[tid] = (float)acc_sum(a.dz_acc, cout, 1, tid);
+  }
   const float4 xmu = ld4(a.x_mean + cx), xsc = ld4(a.x_a + cx);
   const float4 xbe = a.x_beta ? ld4(a.x_beta + cx) : make_float4(0.f, 0.f, 0.f, 0.f);
 

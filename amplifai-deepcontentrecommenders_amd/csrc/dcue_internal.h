@@ -4,6 +4,7 @@
 #include <vector>
 
 #include "dcue_common.h"
+#include "bnacc.h"
 
 namespace dcue {
 
@@ -18,23 +19,28 @@ enum SlabSrc { SRC_TRACK_F16 = 0, SRC_TRACK_F32 = 1, SRC_ACT = 2, SRC_DZ = 3 };
 struct RowsArgs {
   const void* src;            // tracks [n_tracks][131][128] | y_{l-1} [M][Lin][KC] | g_l [M][Lp_l][KC]
   const int32_t* item_track;  // tracks only
-  const float* in_mean;       // forward BN apply: (x - mean) * a + beta
+  const float* in_mean;       // forward BN apply: (x - mean) * a + beta  (in_bn.acc == null)
   const float* in_a;
   const float* in_beta;
+  BnPublish in_bn;            // forward, train: input BN finalized from its accumulators; block 0
+                              // publishes it (mean/invstd/a buffers + running statistics)
   const float* y_l;           // dgrad: layer-l ReLU output (pre-BN) [M][Lp_l][KC]
   const uint8_t* idx_l;       // dgrad: layer-l max-pool argmax [M][Lp_l][KC]
   const float* mean_l;
   const float* invstd_l;
   const float* a_l;           // gamma_l * invstd_l
-  const float* sD;            // sum of g_l per channel
-  const float* sDx;           // sum of g_l * xhat_l per channel
+  const unsigned long long* dz_acc;  // dgrad: [sum g_l, sum g_l*xhat_l] accumulators of layer l
   float invN;                 // 1 / (copies * positions)
   const float* counts;        // [M] copies per item (nullable -> 1)
   const float* wpack;         // [KS][KC/4][nout][4]
   const float* bias;          // forward [nout]
   float* out;                 // forward y_l [M][Lp][nout]; dgrad g_{l-1} [M][R][nout]
   uint8_t* out_idx;           // forward argmax [M][Lp][nout]
-  float* partials;            // forward BN stats partials [grid.x][2][nout] (null: eval)
+  unsigned long long* out_acc;  // forward: BN_l stats of the output (null: eval); dgrad: the
+                                // BN_{l-1} backward sums of the produced gradient
+  const float* oy;            // dgrad: y_{l-1} [M][R][nout], mean/invstd of BN_{l-1} (xhat of out)
+  const float* omean;
+  const float* oinvstd;
   int M;
   int nout;
 };
@@ -51,8 +57,9 @@ struct WgradArgs {
   const float* mean_l;
   const float* invstd_l;
   const float* a_l;
-  const float* sD;
-  const float* sDx;
+  const unsigned long long* dz_acc;  // [sum g_l, sum g_l*xhat_l] accumulators of layer l
+  float* dgamma;              // block (0,0,0) publishes BN_l's gradients: sum g*xhat, sum g
+  float* dbeta;
   float invN;
   const float* counts;
   int M, cout, cin;
@@ -63,7 +70,6 @@ struct WgradArgs {
 
 int launch_conv_fwd(int layer, int kc, int src, const RowsArgs& a, hipStream_t s);
 int launch_conv_dgrad(int layer, int kc, const RowsArgs& a, hipStream_t s);
-int conv_fwd_grid(int layer, int kc, int M);  // grid.x of the forward launch (partials rows)
 int launch_conv_wgrad(int layer, int src, const WgradArgs& a, int nchunk, hipStream_t s);
 int wgrad_nchunk(int layer, int M, int cout, int cin);
 int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int nchunk, int cout,
@@ -73,15 +79,12 @@ int launch_bn0_grads(const float* G, const float* S, const float* W1, const floa
                      hipStream_t s);
 
 // ------------------------------------------------------------------------------- BatchNorm
+// bn0 statistics of the gathered spectrograms (count-weighted) into accumulators [2][128]
 int launch_input_stats(int src, const void* tracks, const int32_t* item_track, const float* counts,
-                       int M, float* partials, int* nparts, hipStream_t s);
-int launch_bn_finalize(const float* partials, int nparts, int C, double count, const float* gamma,
-                       float* rmean, float* rvar, int64_t* nbt, int train, float* mean,
-                       float* invstd, float* a, hipStream_t s);
-int launch_bwd_partials(const float* g, const float* y, const float* mean, const float* invstd,
-                        long rows, int C, float* partials, int* nparts, hipStream_t s);
-int launch_bwd_finalize(const float* partials, int nparts, int C, float* sD, float* sDx,
-                        float* dgamma, float* dbeta, hipStream_t s);
+                       int M, unsigned long long* acc, hipStream_t s);
+// eval mode: running statistics -> mean / invstd / gamma*invstd
+int launch_bn_eval(int C, const float* gamma, const float* rmean, const float* rvar, float* mean,
+                   float* invstd, float* a, hipStream_t s);
 
 // ------------------------------------------------------------------ packed weight layout
 // wpack = conv B operands (forward per layer, dgrad per layer >= 2). Dense weights are read in place.
@@ -116,11 +119,16 @@ struct TGemmArgs {
   const float* A; long sam, sak; const int64_t* arow;
   const float* B; long sbk, sbn; const int64_t* brow;
   const float *amean, *aa, *abeta;
+  BnPublish abn;  // TA == 2, train: the per-k BatchNorm comes from accumulators (block 0 publishes)
   const float *bmean, *ba, *bbeta;
   const float* bias;
   float* C; long scm, scn;
   const float* cmask; long smm, smn; const int64_t* cmrow;
   float* rowsum;  // nullable: sum_k TA(A(m,k)) per row m
+  // nullable: per-column BN-backward sums of C into accumulators [2][N]: sum C, sum C * xhat with
+  // xhat = (xy[m][n] - xmean[n]) * xinvstd[n]
+  unsigned long long* colacc;
+  const float *xy, *xmean, *xinvstd;
 };
 int launch_tgemm(int ta, int tb, const TGemmArgs& g, hipStream_t s);
 

@@ -105,7 +105,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       const int k = k0 + kk;
       float a = ra[j];
       if constexpr (TA == 1) a = a > 0.f ? a : 0.f;
-      if constexpr (TA == 2) a = (a - g.amean[min(k, g.K - 1)]) * g.aa[min(k, g.K - 1)] + g.abeta[min(k, g.K - 1)];
+      if constexpr (TA == 2) {
+        const int kc = min(k, g.K - 1);
+        if (g.abn.acc) {  // train: BatchNorm of A's columns finalized from its accumulators
+          const BnChan st = bn_chan_train(g.abn.acc, g.K, kc, g.abn.count, g.abn.inv_count);
+          a = (a - st.mean) * (g.abn.gamma[kc] * st.invstd) + g.abn.beta[kc];
+        } else {
+          a = (a - g.amean[kc]) * g.aa[kc] + g.abeta[kc];
+        }
+      }
       As[kk][mm] = k < g.K ? a : 0.f;
     }
 #pragma unroll
@@ -126,6 +134,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     }
     __syncthreads();
   }
+  if constexpr (TA == 2)
+    if (blockIdx.x == 0 && blockIdx.y == 0) bn_publish(g.abn, t);
   const int m = m0 + l16;
   const bool mok = m < g.M;
   if (g.rowsum && n0 == 0) {  // sum_k TA(A(m,k)) for the tile's rows: lanes with equal l16
@@ -133,6 +143,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     rsum += __shfl_xor(rsum, 32, 64);
     if (kq == 0 && mok) g.rowsum[m] = rsum;
   }
+  float cs = 0.f, csx = 0.f;
+  const float xmu = g.colacc && nok ? g.xmean[n] : 0.f, xis = g.colacc && nok ? g.xinvstd[n] : 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int mm = m0 + 4 * kq + j;
@@ -140,6 +152,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       float v = acc[j] + (g.bias ? g.bias[n] : 0.f);
       if (g.cmask && !(g.cmask[(g.cmrow ? g.cmrow[mm] : mm) * g.smm + (long)n * g.smn] > 0.f)) v = 0.f;
       g.C[(long)mm * g.scm + (long)n * g.scn] = v;
+      if (g.colacc) {
+        cs += v;
+        csx += v * ((g.xy[(long)mm * g.N + n] - xmu) * xis);
+      }
+    }
+  }
+  if (g.colacc) {  // this tile's share of the column sums (BN backward of C's channels)
+    cs += __shfl_xor(cs, 16, 64); cs += __shfl_xor(cs, 32, 64);
+    csx += __shfl_xor(csx, 16, 64); csx += __shfl_xor(csx, 32, 64);
+    if (kq == 0 && nok) {
+      acc128_add(acc_at(g.colacc, g.N, 0, n), cs);
+      acc128_add(acc_at(g.colacc, g.N, 1, n), csx);
     }
   }
 }
