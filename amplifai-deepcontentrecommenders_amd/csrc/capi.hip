@@ -120,6 +120,9 @@ struct Ws {
   float *mean[6], *invstd[6], *a[6];
   // exact BN sums (bnacc.h), [6 layers][2 sums][Cmax][2 words]: forward stats, backward sums
   unsigned long long *bnacc, *bnbacc;
+  unsigned int* ticket;  // score_fused's arrival counter; cleared with the accumulators
+  long nzero;            // words from bnacc through the ticket (one clear per step)
+  float* rowsum;         // [B] per-row hinge sums (score_fused)
   int cmax;
   float* y[6];
   uint8_t* idx[6];
@@ -143,8 +146,11 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
     w->a[l] = ar.take<float>(C);
   }
   w->cmax = Cmax > D ? Cmax : D;
-  w->bnacc = ar.take<unsigned long long>(2L * 6 * 2 * w->cmax * 2);
+  w->nzero = 2L * 6 * 2 * w->cmax * 2 + 2;
+  w->bnacc = ar.take<unsigned long long>(w->nzero);
   w->bnbacc = w->bnacc + 6L * 2 * w->cmax * 2;
+  w->ticket = reinterpret_cast<unsigned int*>(w->bnacc + 2L * 6 * 2 * w->cmax * 2);
+  w->rowsum = ar.take<float>(B);
   w->y[0] = nullptr;
   w->idx[0] = nullptr;
   for (int l = 1; l <= 5; ++l) {
@@ -181,7 +187,7 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
     w->bpart[i] = ar.take<float>(bp);
   }
   w->G = ar.take<float>((long)H * 4 * kMels);
-  w->S = ar.take<float>(9L * H);  // S[4][H] + the five layer-1 bias partial sums
+  w->S = ar.take<float>(5L * H);  // the five layer-1 bias partial sums E[5][H]
   return ar.used + 256;
 }
 
@@ -232,7 +238,8 @@ int init_ctx(Ctx* c, const dcue_model* m) {
 // Item tower forward. train: batch statistics (weighted by counts, accumulated exactly by the
 // producing kernels) + running-stat update by each BN's first consumer; eval: running statistics.
 int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t* item_track, int M,
-                 double copies, bool train, const float* counts, float* f_out, hipStream_t s) {
+                 double copies, bool train, const float* counts, float* f_out, hipStream_t s,
+                 bool acc_cleared = false) {
   const dcue_model* m = c.m;
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
   // one BN's finalize/publish record for its first consumer (train) -- bnacc.h
@@ -250,7 +257,8 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     return p;
   };
   if (train) {
-    DCUE_HIP_CHECK(hipMemsetAsync(w.bnacc, 0, sizeof(unsigned long long) * 6 * 2 * w.cmax * 2, s));
+    if (!acc_cleared)
+      DCUE_HIP_CHECK(hipMemsetAsync(w.bnacc, 0, sizeof(unsigned long long) * 6 * 2 * w.cmax * 2, s));
     TRY(launch_input_stats(src, t->data, item_track, counts, M, bn_acc(w.bnacc, w.cmax, 0), s));
   } else {
     for (int l = 0; l < 6; ++l)
@@ -381,14 +389,40 @@ int dcue_pack_weights(const dcue_model* m, void* stream) {
 int dcue_forward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws,
                  size_t ws_bytes, int32_t train, float margin, float* scores, float* user_feat,
                  float* item_feat, float* loss, void* stream) {
+  TRY(dcue::forward_impl(m, b, t, ws, ws_bytes, train, margin, StepOpts{}, (hipStream_t)stream));
+  // the outputs live in the workspace (dcue_workspace_outputs gives their offsets); copies are
+  // made only for callers that ask for their own buffers
+  Ws w;
+  carve(&m->dims, b->n_rows, b->n_neg, b->n_items, ws, &w);
+  hipStream_t s = (hipStream_t)stream;
+  const int B = b->n_rows, N = b->n_neg, M = b->n_items, D = m->dims.feature_dim;
+  if (scores && N > 0) DCUE_HIP_CHECK(hipMemcpyAsync(scores, w.scores, sizeof(float) * B * N, hipMemcpyDeviceToDevice, s));
+  if (user_feat) DCUE_HIP_CHECK(hipMemcpyAsync(user_feat, w.uf, sizeof(float) * B * D, hipMemcpyDeviceToDevice, s));
+  if (item_feat) DCUE_HIP_CHECK(hipMemcpyAsync(item_feat, w.f, sizeof(float) * (size_t)M * D, hipMemcpyDeviceToDevice, s));
+  if (loss) DCUE_HIP_CHECK(hipMemcpyAsync(loss, w.loss, sizeof(float), hipMemcpyDeviceToDevice, s));
+  return DCUE_OK;
+}
+
+int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws,
+                        size_t ws_bytes, const float* dscores, float emb_grad_scale, void* stream) {
+  return dcue::backward_impl(m, b, t, ws, ws_bytes, dscores, emb_grad_scale, StepOpts{},
+                             (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+namespace dcue {
+
+int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
+                 int train, float margin, const StepOpts& o, hipStream_t s) {
   Ctx c;
   TRY(init_ctx(&c, m));
   TRY(check_batch(b));
   if (!t || !t->data || !ws || !m->emb) return DCUE_ERR_INVALID;
+  if (o.fuse_score && !train) return DCUE_ERR_INVALID;
   Ws w;
   if (carve(&m->dims, b->n_rows, b->n_neg, b->n_items, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
   carve(&m->dims, b->n_rows, b->n_neg, b->n_items, ws, &w);
-  hipStream_t s = (hipStream_t)stream;
   const double copies = (double)b->n_rows * (1 + b->n_neg);
   SidePool* sp = side_pool();
   if (!sp) return DCUE_ERR_HIP;
@@ -396,23 +430,36 @@ int dcue_forward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   TRY(stream_wait(sp, su, s));  // user tower beside the item tower
   if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
   TRY(user_forward(c, w, b->users, b->n_rows, nullptr, su));
-  TRY(launch_item_counts(b, w.counts, s));
-  TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s));
+  if (!o.prologue_done) TRY(launch_item_counts(b, w.counts, s));
+  TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s,
+                   o.prologue_done));
   TRY(stream_wait(sp, s, su));
-  TRY(launch_score_fwd(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.hinge, w.loss,
-                       w.dhinge, s));
-  // the outputs live in the workspace (dcue_workspace_outputs gives their offsets); copies are
-  // made only for callers that ask for their own buffers
-  const int B = b->n_rows, N = b->n_neg, M = b->n_items;
-  if (scores && N > 0) DCUE_HIP_CHECK(hipMemcpyAsync(scores, w.scores, sizeof(float) * B * N, hipMemcpyDeviceToDevice, s));
-  if (user_feat) DCUE_HIP_CHECK(hipMemcpyAsync(user_feat, w.uf, sizeof(float) * B * c.D, hipMemcpyDeviceToDevice, s));
-  if (item_feat) DCUE_HIP_CHECK(hipMemcpyAsync(item_feat, w.f, sizeof(float) * (size_t)M * c.D, hipMemcpyDeviceToDevice, s));
-  if (loss) DCUE_HIP_CHECK(hipMemcpyAsync(loss, w.loss, sizeof(float), hipMemcpyDeviceToDevice, s));
-  return DCUE_OK;
+  if (o.fuse_score)
+    return launch_score_fused(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.rowsum, w.loss,
+                              w.du, w.dfcopy, w.ticket, s);
+  return launch_score_fwd(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.hinge, w.loss,
+                          w.dhinge, s);
 }
 
-int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws,
-                        size_t ws_bytes, const float* dscores, float emb_grad_scale, void* stream) {
+int step_prologue(const dcue_model* m, const dcue_batch* b, void* ws, size_t ws_bytes, dcue_mt_state* mt,
+                  const int64_t* users_src, const int32_t* items_src, hipStream_t s) {
+  Ws w;
+  if (carve(&m->dims, b->n_rows, b->n_neg, b->n_items, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
+  carve(&m->dims, b->n_rows, b->n_neg, b->n_items, ws, &w);
+  StepPrologue p = {};
+  p.mt = mt;
+  p.B = b->n_rows; p.N = b->n_neg; p.M = b->n_items;
+  p.gather = b->layout == DCUE_LAYOUT_GATHER;
+  p.neg = const_cast<int32_t*>(b->neg_item);
+  p.users_dst = const_cast<int64_t*>(b->users); p.users_src = users_src;
+  p.items_dst = const_cast<int32_t*>(b->item_track); p.items_src = items_src;
+  p.zero = w.bnacc; p.nzero = w.nzero;
+  p.counts = w.counts;
+  return launch_step_prologue(p, s);
+}
+
+int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
+                  const float* dscores, float emb_grad_scale, const StepOpts& o, hipStream_t s) {
   Ctx c;
   TRY(init_ctx(&c, m));
   TRY(check_batch(b));
@@ -420,15 +467,17 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
   Ws w;
   if (carve(&m->dims, b->n_rows, b->n_neg, b->n_items, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
   carve(&m->dims, b->n_rows, b->n_neg, b->n_items, ws, &w);
-  hipStream_t s = (hipStream_t)stream;
   const int B = b->n_rows, N = b->n_neg, M = b->n_items;
   const int H = c.H, D = c.D, E = c.E;
   const double copies = (double)B * (1 + N);
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
+  if (o.fuse_score && dscores) return DCUE_ERR_INVALID;
 
-  DCUE_HIP_CHECK(hipMemsetAsync(w.bnbacc, 0, sizeof(unsigned long long) * 6 * 2 * w.cmax * 2, s));
-  TRY(launch_score_bwd(w.uf, w.f, b, D, dscores ? dscores : w.dhinge, w.cosv, w.norms, w.du,
-                       w.dfcopy, s));
+  if (!o.prologue_done)
+    DCUE_HIP_CHECK(hipMemsetAsync(w.bnbacc, 0, sizeof(unsigned long long) * 6 * 2 * w.cmax * 2, s));
+  if (!o.fuse_score)  // else the fused score kernel already produced du / dfcopy
+    TRY(launch_score_bwd(w.uf, w.f, b, D, dscores ? dscores : w.dhinge, w.cosv, w.norms, w.du,
+                         w.dfcopy, s));
   SidePool* sp = side_pool();
   if (!sp) return DCUE_ERR_HIP;
   hipStream_t su = sp->st[0], sw[2] = {sp->st[1], sp->st[2]};
@@ -521,7 +570,8 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
                             c.Gd(seg_conv_b(l)), w.G, w.S, so));
     if (l == 1) {
       TRY(launch_bn0_grads(w.G, w.S, c.P(seg_conv_w(1)), c.P(seg_bn_w(0)), c.P(seg_bn_b(0)), H,
-                           c.Gd(seg_conv_w(1)), c.Gd(seg_bn_w(0)), c.Gd(seg_bn_b(0)), so));
+                           c.Gd(seg_conv_w(1)), c.Gd(seg_bn_w(0)), c.Gd(seg_bn_b(0)),
+                           c.Gd(seg_conv_b(1)), so));
     } else {
       RowsArgs ra = {};
       ra.src = w.g[l]; ra.y_l = w.y[l]; ra.idx_l = w.idx[l];
@@ -539,6 +589,10 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
   for (hipStream_t x : {su, sw[0], sw[1]}) TRY(stream_wait(sp, s, x));
   return DCUE_OK;
 }
+
+}  // namespace dcue
+
+extern "C" {
 
 int dcue_adam_step(const dcue_model* m, const dcue_adam_args* a, void* stream) {
   Ctx c;

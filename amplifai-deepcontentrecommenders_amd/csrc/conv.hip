@@ -759,7 +759,8 @@ int launch_conv_wgrad(int layer, int src, const WgradArgs& a, int nchunk, hipStr
 // load of a batch of 8 in flight (the chunk count is small, so this is one or two load rounds), and
 // the eight group sums are combined in a fixed order (deterministic). The bias (+ layer-1 edge)
 // sums use the same shape over the [chunk][nb][cout] bias partials. Layer 1 writes
-// G[o][k*cin+c] (the xhat0 contraction) and S[k][o] instead of dW1 (see k_bn0_grads).
+// G[o][k*cin+c] (the xhat0 contraction) and the five bias sums E[5][o] instead of dW1 and db1
+// (k_bn0_grads finishes them).
 constexpr int kRedGroups = 8, kRedBatch = 8;
 
 __device__ __forceinline__ float4 sum_chunks(const float* __restrict__ base, size_t stride, int nchunk,
@@ -821,46 +822,31 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
   const long e4 = ((long)blockIdx.x - nwblk) * 128 + 4 * col;
   red[grp][col] = e4 < nbo ? sum_chunks(bpart + e4, (size_t)nbo, nchunk, grp) : make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
-  if (grp == 0 && e4 < nbo) st4(G ? S + 4 * cout + e4 : db + e4, combine_groups(red, col));
-}
-
-// layer 1: the five bias-partial sums (db, and dz summed at t = 0, 1, R-2, R-1) -> db and S[k][o]:
-// tap k of conv row t reads input t+k-2, zero padding at t+k-2 < 0 or > 130
-__global__ void k_wgrad_edges(int cout, const float* e, float* db, float* S) {
-  const int o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= cout) return;
-  const float e0 = e[o], e1 = e[cout + o], e2 = e[2 * cout + o], e3 = e[3 * cout + o], e4 = e[4 * cout + o];
-  db[o] = e0;
-  S[0 * cout + o] = e0 - e1 - e2;
-  S[1 * cout + o] = e0 - e1;
-  S[2 * cout + o] = e0 - e4;
-  S[3 * cout + o] = e0 - e3 - e4;
+  if (grp == 0 && e4 < nbo) st4(G ? S + e4 : db + e4, combine_groups(red, col));
 }
 
 int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int nchunk, int cout,
-                        int cin, float* dW, float* db, float* G_tmp, float* S_tmp, hipStream_t s) {
+                        int cin, float* dW, float* db, float* G_tmp, float* E_tmp, hipStream_t s) {
   const LayerGeom gm = layer_geom(layer);
   const int nb = layer == 1 ? 5 : 1;
   const long nblk = ((long)cout * gm.ks * cin + 127) / 128 + ((long)nb * cout + 127) / 128;
-  // layer 1: the bias partial sums land in S_tmp[4*cout ..) and k_wgrad_edges finishes db and S
+  // layer 1: the five bias partial sums land in E_tmp[5][cout]; k_bn0_grads derives db1 and S
   hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)nblk), dim3(256), 0, s, wpart, bpart, nchunk, cout, cin,
-                     gm.ks, nb, dW, db, layer == 1 ? G_tmp : nullptr, layer == 1 ? S_tmp : nullptr);
+                     gm.ks, nb, dW, db, layer == 1 ? G_tmp : nullptr, layer == 1 ? E_tmp : nullptr);
   DCUE_LAUNCH_CHECK();
-  if (layer == 1) {
-    hipLaunchKernelGGL(k_wgrad_edges, dim3((cout + 127) / 128), dim3(128), 0, s, cout, S_tmp + 4 * cout, db,
-                       S_tmp);
-    DCUE_LAUNCH_CHECK();
-  }
   return DCUE_OK;
 }
 
 // bn0 gradients without conv1's input gradient: with xhat0 the normalised input and
 // G[o][k*128+c] = sum dz1 * xhat0_pad, S[k][o] = sum of dz1 over rows whose tap-k input is real,
 //   dW1[o][c][k] = gamma0[c] G + beta0[c] S,   dgamma0[c] = sum_{o,k} W1 G,   dbeta0[c] = sum_{o,k} W1 S.
-__global__ __launch_bounds__(256) void k_bn0_grads(const float* __restrict__ G, const float* __restrict__ S,
+__global__ __launch_bounds__(256) void k_bn0_grads(const float* __restrict__ G, const float* __restrict__ E,
                                                    const float* __restrict__ W1, const float* gamma0,
                                                    const float* beta0, int H, float* dW1,
-                                                   float* dgamma0, float* dbeta0) {
+                                                   float* dgamma0, float* dbeta0, float* db1) {
+  // E = the five layer-1 bias-partial sums [5][H]: sum dz1 and its parts at t = 0, 1, R-2, R-1.
+  // Tap k of conv row t reads input t+k-2 (zero padding at t+k-2 < 0 or > 130), so
+  //   S[0] = e0-e1-e2, S[1] = e0-e1, S[2] = e0-e4, S[3] = e0-e3-e4;  db1 = e0.
   __shared__ float rg[256], rb[256];
   const int c = blockIdx.x, t = threadIdx.x;
   const float ga = gamma0[c], be = beta0[c];
@@ -868,12 +854,15 @@ __global__ __launch_bounds__(256) void k_bn0_grads(const float* __restrict__ G, 
   for (int e = t; e < 4 * H; e += blockDim.x) {  // e = o*4 + k: dW1[o][c][k] layout
     const int o = e >> 2, k = e & 3;
     const float gv = G[(size_t)o * 4 * kMels + k * kMels + c];
-    const float sv = S[k * H + o];
+    const float e0 = E[o], e1 = E[H + o], e2 = E[2 * H + o], e3 = E[3 * H + o], e4 = E[4 * H + o];
+    const float sv = k == 0 ? e0 - e1 - e2 : k == 1 ? e0 - e1 : k == 2 ? e0 - e4 : e0 - e3 - e4;
     const float w = W1[((size_t)o * kMels + c) * 4 + k];
     dg += w * gv;
     db += w * sv;
     dW1[((size_t)o * kMels + c) * 4 + k] = ga * gv + be * sv;
   }
+  if (c == 0)
+    for (int o = t; o < H; o += blockDim.x) db1[o] = E[o];
   rg[t] = dg;
   rb[t] = db;
   __syncthreads();
@@ -890,11 +879,11 @@ __global__ __launch_bounds__(256) void k_bn0_grads(const float* __restrict__ G, 
   }
 }
 
-int launch_bn0_grads(const float* G, const float* S, const float* W1, const float* gamma0,
-                     const float* beta0, int H, float* dW1, float* dgamma0, float* dbeta0,
+int launch_bn0_grads(const float* G, const float* E, const float* W1, const float* gamma0,
+                     const float* beta0, int H, float* dW1, float* dgamma0, float* dbeta0, float* db1,
                      hipStream_t s) {
-  hipLaunchKernelGGL(k_bn0_grads, dim3(kMels), dim3(256), 0, s, G, S, W1, gamma0, beta0, H, dW1, dgamma0,
-                     dbeta0);
+  hipLaunchKernelGGL(k_bn0_grads, dim3(kMels), dim3(256), 0, s, G, E, W1, gamma0, beta0, H, dW1, dgamma0,
+                     dbeta0, db1);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }

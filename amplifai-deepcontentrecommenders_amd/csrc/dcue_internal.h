@@ -73,9 +73,9 @@ int launch_conv_dgrad(int layer, int kc, const RowsArgs& a, hipStream_t s);
 int launch_conv_wgrad(int layer, int src, const WgradArgs& a, int nchunk, hipStream_t s);
 int wgrad_nchunk(int layer, int M, int cout, int cin);
 int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int nchunk, int cout,
-                        int cin, float* dW, float* db, float* G_tmp, float* S_tmp, hipStream_t s);
-int launch_bn0_grads(const float* G, const float* S, const float* W1, const float* gamma0,
-                     const float* beta0, int H, float* dW1, float* dgamma0, float* dbeta0,
+                        int cin, float* dW, float* db, float* G_tmp, float* E_tmp, hipStream_t s);
+int launch_bn0_grads(const float* G, const float* E, const float* W1, const float* gamma0,
+                     const float* beta0, int H, float* dW1, float* dgamma0, float* dbeta0, float* db1,
                      hipStream_t s);
 
 // ------------------------------------------------------------------------------- BatchNorm
@@ -112,6 +112,22 @@ inline WpackLayout wpack_layout(const dcue_dims* dm) {
 // copies per item (BatchNorm weights); in-batch negatives are found by wave ballots over neg_item
 int launch_item_counts(const dcue_batch* b, float* counts, hipStream_t s);
 
+// step prologue of a plan (sampler.hip): batch copies, accumulator clear, in-batch draw, counts
+struct StepPrologue {
+  dcue_mt_state* mt;  // null: no draw (neg already given, or catalogue)
+  int B, N, M;
+  int gather;         // layout GATHER: counts from neg (else every item counts 1)
+  int32_t* neg;
+  int64_t* users_dst;
+  const int64_t* users_src;  // nullable
+  int32_t* items_dst;
+  const int32_t* items_src;  // nullable
+  unsigned long long* zero;  // words to clear
+  long nzero;
+  float* counts;             // [M] (nullable)
+};
+int launch_step_prologue(const StepPrologue& p, hipStream_t s);
+
 // small GEMM: C(m,n) = sum_k TA(A(m,k)) TB(B(k,n)) (+bias[n]) (*[cmask > 0]); TA: 0 none, 1 relu,
 // 2 affine per k; TB: 0 none, 1 relu, 2 affine per n (affine = BatchNorm apply (x-mean)*a+beta)
 struct TGemmArgs {
@@ -135,6 +151,11 @@ int launch_tgemm(int ta, int tb, const TGemmArgs& g, hipStream_t s);
 int launch_score_fwd(const float* uf, const float* f, const dcue_batch* b, int d, float margin,
                      float* scores, float* cosv, float* norms, float* hinge, float* loss,
                      float* dhinge, hipStream_t s);
+// forward + hinge backward in one pass (the loss gradient is known in the forward): also writes
+// du / dfcopy; the loss mean is taken by the last row block to finish (ticket, cleared by the caller)
+int launch_score_fused(const float* uf, const float* f, const dcue_batch* b, int d, float margin,
+                       float* scores, float* cosv, float* norms, float* rowsum, float* loss,
+                       float* du, float* dfcopy, unsigned int* ticket, hipStream_t s);
 int launch_score_bwd(const float* uf, const float* f, const dcue_batch* b, int d,
                      const float* dscores, const float* cosv, const float* norms, float* du,
                      float* dfcopy, hipStream_t s);
@@ -177,5 +198,17 @@ struct SidePool {
 };
 SidePool* side_pool();
 int stream_wait(SidePool* p, hipStream_t to, hipStream_t from);
+
+// ------------------------------------------------------------- step implementation (capi.hip)
+struct StepOpts {
+  bool prologue_done = false;  // counts written + accumulators (and ticket) cleared by the prologue
+  bool fuse_score = false;     // train forward also runs the hinge backward (k_score_fused)
+};
+int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
+                 int train, float margin, const StepOpts& o, hipStream_t s);
+int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
+                  const float* dscores, float emb_grad_scale, const StepOpts& o, hipStream_t s);
+int step_prologue(const dcue_model* m, const dcue_batch* b, void* ws, size_t ws_bytes, dcue_mt_state* mt,
+                  const int64_t* users_src, const int32_t* items_src, hipStream_t s);
 
 }  // namespace dcue

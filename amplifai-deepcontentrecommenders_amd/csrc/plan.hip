@@ -33,15 +33,26 @@ struct dcue_plan {
 
 namespace {
 
+// The step as the plan issues it: one prologue block (batch copies, accumulator clear, in-batch
+// draw, copy counts), the train forward with the hinge backward fused into its score kernel, and
+// the rest of the backward.
+int issue_step(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
+               const dcue_plan_config* cfg, const int64_t* users_src, const int32_t* items_src,
+               hipStream_t s) {
+  dcue::StepOpts o;
+  o.prologue_done = true;
+  o.fuse_score = true;
+  int st = dcue::step_prologue(m, b, ws, ws_bytes,
+                               (cfg->flags & DCUE_PLAN_SAMPLE_INBATCH) ? cfg->mt : nullptr, users_src,
+                               items_src, s);
+  if (!st) st = dcue::forward_impl(m, b, t, ws, ws_bytes, 1, cfg->margin, o, s);
+  if (!st) st = dcue::backward_impl(m, b, t, ws, ws_bytes, nullptr, cfg->emb_grad_scale, o, s);
+  return st;
+}
+
 int capture(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
             const dcue_plan_config* cfg, hipStream_t cs) {
-  int st = DCUE_OK;
-  if (cfg->flags & DCUE_PLAN_SAMPLE_INBATCH)
-    st = dcue_sample_inbatch(cfg->mt, b->n_rows, b->n_neg, const_cast<int32_t*>(b->neg_item), cs);
-  if (!st)
-    st = dcue_forward(m, b, t, ws, ws_bytes, 1, cfg->margin, nullptr, nullptr, nullptr, nullptr, cs);
-  if (!st) st = dcue_train_backward(m, b, t, ws, ws_bytes, nullptr, cfg->emb_grad_scale, cs);
-  return st;
+  return issue_step(m, b, t, ws, ws_bytes, cfg, nullptr, nullptr, cs);
 }
 
 }  // namespace
@@ -128,24 +139,16 @@ extern "C" int dcue_plan_launch(dcue_plan* p, const int64_t* users_src, const in
   if (!p) return DCUE_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   const dcue_batch& b = p->batch;
-  if (users_src && users_src != b.users)
+  if (users_src == b.users) users_src = nullptr;
+  if (item_track_src == b.item_track) item_track_src = nullptr;
+  if (!p->exec)  // eager replay: the batch copies ride in the prologue block
+    return issue_step(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, &p->cfg, users_src, item_track_src, s);
+  if (users_src)
     DCUE_HIP_CHECK(hipMemcpyAsync(const_cast<int64_t*>(b.users), users_src, sizeof(int64_t) * b.n_rows,
                                   hipMemcpyDeviceToDevice, s));
-  if (item_track_src && item_track_src != b.item_track)
+  if (item_track_src)
     DCUE_HIP_CHECK(hipMemcpyAsync(const_cast<int32_t*>(b.item_track), item_track_src,
                                   sizeof(int32_t) * b.n_items, hipMemcpyDeviceToDevice, s));
-  if (!p->exec) {  // eager replay
-    int st = DCUE_OK;
-    if (p->cfg.flags & DCUE_PLAN_SAMPLE_INBATCH)
-      st = dcue_sample_inbatch(p->cfg.mt, b.n_rows, b.n_neg, const_cast<int32_t*>(b.neg_item), s);
-    if (!st)
-      st = dcue_forward(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, 1, p->cfg.margin, nullptr, nullptr,
-                        nullptr, nullptr, s);
-    if (!st)
-      st = dcue_train_backward(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, nullptr,
-                               p->cfg.emb_grad_scale, s);
-    return st;
-  }
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> fresh;
   for (auto& tn : p->timers) {
     hipEvent_t a = dcue::timer_event(), e = dcue::timer_event();

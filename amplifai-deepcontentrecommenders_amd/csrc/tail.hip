@@ -27,9 +27,16 @@ __global__ __launch_bounds__(256) void k_item_counts(dcue_batch b, float* counts
   }
   const int nneg = b.n_rows * b.n_neg;
   int cnt = i < b.n_rows ? 1 : 0;
-  for (int e0 = 0; e0 < nneg; e0 += 64) {
-    const int e = e0 + lane;
-    cnt += __popcll(__ballot(e < nneg && b.neg_item[e] == i));
+  constexpr int kBatch = 16;  // loads in flight per lane before the ballots
+  for (int e0 = 0; e0 < nneg; e0 += 64 * kBatch) {
+    int32_t v[kBatch];
+#pragma unroll
+    for (int q = 0; q < kBatch; ++q) {
+      const int e = e0 + 64 * q + lane;
+      v[q] = e < nneg ? b.neg_item[e] : -1;
+    }
+#pragma unroll
+    for (int q = 0; q < kBatch; ++q) cnt += __popcll(__ballot(v[q] == i));
   }
   if (lane == 0) counts[i] = (float)cnt;
 }
@@ -279,6 +286,129 @@ int launch_score_fwd(const float* uf, const float* f, const dcue_batch* b, int d
   return DCUE_OK;
 }
 
+// Forward + hinge backward of one row per workgroup (plans: the loss gradient is known here, so
+// k_score_bwd's pass is folded in). Same arithmetic and summation orders as k_score_fwd,
+// k_loss_mean and k_score_bwd; the loss mean is taken by the last row block to finish.
+__global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ uf,
+                                                     const float* __restrict__ f, dcue_batch b, int d,
+                                                     float margin, float* scores, float* cosv,
+                                                     float* norms, float* rowsum, float* loss, float* dU,
+                                                     float* dfcopy, unsigned int* ticket) {
+  __shared__ float cs[1025], dcs[1025], hs[1024];
+  __shared__ float gus[4][256];
+  __shared__ bool last;
+  const int row = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int N = b.n_neg, per = (d + 63) / 64;
+  const float eps = 1e-8f;
+  float u[4];
+  float su = 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = lane + 64 * e;
+    u[e] = (e < per && k < d) ? uf[(long)row * d + k] : 0.f;
+    su += u[e] * u[e];
+  }
+  const float nu = sqrtf(wave_sum(su));
+  const float du = fmaxf(nu, eps);
+  if (wave == 0 && lane == 0) norms[(long)row * (N + 2)] = nu;
+  for (int c = wave; c <= N; c += 4) {
+    const long item = copy_item(b, row, c);
+    float v[4], sf = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = lane + 64 * e;
+      v[e] = (e < per && k < d) ? f[item * d + k] : 0.f;
+      sf += v[e] * v[e];
+    }
+    const float nf = sqrtf(wave_sum(sf));
+    const float dfn = fmaxf(nf, eps);
+    float dot = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dot += (u[e] / du) * (v[e] / dfn);
+    const float cv = wave_sum(dot);
+    if (lane == 0) {
+      norms[(long)row * (N + 2) + 1 + c] = nf;
+      cosv[(long)row * (N + 1) + c] = cv;
+      cs[c] = cv;
+    }
+  }
+  __syncthreads();
+  const float invB = 1.f / (float)b.n_rows;
+  for (int j = threadIdx.x; j < N; j += blockDim.x) {
+    const float sc = cs[0] - cs[1 + j];
+    const float h = margin - sc;
+    scores[(long)row * N + j] = sc;
+    hs[j] = h > 0.f ? h : 0.f;
+    // dL/dscore (torch.max splits ties 1/2); d score / d neg cos = -1
+    const float dh = h > 0.f ? -1.f * invB : (h == 0.f ? -0.5f * invB : 0.f);
+    dcs[1 + j] = -dh;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f, dpos = 0.f;
+    for (int j = 0; j < N; ++j) {
+      s += hs[j];
+      dpos += -dcs[1 + j];  // the positive collects every score's gradient, in j order
+    }
+    dcs[0] = dpos;
+    rowsum[row] = s;
+  }
+  __syncthreads();
+  // backward of the cosines: d cos/dx = (yhat - cos*xhat)/|x|
+  const float nuc = fmaxf(nu, eps);
+  float uh[4], gu[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    uh[e] = u[e] / nuc;
+    gu[e] = 0.f;
+  }
+  for (int c = wave; c <= N; c += 4) {
+    const long item = copy_item(b, row, c);
+    const float dc = dcs[c];
+    const float cv = cs[c];
+    const float nf = fmaxf(norms[(long)row * (N + 2) + 1 + c], eps);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = lane + 64 * e;
+      if (e < per && k < d) {
+        const float fh = f[item * d + k] / nf;
+        gu[e] += dc * (fh - cv * uh[e]) / nuc;
+        dfcopy[((long)row * (N + 1) + c) * d + k] = dc * (uh[e] - cv * fh) / nf;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = lane + 64 * e;
+    if (e < per && k < d) gus[wave][k] = gu[e];
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < d; k += blockDim.x)
+    dU[(long)row * d + k] = ((gus[0][k] + gus[1][k]) + gus[2][k]) + gus[3][k];
+  // loss = mean over rows of the row sums, in row order, by the last block to arrive
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(ticket, 1u) == (unsigned)(b.n_rows - 1);
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    __threadfence();
+    float s = 0.f;
+    for (int r = 0; r < b.n_rows; ++r) s += __builtin_nontemporal_load(rowsum + r);
+    *loss = s / (float)b.n_rows;
+  }
+}
+
+int launch_score_fused(const float* uf, const float* f, const dcue_batch* b, int d, float margin,
+                       float* scores, float* cosv, float* norms, float* rowsum, float* loss,
+                       float* du, float* dfcopy, unsigned int* ticket, hipStream_t s) {
+  if (d > 256 || b->n_neg > 1024 || b->n_rows > 1024) return DCUE_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(k_score_fused, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, margin, scores, cosv,
+                     norms, rowsum, loss, du, dfcopy, ticket);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
 // dL/dscores -> dL/du (waves' partial sums combined in wave order) and dL/df per copy.
 // d cos/dx = (yhat - cos*xhat)/|x| (non-degenerate norms).
 __global__ __launch_bounds__(256) void k_score_bwd(const float* __restrict__ uf,
@@ -377,17 +507,27 @@ __global__ __launch_bounds__(256) void k_item_grad(const float* __restrict__ dfc
       len = 0;
     };
     const int nneg = B * N;
-    for (int e0 = 0; e0 < nneg; e0 += 64) {
-      const int e = e0 + lane;
-      const bool hit = e < nneg && b.neg_item[e] == i;
-      const unsigned long long bal = __ballot(hit);
-      const int cnt = __popcll(bal);
-      if (len + cnt > kCap) drain();
-      if (hit) {
-        const int row = e / N;
-        my[len + __popcll(bal & ((1ull << lane) - 1ull))] = row * (N + 1) + 1 + (e - row * N);
+    constexpr int kBatch = 16;  // neg_item loads in flight per lane before the ballots use them
+    for (int e0 = 0; e0 < nneg; e0 += 64 * kBatch) {
+      int32_t v[kBatch];
+#pragma unroll
+      for (int q = 0; q < kBatch; ++q) {
+        const int e = e0 + 64 * q + lane;
+        v[q] = e < nneg ? b.neg_item[e] : -1;
       }
-      len += cnt;
+#pragma unroll
+      for (int q = 0; q < kBatch; ++q) {
+        const int e = e0 + 64 * q + lane;
+        const bool hit = v[q] == i;
+        const unsigned long long bal = __ballot(hit);
+        const int cnt = __popcll(bal);
+        if (len + cnt > kCap) drain();
+        if (hit) {
+          const int row = e / N;
+          my[len + __popcll(bal & ((1ull << lane) - 1ull))] = row * (N + 1) + 1 + (e - row * N);
+        }
+        len += cnt;
+      }
     }
     drain();
   }
