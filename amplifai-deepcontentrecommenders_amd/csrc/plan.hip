@@ -162,6 +162,13 @@ extern "C" int dcue_plan_launch(dcue_plan* p, const int64_t* users_src, const in
   return DCUE_OK;
 }
 
+extern "C" int dcue_plan_step(dcue_plan* p, const int64_t* users_src, const int32_t* item_track_src,
+                              const dcue_adam_args* adam, void* stream) {
+  const int st = dcue_plan_launch(p, users_src, item_track_src, stream);
+  if (st || !adam) return st;
+  return dcue_adam_step(&p->model, adam, stream);
+}
+
 extern "C" int dcue_plan_destroy(dcue_plan* p) {
   if (!p) return DCUE_OK;
   if (p->exec) (void)hipGraphExecDestroy(p->exec);

@@ -391,11 +391,15 @@ __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ u
     last = atomicAdd(ticket, 1u) == (unsigned)(b.n_rows - 1);
   }
   __syncthreads();
-  if (last && threadIdx.x == 0) {
+  if (last) {  // every row sum is loaded at once, then added in row order
     __threadfence();
-    float s = 0.f;
-    for (int r = 0; r < b.n_rows; ++r) s += __builtin_nontemporal_load(rowsum + r);
-    *loss = s / (float)b.n_rows;
+    for (int r = threadIdx.x; r < b.n_rows; r += blockDim.x) hs[r] = __builtin_nontemporal_load(rowsum + r);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float s = 0.f;
+      for (int r = 0; r < b.n_rows; ++r) s += hs[r];
+      *loss = s / (float)b.n_rows;
+    }
   }
 }
 
@@ -463,51 +467,34 @@ int launch_score_bwd(const float* uf, const float* f, const dcue_batch* b, int d
   return DCUE_OK;
 }
 
-// df[i] = sum over item i's copies, in (positive, (b,j) row-major) order; one wave per item.
+constexpr int kItemGradCap = 4096;  // copies per item (B*N + 1 in gather layout)
+
+// df[i] = sum over item i's copies. One workgroup per item: wave 0 lists the item's copies in
+// (positive, (b,j) row-major) order with ballots over neg_item (loads batched ahead of the ballots);
+// the four waves then each sum a contiguous quarter of the list with all its row loads in flight,
+// and the quarters are added in wave order (deterministic).
 __global__ __launch_bounds__(256) void k_item_grad(const float* __restrict__ dfcopy, dcue_batch b, int d,
                                                    float* df) {
-  const int lane = threadIdx.x & 63;
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= b.n_items) return;
-  const int N = b.n_neg, B = b.n_rows, per = (d + 63) / 64;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  auto add_copy = [&](long c) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = lane + 64 * e;
-      if (e < per && k < d) acc[e] += dfcopy[c * d + k];
-    }
-  };
+  constexpr int kCap = kItemGradCap;
+  __shared__ int list[kCap];
+  __shared__ int s_len;
+  __shared__ float part[4][256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = blockIdx.x;
+  const int N = b.n_neg, B = b.n_rows;
   if (b.layout == DCUE_LAYOUT_CATALOGUE) {
-    add_copy(i < B ? (long)i * (N + 1) : (long)((i - B) / N) * (N + 1) + 1 + (i - B) % N);
-  } else {
-    // pass 1: ballots over neg_item append the item's copies, in order, to a per-wave LDS list;
-    // pass 2 drains the list 8 rows at a time (8 loads in flight, then the adds in list order)
-    constexpr int kCap = 256;
-    __shared__ int list[4][kCap];
-    int* my = list[threadIdx.x >> 6];
+    const long cidx = i < B ? (long)i * (N + 1) : (long)((i - B) / N) * (N + 1) + 1 + (i - B) % N;
+    for (int k = threadIdx.x; k < d; k += blockDim.x) df[(long)i * d + k] = dfcopy[cidx * d + k];
+    return;
+  }
+  if (wave == 0) {
     int len = 0;
-    if (i < B) my[len++] = i * (N + 1);
-    auto drain = [&]() {
-      for (int q0 = 0; q0 < len; q0 += 8) {
-        float v[8][4];
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int k = lane + 64 * e;
-            v[q][e] = (q0 + q < len && e < per && k < d) ? dfcopy[(long)my[q0 + q] * d + k] : 0.f;
-          }
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (q0 + q < len)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[e] += v[q][e];
-      }
-      len = 0;
-    };
+    if (i < B) {
+      if (lane == 0) list[0] = i * (N + 1);
+      len = 1;
+    }
     const int nneg = B * N;
-    constexpr int kBatch = 16;  // neg_item loads in flight per lane before the ballots use them
+    constexpr int kBatch = 16;
     for (int e0 = 0; e0 < nneg; e0 += 64 * kBatch) {
       int32_t v[kBatch];
 #pragma unroll
@@ -520,27 +507,50 @@ __global__ __launch_bounds__(256) void k_item_grad(const float* __restrict__ dfc
         const int e = e0 + 64 * q + lane;
         const bool hit = v[q] == i;
         const unsigned long long bal = __ballot(hit);
-        const int cnt = __popcll(bal);
-        if (len + cnt > kCap) drain();
-        if (hit) {
+        const int pos = len + __popcll(bal & ((1ull << lane) - 1ull));
+        if (hit && pos < kCap) {
           const int row = e / N;
-          my[len + __popcll(bal & ((1ull << lane) - 1ull))] = row * (N + 1) + 1 + (e - row * N);
+          list[pos] = row * (N + 1) + 1 + (e - row * N);
         }
-        len += cnt;
+        len += __popcll(bal);
       }
     }
-    drain();
+    if (lane == 0) s_len = len < kCap ? len : kCap;
+  }
+  __syncthreads();
+  const int len = s_len;
+  const int q0 = (len * wave) / 4, q1 = (len * (wave + 1)) / 4;  // this wave's quarter
+  const int per = (d + 63) / 64;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  constexpr int kRows = 8;
+  for (int qb = q0; qb < q1; qb += kRows) {
+    float v[kRows][4];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = lane + 64 * e;
+        v[r][e] = (qb + r < q1 && e < per && k < d) ? dfcopy[(long)list[qb + r] * d + k] : 0.f;
+      }
+#pragma unroll
+    for (int r = 0; r < kRows; ++r)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += v[r][e];
   }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int k = lane + 64 * e;
-    if (e < per && k < d) df[(long)i * d + k] = acc[e];
+    if (e < per && k < d) part[wave][k] = acc[e];
   }
+  __syncthreads();
+  for (int k = threadIdx.x; k < d; k += blockDim.x)
+    df[(long)i * d + k] = ((part[0][k] + part[1][k]) + part[2][k]) + part[3][k];
 }
 
 int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df, hipStream_t s) {
   if (d > 256) return DCUE_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL(k_item_grad, dim3((b->n_items + 3) / 4), dim3(256), 0, s, dfcopy, *b, d, df);
+  if (b->layout == DCUE_LAYOUT_GATHER && (long)b->n_rows * b->n_neg + 1 > kItemGradCap) return DCUE_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(k_item_grad, dim3(b->n_items), dim3(256), 0, s, dfcopy, *b, d, df);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }

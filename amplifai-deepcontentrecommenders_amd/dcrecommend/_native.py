@@ -117,6 +117,7 @@ _SIGS = {
                           ctypes.POINTER(PlanConfig), ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
     "dcue_plan_launch": ([_P, _P, _P, _P], ctypes.c_int),
     "dcue_plan_destroy": ([_P], ctypes.c_int),
+    "dcue_plan_step": ([_P, _P, _P, ctypes.POINTER(AdamArgs), _P], ctypes.c_int),
     "dcue_timer_enable": ([ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
     "dcue_timer_read": ([ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)],
                         ctypes.c_int),

@@ -20,7 +20,7 @@ from dcrecommend import _native as nat
 class TrainPlan:
 
     def __init__(self, net, tracks, n_rows, n_neg, mt_state=None, item_track=None, margin=0.2,
-                 emb_grad_scale=1.0, graph=False):
+                 emb_grad_scale=1.0, graph=False, optimizer=None):
         """tracks: HBM track table [n_tracks][131][128] (fp16/fp32). In-batch mode (mt_state given):
         positives are items 0..B-1 of item_track, negatives drawn in-graph. Otherwise item_track holds
         B*(1+N) items in catalogue order (datasets/dcuedataset.py:242-250)."""
@@ -37,7 +37,9 @@ class TrainPlan:
         self.neg_item = torch.zeros((B, N), dtype=torch.int32, device=dev) if self.inbatch else None
         self.mt_state = mt_state
         self.ws = net._workspace(B, N, M)
-        model = net._model_struct()  # creates the deferred optimizer state if it does not exist yet
+        self.optimizer = optimizer
+        # with an optimizer the plan also owns the Adam step (step()); the struct then carries its state
+        model = net._model_struct(optimizer._adam_state() if optimizer is not None else None)
         opt = net._deferred_opt() if getattr(net, "_deferred_opt", None) is not None else None
         self._bound = (fl, self.ws, fl["emb_grad"], opt._moments if opt is not None else None)
         self._keep = (fl["emb_grad"], fl["emb_rows"])
@@ -82,6 +84,25 @@ class TrainPlan:
                                         nat.stream_handle() if stream is None else stream)
         if st != 0:
             nat.check(st, "dcue_plan_launch")
+
+    def step(self, users=None, item_track=None, stream=None):
+        """One whole single-GPU training step in one host call: launch() + the optimizer step
+        (NativeAdam semantics with the optimizer's current param_group lr / weight_decay)."""
+        opt = self.optimizer
+        if opt is None:
+            raise RuntimeError("TrainPlan.step needs the plan built with optimizer=...")
+        if self._handle is None:
+            raise RuntimeError("TrainPlan was closed")
+        self._check_bound()
+        g = opt.param_groups[0]
+        opt.step_count += 1
+        args = nat.AdamArgs(float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]),
+                            float(g["weight_decay"]), opt.step_count, 0)
+        st = self._lib.dcue_plan_step(self._handle, None if users is None else users.data_ptr(),
+                                      None if item_track is None else item_track.data_ptr(),
+                                      ctypes.byref(args), nat.stream_handle() if stream is None else stream)
+        if st != 0:
+            nat.check(st, "dcue_plan_step")
 
     def close(self):
         if getattr(self, "_handle", None) is not None:

@@ -145,13 +145,15 @@ def main():
     # the step's sample + forward + backward replay as one HIP graph; Adam and the all-reduce between.
     # The roofline kernel's timer is on before capture so the graph carries its event-record nodes.
     nat.timer_enable(TIMED, True)
-    plan = TrainPlan(net, tracks, B, N, mt_state=mt, emb_grad_scale=1.0 / world)
+    plan = TrainPlan(net, tracks, B, N, mt_state=mt, emb_grad_scale=1.0 / world, optimizer=opt)
 
     def step(s):
-        plan.launch(users_b[s], items_b[s])
         if world > 1:
+            plan.launch(users_b[s], items_b[s])
             D.allreduce_mean_(G)  # RCCL: the one exchange of the step (1.57 MB)
-        opt.step()
+            opt.step()
+        else:
+            plan.step(users_b[s], items_b[s])  # sample + forward + backward + Adam, one host call
         sched.batch_step()
 
     for s in range(args.warmup):

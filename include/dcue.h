@@ -244,6 +244,11 @@ int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const dcue_tracks
 /* users_src / item_track_src (nullable): copied into the bound batch buffers before the replay. */
 int dcue_plan_launch(dcue_plan* plan, const int64_t* users_src, const int32_t* item_track_src,
                      void* stream);
+/* dcue_plan_launch, then (adam != NULL) dcue_adam_step on the plan's model: one host call per
+ * single-GPU training step (under data parallelism the gradient all-reduce sits between the two,
+ * so launch and dcue_adam_step are issued separately). */
+int dcue_plan_step(dcue_plan* plan, const int64_t* users_src, const int32_t* item_track_src,
+                   const dcue_adam_args* adam, void* stream);
 int dcue_plan_destroy(dcue_plan* plan);
 
 /* ------------------------------------------------------------------- live kernel timing */

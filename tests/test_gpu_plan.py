@@ -38,8 +38,10 @@ def _state(net, opt):
     return out
 
 
-@pytest.mark.parametrize("inbatch,graph", [(True, False), (False, False), (True, True), (False, True)])
-def test_plan_replay_matches_eager(inbatch, graph):
+@pytest.mark.parametrize("inbatch,graph,fused_adam", [(True, False, False), (False, False, False),
+                                                      (True, True, False), (False, True, False),
+                                                      (True, False, True)])
+def test_plan_replay_matches_eager(inbatch, graph, fused_adam):
     from dcrecommend import _native as nat
     from dcrecommend.dcue.plan import TrainPlan
     from dcrecommend.optim import NativeAdam
@@ -51,7 +53,8 @@ def test_plan_replay_matches_eager(inbatch, graph):
             for n in (eager, replayed)]
     mts = [_mt(21), _mt(21)]
     M = B if inbatch else B * (1 + N)
-    plan = TrainPlan(replayed, tracks, B, N, mt_state=mts[1] if inbatch else None, graph=graph)
+    plan = TrainPlan(replayed, tracks, B, N, mt_state=mts[1] if inbatch else None, graph=graph,
+                     optimizer=opts[1] if fused_adam else None)
     neg = torch.zeros((B, N), dtype=torch.int32, device=DEV)
     for s in range(steps):
         users = torch.randint(0, n_users, (B,), generator=gen, device=DEV)
@@ -64,8 +67,11 @@ def test_plan_replay_matches_eager(inbatch, graph):
             eager.native_forward(users, tracks, items, N, nat.LAYOUT_CATALOGUE, None, train=True, margin=0.2)
         eager.native_backward(None)
         opts[0].step()
-        plan.launch(users, items)
-        opts[1].step()
+        if fused_adam:
+            plan.step(users, items)  # launch + Adam in one call
+        else:
+            plan.launch(users, items)
+            opts[1].step()
     if inbatch:
         assert torch.equal(neg, plan.neg_item)
     a, b = _state(eager, opts[0]), _state(replayed, opts[1])
