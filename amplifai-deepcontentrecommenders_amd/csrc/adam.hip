@@ -8,7 +8,8 @@ namespace dcue {
 //   g += wd*p (wd != 0);  m.lerp_(g, 1-b1);  v = v*b2 + (1-b2)*g*g;
 //   p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
 struct AdamScalars {
-  float lr_bc1, one_m_b1, b2, one_m_b2, bc2_sqrt, eps, wd, pad;
+  float lr_bc1, one_m_b1, b2, one_m_b2, bc2_sqrt, eps, wd;
+  float inv_bc2_sqrt;  // RN(1 / bc2_sqrt): Markstein division by the per-step constant
 };
 static_assert(sizeof(AdamScalars) == 32, "history entry is [8] floats");
 
@@ -23,6 +24,35 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   v = __fadd_rn(__fmul_rn(v, s.b2), __fmul_rn(__fmul_rn(s.one_m_b2, g), g));
   const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), s.bc2_sqrt), s.eps);
   p = __fadd_rn(p, __fmul_rn(-s.lr_bc1, __fdiv_rn(m, denom)));
+}
+
+// The zero-gradient step (a row outside the batch, wd == 0), bit-identical to adam_elem(p, +0, m, v, s):
+//   m + w*(0 - m) == m - w*m (signed zeros included), v*b2 + w2*0*0 == v*b2 (v >= 0), and
+//   sqrt(v)/bc2_sqrt by Markstein's correction with r = RN(1/bc2_sqrt): q = RN(a r),
+//   q' = RN(q + RN?(a - q bc2)*r) is the correctly rounded quotient for a >= 2^-100 (below it the
+//   plain division runs). This is the deferred replay's inner loop (VALU-bound).
+__device__ __forceinline__ void adam_zero_elem(float& p, float& m, float& v, const AdamScalars& s) {
+  m = __fsub_rn(m, __fmul_rn(s.one_m_b1, m));
+  v = __fmul_rn(v, s.b2);
+  const float sq = __fsqrt_rn(v);
+  float t;
+  if (sq >= 0x1p-100f) {
+    const float q = __fmul_rn(sq, s.inv_bc2_sqrt);
+    const float r = __fmaf_rn(-q, s.bc2_sqrt, sq);
+    t = __fmaf_rn(r, s.inv_bc2_sqrt, q);
+  } else {
+    t = __fdiv_rn(sq, s.bc2_sqrt);
+  }
+  const float denom = __fadd_rn(t, s.eps);
+  p = __fadd_rn(p, __fmul_rn(-s.lr_bc1, __fdiv_rn(m, denom)));
+}
+
+// replay of a zero-gradient step: the fast form when no weight decay touches g
+__device__ __forceinline__ void adam_replay(float& p, float& m, float& v, const AdamScalars& s, float gz) {
+  if (s.wd == 0.f)
+    adam_zero_elem(p, m, v, s);
+  else
+    adam_elem(p, gz, m, v, s);
 }
 
 __global__ __launch_bounds__(256) void k_adam_dense(float* __restrict__ p, const float* __restrict__ g,
@@ -108,7 +138,7 @@ __global__ __launch_bounds__(256) void k_emb_sync(float* __restrict__ p, float* 
   float* vr = v + u * E;
   for (int k = threadIdx.x; k < E; k += blockDim.x) {
     float pp = pr[k], mm = mr[k], vv = vr[k];
-    for (int j = from + 1; j <= T; ++j) adam_elem(pp, gz, mm, vv, hs[j % cap]);
+    for (int j = from + 1; j <= T; ++j) adam_replay(pp, mm, vv, hs[j % cap], gz);
     pr[k] = pp; mr[k] = mm; vr[k] = vv;
   }
   __syncthreads();
@@ -140,10 +170,10 @@ __global__ __launch_bounds__(256) void k_emb_flush(float* __restrict__ p, float*
       for (int j = F + 1; j <= T; ++j) {
         if (j <= from) continue;
         const AdamScalars s = hs[j - F - 1];
-        adam_elem(pp.x, gz, mm.x, vv.x, s);
-        adam_elem(pp.y, gz, mm.y, vv.y, s);
-        adam_elem(pp.z, gz, mm.z, vv.z, s);
-        adam_elem(pp.w, gz, mm.w, vv.w, s);
+        adam_replay(pp.x, mm.x, vv.x, s, gz);
+        adam_replay(pp.y, mm.y, vv.y, s, gz);
+        adam_replay(pp.z, mm.z, vv.z, s, gz);
+        adam_replay(pp.w, mm.w, vv.w, s, gz);
       }
       st4(p + 4 * i, pp); st4(m + 4 * i, mm); st4(v + 4 * i, vv);
     }
@@ -153,7 +183,7 @@ __global__ __launch_bounds__(256) void k_emb_flush(float* __restrict__ p, float*
       const int from = max(emb_step[i / E], F);
       float pp = p[i], mm = m[i], vv = v[i];
       for (int j = F + 1; j <= T; ++j)
-        if (j > from) adam_elem(pp, gz, mm, vv, hs[j - F - 1]);
+        if (j > from) adam_replay(pp, mm, vv, hs[j - F - 1], gz);
       p[i] = pp; m[i] = mm; v[i] = vv;
     }
   }
@@ -184,7 +214,7 @@ __global__ __launch_bounds__(256) void k_adam_touched(float* __restrict__ p, flo
     const float* gr = gcompact + (long)b * E;
     for (int k = threadIdx.x; k < E; k += blockDim.x) {
       float pp = pr[k], mm = mr[k], vv = vr[k];
-      for (int j = from + 1; j < t; ++j) adam_elem(pp, gz, mm, vv, hist[j % cap]);  // normally none
+      for (int j = from + 1; j < t; ++j) adam_replay(pp, mm, vv, hist[j % cap], gz);  // normally none
       adam_elem(pp, gr[k], mm, vv, s);
       pr[k] = pp; mr[k] = mm; vr[k] = vv;
     }
@@ -248,7 +278,7 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
   sc.bc2_sqrt = (float)sqrt(bc2);
   sc.eps = a->eps;
   sc.wd = a->weight_decay;
-  sc.pad = 0.f;
+  sc.inv_bc2_sqrt = 1.0f / sc.bc2_sqrt;  // IEEE single division on the host: RN(1/bc2_sqrt)
   const int parts = a->parts ? a->parts : (DCUE_ADAM_DENSE | DCUE_ADAM_EMBEDDING);
   const long n = poff[DCUE_N_DENSE_SEGMENTS];
   if (parts & DCUE_ADAM_DENSE) {
