@@ -191,6 +191,71 @@ __global__ __launch_bounds__(256) void k_emb_flush(float* __restrict__ p, float*
 
 __global__ void k_emb_flush_done(dcue_emb_log* hdr) { hdr->flush_step = hdr->step_done; }
 
+// Rolling flush: at step t the rows of chunk t mod cap (a contiguous 1/cap of the table) are brought
+// current, so every row is replayed at least once per `cap` steps -- the replay work spread evenly
+// over the steps (it runs on the user-tower stream, beside the item tower) instead of a full-table
+// sweep every cap steps. A workgroup owns whole rows: it reads their clocks, replays, then sets them.
+__global__ __launch_bounds__(256) void k_emb_flush_rows(float* __restrict__ p, float* __restrict__ m,
+                                                        float* __restrict__ v, const dcue_emb_log* hdr,
+                                                        int32_t* emb_step, long r0, long r1, int E,
+                                                        int rows_per_block, float gz) {
+  __shared__ AdamScalars hs[DCUE_MAX_LOG_CAP];
+  __shared__ int from_s[256];
+  const int T = hdr->step_done, F = hdr->flush_step, cap = hdr->cap;
+  const long rb = r0 + (long)blockIdx.x * rows_per_block;
+  const int nr = (int)min((long)rows_per_block, r1 - rb);
+  if (nr <= 0) return;
+  const AdamScalars* hist = reinterpret_cast<const AdamScalars*>(hdr + 1);
+  const int lo = max(F + 1, T - cap + 1);
+  for (int j = lo + (int)threadIdx.x; j <= T; j += blockDim.x) hs[j % cap] = hist[j % cap];
+  for (int i = threadIdx.x; i < nr; i += blockDim.x) from_s[i] = max(emb_step[rb + i], F);
+  __syncthreads();
+  if ((E & 3) == 0) {
+    const int E4 = E >> 2;
+    for (int e = threadIdx.x; e < nr * E4; e += blockDim.x) {
+      const int i = e / E4;
+      const long off = (rb + i) * E + 4 * (e - i * E4);
+      float4 pp = ld4(p + off), mm = ld4(m + off), vv = ld4(v + off);
+      for (int j = from_s[i] + 1; j <= T; ++j) {
+        const AdamScalars s = hs[j % cap];
+        adam_replay(pp.x, mm.x, vv.x, s, gz);
+        adam_replay(pp.y, mm.y, vv.y, s, gz);
+        adam_replay(pp.z, mm.z, vv.z, s, gz);
+        adam_replay(pp.w, mm.w, vv.w, s, gz);
+      }
+      st4(p + off, pp); st4(m + off, mm); st4(v + off, vv);
+    }
+  } else {
+    for (int e = threadIdx.x; e < nr * E; e += blockDim.x) {
+      const int i = e / E;
+      const long off = (rb + i) * E + (e - i * E);
+      float pp = p[off], mm = m[off], vv = v[off];
+      for (int j = from_s[i] + 1; j <= T; ++j) adam_replay(pp, mm, vv, hs[j % cap], gz);
+      p[off] = pp; m[off] = mm; v[off] = vv;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nr; i += blockDim.x) emb_step[rb + i] = T;
+}
+
+int launch_emb_flush_rows(const dcue_model* md, int step, hipStream_t s) {
+  const long n = md->dims.n_users;
+  const int cap = md->emb_log_cap, E = md->dims.user_embdim;
+  const int k = step % cap;
+  const long r0 = n * k / cap, r1 = n * (k + 1) / cap;
+  if (r1 <= r0) return DCUE_OK;
+  int rpb = 1024 / E;
+  if (rpb < 1) rpb = 1;
+  if (rpb > 256) rpb = 256;
+  const long blocks = (r1 - r0 + rpb - 1) / rpb;
+  hipLaunchKernelGGL(k_emb_flush_rows, dim3((unsigned)blocks), dim3(256), 0, s, md->emb, md->emb_exp_avg,
+                     md->emb_exp_avg_sq, md->emb_log, md->emb_step, r0, r1, E, rpb, 0.f);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+
+
 // Step t for the rows that have a gradient (emb_rows from the backward); records step t's scalars.
 __global__ __launch_bounds__(256) void k_adam_touched(float* __restrict__ p, float* __restrict__ m,
                                                       float* __restrict__ v,
@@ -291,7 +356,7 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
                        md->emb_exp_avg_sq, md->emb_grad, md->emb_rows, md->emb_step, md->emb_log,
                        md->dims.user_embdim, a->step, sc, 0.f);
     DCUE_LAUNCH_CHECK();
-    if (a->step % md->emb_log_cap == 0) return launch_emb_flush(md, s);
+    return launch_emb_flush_rows(md, a->step, s);  // this step's slice of the rolling flush
   } else if ((parts & DCUE_ADAM_EMBEDDING) && md->dims.n_users > 0) {
     long blocks = (md->dims.n_users + 3) / 4;
     if (blocks > 8192) blocks = 8192;

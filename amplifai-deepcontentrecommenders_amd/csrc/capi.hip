@@ -34,6 +34,22 @@ SidePool* side_pool() {
   return &p;
 }
 
+// A point on `from` that other streams can wait for later (wait_point): a ring event is recorded
+// now. The ring (32) is long enough that no event is re-recorded before its waits are enqueued
+// (a step records fewer than 16 points).
+int fork_point(SidePool* p, hipStream_t from, hipEvent_t* ev) {
+  hipEvent_t e = p->ev[p->next];
+  p->next = (p->next + 1) % 32;
+  DCUE_HIP_CHECK(hipEventRecord(e, from));
+  *ev = e;
+  return DCUE_OK;
+}
+
+int wait_point(hipStream_t to, hipEvent_t ev) {
+  DCUE_HIP_CHECK(hipStreamWaitEvent(to, ev, 0));
+  return DCUE_OK;
+}
+
 // `to` waits for everything enqueued on `from` so far. An event is re-recorded only after the
 // wait on its previous record has been enqueued, so a small ring of events suffices.
 int stream_wait(SidePool* p, hipStream_t to, hipStream_t from) {
@@ -427,12 +443,15 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   SidePool* sp = side_pool();
   if (!sp) return DCUE_ERR_HIP;
   hipStream_t su = sp->st[0];
-  TRY(stream_wait(sp, su, s));  // user tower beside the item tower
-  if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
-  TRY(user_forward(c, w, b->users, b->n_rows, nullptr, su));
+  // the user tower runs beside the item tower; the item tower's chain is issued first
+  hipEvent_t ev_in = nullptr;
+  TRY(fork_point(sp, s, &ev_in));
   if (!o.prologue_done) TRY(launch_item_counts(b, w.counts, s));
   TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s,
                    o.prologue_done));
+  TRY(wait_point(su, ev_in));
+  if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
+  TRY(user_forward(c, w, b->users, b->n_rows, nullptr, su));
   TRY(stream_wait(sp, s, su));
   if (o.fuse_score)
     return launch_score_fused(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.rowsum, w.loss,
@@ -472,17 +491,55 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   const double copies = (double)B * (1 + N);
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
   if (o.fuse_score && dscores) return DCUE_ERR_INVALID;
+  if (o.emb_adam && (o.emb_adam->parts & ~DCUE_ADAM_EMBEDDING)) return DCUE_ERR_INVALID;
+  SidePool* sp = side_pool();
+  if (!sp) return DCUE_ERR_HIP;
+  hipStream_t su = sp->st[0], sw[2] = {sp->st[1], sp->st[2]};
 
+  // Host issue order follows the critical path: the main stream's chain (item grads -> fc -> the
+  // dgrad chain) is enqueued first, recording a fork point before each layer; the side streams'
+  // work (user tower, fc weight gradient, per-layer weight gradients) is enqueued afterwards
+  // against those recorded points, so issuing it never delays the chain.
   if (!o.prologue_done)
     DCUE_HIP_CHECK(hipMemsetAsync(w.bnbacc, 0, sizeof(unsigned long long) * 6 * 2 * w.cmax * 2, s));
   if (!o.fuse_score)  // else the fused score kernel already produced du / dfcopy
     TRY(launch_score_bwd(w.uf, w.f, b, D, dscores ? dscores : w.dhinge, w.cosv, w.norms, w.du,
                          w.dfcopy, s));
-  SidePool* sp = side_pool();
-  if (!sp) return DCUE_ERR_HIP;
-  hipStream_t su = sp->st[0], sw[2] = {sp->st[1], sp->st[2]};
-  TRY(stream_wait(sp, su, s));
-  // user tower (userembedding.py:33-44 backward), then the compact embedding rows
+  hipEvent_t ev_score = nullptr, ev_df = nullptr, ev_layer[6] = {};
+  TRY(fork_point(sp, s, &ev_score));
+  TRY(launch_item_grad(w.dfcopy, b, D, w.df, s));
+  TRY(fork_point(sp, s, &ev_df));
+  {  // g5 = df W (fc input gradient) + BN5 backward sums of g5
+    TGemmArgs g = {};
+    g.M = M; g.N = D; g.K = D;
+    g.A = w.df; g.sam = D; g.sak = 1;
+    g.B = c.P(SEG_FC_W); g.sbk = D; g.sbn = 1;
+    g.C = w.g[5]; g.scm = D; g.scn = 1;
+    g.colacc = bn_acc(w.bnbacc, w.cmax, 5);
+    g.xy = w.y[5]; g.xmean = w.mean[5]; g.xinvstd = w.invstd[5];
+    TRY(launch_tgemm(0, 0, g, s));
+  }
+  for (int l = 5; l >= 2; --l) {  // dgrad chain: g_l (+ BN_l sums) -> g_{l-1} (+ BN_{l-1} sums)
+    const LayerGeom gm = layer_geom(l);
+    TRY(fork_point(sp, s, &ev_layer[l]));
+    RowsArgs ra = {};
+    ra.src = w.g[l]; ra.y_l = w.y[l]; ra.idx_l = w.idx[l];
+    ra.mean_l = w.mean[l]; ra.invstd_l = w.invstd[l]; ra.a_l = w.a[l];
+    ra.dz_acc = bn_acc(w.bnbacc, w.cmax, l);
+    ra.invN = (float)(1.0 / (copies * gm.lp)); ra.counts = w.counts;
+    ra.wpack = m->wpack + wpack_offset(&m->dims, l, true);
+    ra.out = w.g[l - 1];
+    ra.out_acc = bn_acc(w.bnbacc, w.cmax, l - 1);
+    ra.oy = w.y[l - 1]; ra.omean = w.mean[l - 1]; ra.oinvstd = w.invstd[l - 1];
+    ra.M = M;
+    ra.nout = H;
+    TRY(launch_conv_dgrad(l, l == 5 ? D : H, ra, s));
+  }
+  TRY(fork_point(sp, s, &ev_layer[1]));
+
+  // user tower (userembedding.py:33-44 backward), the compact embedding rows, and -- when the step
+  // carries it -- the user table's Adam step (it needs nothing from the item tower)
+  TRY(wait_point(su, ev_score));
   {
     TGemmArgs g = {};
     // dW2[n][k] = sum_b du[b][n] relu(h1)[b][k]; db2[n] = sum_b du[b][n]
@@ -519,9 +576,10 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   }
   TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, m->emb_rows,
                       m->emb_step ? m->emb_log : nullptr, su));
-  TRY(launch_item_grad(w.dfcopy, b, D, w.df, s));
-  // fc: dW[n][k] = sum_m df[m][n] bn5(y5)[m][k], db = sum_m df (row sums of A); g5 = df W
-  {
+  if (o.emb_adam) TRY(launch_adam(m, o.emb_adam, c.poff, su));
+
+  {  // fc weight gradient: dW[n][k] = sum_m df[m][n] bn5(y5)[m][k], db = sum_m df
+    TRY(wait_point(sw[0], ev_df));
     TGemmArgs g = {};
     g.M = D; g.N = D; g.K = M;
     g.A = w.df; g.sam = 1; g.sak = D;
@@ -529,26 +587,15 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     g.bmean = w.mean[5]; g.ba = w.a[5]; g.bbeta = c.P(seg_bn_b(5));
     g.C = c.Gd(SEG_FC_W); g.scm = D; g.scn = 1;
     g.rowsum = c.Gd(SEG_FC_B);
-    TRY(launch_tgemm(0, 2, g, s));
-    g = TGemmArgs{};
-    g.M = M; g.N = D; g.K = D;
-    g.A = w.df; g.sam = D; g.sak = 1;
-    g.B = c.P(SEG_FC_W); g.sbk = D; g.sbn = 1;
-    g.C = w.g[5]; g.scm = D; g.scn = 1;
-    g.colacc = bn_acc(w.bnbacc, w.cmax, 5);  // BN5 backward sums of g5
-    g.xy = w.y[5]; g.xmean = w.mean[5]; g.xinvstd = w.invstd[5];
-    TRY(launch_tgemm(0, 0, g, s));
+    TRY(launch_tgemm(0, 2, g, sw[0]));
   }
-  // conv layers 5..1
+  // conv weight gradients, alternating between the two wgrad streams (each with its own partials)
   for (int l = 5; l >= 1; --l) {
     const LayerGeom gm = layer_geom(l);
     const int C = l == 5 ? D : H;
     const int cin = l == 1 ? kMels : H;
-    unsigned long long* dzacc = bn_acc(w.bnbacc, w.cmax, l);  // complete: g_l's producer has run
-    const float invN = (float)(1.0 / (copies * gm.lp));
-    // weight gradient of layer l on a side stream (alternating, own partials); dgrad continues here
     hipStream_t so = sw[l & 1];
-    TRY(stream_wait(sp, so, s));
+    TRY(wait_point(so, ev_layer[l]));
     WgradArgs wa = {};
     wa.xsrc = l == 1 ? t->data : (const void*)w.y[l - 1];
     wa.item_track = b->item_track;
@@ -557,8 +604,8 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     wa.x_beta = l == 1 ? nullptr : c.P(seg_bn_b(l - 1));
     wa.g_l = w.g[l]; wa.y_l = w.y[l]; wa.idx_l = w.idx[l];
     wa.mean_l = w.mean[l]; wa.invstd_l = w.invstd[l]; wa.a_l = w.a[l];
-    wa.dz_acc = dzacc; wa.dgamma = c.Gd(seg_bn_w(l)); wa.dbeta = c.Gd(seg_bn_b(l));
-    wa.invN = invN; wa.counts = w.counts;
+    wa.dz_acc = bn_acc(w.bnbacc, w.cmax, l); wa.dgamma = c.Gd(seg_bn_w(l)); wa.dbeta = c.Gd(seg_bn_b(l));
+    wa.invN = (float)(1.0 / (copies * gm.lp)); wa.counts = w.counts;
     wa.M = M; wa.cout = C; wa.cin = cin;
     wa.wpart = w.wpart[l & 1]; wa.bpart = w.bpart[l & 1];
     const int nch = wgrad_nchunk(l, M, C, cin);
@@ -568,23 +615,10 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(timer_end(&tsc));
     TRY(launch_wgrad_reduce(l, wa.wpart, wa.bpart, nch, C, cin, c.Gd(seg_conv_w(l)),
                             c.Gd(seg_conv_b(l)), w.G, w.S, so));
-    if (l == 1) {
+    if (l == 1)
       TRY(launch_bn0_grads(w.G, w.S, c.P(seg_conv_w(1)), c.P(seg_bn_w(0)), c.P(seg_bn_b(0)), H,
                            c.Gd(seg_conv_w(1)), c.Gd(seg_bn_w(0)), c.Gd(seg_bn_b(0)),
                            c.Gd(seg_conv_b(1)), so));
-    } else {
-      RowsArgs ra = {};
-      ra.src = w.g[l]; ra.y_l = w.y[l]; ra.idx_l = w.idx[l];
-      ra.mean_l = w.mean[l]; ra.invstd_l = w.invstd[l]; ra.a_l = w.a[l];
-      ra.dz_acc = dzacc; ra.invN = invN; ra.counts = w.counts;
-      ra.wpack = m->wpack + wpack_offset(&m->dims, l, true);
-      ra.out = w.g[l - 1];
-      ra.out_acc = bn_acc(w.bnbacc, w.cmax, l - 1);  // BN_{l-1} backward sums of g_{l-1}
-      ra.oy = w.y[l - 1]; ra.omean = w.mean[l - 1]; ra.oinvstd = w.invstd[l - 1];
-      ra.M = M;
-      ra.nout = H;
-      TRY(launch_conv_dgrad(l, C, ra, s));
-    }
   }
   for (hipStream_t x : {su, sw[0], sw[1]}) TRY(stream_wait(sp, s, x));
   return DCUE_OK;

@@ -198,11 +198,14 @@ struct SidePool {
 };
 SidePool* side_pool();
 int stream_wait(SidePool* p, hipStream_t to, hipStream_t from);
+int fork_point(SidePool* p, hipStream_t from, hipEvent_t* ev);
+int wait_point(hipStream_t to, hipEvent_t ev);
 
 // ------------------------------------------------------------- step implementation (capi.hip)
 struct StepOpts {
   bool prologue_done = false;  // counts written + accumulators (and ticket) cleared by the prologue
   bool fuse_score = false;     // train forward also runs the hinge backward (k_score_fused)
+  const dcue_adam_args* emb_adam = nullptr;  // backward: also step the user table (parts = EMBEDDING)
 };
 int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
                  int train, float margin, const StepOpts& o, hipStream_t s);

@@ -38,10 +38,11 @@ namespace {
 // the rest of the backward.
 int issue_step(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
                const dcue_plan_config* cfg, const int64_t* users_src, const int32_t* items_src,
-               hipStream_t s) {
+               hipStream_t s, const dcue_adam_args* emb_adam = nullptr) {
   dcue::StepOpts o;
   o.prologue_done = true;
   o.fuse_score = true;
+  o.emb_adam = emb_adam;
   int st = dcue::step_prologue(m, b, ws, ws_bytes,
                                (cfg->flags & DCUE_PLAN_SAMPLE_INBATCH) ? cfg->mt : nullptr, users_src,
                                items_src, s);
@@ -164,9 +165,25 @@ extern "C" int dcue_plan_launch(dcue_plan* p, const int64_t* users_src, const in
 
 extern "C" int dcue_plan_step(dcue_plan* p, const int64_t* users_src, const int32_t* item_track_src,
                               const dcue_adam_args* adam, void* stream) {
-  const int st = dcue_plan_launch(p, users_src, item_track_src, stream);
-  if (st || !adam) return st;
-  return dcue_adam_step(&p->model, adam, stream);
+  if (!p) return DCUE_ERR_INVALID;
+  if (!adam || p->exec) {  // graph replay (or no optimizer): the Adam step follows as one call
+    const int st = dcue_plan_launch(p, users_src, item_track_src, stream);
+    if (st || !adam) return st;
+    return dcue_adam_step(&p->model, adam, stream);
+  }
+  if (adam->parts) return DCUE_ERR_INVALID;
+  // eager: the user table's part of Adam rides on the user-tower stream inside the backward (it
+  // needs only the embedding rows' gradient); the dense part follows once every gradient is in
+  const dcue_batch& b = p->batch;
+  if (users_src == b.users) users_src = nullptr;
+  if (item_track_src == b.item_track) item_track_src = nullptr;
+  dcue_adam_args emb = *adam, dense = *adam;
+  emb.parts = DCUE_ADAM_EMBEDDING;
+  dense.parts = DCUE_ADAM_DENSE;
+  const int st = issue_step(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, &p->cfg, users_src,
+                            item_track_src, (hipStream_t)stream, &emb);
+  if (st) return st;
+  return dcue_adam_step(&p->model, &dense, stream);
 }
 
 extern "C" int dcue_plan_destroy(dcue_plan* p) {

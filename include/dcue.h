@@ -55,8 +55,9 @@ typedef struct dcue_dims {
  * with g = 0 (+ wd*p) for rows outside the batch (nn/dcue.py:143-147,209). Deferred mode performs
  * exactly those steps, later: a row's zero-gradient steps are replayed with the same fp32
  * operations and the same per-step scalars (kept in this log's history ring) right before the row
- * is next read (dcue_forward / dcue_user_tower bring their users' rows current), for every row each
- * `cap` steps, and on dcue_embedding_flush. After a flush the table and both moments are
+ * is next read (dcue_forward / dcue_user_tower bring their users' rows current), for a rolling
+ * 1/cap slice of the table every step (so every row at least once per `cap` steps), and for all
+ * rows on dcue_embedding_flush. After a flush the table and both moments are
  * bit-identical to the dense sweep's; between flushes rows outside recent batches lag behind, so
  * read the table directly only after a flush. The [cap][8] float history follows this header. */
 typedef struct dcue_emb_log {
