@@ -147,7 +147,7 @@ struct Ws {
   float *du, *dfcopy, *df;
   float* g[6];
   float *dh1, *de;
-  float *wpart[2], *bpart[2], *G, *S;  // wgrad partials: one set per wgrad stream
+  float *wpart[3], *bpart[3], *G, *S;  // wgrad partials: one set per wgrad stream
 };
 
 size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
@@ -198,7 +198,7 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
     if (e > wp) wp = e;
     if (nch * 5 * cout > bp) bp = nch * 5 * cout;
   }
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < 3; ++i) {
     w->wpart[i] = ar.take<float>(wp);
     w->bpart[i] = ar.take<float>(bp);
   }
@@ -444,13 +444,14 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   if (!sp) return DCUE_ERR_HIP;
   hipStream_t su = sp->st[0];
   // the user tower runs beside the item tower; the item tower's chain is issued first
+  if (m->emb_step && o.sync_users) TRY(launch_emb_sync(m, o.sync_users, b->n_rows, su));
   hipEvent_t ev_in = nullptr;
   TRY(fork_point(sp, s, &ev_in));
   if (!o.prologue_done) TRY(launch_item_counts(b, w.counts, s));
   TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s,
                    o.prologue_done));
   TRY(wait_point(su, ev_in));
-  if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
+  if (m->emb_step && !o.sync_users) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
   TRY(user_forward(c, w, b->users, b->n_rows, nullptr, su));
   TRY(stream_wait(sp, s, su));
   if (o.fuse_score)
@@ -494,7 +495,8 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   if (o.emb_adam && (o.emb_adam->parts & ~DCUE_ADAM_EMBEDDING)) return DCUE_ERR_INVALID;
   SidePool* sp = side_pool();
   if (!sp) return DCUE_ERR_HIP;
-  hipStream_t su = sp->st[0], sw[2] = {sp->st[1], sp->st[2]};
+  // layer 1's weight gradient (the step's tail) runs on the caller's stream right after the chain
+  hipStream_t su = sp->st[0], sw[3] = {sp->st[1], sp->st[2], s};
 
   // Host issue order follows the critical path: the main stream's chain (item grads -> fc -> the
   // dgrad chain) is enqueued first, recording a fork point before each layer; the side streams'
@@ -594,8 +596,8 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     const LayerGeom gm = layer_geom(l);
     const int C = l == 5 ? D : H;
     const int cin = l == 1 ? kMels : H;
-    hipStream_t so = sw[l & 1];
-    TRY(wait_point(so, ev_layer[l]));
+    hipStream_t so = l == 1 ? sw[2] : sw[l & 1];
+    if (so != s) TRY(wait_point(so, ev_layer[l]));
     WgradArgs wa = {};
     wa.xsrc = l == 1 ? t->data : (const void*)w.y[l - 1];
     wa.item_track = b->item_track;
@@ -607,7 +609,8 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     wa.dz_acc = bn_acc(w.bnbacc, w.cmax, l); wa.dgamma = c.Gd(seg_bn_w(l)); wa.dbeta = c.Gd(seg_bn_b(l));
     wa.invN = (float)(1.0 / (copies * gm.lp)); wa.counts = w.counts;
     wa.M = M; wa.cout = C; wa.cin = cin;
-    wa.wpart = w.wpart[l & 1]; wa.bpart = w.bpart[l & 1];
+    const int ps = l == 1 ? 2 : (l & 1);  // partial set of the stream the layer runs on
+    wa.wpart = w.wpart[ps]; wa.bpart = w.bpart[ps];
     const int nch = wgrad_nchunk(l, M, C, cin);
     TimerScope tsc;
     TRY(timer_begin(&tsc, l == 1 ? DCUE_TIMED_CONV1_WGRAD : -1, so));

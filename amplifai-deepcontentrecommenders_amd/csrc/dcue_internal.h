@@ -192,6 +192,9 @@ std::vector<CapturedTimer> timer_take_captured();
 
 // side streams (capi.hip): three per device, plus a ring of fork/join events
 struct SidePool {
+  // st[0]: user tower + user-table Adam; st[1], st[2]: weight gradients of layers 5..2
+  // (alternating). Three side streams + the caller's = the box's 4 hardware queues: a fifth stream
+  // would share a queue with another and serialize behind it.
   hipStream_t st[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev[32] = {};
   int next = 0;
@@ -206,6 +209,8 @@ struct StepOpts {
   bool prologue_done = false;  // counts written + accumulators (and ticket) cleared by the prologue
   bool fuse_score = false;     // train forward also runs the hinge backward (k_score_fused)
   const dcue_adam_args* emb_adam = nullptr;  // backward: also step the user table (parts = EMBEDDING)
+  const int64_t* sync_users = nullptr;  // forward: bring these users' rows current first, without
+                                        // waiting for anything else on the caller's stream
 };
 int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
                  int train, float margin, const StepOpts& o, hipStream_t s);

@@ -38,11 +38,14 @@ namespace {
 // the rest of the backward.
 int issue_step(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
                const dcue_plan_config* cfg, const int64_t* users_src, const int32_t* items_src,
-               hipStream_t s, const dcue_adam_args* emb_adam = nullptr) {
+               hipStream_t s, const dcue_adam_args* emb_adam = nullptr, bool captured = false) {
   dcue::StepOpts o;
   o.prologue_done = true;
   o.fuse_score = true;
   o.emb_adam = emb_adam;
+  // the user rows' sync starts with the step (eager only: under capture a side stream joins the
+  // graph only through an event of the capturing stream)
+  if (!captured) o.sync_users = users_src ? users_src : b->users;
   int st = dcue::step_prologue(m, b, ws, ws_bytes,
                                (cfg->flags & DCUE_PLAN_SAMPLE_INBATCH) ? cfg->mt : nullptr, users_src,
                                items_src, s);
@@ -53,7 +56,7 @@ int issue_step(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, v
 
 int capture(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
             const dcue_plan_config* cfg, hipStream_t cs) {
-  return issue_step(m, b, t, ws, ws_bytes, cfg, nullptr, nullptr, cs);
+  return issue_step(m, b, t, ws, ws_bytes, cfg, nullptr, nullptr, cs, nullptr, /*captured=*/true);
 }
 
 }  // namespace
