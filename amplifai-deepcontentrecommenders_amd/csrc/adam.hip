@@ -136,10 +136,24 @@ __global__ __launch_bounds__(256) void k_emb_sync(float* __restrict__ p, float* 
   float* pr = p + u * E;
   float* mr = m + u * E;
   float* vr = v + u * E;
-  for (int k = threadIdx.x; k < E; k += blockDim.x) {
-    float pp = pr[k], mm = mr[k], vv = vr[k];
-    for (int j = from + 1; j <= T; ++j) adam_replay(pp, mm, vv, hs[j % cap], gz);
-    pr[k] = pp; mr[k] = mm; vr[k] = vv;
+  if ((E & 3) == 0) {  // four independent chains per thread (the replay is a long dependent chain)
+    for (int k4 = threadIdx.x; k4 < (E >> 2); k4 += blockDim.x) {
+      float4 pp = ld4(pr + 4 * k4), mm = ld4(mr + 4 * k4), vv = ld4(vr + 4 * k4);
+      for (int j = from + 1; j <= T; ++j) {
+        const AdamScalars s = hs[j % cap];
+        adam_replay(pp.x, mm.x, vv.x, s, gz);
+        adam_replay(pp.y, mm.y, vv.y, s, gz);
+        adam_replay(pp.z, mm.z, vv.z, s, gz);
+        adam_replay(pp.w, mm.w, vv.w, s, gz);
+      }
+      st4(pr + 4 * k4, pp); st4(mr + 4 * k4, mm); st4(vr + 4 * k4, vv);
+    }
+  } else {
+    for (int k = threadIdx.x; k < E; k += blockDim.x) {
+      float pp = pr[k], mm = mr[k], vv = vr[k];
+      for (int j = from + 1; j <= T; ++j) adam_replay(pp, mm, vv, hs[j % cap], gz);
+      pr[k] = pp; mr[k] = mm; vr[k] = vv;
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) {

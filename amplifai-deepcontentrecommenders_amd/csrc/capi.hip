@@ -35,14 +35,22 @@ SidePool* side_pool() {
 }
 
 // A point on `from` that other streams can wait for later (wait_point): a ring event is recorded
-// now. The ring (32) is long enough that no event is re-recorded before its waits are enqueued
+// now. The ring is long enough that no event is re-recorded before its waits are enqueued
 // (a step records fewer than 16 points).
 int fork_point(SidePool* p, hipStream_t from, hipEvent_t* ev) {
   hipEvent_t e = p->ev[p->next];
-  p->next = (p->next + 1) % 32;
+  p->next = (p->next + 1) % SidePool::kEvents;
   DCUE_HIP_CHECK(hipEventRecord(e, from));
   *ev = e;
   return DCUE_OK;
+}
+
+// Plans leave the user table's Adam step (and its rolling flush slice) running on the user stream
+// past the end of a step; entry points that touch the table from the caller's stream join it first.
+int join_user_stream(hipStream_t s) {
+  SidePool* sp = side_pool();
+  if (!sp) return DCUE_ERR_HIP;
+  return stream_wait(sp, s, sp->st[0]);
 }
 
 int wait_point(hipStream_t to, hipEvent_t ev) {
@@ -54,7 +62,7 @@ int wait_point(hipStream_t to, hipEvent_t ev) {
 // wait on its previous record has been enqueued, so a small ring of events suffices.
 int stream_wait(SidePool* p, hipStream_t to, hipStream_t from) {
   hipEvent_t e = p->ev[p->next];
-  p->next = (p->next + 1) % 32;
+  p->next = (p->next + 1) % SidePool::kEvents;
   DCUE_HIP_CHECK(hipEventRecord(e, from));
   DCUE_HIP_CHECK(hipStreamWaitEvent(to, e, 0));
   return DCUE_OK;
@@ -495,8 +503,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   if (o.emb_adam && (o.emb_adam->parts & ~DCUE_ADAM_EMBEDDING)) return DCUE_ERR_INVALID;
   SidePool* sp = side_pool();
   if (!sp) return DCUE_ERR_HIP;
-  // layer 1's weight gradient (the step's tail) runs on the caller's stream right after the chain
-  hipStream_t su = sp->st[0], sw[3] = {sp->st[1], sp->st[2], s};
+  hipStream_t su = sp->st[0], sw[2] = {sp->st[1], sp->st[2]};
 
   // Host issue order follows the critical path: the main stream's chain (item grads -> fc -> the
   // dgrad chain) is enqueued first, recording a fork point before each layer; the side streams'
@@ -538,7 +545,53 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(launch_conv_dgrad(l, l == 5 ? D : H, ra, s));
   }
   TRY(fork_point(sp, s, &ev_layer[1]));
+  // conv weight gradient of layer l on stream `so` (its own split-K partial set `ps`)
+  auto issue_wgrad = [&](int l, hipStream_t so, int ps) -> int {
+    const LayerGeom gm = layer_geom(l);
+    const int C = l == 5 ? D : H;
+    const int cin = l == 1 ? kMels : H;
+    if (so != s) TRY(wait_point(so, ev_layer[l]));
+    WgradArgs wa = {};
+    wa.xsrc = l == 1 ? t->data : (const void*)w.y[l - 1];
+    wa.item_track = b->item_track;
+    wa.x_mean = w.mean[l - 1];
+    wa.x_a = l == 1 ? w.invstd[0] : w.a[l - 1];
+    wa.x_beta = l == 1 ? nullptr : c.P(seg_bn_b(l - 1));
+    wa.g_l = w.g[l]; wa.y_l = w.y[l]; wa.idx_l = w.idx[l];
+    wa.mean_l = w.mean[l]; wa.invstd_l = w.invstd[l]; wa.a_l = w.a[l];
+    wa.dz_acc = bn_acc(w.bnbacc, w.cmax, l); wa.dgamma = c.Gd(seg_bn_w(l)); wa.dbeta = c.Gd(seg_bn_b(l));
+    wa.invN = (float)(1.0 / (copies * gm.lp)); wa.counts = w.counts;
+    wa.M = M; wa.cout = C; wa.cin = cin;
+    wa.wpart = w.wpart[ps]; wa.bpart = w.bpart[ps];
+    const int nch = wgrad_nchunk(l, M, C, cin);
+    TimerScope tsc;
+    TRY(timer_begin(&tsc, l == 1 ? DCUE_TIMED_CONV1_WGRAD : -1, so));
+    TRY(launch_conv_wgrad(l, l == 1 ? src : SRC_ACT, wa, nch, so));
+    TRY(timer_end(&tsc));
+    TRY(launch_wgrad_reduce(l, wa.wpart, wa.bpart, nch, C, cin, c.Gd(seg_conv_w(l)),
+                            c.Gd(seg_conv_b(l)), w.G, w.S, so));
+    if (l == 1)
+      TRY(launch_bn0_grads(w.G, w.S, c.P(seg_conv_w(1)), c.P(seg_bn_w(0)), c.P(seg_bn_b(0)), H,
+                           c.Gd(seg_conv_w(1)), c.Gd(seg_bn_w(0)), c.Gd(seg_bn_b(0)),
+                           c.Gd(seg_conv_b(1)), so));
+    return DCUE_OK;
+  };
+  // layer 1 (the step's tail) follows the chain on the caller's stream, issued right away
+  TRY(issue_wgrad(1, s, 2));
 
+  {  // fc weight gradient: dW[n][k] = sum_m df[m][n] bn5(y5)[m][k], db = sum_m df
+    TRY(wait_point(sw[0], ev_df));
+    TGemmArgs g = {};
+    g.M = D; g.N = D; g.K = M;
+    g.A = w.df; g.sam = 1; g.sak = D;
+    g.B = w.y[5]; g.sbk = D; g.sbn = 1;
+    g.bmean = w.mean[5]; g.ba = w.a[5]; g.bbeta = c.P(seg_bn_b(5));
+    g.C = c.Gd(SEG_FC_W); g.scm = D; g.scn = 1;
+    g.rowsum = c.Gd(SEG_FC_B);
+    TRY(launch_tgemm(0, 2, g, sw[0]));
+  }
+  // layers 5..2: alternating between the two wgrad streams (each with its own partial set)
+  for (int l = 5; l >= 2; --l) TRY(issue_wgrad(l, sw[l & 1], l & 1));
   // user tower (userembedding.py:33-44 backward), the compact embedding rows, and -- when the step
   // carries it -- the user table's Adam step (it needs nothing from the item tower)
   TRY(wait_point(su, ev_score));
@@ -578,52 +631,14 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   }
   TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, m->emb_rows,
                       m->emb_step ? m->emb_log : nullptr, su));
+  // the step's end joins the user stream here: its Adam part (and the rolling flush slice) below
+  // needs nothing more from this step and runs on into the next one, ordered on this stream
+  hipEvent_t ev_user = nullptr;
+  TRY(fork_point(sp, su, &ev_user));
   if (o.emb_adam) TRY(launch_adam(m, o.emb_adam, c.poff, su));
 
-  {  // fc weight gradient: dW[n][k] = sum_m df[m][n] bn5(y5)[m][k], db = sum_m df
-    TRY(wait_point(sw[0], ev_df));
-    TGemmArgs g = {};
-    g.M = D; g.N = D; g.K = M;
-    g.A = w.df; g.sam = 1; g.sak = D;
-    g.B = w.y[5]; g.sbk = D; g.sbn = 1;
-    g.bmean = w.mean[5]; g.ba = w.a[5]; g.bbeta = c.P(seg_bn_b(5));
-    g.C = c.Gd(SEG_FC_W); g.scm = D; g.scn = 1;
-    g.rowsum = c.Gd(SEG_FC_B);
-    TRY(launch_tgemm(0, 2, g, sw[0]));
-  }
-  // conv weight gradients, alternating between the two wgrad streams (each with its own partials)
-  for (int l = 5; l >= 1; --l) {
-    const LayerGeom gm = layer_geom(l);
-    const int C = l == 5 ? D : H;
-    const int cin = l == 1 ? kMels : H;
-    hipStream_t so = l == 1 ? sw[2] : sw[l & 1];
-    if (so != s) TRY(wait_point(so, ev_layer[l]));
-    WgradArgs wa = {};
-    wa.xsrc = l == 1 ? t->data : (const void*)w.y[l - 1];
-    wa.item_track = b->item_track;
-    wa.x_mean = w.mean[l - 1];
-    wa.x_a = l == 1 ? w.invstd[0] : w.a[l - 1];
-    wa.x_beta = l == 1 ? nullptr : c.P(seg_bn_b(l - 1));
-    wa.g_l = w.g[l]; wa.y_l = w.y[l]; wa.idx_l = w.idx[l];
-    wa.mean_l = w.mean[l]; wa.invstd_l = w.invstd[l]; wa.a_l = w.a[l];
-    wa.dz_acc = bn_acc(w.bnbacc, w.cmax, l); wa.dgamma = c.Gd(seg_bn_w(l)); wa.dbeta = c.Gd(seg_bn_b(l));
-    wa.invN = (float)(1.0 / (copies * gm.lp)); wa.counts = w.counts;
-    wa.M = M; wa.cout = C; wa.cin = cin;
-    const int ps = l == 1 ? 2 : (l & 1);  // partial set of the stream the layer runs on
-    wa.wpart = w.wpart[ps]; wa.bpart = w.bpart[ps];
-    const int nch = wgrad_nchunk(l, M, C, cin);
-    TimerScope tsc;
-    TRY(timer_begin(&tsc, l == 1 ? DCUE_TIMED_CONV1_WGRAD : -1, so));
-    TRY(launch_conv_wgrad(l, l == 1 ? src : SRC_ACT, wa, nch, so));
-    TRY(timer_end(&tsc));
-    TRY(launch_wgrad_reduce(l, wa.wpart, wa.bpart, nch, C, cin, c.Gd(seg_conv_w(l)),
-                            c.Gd(seg_conv_b(l)), w.G, w.S, so));
-    if (l == 1)
-      TRY(launch_bn0_grads(w.G, w.S, c.P(seg_conv_w(1)), c.P(seg_bn_w(0)), c.P(seg_bn_b(0)), H,
-                           c.Gd(seg_conv_w(1)), c.Gd(seg_bn_w(0)), c.Gd(seg_bn_b(0)),
-                           c.Gd(seg_conv_b(1)), so));
-  }
-  for (hipStream_t x : {su, sw[0], sw[1]}) TRY(stream_wait(sp, s, x));
+  TRY(wait_point(s, ev_user));
+  for (hipStream_t x : {sw[0], sw[1]}) TRY(stream_wait(sp, s, x));
   return DCUE_OK;
 }
 
@@ -641,6 +656,7 @@ int dcue_adam_step(const dcue_model* m, const dcue_adam_args* a, void* stream) {
       (!m->emb || !m->emb_exp_avg || !m->emb_exp_avg_sq || !m->emb_slot || !m->emb_grad))
     return DCUE_ERR_INVALID;
   if ((parts & DCUE_ADAM_EMBEDDING) && m->emb_step && !m->emb_rows) return DCUE_ERR_INVALID;
+  if (parts & DCUE_ADAM_EMBEDDING) TRY(join_user_stream((hipStream_t)stream));
   TRY(launch_adam(m, a, c.poff, (hipStream_t)stream));
   if (parts & DCUE_ADAM_DENSE) return launch_pack(m, c.poff, (hipStream_t)stream);
   return DCUE_OK;
@@ -667,6 +683,7 @@ int dcue_user_tower(const dcue_model* m, const int64_t* users, int32_t n, void* 
   Ws w;
   if (carve(&m->dims, n, 0, 1, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
   carve(&m->dims, n, 0, 1, ws, &w);
+  TRY(join_user_stream((hipStream_t)stream));
   if (m->emb_step) TRY(launch_emb_sync(m, users, n, (hipStream_t)stream));
   return user_forward(c, w, users, n, user_feat, (hipStream_t)stream);
 }
@@ -683,6 +700,7 @@ int dcue_emb_log_init(const dcue_model* m, int32_t cap, int32_t step, void* stre
   if (!m->emb_step || !m->emb_log || cap < 1 || cap > DCUE_MAX_LOG_CAP || cap != m->emb_log_cap ||
       step < 0)
     return DCUE_ERR_INVALID;
+  TRY(join_user_stream((hipStream_t)stream));
   return launch_emb_log_init(m, cap, step, (hipStream_t)stream);
 }
 
@@ -691,6 +709,7 @@ int dcue_embedding_sync(const dcue_model* m, const int64_t* users, int32_t n, vo
   TRY(init_ctx(&c, m));
   if (!users || n < 0) return DCUE_ERR_INVALID;
   if (!m->emb_step) return DCUE_OK;  // dense mode: rows are always current
+  TRY(join_user_stream((hipStream_t)stream));
   return launch_emb_sync(m, users, n, (hipStream_t)stream);
 }
 
@@ -698,6 +717,7 @@ int dcue_embedding_flush(const dcue_model* m, void* stream) {
   Ctx c;
   TRY(init_ctx(&c, m));
   if (!m->emb_step) return DCUE_OK;
+  TRY(join_user_stream((hipStream_t)stream));
   return launch_emb_flush(m, (hipStream_t)stream);
 }
 

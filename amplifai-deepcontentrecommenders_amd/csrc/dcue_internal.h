@@ -196,13 +196,15 @@ struct SidePool {
   // (alternating). Three side streams + the caller's = the box's 4 hardware queues: a fifth stream
   // would share a queue with another and serialize behind it.
   hipStream_t st[3] = {nullptr, nullptr, nullptr};
-  hipEvent_t ev[32] = {};
+  static constexpr int kEvents = 512;
+  hipEvent_t ev[kEvents] = {};
   int next = 0;
 };
 SidePool* side_pool();
 int stream_wait(SidePool* p, hipStream_t to, hipStream_t from);
 int fork_point(SidePool* p, hipStream_t from, hipEvent_t* ev);
 int wait_point(hipStream_t to, hipEvent_t ev);
+int join_user_stream(hipStream_t s);
 
 // ------------------------------------------------------------- step implementation (capi.hip)
 struct StepOpts {
