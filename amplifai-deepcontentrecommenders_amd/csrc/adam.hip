@@ -55,6 +55,62 @@ __device__ __forceinline__ void adam_replay(float& p, float& m, float& v, const 
     adam_elem(p, gz, m, v, s);
 }
 
+struct PackSeg {
+  long src, fwd, bwd;  // floats: W in params; forward pack; dgrad pack (-1: none)
+  int cout, cin, ks;
+};
+struct PackArgs;
+PackArgs pack_args(const dcue_model* md, const int64_t* poff);
+struct PackArgs {
+  PackSeg seg[5];
+};
+
+// Packed position of element e of conv segment sg (W[o][c][k], k fastest): the forward B operand
+// [k][cin/4][cout][4] and (layers >= 2) the dgrad one [ks-1-k][cout/4][cin][4].
+__device__ __forceinline__ void pack_store(const PackSeg& sg, long e, float w, float* wpack) {
+  const long ks = sg.ks;
+  const long o = e / ((long)sg.cin * ks);
+  const long rem = e - o * sg.cin * ks;
+  const long cc = rem / ks, k = rem - cc * ks;
+  wpack[sg.fwd + (((k * (sg.cin / 4) + cc / 4) * sg.cout + o) * 4 + (cc & 3))] = w;
+  if (sg.bwd >= 0) {
+    const long kr = sg.ks - 1 - k;
+    wpack[sg.bwd + (((kr * (sg.cout / 4) + o / 4) * sg.cin + cc) * 4 + (o & 3))] = w;
+  }
+}
+
+// Adam over the flat dense buffer with the conv-weight repack fused in: a float4 that lies in a
+// conv weight segment (segments are 4-float aligned) also writes its four packed copies.
+__global__ __launch_bounds__(256) void k_adam_dense_pack(float* __restrict__ p, const float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v,
+                                                         long n, AdamScalars s, PackArgs pa,
+                                                         float* __restrict__ wpack) {
+  const long n4 = n / 4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float4 pp = ld4(p + 4 * i), gg = ld4(g + 4 * i), mm = ld4(m + 4 * i), vv = ld4(v + 4 * i);
+    adam_elem(pp.x, gg.x, mm.x, vv.x, s);
+    adam_elem(pp.y, gg.y, mm.y, vv.y, s);
+    adam_elem(pp.z, gg.z, mm.z, vv.z, s);
+    adam_elem(pp.w, gg.w, mm.w, vv.w, s);
+    st4(p + 4 * i, pp); st4(m + 4 * i, mm); st4(v + 4 * i, vv);
+    const long e0 = 4 * i;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      const PackSeg& sg = pa.seg[q];
+      const long len = (long)sg.cout * sg.cin * sg.ks;
+      if (e0 >= sg.src && e0 < sg.src + len) {
+        const long e = e0 - sg.src;
+        pack_store(sg, e + 0, pp.x, wpack);
+        pack_store(sg, e + 1, pp.y, wpack);
+        pack_store(sg, e + 2, pp.z, wpack);
+        pack_store(sg, e + 3, pp.w, wpack);
+      }
+    }
+  }
+  for (long i = 4 * n4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    adam_elem(p[i], g[i], m[i], v[i], s);  // tail past the last float4: never a conv weight
+}
+
 __global__ __launch_bounds__(256) void k_adam_dense(float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     long n, AdamScalars s) {
@@ -360,9 +416,9 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
   sc.inv_bc2_sqrt = 1.0f / sc.bc2_sqrt;  // IEEE single division on the host: RN(1/bc2_sqrt)
   const int parts = a->parts ? a->parts : (DCUE_ADAM_DENSE | DCUE_ADAM_EMBEDDING);
   const long n = poff[DCUE_N_DENSE_SEGMENTS];
-  if (parts & DCUE_ADAM_DENSE) {
-    hipLaunchKernelGGL(k_adam_dense, dim3(512), dim3(256), 0, s, md->params, md->grads, md->exp_avg,
-                       md->exp_avg_sq, n, sc);
+  if (parts & DCUE_ADAM_DENSE) {  // Adam + the conv-weight repack in one sweep
+    hipLaunchKernelGGL(k_adam_dense_pack, dim3(512), dim3(256), 0, s, md->params, md->grads, md->exp_avg,
+                       md->exp_avg_sq, n, sc, pack_args(md, poff), md->wpack);
     DCUE_LAUNCH_CHECK();
   }
   if ((parts & DCUE_ADAM_EMBEDDING) && md->emb_step) {
@@ -389,14 +445,6 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
 // ------------------------------------------------------------------------- weight packing
 // conv layer l forward B operand: [k][cin/4][cout][4]; dgrad (l >= 2): [k'][cout/4][cin][4] with
 // k' = ks-1-k.
-struct PackSeg {
-  long src, fwd, bwd;  // floats: W in params; forward pack; dgrad pack (-1: none)
-  int cout, cin, ks;
-};
-struct PackArgs {
-  PackSeg seg[5];
-};
-
 __global__ void k_pack(const float* __restrict__ params, float* wpack, PackArgs pa) {
   const PackSeg sg = pa.seg[blockIdx.y];
   const long ks = sg.ks;
@@ -414,7 +462,7 @@ __global__ void k_pack(const float* __restrict__ params, float* wpack, PackArgs 
   }
 }
 
-int launch_pack(const dcue_model* md, const int64_t* poff, hipStream_t s) {
+PackArgs pack_args(const dcue_model* md, const int64_t* poff) {
   const int H = md->dims.conv_hidden, d = md->dims.feature_dim;
   const WpackLayout wl = wpack_layout(&md->dims);
   PackArgs pa;
@@ -427,6 +475,11 @@ int launch_pack(const dcue_model* md, const int64_t* poff, hipStream_t s) {
     sg.fwd = wl.conv_fwd[l];
     sg.bwd = l >= 2 ? wl.conv_bwd[l] : -1;
   }
+  return pa;
+}
+
+int launch_pack(const dcue_model* md, const int64_t* poff, hipStream_t s) {
+  const PackArgs pa = pack_args(md, poff);
   hipLaunchKernelGGL(k_pack, dim3(64, 5), dim3(256), 0, s, md->params, md->wpack, pa);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;

@@ -516,18 +516,10 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
                          w.dfcopy, s));
   hipEvent_t ev_score = nullptr, ev_df = nullptr, ev_layer[6] = {};
   TRY(fork_point(sp, s, &ev_score));
-  TRY(launch_item_grad(w.dfcopy, b, D, w.df, s));
+  // per-item feature gradients df, then (same kernel) the fc input gradient g5 = df W and BN5's sums
+  TRY(launch_item_grad(w.dfcopy, b, D, w.df, c.P(SEG_FC_W), w.g[5], bn_acc(w.bnbacc, w.cmax, 5), w.y[5],
+                       w.mean[5], w.invstd[5], s));
   TRY(fork_point(sp, s, &ev_df));
-  {  // g5 = df W (fc input gradient) + BN5 backward sums of g5
-    TGemmArgs g = {};
-    g.M = M; g.N = D; g.K = D;
-    g.A = w.df; g.sam = D; g.sak = 1;
-    g.B = c.P(SEG_FC_W); g.sbk = D; g.sbn = 1;
-    g.C = w.g[5]; g.scm = D; g.scn = 1;
-    g.colacc = bn_acc(w.bnbacc, w.cmax, 5);
-    g.xy = w.y[5]; g.xmean = w.mean[5]; g.xinvstd = w.invstd[5];
-    TRY(launch_tgemm(0, 0, g, s));
-  }
   for (int l = 5; l >= 2; --l) {  // dgrad chain: g_l (+ BN_l sums) -> g_{l-1} (+ BN_{l-1} sums)
     const LayerGeom gm = layer_geom(l);
     TRY(fork_point(sp, s, &ev_layer[l]));
@@ -658,7 +650,7 @@ int dcue_adam_step(const dcue_model* m, const dcue_adam_args* a, void* stream) {
   if ((parts & DCUE_ADAM_EMBEDDING) && m->emb_step && !m->emb_rows) return DCUE_ERR_INVALID;
   if (parts & DCUE_ADAM_EMBEDDING) TRY(join_user_stream((hipStream_t)stream));
   TRY(launch_adam(m, a, c.poff, (hipStream_t)stream));
-  if (parts & DCUE_ADAM_DENSE) return launch_pack(m, c.poff, (hipStream_t)stream);
+  // the dense sweep repacked the conv weights as it went (k_adam_dense_pack)
   return DCUE_OK;
 }
 

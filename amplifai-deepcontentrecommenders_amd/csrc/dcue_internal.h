@@ -159,7 +159,10 @@ int launch_score_fused(const float* uf, const float* f, const dcue_batch* b, int
 int launch_score_bwd(const float* uf, const float* f, const dcue_batch* b, int d,
                      const float* dscores, const float* cosv, const float* norms, float* du,
                      float* dfcopy, hipStream_t s);
-int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df, hipStream_t s);
+// per-item feature gradients; with fcW also the fc input gradient g5 = df W and BN5's backward sums
+int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df, const float* fcW, float* g5,
+                     unsigned long long* acc5, const float* y5, const float* mean5, const float* invstd5,
+                     hipStream_t s);
 int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float scale,
                     float* emb_grad, int32_t* slot, int64_t* emb_rows, dcue_emb_log* log,
                     hipStream_t s);

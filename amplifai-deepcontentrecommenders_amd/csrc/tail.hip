@@ -472,85 +472,115 @@ constexpr int kItemGradCap = 4096;  // copies per item (B*N + 1 in gather layout
 // df[i] = sum over item i's copies. One workgroup per item: wave 0 lists the item's copies in
 // (positive, (b,j) row-major) order with ballots over neg_item (loads batched ahead of the ballots);
 // the four waves then each sum a contiguous quarter of the list with all its row loads in flight,
-// and the quarters are added in wave order (deterministic).
+// and the quarters are added in wave order (deterministic). With `fc` set the fc input gradient of
+// the item follows in the same workgroup -- g5[i][n] = sum_k df[i][k] W[k][n] (k in order) -- with
+// its share of BN5's backward sums (sum g5, sum g5*xhat5) into the accumulators.
+struct ItemGradFc {
+  const float* W;          // fc.weight [d][d] (null: df only)
+  float* g5;               // [M][d]
+  unsigned long long* acc; // BN5 backward accumulators [2][d]
+  const float *y5, *mean5, *invstd5;
+};
+
 __global__ __launch_bounds__(256) void k_item_grad(const float* __restrict__ dfcopy, dcue_batch b, int d,
-                                                   float* df) {
+                                                   float* df, ItemGradFc fc) {
   constexpr int kCap = kItemGradCap;
   __shared__ int list[kCap];
   __shared__ int s_len;
   __shared__ float part[4][256];
+  __shared__ float dfs[256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = blockIdx.x;
   const int N = b.n_neg, B = b.n_rows;
   if (b.layout == DCUE_LAYOUT_CATALOGUE) {
     const long cidx = i < B ? (long)i * (N + 1) : (long)((i - B) / N) * (N + 1) + 1 + (i - B) % N;
-    for (int k = threadIdx.x; k < d; k += blockDim.x) df[(long)i * d + k] = dfcopy[cidx * d + k];
-    return;
-  }
-  if (wave == 0) {
-    int len = 0;
-    if (i < B) {
-      if (lane == 0) list[0] = i * (N + 1);
-      len = 1;
+    for (int k = threadIdx.x; k < d; k += blockDim.x) {
+      const float v = dfcopy[cidx * d + k];
+      df[(long)i * d + k] = v;
+      dfs[k] = v;
     }
-    const int nneg = B * N;
-    constexpr int kBatch = 16;
-    for (int e0 = 0; e0 < nneg; e0 += 64 * kBatch) {
-      int32_t v[kBatch];
-#pragma unroll
-      for (int q = 0; q < kBatch; ++q) {
-        const int e = e0 + 64 * q + lane;
-        v[q] = e < nneg ? b.neg_item[e] : -1;
+  } else {
+    if (wave == 0) {
+      int len = 0;
+      if (i < B) {
+        if (lane == 0) list[0] = i * (N + 1);
+        len = 1;
       }
+      const int nneg = B * N;
+      constexpr int kBatch = 16;
+      for (int e0 = 0; e0 < nneg; e0 += 64 * kBatch) {
+        int32_t v[kBatch];
 #pragma unroll
-      for (int q = 0; q < kBatch; ++q) {
-        const int e = e0 + 64 * q + lane;
-        const bool hit = v[q] == i;
-        const unsigned long long bal = __ballot(hit);
-        const int pos = len + __popcll(bal & ((1ull << lane) - 1ull));
-        if (hit && pos < kCap) {
-          const int row = e / N;
-          list[pos] = row * (N + 1) + 1 + (e - row * N);
+        for (int q = 0; q < kBatch; ++q) {
+          const int e = e0 + 64 * q + lane;
+          v[q] = e < nneg ? b.neg_item[e] : -1;
         }
-        len += __popcll(bal);
+#pragma unroll
+        for (int q = 0; q < kBatch; ++q) {
+          const int e = e0 + 64 * q + lane;
+          const bool hit = v[q] == i;
+          const unsigned long long bal = __ballot(hit);
+          const int pos = len + __popcll(bal & ((1ull << lane) - 1ull));
+          if (hit && pos < kCap) {
+            const int row = e / N;
+            list[pos] = row * (N + 1) + 1 + (e - row * N);
+          }
+          len += __popcll(bal);
+        }
       }
+      if (lane == 0) s_len = len < kCap ? len : kCap;
     }
-    if (lane == 0) s_len = len < kCap ? len : kCap;
+    __syncthreads();
+    const int len = s_len;
+    const int q0 = (len * wave) / 4, q1 = (len * (wave + 1)) / 4;  // this wave's quarter
+    const int per = (d + 63) / 64;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    constexpr int kRows = 8;
+    for (int qb = q0; qb < q1; qb += kRows) {
+      float v[kRows][4];
+#pragma unroll
+      for (int r = 0; r < kRows; ++r)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = lane + 64 * e;
+          v[r][e] = (qb + r < q1 && e < per && k < d) ? dfcopy[(long)list[qb + r] * d + k] : 0.f;
+        }
+#pragma unroll
+      for (int r = 0; r < kRows; ++r)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] += v[r][e];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = lane + 64 * e;
+      if (e < per && k < d) part[wave][k] = acc[e];
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < d; k += blockDim.x) {
+      const float v = ((part[0][k] + part[1][k]) + part[2][k]) + part[3][k];
+      df[(long)i * d + k] = v;
+      dfs[k] = v;
+    }
   }
+  if (!fc.W) return;
   __syncthreads();
-  const int len = s_len;
-  const int q0 = (len * wave) / 4, q1 = (len * (wave + 1)) / 4;  // this wave's quarter
-  const int per = (d + 63) / 64;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  constexpr int kRows = 8;
-  for (int qb = q0; qb < q1; qb += kRows) {
-    float v[kRows][4];
-#pragma unroll
-    for (int r = 0; r < kRows; ++r)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = lane + 64 * e;
-        v[r][e] = (qb + r < q1 && e < per && k < d) ? dfcopy[(long)list[qb + r] * d + k] : 0.f;
-      }
-#pragma unroll
-    for (int r = 0; r < kRows; ++r)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc[e] += v[r][e];
+  for (int n = threadIdx.x; n < d; n += blockDim.x) {
+    float g = 0.f;
+    for (int k = 0; k < d; ++k) g += dfs[k] * fc.W[(long)k * d + n];
+    fc.g5[(long)i * d + n] = g;
+    const float xh = (fc.y5[(long)i * d + n] - fc.mean5[n]) * fc.invstd5[n];
+    acc128_add(acc_at(fc.acc, d, 0, n), g);
+    acc128_add(acc_at(fc.acc, d, 1, n), g * xh);
   }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int k = lane + 64 * e;
-    if (e < per && k < d) part[wave][k] = acc[e];
-  }
-  __syncthreads();
-  for (int k = threadIdx.x; k < d; k += blockDim.x)
-    df[(long)i * d + k] = ((part[0][k] + part[1][k]) + part[2][k]) + part[3][k];
 }
 
-int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df, hipStream_t s) {
+int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df, const float* fcW, float* g5,
+                     unsigned long long* acc5, const float* y5, const float* mean5, const float* invstd5,
+                     hipStream_t s) {
   if (d > 256) return DCUE_ERR_UNSUPPORTED;
   if (b->layout == DCUE_LAYOUT_GATHER && (long)b->n_rows * b->n_neg + 1 > kItemGradCap) return DCUE_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL(k_item_grad, dim3(b->n_items), dim3(256), 0, s, dfcopy, *b, d, df);
+  const ItemGradFc fc = {fcW, g5, acc5, y5, mean5, invstd5};
+  hipLaunchKernelGGL(k_item_grad, dim3(b->n_items), dim3(256), 0, s, dfcopy, *b, d, df, fc);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }

@@ -56,6 +56,9 @@ class TrainPlan:
                                              ctypes.byref(handle)), "dcue_plan_create")
         self._handle = handle
         self._lib = nat.lib()
+        # the stream the plan issues on: torch's current stream at creation (pass stream= to override)
+        self._stream = nat.stream_handle()
+        self._adam_args = nat.AdamArgs()
         # the replayed backward writes the flat gradient: expose the reference-shaped .grad views
         named = dict(net.named_parameters())
         for s, name in enumerate(nat.DENSE_NAMES):
@@ -81,7 +84,7 @@ class TrainPlan:
         self._check_bound()
         st = self._lib.dcue_plan_launch(self._handle, None if users is None else users.data_ptr(),
                                         None if item_track is None else item_track.data_ptr(),
-                                        nat.stream_handle() if stream is None else stream)
+                                        self._stream if stream is None else stream)
         if st != 0:
             nat.check(st, "dcue_plan_launch")
 
@@ -96,11 +99,12 @@ class TrainPlan:
         self._check_bound()
         g = opt.param_groups[0]
         opt.step_count += 1
-        args = nat.AdamArgs(float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]),
-                            float(g["weight_decay"]), opt.step_count, 0)
+        args = self._adam_args
+        args.lr, (args.beta1, args.beta2) = g["lr"], g["betas"]
+        args.eps, args.weight_decay, args.step, args.parts = g["eps"], g["weight_decay"], opt.step_count, 0
         st = self._lib.dcue_plan_step(self._handle, None if users is None else users.data_ptr(),
                                       None if item_track is None else item_track.data_ptr(),
-                                      ctypes.byref(args), nat.stream_handle() if stream is None else stream)
+                                      ctypes.byref(args), self._stream if stream is None else stream)
         if st != 0:
             nat.check(st, "dcue_plan_step")
 
