@@ -318,7 +318,7 @@ int launch_emb_flush_rows(const dcue_model* md, int step, hipStream_t s) {
   if (rpb < 1) rpb = 1;
   if (rpb > 256) rpb = 256;
   const long blocks = (r1 - r0 + rpb - 1) / rpb;
-  hipLaunchKernelGGL(k_emb_flush_rows, dim3((unsigned)blocks), dim3(256), 0, s, md->emb, md->emb_exp_avg,
+  DCUE_LAUNCH(k_emb_flush_rows, dim3((unsigned)blocks), dim3(256), 0, s, md->emb, md->emb_exp_avg,
                      md->emb_exp_avg_sq, md->emb_log, md->emb_step, r0, r1, E, rpb, 0.f);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
@@ -372,14 +372,14 @@ __global__ void k_emb_log_init(dcue_emb_log* hdr, int cap, int step) {
 
 int launch_emb_log_init(const dcue_model* md, int cap, int step, hipStream_t s) {
   DCUE_HIP_CHECK(hipMemsetAsync(md->emb_step, 0, sizeof(int32_t) * md->dims.n_users, s));
-  hipLaunchKernelGGL(k_emb_log_init, dim3(1), dim3(1), 0, s, md->emb_log, cap, step);
+  DCUE_LAUNCH(k_emb_log_init, dim3(1), dim3(1), 0, s, md->emb_log, cap, step);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
 
 int launch_emb_sync(const dcue_model* md, const int64_t* users, int n, hipStream_t s) {
   if (n <= 0) return DCUE_OK;
-  hipLaunchKernelGGL(k_emb_sync, dim3((unsigned)n), dim3(256), 0, s, md->emb, md->emb_exp_avg,
+  DCUE_LAUNCH(k_emb_sync, dim3((unsigned)n), dim3(256), 0, s, md->emb, md->emb_exp_avg,
                      md->emb_exp_avg_sq, md->emb_log, md->emb_step, users, md->dims.user_embdim, 0.f);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
@@ -392,12 +392,12 @@ int launch_emb_flush(const dcue_model* md, hipStream_t s) {
   TimerScope tsc;
   int st = timer_begin(&tsc, DCUE_TIMED_EMB_FLUSH, s);
   if (st) return st;
-  hipLaunchKernelGGL(k_emb_flush, dim3((unsigned)blocks), dim3(256), 0, s, md->emb, md->emb_exp_avg,
+  DCUE_LAUNCH(k_emb_flush, dim3((unsigned)blocks), dim3(256), 0, s, md->emb, md->emb_exp_avg,
                      md->emb_exp_avg_sq, md->emb_log, md->emb_step, (long)md->dims.n_users,
                      md->dims.user_embdim, 0.f);
   DCUE_LAUNCH_CHECK();
   if ((st = timer_end(&tsc))) return st;
-  hipLaunchKernelGGL(k_emb_flush_done, dim3(1), dim3(1), 0, s, md->emb_log);
+  DCUE_LAUNCH(k_emb_flush_done, dim3(1), dim3(1), 0, s, md->emb_log);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
@@ -417,12 +417,12 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
   const int parts = a->parts ? a->parts : (DCUE_ADAM_DENSE | DCUE_ADAM_EMBEDDING);
   const long n = poff[DCUE_N_DENSE_SEGMENTS];
   if (parts & DCUE_ADAM_DENSE) {  // Adam + the conv-weight repack in one sweep
-    hipLaunchKernelGGL(k_adam_dense_pack, dim3(512), dim3(256), 0, s, md->params, md->grads, md->exp_avg,
+    DCUE_LAUNCH(k_adam_dense_pack, dim3(512), dim3(256), 0, s, md->params, md->grads, md->exp_avg,
                        md->exp_avg_sq, n, sc, pack_args(md, poff), md->wpack);
     DCUE_LAUNCH_CHECK();
   }
   if ((parts & DCUE_ADAM_EMBEDDING) && md->emb_step) {
-    hipLaunchKernelGGL(k_adam_touched, dim3(256), dim3(256), 0, s, md->emb, md->emb_exp_avg,
+    DCUE_LAUNCH(k_adam_touched, dim3(256), dim3(256), 0, s, md->emb, md->emb_exp_avg,
                        md->emb_exp_avg_sq, md->emb_grad, md->emb_rows, md->emb_step, md->emb_log,
                        md->dims.user_embdim, a->step, sc, 0.f);
     DCUE_LAUNCH_CHECK();
@@ -433,7 +433,7 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
     TimerScope tsc;
     int st = timer_begin(&tsc, DCUE_TIMED_ADAM_EMBED, s);
     if (st) return st;
-    hipLaunchKernelGGL(k_adam_embed, dim3((unsigned)blocks), dim3(256), 0, s, md->emb,
+    DCUE_LAUNCH(k_adam_embed, dim3((unsigned)blocks), dim3(256), 0, s, md->emb,
                        md->emb_exp_avg, md->emb_exp_avg_sq, md->emb_grad, md->emb_slot,
                        (long)md->dims.n_users, md->dims.user_embdim, sc);
     DCUE_LAUNCH_CHECK();
@@ -480,7 +480,7 @@ PackArgs pack_args(const dcue_model* md, const int64_t* poff) {
 
 int launch_pack(const dcue_model* md, const int64_t* poff, hipStream_t s) {
   const PackArgs pa = pack_args(md, poff);
-  hipLaunchKernelGGL(k_pack, dim3(64, 5), dim3(256), 0, s, md->params, md->wpack, pa);
+  DCUE_LAUNCH(k_pack, dim3(64, 5), dim3(256), 0, s, md->params, md->wpack, pa);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }

@@ -78,10 +78,10 @@ int launch_input_stats(int src, const void* tracks, const int32_t* item_track, c
   const int rpb = (int)((rows + nb - 1) / nb);
   nb = (int)((rows + rpb - 1) / rpb);
   if (src == SRC_TRACK_F16)
-    hipLaunchKernelGGL(k_input_stats<SRC_TRACK_F16>, dim3(nb), dim3(256), 0, s, tracks, item_track,
+    DCUE_LAUNCH(k_input_stats<SRC_TRACK_F16>, dim3(nb), dim3(256), 0, s, tracks, item_track,
                        counts, M, rpb, acc);
   else
-    hipLaunchKernelGGL(k_input_stats<SRC_TRACK_F32>, dim3(nb), dim3(256), 0, s, tracks, item_track,
+    DCUE_LAUNCH(k_input_stats<SRC_TRACK_F32>, dim3(nb), dim3(256), 0, s, tracks, item_track,
                        counts, M, rpb, acc);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
@@ -100,7 +100,7 @@ __global__ void k_bn_eval(int C, const float* gamma, const float* rmean, const f
 
 int launch_bn_eval(int C, const float* gamma, const float* rmean, const float* rvar, float* mean,
                    float* invstd, float* a, hipStream_t s) {
-  hipLaunchKernelGGL(k_bn_eval, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, rmean, rvar, mean, invstd, a);
+  DCUE_LAUNCH(k_bn_eval, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, rmean, rvar, mean, invstd, a);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }

@@ -45,6 +45,50 @@ int fork_point(SidePool* p, hipStream_t from, hipEvent_t* ev) {
   return DCUE_OK;
 }
 
+hipEvent_t ring_event(SidePool* p) {
+  hipEvent_t e = p->ev[p->next];
+  p->next = (p->next + 1) % SidePool::kEvents;
+  return e;
+}
+
+LaunchTag& launch_tag() {
+  thread_local LaunchTag t;
+  return t;
+}
+
+bool& capturing_step() {
+  thread_local bool c = false;
+  return c;
+}
+
+ForkAfter::ForkAfter(SidePool* p, hipStream_t s, hipEvent_t* ev) : s_(s), out_(ev), e_(ring_event(p)) {
+  saved_ = launch_tag();
+  if (!capturing_step()) {
+    launch_tag() = LaunchTag{nullptr, e_, 0, false};
+    armed_ = true;
+  }
+}
+
+void ForkAfter::restore() {
+  if (!armed_) return;
+  const int n = launch_tag().launches;
+  launch_tag() = saved_;
+  if (n && saved_.stop) launch_tag().missed = true;
+  armed_ = false;
+}
+
+int ForkAfter::done() {
+  if (finished_) return DCUE_OK;
+  finished_ = true;
+  const bool bound = armed_ && launch_tag().launches > 0 && !launch_tag().missed;
+  restore();
+  if (!bound) DCUE_HIP_CHECK(hipEventRecord(e_, s_));
+  *out_ = e_;
+  return DCUE_OK;
+}
+
+ForkAfter::~ForkAfter() { restore(); }
+
 // Plans leave the user table's Adam step (and its rolling flush slice) running on the user stream
 // past the end of a step; entry points that touch the table from the caller's stream join it first.
 int join_user_stream(hipStream_t s) {
@@ -158,6 +202,13 @@ struct Ws {
   float *wpart[3], *bpart[3], *G, *S;  // wgrad partials: one set per wgrad stream
 };
 
+// the accumulator block's parts: [6][2][Cmax][2] forward sums, the same for the backward, ticket
+void rebase_acc(Ws* w, unsigned long long* acc) {
+  w->bnacc = acc;
+  w->bnbacc = acc + 6L * 2 * w->cmax * 2;
+  w->ticket = reinterpret_cast<unsigned int*>(acc + 2L * 6 * 2 * w->cmax * 2);
+}
+
 size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   Arena ar{(char*)base, 0, 0};
   const int H = d->conv_hidden, D = d->feature_dim, E = d->user_embdim;
@@ -172,8 +223,7 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   w->cmax = Cmax > D ? Cmax : D;
   w->nzero = 2L * 6 * 2 * w->cmax * 2 + 2;
   w->bnacc = ar.take<unsigned long long>(w->nzero);
-  w->bnbacc = w->bnacc + 6L * 2 * w->cmax * 2;
-  w->ticket = reinterpret_cast<unsigned int*>(w->bnacc + 2L * 6 * 2 * w->cmax * 2);
+  rebase_acc(w, w->bnacc);
   w->rowsum = ar.take<float>(B);
   w->y[0] = nullptr;
   w->idx[0] = nullptr;
@@ -252,12 +302,6 @@ int init_ctx(Ctx* c, const dcue_model* m) {
   c->E = m->dims.user_embdim;
   return DCUE_OK;
 }
-
-#define TRY(x)                 \
-  do {                         \
-    int _st = (x);             \
-    if (_st) return _st;       \
-  } while (0)
 
 // Item tower forward. train: batch statistics (weighted by counts, accumulated exactly by the
 // producing kernels) + running-stat update by each BN's first consumer; eval: running statistics.
@@ -447,26 +491,44 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   Ws w;
   if (carve(&m->dims, b->n_rows, b->n_neg, b->n_items, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
   carve(&m->dims, b->n_rows, b->n_neg, b->n_items, ws, &w);
+  if (o.acc) rebase_acc(&w, o.acc);
+  if (o.counts) w.counts = const_cast<float*>(o.counts);
   const double copies = (double)b->n_rows * (1 + b->n_neg);
   SidePool* sp = side_pool();
   if (!sp) return DCUE_ERR_HIP;
   hipStream_t su = sp->st[0];
   // the user tower runs beside the item tower; the item tower's chain is issued first
-  if (m->emb_step && o.sync_users) TRY(launch_emb_sync(m, o.sync_users, b->n_rows, su));
   hipEvent_t ev_in = nullptr;
   TRY(fork_point(sp, s, &ev_in));
   if (!o.prologue_done) TRY(launch_item_counts(b, w.counts, s));
   TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s,
                    o.prologue_done));
   TRY(wait_point(su, ev_in));
-  if (m->emb_step && !o.sync_users) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
-  TRY(user_forward(c, w, b->users, b->n_rows, nullptr, su));
-  TRY(stream_wait(sp, s, su));
-  if (o.fuse_score)
-    return launch_score_fused(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.rowsum, w.loss,
-                              w.du, w.dfcopy, w.ticket, s);
+  if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
+  hipEvent_t ev_uf = nullptr;
+  {
+    ForkAfter fk(sp, su, &ev_uf);
+    TRY(user_forward(c, w, b->users, b->n_rows, nullptr, su));
+    TRY(fk.done());
+  }
+  TRY(wait_point(s, ev_uf));
+  if (o.fuse_score) {
+    hipEvent_t ev = nullptr;
+    ForkAfter fk(sp, s, &ev);
+    TRY(launch_score_fused(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.rowsum, w.loss,
+                           w.du, w.dfcopy, w.ticket, s));
+    TRY(fk.done());
+    if (o.score_done) *o.score_done = ev;
+    return DCUE_OK;
+  }
   return launch_score_fwd(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.hinge, w.loss,
                           w.dhinge, s);
+}
+
+long step_acc_words(const dcue_dims* d, int B, int N, int M) {
+  Ws w;
+  carve(d, B, N, M, nullptr, &w);
+  return w.nzero;
 }
 
 int step_prologue(const dcue_model* m, const dcue_batch* b, void* ws, size_t ws_bytes, dcue_mt_state* mt,
@@ -495,6 +557,8 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   Ws w;
   if (carve(&m->dims, b->n_rows, b->n_neg, b->n_items, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
   carve(&m->dims, b->n_rows, b->n_neg, b->n_items, ws, &w);
+  if (o.acc) rebase_acc(&w, o.acc);
+  if (o.counts) w.counts = const_cast<float*>(o.counts);
   const int B = b->n_rows, N = b->n_neg, M = b->n_items;
   const int H = c.H, D = c.D, E = c.E;
   const double copies = (double)B * (1 + N);
@@ -514,15 +578,21 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   if (!o.fuse_score)  // else the fused score kernel already produced du / dfcopy
     TRY(launch_score_bwd(w.uf, w.f, b, D, dscores ? dscores : w.dhinge, w.cosv, w.norms, w.du,
                          w.dfcopy, s));
-  hipEvent_t ev_score = nullptr, ev_df = nullptr, ev_layer[6] = {};
-  TRY(fork_point(sp, s, &ev_score));
-  // per-item feature gradients df, then (same kernel) the fc input gradient g5 = df W and BN5's sums
-  TRY(launch_item_grad(w.dfcopy, b, D, w.df, c.P(SEG_FC_W), w.g[5], bn_acc(w.bnbacc, w.cmax, 5), w.y[5],
-                       w.mean[5], w.invstd[5], s));
-  TRY(fork_point(sp, s, &ev_df));
+  // fork points on the chain are bound to its launches (ForkAfter): no record packets between them
+  hipEvent_t ev_score = nullptr, ev_layer[6] = {};
+  if (o.fuse_score && o.score_done && *o.score_done)
+    ev_score = *o.score_done;
+  else
+    TRY(fork_point(sp, s, &ev_score));
+  {  // per-item feature gradients df, then (same kernel) the fc input gradient g5 = df W and BN5's sums
+    ForkAfter fk(sp, s, &ev_layer[5]);
+    TRY(launch_item_grad(w.dfcopy, b, D, w.df, c.P(SEG_FC_W), w.g[5], bn_acc(w.bnbacc, w.cmax, 5),
+                         w.y[5], w.mean[5], w.invstd[5], s));
+    TRY(fk.done());
+  }
+  const hipEvent_t ev_df = ev_layer[5];
   for (int l = 5; l >= 2; --l) {  // dgrad chain: g_l (+ BN_l sums) -> g_{l-1} (+ BN_{l-1} sums)
     const LayerGeom gm = layer_geom(l);
-    TRY(fork_point(sp, s, &ev_layer[l]));
     RowsArgs ra = {};
     ra.src = w.g[l]; ra.y_l = w.y[l]; ra.idx_l = w.idx[l];
     ra.mean_l = w.mean[l]; ra.invstd_l = w.invstd[l]; ra.a_l = w.a[l];
@@ -534,11 +604,13 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     ra.oy = w.y[l - 1]; ra.omean = w.mean[l - 1]; ra.oinvstd = w.invstd[l - 1];
     ra.M = M;
     ra.nout = H;
+    ForkAfter fk(sp, s, &ev_layer[l - 1]);
     TRY(launch_conv_dgrad(l, l == 5 ? D : H, ra, s));
+    TRY(fk.done());
   }
-  TRY(fork_point(sp, s, &ev_layer[1]));
-  // conv weight gradient of layer l on stream `so` (its own split-K partial set `ps`)
-  auto issue_wgrad = [&](int l, hipStream_t so, int ps) -> int {
+  // conv weight gradient of layer l on stream `so` (its own split-K partial set `ps`); `tail`:
+  // a fork point after its last kernel
+  auto issue_wgrad = [&](int l, hipStream_t so, int ps, hipEvent_t* tail) -> int {
     const LayerGeom gm = layer_geom(l);
     const int C = l == 5 ? D : H;
     const int cin = l == 1 ? kMels : H;
@@ -560,16 +632,23 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(timer_begin(&tsc, l == 1 ? DCUE_TIMED_CONV1_WGRAD : -1, so));
     TRY(launch_conv_wgrad(l, l == 1 ? src : SRC_ACT, wa, nch, so));
     TRY(timer_end(&tsc));
+    if (l != 1) {
+      ForkAfter fk(sp, so, tail);
+      TRY(launch_wgrad_reduce(l, wa.wpart, wa.bpart, nch, C, cin, c.Gd(seg_conv_w(l)),
+                              c.Gd(seg_conv_b(l)), w.G, w.S, so));
+      return fk.done();
+    }
     TRY(launch_wgrad_reduce(l, wa.wpart, wa.bpart, nch, C, cin, c.Gd(seg_conv_w(l)),
                             c.Gd(seg_conv_b(l)), w.G, w.S, so));
-    if (l == 1)
-      TRY(launch_bn0_grads(w.G, w.S, c.P(seg_conv_w(1)), c.P(seg_bn_w(0)), c.P(seg_bn_b(0)), H,
-                           c.Gd(seg_conv_w(1)), c.Gd(seg_bn_w(0)), c.Gd(seg_bn_b(0)),
-                           c.Gd(seg_conv_b(1)), so));
-    return DCUE_OK;
+    ForkAfter fk(sp, so, tail);
+    TRY(launch_bn0_grads(w.G, w.S, c.P(seg_conv_w(1)), c.P(seg_bn_w(0)), c.P(seg_bn_b(0)), H,
+                         c.Gd(seg_conv_w(1)), c.Gd(seg_bn_w(0)), c.Gd(seg_bn_b(0)),
+                         c.Gd(seg_conv_b(1)), so));
+    return fk.done();
   };
+  hipEvent_t tail[4] = {};  // caller's stream, user stream, wgrad streams 0 and 1
   // layer 1 (the step's tail) follows the chain on the caller's stream, issued right away
-  TRY(issue_wgrad(1, s, 2));
+  TRY(issue_wgrad(1, s, 2, &tail[0]));
 
   {  // fc weight gradient: dW[n][k] = sum_m df[m][n] bn5(y5)[m][k], db = sum_m df
     TRY(wait_point(sw[0], ev_df));
@@ -583,7 +662,8 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(launch_tgemm(0, 2, g, sw[0]));
   }
   // layers 5..2: alternating between the two wgrad streams (each with its own partial set)
-  for (int l = 5; l >= 2; --l) TRY(issue_wgrad(l, sw[l & 1], l & 1));
+  hipEvent_t scratch_ev = nullptr;
+  for (int l = 5; l >= 2; --l) TRY(issue_wgrad(l, sw[l & 1], l & 1, l <= 3 ? &tail[2 + (l & 1 ? 1 : 0)] : &scratch_ev));
   // user tower (userembedding.py:33-44 backward), the compact embedding rows, and -- when the step
   // carries it -- the user table's Adam step (it needs nothing from the item tower)
   TRY(wait_point(su, ev_score));
@@ -621,16 +701,19 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     g.cmask = m->emb; g.smm = E; g.smn = 1; g.cmrow = b->users;
     TRY(launch_tgemm(0, 0, g, su));
   }
-  TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, m->emb_rows,
-                      m->emb_step ? m->emb_log : nullptr, su));
   // the step's end joins the user stream here: its Adam part (and the rolling flush slice) below
   // needs nothing more from this step and runs on into the next one, ordered on this stream
-  hipEvent_t ev_user = nullptr;
-  TRY(fork_point(sp, su, &ev_user));
+  {
+    ForkAfter fk(sp, su, &tail[1]);
+    TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, m->emb_rows,
+                        m->emb_step ? m->emb_log : nullptr, su));
+    TRY(fk.done());
+  }
   if (o.emb_adam) TRY(launch_adam(m, o.emb_adam, c.poff, su));
 
-  TRY(wait_point(s, ev_user));
-  for (hipStream_t x : {sw[0], sw[1]}) TRY(stream_wait(sp, s, x));
+  for (int k = 1; k < 4; ++k) TRY(wait_point(s, tail[k]));
+  if (o.tails)
+    for (int k = 0; k < 4; ++k) o.tails[k] = tail[k];
   return DCUE_OK;
 }
 

@@ -11,7 +11,7 @@
 //   g_l      [M][Lp_l][C_l]   dL/d(BN_l output), summed over an item's copies
 //   wpack    [ks][cin/4][cout][4] forward B operand; [ks][cout/4][cin][4] (taps reversed) dgrad B
 // Rows of the GEMM are (item, position) pairs packed densely over items; a workgroup owns 16*TW rows
-// and all 128 output channels of its column block (4 waves x 32). Its A operand is an LDS slab of
+// and all 128 output channels of its column block (8 waves x 16). Its A operand is an LDS slab of
 // the input positions those rows touch (taps + zero halos), built once with the neighbouring
 // elementwise op fused into the load, then read with ds_read_b128 (4 consecutive K per lane; the
 // four MFMA k-steps of a 16-deep K chunk take one component each).
@@ -19,7 +19,7 @@
 
 namespace dcue {
 
-// Slab fill: every thread owns one channel quad (256 % (KC/4) == 0), so the per-channel operands
+// Slab fill: every thread owns one channel quad (threads % (KC/4) == 0), so the per-channel operands
 // of the fused elementwise op are loaded once; the raw global reads of a batch of slab slots are
 // issued branch-free (clamped addresses, masked afterwards) before any is used -- the loads are the
 // latency of these small kernels, not the math.
@@ -146,9 +146,15 @@ __device__ __forceinline__ float4 slab_finish(const RowsArgs& a, const ChanOps& 
 // MODE 0 = forward (pool+relu+stats epilogue), 1 = dgrad (plain store).
 // Slab position p of item i is valid for 0 <= p < LIN; rows are (i, t), t < R; tap k of row t reads
 // slab position t + k - PADL.
+// Eight waves per workgroup, two per SIMD: wave w owns output columns [16 (w mod 8), +16) of the
+// block for all TW row tiles, so while one wave of a SIMD waits on its weight loads the other
+// issues MFMAs (with four waves of 32 columns the loads' latency was exposed: ~40% of wave cycles
+// parked on s_waitcnt).
+constexpr int kRowsWaves = 8, kRowsThreads = 64 * kRowsWaves, kRowsCT = 128 / (16 * kRowsWaves);
+
 template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,
           int POOLL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_conv_rows(RowsArgs a) {
+__global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
   constexpr int RX = R + KS - 1;
   constexpr int ROWS = TW * 16;
   constexpr int MAXI = (ROWS + R - 1) / R + 1;
@@ -167,7 +173,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   (void)MAXI;
 
   {
-    static_assert(256 % C4 == 0, "a thread's slab slots share one channel quad");
+    static_assert(kRowsThreads % C4 == 0, "a thread's slab slots share one channel quad");
     constexpr int FB = SRC == SRC_DZ ? 4 : 8;  // slab slots (float4) in flight per thread
     const int nfill = nslab * C4;
     const int c = 4 * (threadIdx.x % C4);
@@ -177,14 +183,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       if (blockIdx.x == 0 && blockIdx.y == 0) bn_publish(a.in_bn, threadIdx.x);
     __syncthreads();
     const ChanOps kop = chan_ops<SRC>(chl, c);
-    for (int base = threadIdx.x; base < nfill; base += 256 * FB) {
+    for (int base = threadIdx.x; base < nfill; base += kRowsThreads * FB) {
       long ii[FB];
       int pp[FB];
       bool ok[FB];
       Raw raw[FB];
 #pragma unroll
       for (int j = 0; j < FB; ++j) {
-        const int e = base + 256 * j;
+        const int e = base + kRowsThreads * j;
         const long E = elo + e / C4;
         const long i = E / RX;
         const int p = (int)(E - i * RX) - PADL;
@@ -203,7 +209,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       for (int j = 0; j < FB; ++j) raw[j] = slab_load<SRC, KC, LIN, LPL, POOLL>(a, ii[j], pp[j], c, trk[j]);
 #pragma unroll
       for (int j = 0; j < FB; ++j) {
-        const int e = base + 256 * j;
+        const int e = base + kRowsThreads * j;
         if (e < nfill) {
           const float4 v = slab_finish<SRC, POOLL>(a, kop, pp[j], raw[j]);
           st4(&slab[(e / C4) * PITCH + c], ok[j] ? v : make_float4(0.f, 0.f, 0.f, 0.f));
@@ -216,7 +222,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, l16 = lane & 15;
   const int nout = a.nout;
-  const int ocol0 = blockIdx.y * 128 + wave * 32;
+  constexpr int CT = kRowsCT;  // 16-column MFMA tiles per wave
+  const int ocol0 = blockIdx.y * 128 + wave * 16 * CT;
   if (ocol0 >= nout) return;  // no barrier follows
 
   int sbase[TW];
@@ -228,23 +235,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     sbase[r] = (int)(i * RX + (gr - i * R) - elo) * PITCH + 4 * g;
   }
 
-  f32x4 acc[TW][2];
+  f32x4 acc[TW][CT];
 #pragma unroll
-  for (int r = 0; r < TW; ++r) acc[r][0] = acc[r][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int r = 0; r < TW; ++r)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[r][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // B operand (packed weights, L2-resident) streamed two k-steps ahead of the MFMAs
   const float* wp = a.wpack + ((size_t)g * nout + ocol0 + l16) * 4;
   const size_t wstep = (size_t)16 * nout;
-  float4 b0 = ld4(wp), b1 = ld4(wp + 64);
-  float4 n0 = NSTEP > 1 ? ld4(wp + wstep) : b0, n1 = NSTEP > 1 ? ld4(wp + wstep + 64) : b1;
+  float4 b[CT], n[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    b[ct] = ld4(wp + 64 * ct);
+    n[ct] = NSTEP > 1 ? ld4(wp + wstep + 64 * ct) : b[ct];
+  }
   // fully unrolled: straight-line code lets the wait counters track the in-flight B loads exactly
 #pragma unroll
   for (int st = 0; st < NSTEP; ++st) {
-    float4 f0 = n0, f1 = n1;
-    if (st + 2 < NSTEP) {
-      f0 = ld4(wp + (st + 2) * wstep);
-      f1 = ld4(wp + (st + 2) * wstep + 64);
-    }
+    float4 f[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) f[ct] = st + 2 < NSTEP ? ld4(wp + (st + 2) * wstep + 64 * ct) : n[ct];
     const int k = st / (KC / 16);
     const int c0 = (st - k * (KC / 16)) * 16;
     const int aoff = k * PITCH + c0;
@@ -252,36 +263,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #pragma unroll
     for (int r = 0; r < TW; ++r) av[r] = *reinterpret_cast<const float4*>(&slab[sbase[r] + aoff]);
 #pragma unroll
-    for (int r = 0; r < TW; ++r) {
-      acc[r][0] = mfma4(av[r].x, b0.x, acc[r][0]);
-      acc[r][1] = mfma4(av[r].x, b1.x, acc[r][1]);
-    }
+    for (int r = 0; r < TW; ++r)
 #pragma unroll
-    for (int r = 0; r < TW; ++r) {
-      acc[r][0] = mfma4(av[r].y, b0.y, acc[r][0]);
-      acc[r][1] = mfma4(av[r].y, b1.y, acc[r][1]);
-    }
+      for (int ct = 0; ct < CT; ++ct) acc[r][ct] = mfma4(av[r].x, b[ct].x, acc[r][ct]);
 #pragma unroll
-    for (int r = 0; r < TW; ++r) {
-      acc[r][0] = mfma4(av[r].z, b0.z, acc[r][0]);
-      acc[r][1] = mfma4(av[r].z, b1.z, acc[r][1]);
-    }
+    for (int r = 0; r < TW; ++r)
 #pragma unroll
-    for (int r = 0; r < TW; ++r) {
-      acc[r][0] = mfma4(av[r].w, b0.w, acc[r][0]);
-      acc[r][1] = mfma4(av[r].w, b1.w, acc[r][1]);
+      for (int ct = 0; ct < CT; ++ct) acc[r][ct] = mfma4(av[r].y, b[ct].y, acc[r][ct]);
+#pragma unroll
+    for (int r = 0; r < TW; ++r)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[r][ct] = mfma4(av[r].z, b[ct].z, acc[r][ct]);
+#pragma unroll
+    for (int r = 0; r < TW; ++r)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[r][ct] = mfma4(av[r].w, b[ct].w, acc[r][ct]);
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      b[ct] = n[ct];
+      n[ct] = f[ct];
     }
-    b0 = n0;
-    b1 = n1;
-    n0 = f0;
-    n1 = f1;
   }
 
   if constexpr (MODE == 1) {
     // g_{l-1} rows, plus this tile's share of BN_{l-1}'s backward sums (sum g, sum g*xhat)
-    float sg[2] = {0.f, 0.f}, sgx[2] = {0.f, 0.f};
+    float sg[CT] = {}, sgx[CT] = {};
 #pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
+    for (int ct = 0; ct < CT; ++ct) {
       const int o = ocol0 + 16 * ct + l16;
       const float mu = a.out_acc ? a.omean[o] : 0.f, is = a.out_acc ? a.oinvstd[o] : 0.f;
 #pragma unroll
@@ -305,7 +313,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     }
     if (a.out_acc) {
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
+      for (int ct = 0; ct < CT; ++ct) {
         float s = sg[ct], q = sgx[ct];
         s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
         q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
@@ -318,9 +326,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     }
   } else {
     constexpr int LP = R / POOL;
-    float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
+    float ssum[CT] = {}, ssq[CT] = {};
 #pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
+    for (int ct = 0; ct < CT; ++ct) {
       const int o = ocol0 + 16 * ct + l16;
       const float bias = a.bias[o];
 #pragma unroll
@@ -352,7 +360,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     }
     if (a.out_acc) {
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
+      for (int ct = 0; ct < CT; ++ct) {
         float s = ssum[ct], q = ssq[ct];
         s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
         q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
@@ -383,18 +391,31 @@ static int run_rows(const RowsArgs& a, hipStream_t s) {
   }
   const long total = (long)a.M * R;
   dim3 grid((unsigned)((total + ROWS - 1) / ROWS), (unsigned)((a.nout + 127) / 128));
-  hipLaunchKernelGGL(kern, grid, dim3(256), LDS, s, a);
+  DCUE_LAUNCH(kern, grid, dim3(kRowsThreads), LDS, s, a);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
 
-// Row tiles per workgroup: the largest of 8/4/2/1 that still gives >= 256 workgroups (one per CU),
-// so small batches (in-batch negatives: M = B) spread over the chip instead of queueing behind a
-// few long-running workgroups.
-static int choose_tw(long rows) {
-  for (int tw : {8, 4, 2})
-    if ((rows + 16 * tw - 1) / (16 * tw) >= 256) return tw;
-  return 1;
+// Row tiles per workgroup. Each wave runs TW 16-row tiles of its 32 columns back to back, and a
+// CU given k workgroups runs their waves on the same four SIMDs, so the launch takes about
+// TW * ceil(workgroups / 256) tile times: 528 tiles (layer 1 at B = 64) cost 4 at TW = 2 (264
+// workgroups, eight CUs doubled up) but 3 at TW = 3 (176). Ties go to the larger TW (fewer
+// re-reads of the weights, which every workgroup streams whole).
+static int choose_tw(long rows, int twmax) {
+  constexpr long kCUs = 256;
+  const long tiles = (rows + 15) / 16;
+  int best = 1;
+  long best_cost = -1;
+  for (int tw : {1, 2, 3, 4, 8}) {
+    if (tw > twmax) break;
+    const long wgs = (tiles + tw - 1) / tw;
+    const long cost = tw * ((wgs + kCUs - 1) / kCUs);
+    if (best_cost < 0 || cost <= best_cost) {
+      best = tw;
+      best_cost = cost;
+    }
+  }
+  return best;
 }
 
 
@@ -420,9 +441,10 @@ template <int L, int KC, int SRC>
 static int fwd_layer(const RowsArgs& a, hipStream_t s) {
   constexpr LayerGeom gm = layer_geom(L);
   constexpr int TWMAX = max_tw(gm.lp * gm.pool, gm.ks, KC);
-  const int tw = min(choose_tw((long)a.M * gm.lp * gm.pool), TWMAX);
+  const int tw = choose_tw((long)a.M * gm.lp * gm.pool, TWMAX);
   if constexpr (TWMAX >= 8) if (tw == 8) return fwd_layer_tw<L, KC, SRC, 8>(a, s);
   if constexpr (TWMAX >= 4) if (tw == 4) return fwd_layer_tw<L, KC, SRC, 4>(a, s);
+  if constexpr (TWMAX >= 3) if (tw == 3) return fwd_layer_tw<L, KC, SRC, 3>(a, s);
   if constexpr (TWMAX >= 2) if (tw == 2) return fwd_layer_tw<L, KC, SRC, 2>(a, s);
   return fwd_layer_tw<L, KC, SRC, 1>(a, s);
 }
@@ -468,9 +490,10 @@ template <int L, int KC>
 static int dgrad_layer(const RowsArgs& a, hipStream_t s) {
   constexpr LayerGeom gm = layer_geom(L);
   constexpr int TWMAX = max_tw(gm.lin, gm.ks, KC);
-  const int tw = min(choose_tw((long)a.M * gm.lin), TWMAX);
+  const int tw = choose_tw((long)a.M * gm.lin, TWMAX);
   if constexpr (TWMAX >= 8) if (tw == 8) return dgrad_layer_tw<L, KC, 8>(a, s);
   if constexpr (TWMAX >= 4) if (tw == 4) return dgrad_layer_tw<L, KC, 4>(a, s);
+  if constexpr (TWMAX >= 3) if (tw == 3) return dgrad_layer_tw<L, KC, 3>(a, s);
   if constexpr (TWMAX >= 2) if (tw == 2) return dgrad_layer_tw<L, KC, 2>(a, s);
   return dgrad_layer_tw<L, KC, 1>(a, s);
 }
@@ -737,7 +760,7 @@ static int wgrad_layer(const WgradArgs& a0, int nchunk, hipStream_t s) {
   const long rpc = (rows + nchunk - 1) / nchunk;  // the last chunk may be short; rows past it are masked
   a.rows_per_chunk = (int)rpc;
   dim3 grid((unsigned)((gm.ks * a.cin + 127) / 128), (unsigned)((a.cout + 127) / 128), (unsigned)nchunk);
-  hipLaunchKernelGGL(kern, grid, dim3(256), LDS, s, a);
+  DCUE_LAUNCH(kern, grid, dim3(256), LDS, s, a);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
@@ -831,7 +854,7 @@ int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int n
   const int nb = layer == 1 ? 5 : 1;
   const long nblk = ((long)cout * gm.ks * cin + 127) / 128 + ((long)nb * cout + 127) / 128;
   // layer 1: the five bias partial sums land in E_tmp[5][cout]; k_bn0_grads derives db1 and S
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)nblk), dim3(256), 0, s, wpart, bpart, nchunk, cout, cin,
+  DCUE_LAUNCH(k_wgrad_reduce, dim3((unsigned)nblk), dim3(256), 0, s, wpart, bpart, nchunk, cout, cin,
                      gm.ks, nb, dW, db, layer == 1 ? G_tmp : nullptr, layer == 1 ? E_tmp : nullptr);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
@@ -882,7 +905,7 @@ __global__ __launch_bounds__(256) void k_bn0_grads(const float* __restrict__ G, 
 int launch_bn0_grads(const float* G, const float* E, const float* W1, const float* gamma0,
                      const float* beta0, int H, float* dW1, float* dgamma0, float* dbeta0, float* db1,
                      hipStream_t s) {
-  hipLaunchKernelGGL(k_bn0_grads, dim3(kMels), dim3(256), 0, s, G, E, W1, gamma0, beta0, H, dW1, dgamma0,
+  DCUE_LAUNCH(k_bn0_grads, dim3(kMels), dim3(256), 0, s, G, E, W1, gamma0, beta0, H, dW1, dgamma0,
                      dbeta0, db1);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;

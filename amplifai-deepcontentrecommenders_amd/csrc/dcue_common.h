@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <climits>
 
@@ -24,6 +25,34 @@ void set_last_error(const char* expr, hipError_t e, const char* file, int line);
     }                                                             \
   } while (0)
 #define DCUE_LAUNCH_CHECK() DCUE_HIP_CHECK(hipGetLastError())
+
+namespace dcue {
+// Events bound to kernel launches (hipExtLaunchKernel) rather than recorded after them. An
+// event-record packet between two dependent kernels idles the stream for ≈3 µs on MI355X / ROCm 7.2
+// (≈5.5 µs when another stream waits on it); an event bound to the kernel's own dispatch costs
+// ≈0.05 µs (measured, scratch-free: DESIGN.md §6). While `stop` is set every launch on this thread
+// binds it (the last binding is the one a wait sees); `start` binds to the next launch only.
+struct LaunchTag {
+  hipEvent_t start = nullptr, stop = nullptr;
+  int launches = 0;     // launches that bound `stop`
+  bool missed = false;  // a nested scope's launches bound another event: `stop` must be recorded
+};
+LaunchTag& launch_tag();
+}  // namespace dcue
+
+// Every kernel launch of the library goes through here (see LaunchTag).
+#define DCUE_LAUNCH(kern, grid, block, shm, stream, ...)                                          \
+  do {                                                                                            \
+    ::dcue::LaunchTag& dcue_tag_ = ::dcue::launch_tag();                                          \
+    if (dcue_tag_.stop) {                                                                         \
+      hipExtLaunchKernelGGL(kern, grid, block, shm, stream, dcue_tag_.start, dcue_tag_.stop, 0,   \
+                            __VA_ARGS__);                                                         \
+      dcue_tag_.start = nullptr;                                                                  \
+      ++dcue_tag_.launches;                                                                       \
+    } else {                                                                                      \
+      hipLaunchKernelGGL(kern, grid, block, shm, stream, __VA_ARGS__);                            \
+    }                                                                                             \
+  } while (0)
 
 namespace dcue {
 

@@ -6,6 +6,13 @@
 #include "dcue_common.h"
 #include "bnacc.h"
 
+// propagate a non-zero dcue_status
+#define TRY(x)                 \
+  do {                         \
+    int _st = (x);             \
+    if (_st) return _st;       \
+  } while (0)
+
 namespace dcue {
 
 // -------------------------------------------------------------- conv as row-GEMM (fwd / dgrad)
@@ -125,6 +132,11 @@ struct StepPrologue {
   unsigned long long* zero;  // words to clear
   long nzero;
   float* counts;             // [M] (nullable)
+  dcue_mt_state* mt_out;     // where the advanced state goes (null: back to mt)
+  dcue_mt_state* mt_commit;  // nullable: receives the state as loaded, before this draw
+  const int32_t* copy_src;   // nullable: copy_dst[0..ncopy) = copy_src[..] (published negatives)
+  int32_t* copy_dst;
+  long ncopy;
 };
 int launch_step_prologue(const StepPrologue& p, hipStream_t s);
 
@@ -176,7 +188,8 @@ int launch_pack(const dcue_model* m, const int64_t* poff, hipStream_t s);
 struct TimerScope {
   int cls = -1;
   hipStream_t s = nullptr;
-  hipEvent_t a = nullptr, b = nullptr;
+  hipEvent_t a = nullptr, b = nullptr;  // bound to the timed launch (LaunchTag start / stop)
+  LaunchTag saved;                      // the enclosing scope's tag, restored by timer_end
   bool capturing = false;
   std::vector<hipGraphNode_t> preds;  // under capture: the stream's dependency set before the launch
 };
@@ -206,6 +219,29 @@ struct SidePool {
 SidePool* side_pool();
 int stream_wait(SidePool* p, hipStream_t to, hipStream_t from);
 int fork_point(SidePool* p, hipStream_t from, hipEvent_t* ev);
+hipEvent_t ring_event(SidePool* p);
+
+// Set while a plan captures its step (bound launch events are not captured; records are).
+bool& capturing_step();
+
+// A fork point at the end of the launches made inside the scope, without an event-record packet:
+// the scope's ring event is bound to each launch (LaunchTag; the last binding is what a wait sees).
+// If the scope launched nothing, or the step is being captured, done() records the event instead.
+// Scopes nest: launches of an inner scope do not bind the outer event, so the outer one records.
+class ForkAfter {
+ public:
+  ForkAfter(SidePool* p, hipStream_t s, hipEvent_t* ev);
+  ~ForkAfter();
+  int done();
+
+ private:
+  void restore();
+  hipStream_t s_;
+  hipEvent_t* out_;
+  hipEvent_t e_;
+  LaunchTag saved_;
+  bool armed_ = false, finished_ = false;
+};
 int wait_point(hipStream_t to, hipEvent_t ev);
 int join_user_stream(hipStream_t s);
 
@@ -214,9 +250,16 @@ struct StepOpts {
   bool prologue_done = false;  // counts written + accumulators (and ticket) cleared by the prologue
   bool fuse_score = false;     // train forward also runs the hinge backward (k_score_fused)
   const dcue_adam_args* emb_adam = nullptr;  // backward: also step the user table (parts = EMBEDDING)
-  const int64_t* sync_users = nullptr;  // forward: bring these users' rows current first, without
-                                        // waiting for anything else on the caller's stream
+  hipEvent_t* score_done = nullptr;     // forward (fuse_score): a fork point after the score kernel
+  // backward: the step's tail on each stream, for a caller that must wait for all of it (plans)
+  hipEvent_t* tails = nullptr;           // [4]: caller's stream, user stream, wgrad streams 0 and 1
+  // prepared ahead (plans): the step's copy counts and its cleared accumulator block, in place of
+  // the workspace's own
+  const float* counts = nullptr;
+  unsigned long long* acc = nullptr;
 };
+// words of the per-step accumulator block (BN sums + score ticket) cleared before each step
+long step_acc_words(const dcue_dims* d, int B, int N, int M);
 int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
                  int train, float margin, const StepOpts& o, hipStream_t s);
 int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,

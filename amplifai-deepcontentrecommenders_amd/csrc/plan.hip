@@ -29,6 +29,18 @@ struct dcue_plan {
   };
   std::vector<TimerNodes> timers;
   std::vector<hipEvent_t> placeholders;  // events the record nodes were built with
+  // eager plans prepare each step's inputs one step ahead (issue_eager): double-buffered draws,
+  // copy counts and cleared accumulator blocks, and the draw stream's state after the last prepared
+  // step
+  void* ahead = nullptr;
+  int32_t* neg[2] = {};
+  float* counts[2] = {};
+  unsigned long long* acc[2] = {};
+  long nacc = 0;
+  dcue_mt_state* mt_ahead = nullptr;
+  long launches = 0;
+  hipEvent_t ev_ahead = nullptr;  // the next step's inputs are ready (a side-pool ring event)
+  hipEvent_t tails[4] = {};       // the last launched step's end on each of its streams
 };
 
 namespace {
@@ -43,9 +55,9 @@ int issue_step(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, v
   o.prologue_done = true;
   o.fuse_score = true;
   o.emb_adam = emb_adam;
-  // the user rows' sync starts with the step (eager only: under capture a side stream joins the
-  // graph only through an event of the capturing stream)
-  if (!captured) o.sync_users = users_src ? users_src : b->users;
+  hipEvent_t score_done = nullptr;
+  o.score_done = &score_done;
+  (void)captured;
   int st = dcue::step_prologue(m, b, ws, ws_bytes,
                                (cfg->flags & DCUE_PLAN_SAMPLE_INBATCH) ? cfg->mt : nullptr, users_src,
                                items_src, s);
@@ -54,9 +66,84 @@ int issue_step(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, v
   return st;
 }
 
+// Eager replay with the step's inputs prepared one step ahead. Step t's draw, copy counts and
+// accumulator clear are made by launch t-1 on a weight-gradient stream while step t-1 computes (one
+// 1024-thread block beside the step's kernels), so step t's first kernel on the caller's stream is
+// already the item tower's input statistics. Buffers alternate by step parity; launch t prepares
+// slot t+1 once step t-1 -- the last reader of that slot -- has ended, and publishes what the
+// caller can see of step t: the negatives into the bound neg_item buffer, the batch indices into
+// the bound batch buffers and, into cfg.mt, the draw stream's state after step t's draw (the
+// plan's own copy runs one step ahead).
+int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src, hipStream_t s,
+                const dcue_adam_args* emb_adam) {
+  using namespace dcue;
+  SidePool* sp = side_pool();
+  if (!sp) return DCUE_ERR_HIP;
+  const dcue_batch& b0 = p->batch;
+  const bool inbatch = (p->cfg.flags & DCUE_PLAN_SAMPLE_INBATCH) != 0;
+  const int cur = (int)(p->launches & 1), nxt = cur ^ 1;
+  hipStream_t sa = sp->st[1];
+  auto inputs = [&](int slot) {
+    StepPrologue q = {};
+    q.B = b0.n_rows; q.N = b0.n_neg; q.M = b0.n_items;
+    q.gather = b0.layout == DCUE_LAYOUT_GATHER;
+    q.neg = inbatch ? p->neg[slot] : const_cast<int32_t*>(b0.neg_item);
+    q.zero = p->acc[slot]; q.nzero = p->nacc;
+    q.counts = p->counts[slot];
+    return q;
+  };
+  if (p->launches == 0) {  // the first step's inputs, on the caller's stream
+    StepPrologue q = inputs(cur);
+    q.mt = inbatch ? p->cfg.mt : nullptr;
+    q.mt_out = p->mt_ahead;
+    TRY(launch_step_prologue(q, s));
+    TRY(fork_point(sp, s, &p->tails[0]));
+  } else {
+    TRY(wait_point(s, p->ev_ahead));
+  }
+  // the next step's inputs + what the caller sees of this one, once the last step is over
+  for (hipEvent_t e : p->tails)
+    if (e) TRY(wait_point(sa, e));
+  {
+    StepPrologue q = inputs(nxt);
+    if (inbatch) {
+      q.mt = p->mt_ahead;
+      q.mt_commit = p->cfg.mt;
+      q.copy_src = p->neg[cur];
+      q.copy_dst = const_cast<int32_t*>(b0.neg_item);
+      q.ncopy = (long)b0.n_rows * b0.n_neg;
+    }
+    q.users_dst = const_cast<int64_t*>(b0.users); q.users_src = users_src;
+    q.items_dst = const_cast<int32_t*>(b0.item_track); q.items_src = items_src;
+    ForkAfter fk(sp, sa, &p->ev_ahead);
+    TRY(launch_step_prologue(q, sa));
+    TRY(fk.done());
+  }
+  dcue_batch b = b0;
+  if (users_src) b.users = users_src;
+  if (items_src) b.item_track = items_src;
+  if (inbatch) b.neg_item = p->neg[cur];
+  StepOpts o;
+  o.prologue_done = true;
+  o.fuse_score = true;
+  o.emb_adam = emb_adam;
+  o.counts = p->counts[cur];
+  o.acc = p->acc[cur];
+  hipEvent_t score_done = nullptr;
+  o.score_done = &score_done;
+  o.tails = p->tails;
+  TRY(forward_impl(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, 1, p->cfg.margin, o, s));
+  TRY(backward_impl(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, nullptr, p->cfg.emb_grad_scale, o, s));
+  ++p->launches;
+  return DCUE_OK;
+}
+
 int capture(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
             const dcue_plan_config* cfg, hipStream_t cs) {
-  return issue_step(m, b, t, ws, ws_bytes, cfg, nullptr, nullptr, cs, nullptr, /*captured=*/true);
+  dcue::capturing_step() = true;
+  const int st = issue_step(m, b, t, ws, ws_bytes, cfg, nullptr, nullptr, cs, nullptr, /*captured=*/true);
+  dcue::capturing_step() = false;
+  return st;
 }
 
 }  // namespace
@@ -74,6 +161,14 @@ extern "C" int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const 
   if (!dcue::side_pool()) return DCUE_ERR_HIP;  // side streams exist before capture starts
   if (!(cfg->flags & DCUE_PLAN_GRAPH)) {
     // eager plan: validate once by issuing nothing but the checks the calls make themselves
+    const int B = b->n_rows, N = b->n_neg, M = b->n_items;
+    const long nneg = (cfg->flags & DCUE_PLAN_SAMPLE_INBATCH) ? (long)B * N : 0;
+    const long nacc = dcue::step_acc_words(&m->dims, B, N, M);
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t bneg = al(sizeof(int32_t) * (nneg > 0 ? nneg : 1)), bcnt = al(sizeof(float) * M),
+                 bacc = al(sizeof(unsigned long long) * nacc), bmt = al(sizeof(dcue_mt_state));
+    void* mem = nullptr;
+    DCUE_HIP_CHECK(hipMalloc(&mem, 2 * (bneg + bcnt + bacc) + bmt));
     dcue_plan* p = new dcue_plan;
     p->model = *m;
     p->batch = *b;
@@ -81,6 +176,15 @@ extern "C" int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const 
     p->cfg = *cfg;
     p->ws = ws;
     p->ws_bytes = ws_bytes;
+    p->ahead = mem;
+    char* q = (char*)mem;
+    for (int i = 0; i < 2; ++i) {
+      p->neg[i] = (int32_t*)q; q += bneg;
+      p->counts[i] = (float*)q; q += bcnt;
+      p->acc[i] = (unsigned long long*)q; q += bacc;
+    }
+    p->mt_ahead = (dcue_mt_state*)q;
+    p->nacc = nacc;
     *plan_host = p;
     return DCUE_OK;
   }
@@ -145,8 +249,7 @@ extern "C" int dcue_plan_launch(dcue_plan* p, const int64_t* users_src, const in
   const dcue_batch& b = p->batch;
   if (users_src == b.users) users_src = nullptr;
   if (item_track_src == b.item_track) item_track_src = nullptr;
-  if (!p->exec)  // eager replay: the batch copies ride in the prologue block
-    return issue_step(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, &p->cfg, users_src, item_track_src, s);
+  if (!p->exec) return issue_eager(p, users_src, item_track_src, s, nullptr);
   if (users_src)
     DCUE_HIP_CHECK(hipMemcpyAsync(const_cast<int64_t*>(b.users), users_src, sizeof(int64_t) * b.n_rows,
                                   hipMemcpyDeviceToDevice, s));
@@ -183,8 +286,7 @@ extern "C" int dcue_plan_step(dcue_plan* p, const int64_t* users_src, const int3
   dcue_adam_args emb = *adam, dense = *adam;
   emb.parts = DCUE_ADAM_EMBEDDING;
   dense.parts = DCUE_ADAM_DENSE;
-  const int st = issue_step(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, &p->cfg, users_src,
-                            item_track_src, (hipStream_t)stream, &emb);
+  const int st = issue_eager(p, users_src, item_track_src, (hipStream_t)stream, &emb);
   if (st) return st;
   return dcue_adam_step(&p->model, &dense, stream);
 }
@@ -194,6 +296,7 @@ extern "C" int dcue_plan_destroy(dcue_plan* p) {
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->graph) (void)hipGraphDestroy(p->graph);
   for (hipEvent_t e : p->placeholders) dcue::timer_release(e);
+  if (p->ahead) (void)hipFree(p->ahead);
   delete p;
   return DCUE_OK;
 }

@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void k_item_counts(dcue_batch b, float* counts
 }
 
 int launch_item_counts(const dcue_batch* b, float* counts, hipStream_t s) {
-  hipLaunchKernelGGL(k_item_counts, dim3((b->n_items + 3) / 4), dim3(256), 0, s, *b, counts);
+  DCUE_LAUNCH(k_item_counts, dim3((b->n_items + 3) / 4), dim3(256), 0, s, *b, counts);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
@@ -182,7 +182,7 @@ int launch_tgemm(int ta, int tb, const TGemmArgs& g, hipStream_t s) {
   const int key = ((ta * 3 + tb) * 2 + akf) * 2 + bnf;
 #define DCUE_TG(TA_, TB_, AK_, BN_)                                                            \
   case ((TA_ * 3 + TB_) * 2 + AK_) * 2 + BN_:                                                  \
-    hipLaunchKernelGGL((k_tgemm<TA_, TB_, AK_, BN_>), grid, dim3(256), 0, s, g);               \
+    DCUE_LAUNCH((k_tgemm<TA_, TB_, AK_, BN_>), grid, dim3(256), 0, s, g);               \
     break;
   switch (key) {
     DCUE_TG(0, 0, 0, 0) DCUE_TG(0, 0, 0, 1) DCUE_TG(0, 0, 1, 0) DCUE_TG(0, 0, 1, 1)
@@ -278,10 +278,10 @@ int launch_score_fwd(const float* uf, const float* f, const dcue_batch* b, int d
                      float* scores, float* cosv, float* norms, float* hinge, float* loss,
                      float* dhinge, hipStream_t s) {
   if (d > 256 || b->n_neg > 1024 || b->n_rows > 1024) return DCUE_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL(k_score_fwd, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, margin, scores, cosv,
+  DCUE_LAUNCH(k_score_fwd, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, margin, scores, cosv,
                      norms, hinge, dhinge);
   DCUE_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_loss_mean, dim3(1), dim3(256), 0, s, hinge, b->n_rows, b->n_neg, loss);
+  DCUE_LAUNCH(k_loss_mean, dim3(1), dim3(256), 0, s, hinge, b->n_rows, b->n_neg, loss);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
@@ -407,7 +407,7 @@ int launch_score_fused(const float* uf, const float* f, const dcue_batch* b, int
                        float* scores, float* cosv, float* norms, float* rowsum, float* loss,
                        float* du, float* dfcopy, unsigned int* ticket, hipStream_t s) {
   if (d > 256 || b->n_neg > 1024 || b->n_rows > 1024) return DCUE_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL(k_score_fused, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, margin, scores, cosv,
+  DCUE_LAUNCH(k_score_fused, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, margin, scores, cosv,
                      norms, rowsum, loss, du, dfcopy, ticket);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
@@ -461,7 +461,7 @@ __global__ __launch_bounds__(256) void k_score_bwd(const float* __restrict__ uf,
 int launch_score_bwd(const float* uf, const float* f, const dcue_batch* b, int d,
                      const float* dscores, const float* cosv, const float* norms, float* du,
                      float* dfcopy, hipStream_t s) {
-  hipLaunchKernelGGL(k_score_bwd, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, dscores, cosv, norms,
+  DCUE_LAUNCH(k_score_bwd, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, dscores, cosv, norms,
                      du, dfcopy);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
@@ -580,7 +580,7 @@ int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df,
   if (d > 256) return DCUE_ERR_UNSUPPORTED;
   if (b->layout == DCUE_LAYOUT_GATHER && (long)b->n_rows * b->n_neg + 1 > kItemGradCap) return DCUE_ERR_UNSUPPORTED;
   const ItemGradFc fc = {fcW, g5, acc5, y5, mean5, invstd5};
-  hipLaunchKernelGGL(k_item_grad, dim3(b->n_items), dim3(256), 0, s, dfcopy, *b, d, df, fc);
+  DCUE_LAUNCH(k_item_grad, dim3(b->n_items), dim3(256), 0, s, dfcopy, *b, d, df, fc);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
@@ -618,7 +618,7 @@ __global__ void k_emb_grad(const float* __restrict__ de, const int64_t* users, i
 int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float scale,
                     float* emb_grad, int32_t* slot, int64_t* emb_rows, dcue_emb_log* log,
                     hipStream_t s) {
-  hipLaunchKernelGGL(k_emb_grad, dim3(B), dim3(256), 0, s, de, users, B, E, scale, emb_grad, slot,
+  DCUE_LAUNCH(k_emb_grad, dim3(B), dim3(256), 0, s, de, users, B, E, scale, emb_grad, slot,
                      emb_rows, log);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
@@ -655,7 +655,7 @@ __global__ void k_build_catalogue(const int64_t* pos, const int64_t* neg, int B,
 extern "C" int dcue_transpose_spectrograms(const float* ncl, int32_t M, float* out, void* stream) {
   if (!ncl || !out || M <= 0) return DCUE_ERR_INVALID;
   dim3 grid((dcue::kFrames + 31) / 32, dcue::kMels / 32, (unsigned)M);
-  hipLaunchKernelGGL(dcue::k_transpose_ncl, grid, dim3(256), 0, (hipStream_t)stream, ncl, M, out);
+  DCUE_LAUNCH(dcue::k_transpose_ncl, grid, dim3(256), 0, (hipStream_t)stream, ncl, M, out);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
@@ -664,7 +664,7 @@ extern "C" int dcue_build_catalogue_batch(const int64_t* pos_items, const int64_
                                           int32_t N, int32_t* item_track, void* stream) {
   if (!pos_items || (N > 0 && !neg_items) || !item_track || B <= 0 || N < 0) return DCUE_ERR_INVALID;
   const long tot = (long)B * (1 + N);
-  hipLaunchKernelGGL(dcue::k_build_catalogue, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+  DCUE_LAUNCH(dcue::k_build_catalogue, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, pos_items, neg_items, B, N, item_track);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;

@@ -1,5 +1,6 @@
 // Live kernel timing with HIP events (dcue_timer_*): the launch sites of the timed kernel classes
-// bracket the launch with an event pair on the stream the kernel runs on. Under stream capture the
+// bind an event pair to the launch itself (hipExtLaunchKernel start/stop, LaunchTag), on every
+// stride-th launch of the class. Under stream capture the
 // launch's graph node and its predecessors are noted instead; the plan adds event-record nodes
 // around the kernel node and re-points them at fresh events on every launch (plan.hip), so each
 // replay is timed. Single host thread per process (the
@@ -15,7 +16,8 @@ namespace dcue {
 
 namespace {
 struct TimerState {
-  bool enabled[DCUE_N_TIMED] = {};
+  int stride[DCUE_N_TIMED] = {};  // time every stride-th launch (0: off)
+  long seen[DCUE_N_TIMED] = {};
   std::vector<hipEvent_t> pool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> recorded[DCUE_N_TIMED];
   std::vector<CapturedTimer> captured;
@@ -46,7 +48,8 @@ int timer_begin(TimerScope* sc, int cls, hipStream_t s) {
   sc->a = sc->b = nullptr;
   sc->capturing = false;
   sc->preds.clear();
-  if (cls < 0 || cls >= DCUE_N_TIMED || !ts().enabled[cls]) return DCUE_OK;
+  if (cls < 0 || cls >= DCUE_N_TIMED || !ts().stride[cls]) return DCUE_OK;
+  if (ts().seen[cls]++ % ts().stride[cls]) return DCUE_OK;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   const hipGraphNode_t* deps = nullptr;
   size_t nd = 0;
@@ -59,7 +62,9 @@ int timer_begin(TimerScope* sc, int cls, hipStream_t s) {
   sc->a = timer_event();
   sc->b = timer_event();
   if (!sc->a || !sc->b) return DCUE_ERR_HIP;
-  DCUE_HIP_CHECK(hipEventRecord(sc->a, s));
+  // the pair is bound to the timed launch itself: its own dispatch timestamps, no record packets
+  sc->saved = launch_tag();
+  launch_tag() = LaunchTag{sc->a, sc->b, 0, false};
   return DCUE_OK;
 }
 
@@ -74,7 +79,15 @@ int timer_end(TimerScope* sc) {
     return DCUE_OK;
   }
   if (!sc->a) return DCUE_OK;
-  DCUE_HIP_CHECK(hipEventRecord(sc->b, sc->s));
+  const int n = launch_tag().launches;
+  launch_tag() = sc->saved;
+  if (n && sc->saved.stop) launch_tag().missed = true;
+  if (n != 1) {  // nothing (or more than the one kernel) launched: time the interval by records
+    timer_release(sc->a);
+    timer_release(sc->b);
+    sc->a = nullptr;
+    return n ? DCUE_ERR_INVALID : DCUE_OK;
+  }
   timer_add_recorded(sc->cls, sc->a, sc->b);
   return DCUE_OK;
 }
@@ -107,7 +120,9 @@ extern "C" const char* dcue_last_error(void) { return dcue::g_last_error; }
 
 extern "C" int dcue_timer_enable(int32_t kernel, int32_t enable) {
   if (kernel < 0 || kernel >= DCUE_N_TIMED) return DCUE_ERR_INVALID;
-  dcue::ts().enabled[kernel] = enable != 0;
+  if (enable < 0) return DCUE_ERR_INVALID;
+  dcue::ts().stride[kernel] = enable;
+  dcue::ts().seen[kernel] = 0;
   return DCUE_OK;
 }
 

@@ -195,7 +195,8 @@ def workspace_outputs(dims, B, N, M):
 
 
 def timer_enable(kernel, enable=True):
-    check(lib().dcue_timer_enable(kernel, int(bool(enable))), "dcue_timer_enable")
+    """enable: True / 1 times every launch of the class, n > 1 every n-th, False / 0 none."""
+    check(lib().dcue_timer_enable(kernel, int(enable)), "dcue_timer_enable")
 
 
 def timer_read(kernel):

@@ -10,6 +10,7 @@ gradient all-reduce stay outside, between replays.
 Build the optimizer (and with it any deferred user-table state) BEFORE the plan: the graph binds the
 buffers that exist at creation and refuses to run if the model or optimizer state was rebuilt.
 """
+import collections
 import ctypes
 
 import torch
@@ -59,6 +60,9 @@ class TrainPlan:
         # the stream the plan issues on: torch's current stream at creation (pass stream= to override)
         self._stream = nat.stream_handle()
         self._adam_args = nat.AdamArgs()
+        # source batches stay referenced for a few steps: the plan's side streams read them
+        # asynchronously (the caching allocator must not hand their memory out meanwhile)
+        self._hold = collections.deque(maxlen=4)
         # the replayed backward writes the flat gradient: expose the reference-shaped .grad views
         named = dict(net.named_parameters())
         for s, name in enumerate(nat.DENSE_NAMES):
@@ -82,6 +86,7 @@ class TrainPlan:
         if self._handle is None:
             raise RuntimeError("TrainPlan was closed")
         self._check_bound()
+        self._hold.append((users, item_track))
         st = self._lib.dcue_plan_launch(self._handle, None if users is None else users.data_ptr(),
                                         None if item_track is None else item_track.data_ptr(),
                                         self._stream if stream is None else stream)
@@ -97,6 +102,7 @@ class TrainPlan:
         if self._handle is None:
             raise RuntimeError("TrainPlan was closed")
         self._check_bound()
+        self._hold.append((users, item_track))
         g = opt.param_groups[0]
         opt.step_count += 1
         args = self._adam_args

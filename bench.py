@@ -44,6 +44,9 @@ def parse():
                          "bit-identical replay")
     ap.add_argument("--flush-every", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gpu-only", action="store_true",
+                    help="diagnostic: hold the stream behind a sleep kernel while the steps are "
+                         "enqueued, then report the GPU's own time for them (no host in the loop)")
     return ap.parse_args()
 
 
@@ -138,13 +141,15 @@ def main():
     nat.check(nat.lib().dcue_mt_seed(nat.ptr(mt), 10 + rank, nat.stream_handle()), "mt_seed")
     G = net._flat["G"]
     TIMED = nat.TIMED_CONV1_WGRAD  # the roofline kernel, timed live by HIP events in the library
+    TIMER_STRIDE = 8
 
     if args.mode == "catalogue":
         raise SystemExit("catalogue mode bench: use --mode inbatch (config 2); catalogue runs in tests")
 
-    # the step's sample + forward + backward replay as one HIP graph; Adam and the all-reduce between.
-    # The roofline kernel's timer is on before capture so the graph carries its event-record nodes.
-    nat.timer_enable(TIMED, True)
+    # The roofline kernel's timer is on before the plan is built. It binds a HIP event pair to every
+    # TIMER_STRIDE-th launch of the kernel (its own dispatch's start and end, on the stream it runs
+    # on); a timed launch costs the stream a few microseconds, so a sample is timed, not every step.
+    nat.timer_enable(TIMED, TIMER_STRIDE)
     plan = TrainPlan(net, tracks, B, N, mt_state=mt, emb_grad_scale=1.0 / world, optimizer=opt)
 
     def step(s):
@@ -163,12 +168,21 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     nat.timer_read(TIMED)  # drop the warm-up records
+    if args.gpu_only:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(int(2.4e6 * args.steps))  # ~1 ms of GPU per step (2.4 GHz cycles)
+        ev0.record()
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k)
     opt.flush()  # deferred user-table steps still pending are part of the timed work
     t_enq = time.perf_counter() - t0  # host time to enqueue the steps (diagnostic)
+    if args.gpu_only:
+        ev1.record()
     torch.cuda.synchronize()
+    if args.gpu_only:
+        print(json.dumps({"gpu_only_ms_per_step": ev0.elapsed_time(ev1) / args.steps,
+                          "host_enqueue_ms_per_step": t_enq / args.steps * 1e3}))
     nat.timer_enable(TIMED, False)
     if world > 1:
         dist.barrier()

@@ -253,9 +253,10 @@ int dcue_plan_step(dcue_plan* plan, const int64_t* users_src, const int32_t* ite
 int dcue_plan_destroy(dcue_plan* plan);
 
 /* ------------------------------------------------------------------- live kernel timing */
-/* While enabled, every launch of the kernel class (also inside plans created afterwards) is
- * bracketed by HIP events on the stream it runs on; dcue_timer_read waits for the recorded pairs,
- * returns their summed time and count, and resets. For bench rooflines. */
+/* enable = n > 0: every n-th launch of the kernel class (also inside plans created afterwards)
+ * gets a HIP event pair bound to the launch itself (its dispatch's start and end); 0 disables.
+ * dcue_timer_read waits for the recorded pairs, returns their summed time and count, and resets.
+ * For bench rooflines: a timed launch costs the stream a few microseconds, so time a sample. */
 #define DCUE_TIMED_CONV1_WGRAD 0 /* conv layer-1 weight gradient (the step's largest MFMA kernel) */
 #define DCUE_TIMED_CONV1_FWD 1   /* conv layer-1 forward */
 #define DCUE_TIMED_EMB_FLUSH 2   /* deferred user-table Adam: full-table flush */
