@@ -251,8 +251,9 @@ struct StepOpts {
   bool fuse_score = false;     // train forward also runs the hinge backward (k_score_fused)
   const dcue_adam_args* emb_adam = nullptr;  // backward: also step the user table (parts = EMBEDDING)
   hipEvent_t* score_done = nullptr;     // forward (fuse_score): a fork point after the score kernel
-  // backward: the step's tail on each stream, for a caller that must wait for all of it (plans)
-  hipEvent_t* tails = nullptr;           // [4]: caller's stream, user stream, wgrad streams 0 and 1
+  // backward: where the step ends, for a caller that prepares the next one (plans): [0] the
+  // caller's stream after its last kernel, [1] wgrad stream 0 once every side stream's part is in
+  hipEvent_t* tails = nullptr;
   // prepared ahead (plans): the step's copy counts and its cleared accumulator block, in place of
   // the workspace's own
   const float* counts = nullptr;

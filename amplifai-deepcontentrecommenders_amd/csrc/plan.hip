@@ -39,8 +39,7 @@ struct dcue_plan {
   long nacc = 0;
   dcue_mt_state* mt_ahead = nullptr;
   long launches = 0;
-  hipEvent_t ev_ahead = nullptr;  // the next step's inputs are ready (a side-pool ring event)
-  hipEvent_t tails[4] = {};       // the last launched step's end on each of its streams
+  hipEvent_t tails[2] = {};       // the last launched step's end (StepOpts::tails)
 };
 
 namespace {
@@ -98,12 +97,12 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
     q.mt_out = p->mt_ahead;
     TRY(launch_step_prologue(q, s));
     TRY(fork_point(sp, s, &p->tails[0]));
-  } else {
-    TRY(wait_point(s, p->ev_ahead));
   }
-  // the next step's inputs + what the caller sees of this one, once the last step is over
-  for (hipEvent_t e : p->tails)
-    if (e) TRY(wait_point(sa, e));
+  // (step t's inputs, prepared by launch t-1 on wgrad stream 0, are covered by that step's join:
+  // the caller's stream waited for everything on that stream before step t was issued)
+  // the next step's inputs + what the caller sees of this one, once the last step is over (its
+  // side-stream part is ordered before this point on wgrad stream 0 itself)
+  if (p->tails[0]) TRY(wait_point(sa, p->tails[0]));
   {
     StepPrologue q = inputs(nxt);
     if (inbatch) {
@@ -115,9 +114,7 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
     }
     q.users_dst = const_cast<int64_t*>(b0.users); q.users_src = users_src;
     q.items_dst = const_cast<int32_t*>(b0.item_track); q.items_src = items_src;
-    ForkAfter fk(sp, sa, &p->ev_ahead);
     TRY(launch_step_prologue(q, sa));
-    TRY(fk.done());
   }
   dcue_batch b = b0;
   if (users_src) b.users = users_src;
