@@ -188,8 +188,7 @@ struct Ws {
   float *mean[6], *invstd[6], *a[6];
   // exact BN sums (bnacc.h), [6 layers][2 sums][Cmax][2 words]: forward stats, backward sums
   unsigned long long *bnacc, *bnbacc;
-  unsigned int* ticket;  // score_fused's arrival counter; cleared with the accumulators
-  long nzero;            // words from bnacc through the ticket (one clear per step)
+  long nzero;            // words of the accumulator block (one clear per step)
   float* rowsum;         // [B] per-row hinge sums (score_fused)
   int cmax;
   float* y[6];
@@ -202,11 +201,10 @@ struct Ws {
   float *wpart[3], *bpart[3], *G, *S;  // wgrad partials: one set per wgrad stream
 };
 
-// the accumulator block's parts: [6][2][Cmax][2] forward sums, the same for the backward, ticket
+// the accumulator block's parts: [6][2][Cmax][2] forward sums, then the same for the backward
 void rebase_acc(Ws* w, unsigned long long* acc) {
   w->bnacc = acc;
   w->bnbacc = acc + 6L * 2 * w->cmax * 2;
-  w->ticket = reinterpret_cast<unsigned int*>(acc + 2L * 6 * 2 * w->cmax * 2);
 }
 
 size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
@@ -221,7 +219,7 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
     w->a[l] = ar.take<float>(C);
   }
   w->cmax = Cmax > D ? Cmax : D;
-  w->nzero = 2L * 6 * 2 * w->cmax * 2 + 2;
+  w->nzero = 2L * 6 * 2 * w->cmax * 2;
   w->bnacc = ar.take<unsigned long long>(w->nzero);
   rebase_acc(w, w->bnacc);
   w->rowsum = ar.take<float>(B);
@@ -485,7 +483,9 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
                  int train, float margin, const StepOpts& o, hipStream_t s) {
   Ctx c;
   TRY(init_ctx(&c, m));
+  HPROF("capi:1");
   TRY(check_batch(b));
+  HPROF("capi:2");
   if (!t || !t->data || !ws || !m->emb) return DCUE_ERR_INVALID;
   if (o.fuse_score && !train) return DCUE_ERR_INVALID;
   Ws w;
@@ -500,24 +500,32 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   // the user tower runs beside the item tower; the item tower's chain is issued first
   hipEvent_t ev_in = nullptr;
   TRY(fork_point(sp, s, &ev_in));
+  HPROF("capi:3");
   if (!o.prologue_done) TRY(launch_item_counts(b, w.counts, s));
+  HPROF("capi:4");
   TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s,
                    o.prologue_done));
   TRY(wait_point(su, ev_in));
+  HPROF("capi:5");
   if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
+  HPROF("capi:6");
   hipEvent_t ev_uf = nullptr;
   {
     ForkAfter fk(sp, su, &ev_uf);
     TRY(user_forward(c, w, b->users, b->n_rows, nullptr, su));
+    HPROF("capi:7");
     TRY(fk.done());
+    HPROF("capi:8");
   }
   TRY(wait_point(s, ev_uf));
+  HPROF("capi:9");
   if (o.fuse_score) {
     hipEvent_t ev = nullptr;
     ForkAfter fk(sp, s, &ev);
-    TRY(launch_score_fused(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.rowsum, w.loss,
-                           w.du, w.dfcopy, w.ticket, s));
+    TRY(launch_score_fused(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.rowsum, w.du,
+                           w.dfcopy, s));
     TRY(fk.done());
+    HPROF("capi:10");
     if (o.score_done) *o.score_done = ev;
     return DCUE_OK;
   }
@@ -552,7 +560,9 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
                   const float* dscores, float emb_grad_scale, const StepOpts& o, hipStream_t s) {
   Ctx c;
   TRY(init_ctx(&c, m));
+  HPROF("capi:11");
   TRY(check_batch(b));
+  HPROF("capi:12");
   if (!t || !t->data || !ws || !m->grads || !m->emb_grad || !m->emb_slot) return DCUE_ERR_INVALID;
   Ws w;
   if (carve(&m->dims, b->n_rows, b->n_neg, b->n_items, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
@@ -575,6 +585,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   // against those recorded points, so issuing it never delays the chain.
   if (!o.prologue_done)
     DCUE_HIP_CHECK(hipMemsetAsync(w.bnbacc, 0, sizeof(unsigned long long) * 6 * 2 * w.cmax * 2, s));
+    HPROF("capi:13");
   if (!o.fuse_score)  // else the fused score kernel already produced du / dfcopy
     TRY(launch_score_bwd(w.uf, w.f, b, D, dscores ? dscores : w.dhinge, w.cosv, w.norms, w.du,
                          w.dfcopy, s));
@@ -584,11 +595,13 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     ev_score = *o.score_done;
   else
     TRY(fork_point(sp, s, &ev_score));
+    HPROF("capi:14");
   {  // per-item feature gradients df, then (same kernel) the fc input gradient g5 = df W and BN5's sums
     ForkAfter fk(sp, s, &ev_layer[5]);
     TRY(launch_item_grad(w.dfcopy, b, D, w.df, c.P(SEG_FC_W), w.g[5], bn_acc(w.bnbacc, w.cmax, 5),
-                         w.y[5], w.mean[5], w.invstd[5], s));
+                         w.y[5], w.mean[5], w.invstd[5], o.fuse_score ? w.rowsum : nullptr, w.loss, s));
     TRY(fk.done());
+    HPROF("capi:15");
   }
   const hipEvent_t ev_df = ev_layer[5];
   for (int l = 5; l >= 2; --l) {  // dgrad chain: g_l (+ BN_l sums) -> g_{l-1} (+ BN_{l-1} sums)
@@ -606,7 +619,9 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     ra.nout = H;
     ForkAfter fk(sp, s, &ev_layer[l - 1]);
     TRY(launch_conv_dgrad(l, l == 5 ? D : H, ra, s));
+    HPROF("capi:16");
     TRY(fk.done());
+    HPROF("capi:17");
   }
   // conv weight gradient of layer l on stream `so` (its own split-K partial set `ps`); `tail`:
   // a fork point after its last kernel
@@ -615,6 +630,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     const int C = l == 5 ? D : H;
     const int cin = l == 1 ? kMels : H;
     if (so != s) TRY(wait_point(so, ev_layer[l]));
+    HPROF("capi:18");
     WgradArgs wa = {};
     wa.xsrc = l == 1 ? t->data : (const void*)w.y[l - 1];
     wa.item_track = b->item_track;
@@ -630,8 +646,11 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     const int nch = wgrad_nchunk(l, M, C, cin);
     TimerScope tsc;
     TRY(timer_begin(&tsc, l == 1 ? DCUE_TIMED_CONV1_WGRAD : -1, so));
+    HPROF("capi:19");
     TRY(launch_conv_wgrad(l, l == 1 ? src : SRC_ACT, wa, nch, so));
+    HPROF("capi:20");
     TRY(timer_end(&tsc));
+    HPROF("capi:21");
     if (l != 1) {
       ForkAfter fk(sp, so, tail);
       TRY(launch_wgrad_reduce(l, wa.wpart, wa.bpart, nch, C, cin, c.Gd(seg_conv_w(l)),
@@ -649,9 +668,11 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   hipEvent_t tail[4] = {};  // caller's stream, user stream, wgrad streams 0 and 1
   // layer 1 (the step's tail) follows the chain on the caller's stream, issued right away
   TRY(issue_wgrad(1, s, 2, &tail[0]));
+  HPROF("capi:22");
 
   {  // fc weight gradient: dW[n][k] = sum_m df[m][n] bn5(y5)[m][k], db = sum_m df
     TRY(wait_point(sw[0], ev_df));
+    HPROF("capi:23");
     TGemmArgs g = {};
     g.M = D; g.N = D; g.K = M;
     g.A = w.df; g.sam = 1; g.sak = D;
@@ -660,13 +681,16 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     g.C = c.Gd(SEG_FC_W); g.scm = D; g.scn = 1;
     g.rowsum = c.Gd(SEG_FC_B);
     TRY(launch_tgemm(0, 2, g, sw[0]));
+    HPROF("capi:24");
   }
   // layers 5..2: alternating between the two wgrad streams (each with its own partial set)
   hipEvent_t scratch_ev = nullptr;
   for (int l = 5; l >= 2; --l) TRY(issue_wgrad(l, sw[l & 1], l & 1, l <= 3 ? &tail[2 + (l & 1 ? 1 : 0)] : &scratch_ev));
+  HPROF("capi:25");
   // user tower (userembedding.py:33-44 backward), the compact embedding rows, and -- when the step
   // carries it -- the user table's Adam step (it needs nothing from the item tower)
   TRY(wait_point(su, ev_score));
+  HPROF("capi:26");
   {
     TGemmArgs g = {};
     // dW2[n][k] = sum_b du[b][n] relu(h1)[b][k]; db2[n] = sum_b du[b][n]
@@ -676,6 +700,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     g.C = c.Gd(SEG_L2_W); g.scm = E; g.scn = 1;
     g.rowsum = c.Gd(SEG_L2_B);
     TRY(launch_tgemm(0, 1, g, su));
+    HPROF("capi:27");
     // dh1 = (du W2) * (h1 > 0)
     g = TGemmArgs{};
     g.M = B; g.N = E; g.K = D;
@@ -684,6 +709,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     g.C = w.dh1; g.scm = E; g.scn = 1;
     g.cmask = w.h1; g.smm = E; g.smn = 1;
     TRY(launch_tgemm(0, 0, g, su));
+    HPROF("capi:28");
     // dW1[n][k] = sum_b dh1[b][n] relu(E[u_b])[k]; db1[n] = sum_b dh1[b][n]
     g = TGemmArgs{};
     g.M = E; g.N = E; g.K = B;
@@ -692,6 +718,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     g.C = c.Gd(SEG_L1_W); g.scm = E; g.scn = 1;
     g.rowsum = c.Gd(SEG_L1_B);
     TRY(launch_tgemm(0, 1, g, su));
+    HPROF("capi:29");
     // de = (dh1 W1) * (E[u_b] > 0)
     g = TGemmArgs{};
     g.M = B; g.N = E; g.K = E;
@@ -700,6 +727,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     g.C = w.de; g.scm = E; g.scn = 1;
     g.cmask = m->emb; g.smm = E; g.smn = 1; g.cmrow = b->users;
     TRY(launch_tgemm(0, 0, g, su));
+    HPROF("capi:30");
   }
   // the step's end joins the user stream here: its Adam part (and the rolling flush slice) below
   // needs nothing more from this step and runs on into the next one, ordered on this stream
@@ -708,17 +736,23 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, m->emb_rows,
                         m->emb_step ? m->emb_log : nullptr, su));
     TRY(fk.done());
+    HPROF("capi:31");
   }
   if (o.emb_adam) TRY(launch_adam(m, o.emb_adam, c.poff, su));
+  HPROF("capi:32");
 
   // the join: wgrad stream 0 collects the user stream's and wgrad stream 1's tails, and the caller's
   // stream waits for it once (each cross-queue wait on a pending event costs the waiting queue
   // ≈4 µs, measured; on the side stream that time is slack, on the caller's it is the step's)
   TRY(wait_point(sw[0], tail[1]));
+  HPROF("capi:33");
   TRY(wait_point(sw[0], tail[3]));
+  HPROF("capi:34");
   hipEvent_t joined = nullptr;
   TRY(fork_point(sp, sw[0], &joined));
+  HPROF("capi:35");
   TRY(wait_point(s, joined));
+  HPROF("capi:36");
   if (o.tails) {
     o.tails[0] = tail[0];
     o.tails[1] = joined;

@@ -6,6 +6,17 @@
 #include "dcue_common.h"
 #include "bnacc.h"
 
+// Host-time attribution of step issue (diagnostic; DCUE_HOST_PROFILE=1 prints the per-label mean
+// host time between consecutive marks at exit)
+namespace dcue {
+bool host_profile_on();
+void host_profile_mark(const char* label);
+}  // namespace dcue
+#define HPROF(label)                                          \
+  do {                                                        \
+    if (::dcue::host_profile_on()) ::dcue::host_profile_mark(label); \
+  } while (0)
+
 // propagate a non-zero dcue_status
 #define TRY(x)                 \
   do {                         \
@@ -164,17 +175,17 @@ int launch_score_fwd(const float* uf, const float* f, const dcue_batch* b, int d
                      float* scores, float* cosv, float* norms, float* hinge, float* loss,
                      float* dhinge, hipStream_t s);
 // forward + hinge backward in one pass (the loss gradient is known in the forward): also writes
-// du / dfcopy; the loss mean is taken by the last row block to finish (ticket, cleared by the caller)
+// du / dfcopy and the per-row hinge sums; k_item_grad (given the row sums) takes the loss mean
 int launch_score_fused(const float* uf, const float* f, const dcue_batch* b, int d, float margin,
-                       float* scores, float* cosv, float* norms, float* rowsum, float* loss,
-                       float* du, float* dfcopy, unsigned int* ticket, hipStream_t s);
+                       float* scores, float* cosv, float* norms, float* rowsum, float* du,
+                       float* dfcopy, hipStream_t s);
 int launch_score_bwd(const float* uf, const float* f, const dcue_batch* b, int d,
                      const float* dscores, const float* cosv, const float* norms, float* du,
                      float* dfcopy, hipStream_t s);
 // per-item feature gradients; with fcW also the fc input gradient g5 = df W and BN5's backward sums
 int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df, const float* fcW, float* g5,
                      unsigned long long* acc5, const float* y5, const float* mean5, const float* invstd5,
-                     hipStream_t s);
+                     const float* rowsum, float* loss, hipStream_t s);
 int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float scale,
                     float* emb_grad, int32_t* slot, int64_t* emb_rows, dcue_emb_log* log,
                     hipStream_t s);
@@ -247,7 +258,7 @@ int join_user_stream(hipStream_t s);
 
 // ------------------------------------------------------------- step implementation (capi.hip)
 struct StepOpts {
-  bool prologue_done = false;  // counts written + accumulators (and ticket) cleared by the prologue
+  bool prologue_done = false;  // counts written + accumulators cleared by the prologue
   bool fuse_score = false;     // train forward also runs the hinge backward (k_score_fused)
   const dcue_adam_args* emb_adam = nullptr;  // backward: also step the user table (parts = EMBEDDING)
   hipEvent_t* score_done = nullptr;     // forward (fuse_score): a fork point after the score kernel
@@ -259,7 +270,7 @@ struct StepOpts {
   const float* counts = nullptr;
   unsigned long long* acc = nullptr;
 };
-// words of the per-step accumulator block (BN sums + score ticket) cleared before each step
+// words of the per-step accumulator block (BN sums) cleared before each step
 long step_acc_words(const dcue_dims* d, int B, int N, int M);
 int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
                  int train, float margin, const StepOpts& o, hipStream_t s);

@@ -96,7 +96,9 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
     q.mt = inbatch ? p->cfg.mt : nullptr;
     q.mt_out = p->mt_ahead;
     TRY(launch_step_prologue(q, s));
+    HPROF("plan:1");
     TRY(fork_point(sp, s, &p->tails[0]));
+    HPROF("plan:2");
   }
   // (step t's inputs, prepared by launch t-1 on wgrad stream 0, are covered by that step's join:
   // the caller's stream waited for everything on that stream before step t was issued)
@@ -115,6 +117,7 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
     q.users_dst = const_cast<int64_t*>(b0.users); q.users_src = users_src;
     q.items_dst = const_cast<int32_t*>(b0.item_track); q.items_src = items_src;
     TRY(launch_step_prologue(q, sa));
+    HPROF("plan:3");
   }
   dcue_batch b = b0;
   if (users_src) b.users = users_src;
@@ -130,7 +133,9 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   o.score_done = &score_done;
   o.tails = p->tails;
   TRY(forward_impl(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, 1, p->cfg.margin, o, s));
+  HPROF("plan:4");
   TRY(backward_impl(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, nullptr, p->cfg.emb_grad_scale, o, s));
+  HPROF("plan:5");
   ++p->launches;
   return DCUE_OK;
 }
@@ -268,6 +273,7 @@ extern "C" int dcue_plan_launch(dcue_plan* p, const int64_t* users_src, const in
 
 extern "C" int dcue_plan_step(dcue_plan* p, const int64_t* users_src, const int32_t* item_track_src,
                               const dcue_adam_args* adam, void* stream) {
+  HPROF("plan_step:enter (python)");
   if (!p) return DCUE_ERR_INVALID;
   if (!adam || p->exec) {  // graph replay (or no optimizer): the Adam step follows as one call
     const int st = dcue_plan_launch(p, users_src, item_track_src, stream);
@@ -285,7 +291,10 @@ extern "C" int dcue_plan_step(dcue_plan* p, const int64_t* users_src, const int3
   dense.parts = DCUE_ADAM_DENSE;
   const int st = issue_eager(p, users_src, item_track_src, (hipStream_t)stream, &emb);
   if (st) return st;
-  return dcue_adam_step(&p->model, &dense, stream);
+  HPROF("plan_step:issue");
+  const int r = dcue_adam_step(&p->model, &dense, stream);
+  HPROF("plan_step:adam");
+  return r;
 }
 
 extern "C" int dcue_plan_destroy(dcue_plan* p) {

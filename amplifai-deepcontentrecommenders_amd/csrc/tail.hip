@@ -288,18 +288,40 @@ int launch_score_fwd(const float* uf, const float* f, const dcue_batch* b, int d
 
 // Forward + hinge backward of one row per workgroup (plans: the loss gradient is known here, so
 // k_score_bwd's pass is folded in). Same arithmetic and summation orders as k_score_fwd,
-// k_loss_mean and k_score_bwd; the loss mean is taken by the last row block to finish.
+// k_loss_mean and k_score_bwd; the loss mean (k_loss_mean's sums) is taken by the next kernel,
+// k_item_grad, from the row sums. CPW > 0: at most CPW copies per wave -- every copy's index and
+// feature row are loaded at once, up front, and the rows stay in registers for the backward (one
+// load round instead of two per copy); CPW == 0: any N, copy by copy.
+template <int CPW>
 __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ uf,
                                                      const float* __restrict__ f, dcue_batch b, int d,
                                                      float margin, float* scores, float* cosv,
-                                                     float* norms, float* rowsum, float* loss, float* dU,
-                                                     float* dfcopy, unsigned int* ticket) {
-  __shared__ float cs[1025], dcs[1025], hs[1024];
+                                                     float* norms, float* rowsum, float* dU,
+                                                     float* dfcopy) {
+  constexpr int CMAX = CPW > 0 ? 4 * CPW : 1025;
+  __shared__ float cs[CMAX], dcs[CMAX], hs[CMAX];
   __shared__ float gus[4][256];
-  __shared__ bool last;
   const int row = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int N = b.n_neg, per = (d + 63) / 64;
   const float eps = 1e-8f;
+  constexpr int CR = CPW > 0 ? CPW : 1;  // register-resident copies
+  float v[CR][4];
+  float nfr[CR];
+  if constexpr (CPW > 0) {
+    int item[CPW];
+#pragma unroll
+    for (int q = 0; q < CPW; ++q) {
+      const int c = wave + 4 * q;
+      item[q] = c <= N ? copy_item(b, row, c) : row;
+    }
+#pragma unroll
+    for (int q = 0; q < CPW; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = lane + 64 * e;
+        v[q][e] = (wave + 4 * q <= N && e < per && k < d) ? f[(long)item[q] * d + k] : 0.f;
+      }
+  }
   float u[4];
   float su = 0.f;
 #pragma unroll
@@ -311,25 +333,37 @@ __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ u
   const float nu = sqrtf(wave_sum(su));
   const float du = fmaxf(nu, eps);
   if (wave == 0 && lane == 0) norms[(long)row * (N + 2)] = nu;
-  for (int c = wave; c <= N; c += 4) {
-    const long item = copy_item(b, row, c);
-    float v[4], sf = 0.f;
+  auto score_copy = [&](int c, const float (&w)[4]) {
+    float sf = 0.f;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = lane + 64 * e;
-      v[e] = (e < per && k < d) ? f[item * d + k] : 0.f;
-      sf += v[e] * v[e];
-    }
+    for (int e = 0; e < 4; ++e) sf += w[e] * w[e];
     const float nf = sqrtf(wave_sum(sf));
     const float dfn = fmaxf(nf, eps);
     float dot = 0.f;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) dot += (u[e] / du) * (v[e] / dfn);
+    for (int e = 0; e < 4; ++e) dot += (u[e] / du) * (w[e] / dfn);
     const float cv = wave_sum(dot);
     if (lane == 0) {
       norms[(long)row * (N + 2) + 1 + c] = nf;
       cosv[(long)row * (N + 1) + c] = cv;
       cs[c] = cv;
+    }
+    return nf;
+  };
+  if constexpr (CPW > 0) {
+#pragma unroll
+    for (int q = 0; q < CPW; ++q)
+      if (wave + 4 * q <= N) nfr[q] = score_copy(wave + 4 * q, v[q]);
+  } else {
+    for (int c = wave; c <= N; c += 4) {
+      const long item = copy_item(b, row, c);
+      float w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = lane + 64 * e;
+        w[e] = (e < per && k < d) ? f[item * d + k] : 0.f;
+      }
+      score_copy(c, w);
     }
   }
   __syncthreads();
@@ -362,19 +396,34 @@ __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ u
     uh[e] = u[e] / nuc;
     gu[e] = 0.f;
   }
-  for (int c = wave; c <= N; c += 4) {
-    const long item = copy_item(b, row, c);
+  auto back_copy = [&](int c, const float (&w)[4], float nf_raw) {
     const float dc = dcs[c];
     const float cv = cs[c];
-    const float nf = fmaxf(norms[(long)row * (N + 2) + 1 + c], eps);
+    const float nf = fmaxf(nf_raw, eps);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int k = lane + 64 * e;
       if (e < per && k < d) {
-        const float fh = f[item * d + k] / nf;
+        const float fh = w[e] / nf;
         gu[e] += dc * (fh - cv * uh[e]) / nuc;
         dfcopy[((long)row * (N + 1) + c) * d + k] = dc * (uh[e] - cv * fh) / nf;
       }
+    }
+  };
+  if constexpr (CPW > 0) {
+#pragma unroll
+    for (int q = 0; q < CPW; ++q)
+      if (wave + 4 * q <= N) back_copy(wave + 4 * q, v[q], nfr[q]);
+  } else {
+    for (int c = wave; c <= N; c += 4) {
+      const long item = copy_item(b, row, c);
+      float w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = lane + 64 * e;
+        w[e] = (e < per && k < d) ? f[item * d + k] : 0.f;
+      }
+      back_copy(c, w, norms[(long)row * (N + 2) + 1 + c]);
     }
   }
 #pragma unroll
@@ -385,30 +434,21 @@ __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ u
   __syncthreads();
   for (int k = threadIdx.x; k < d; k += blockDim.x)
     dU[(long)row * d + k] = ((gus[0][k] + gus[1][k]) + gus[2][k]) + gus[3][k];
-  // loss = mean over rows of the row sums, in row order, by the last block to arrive
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(ticket, 1u) == (unsigned)(b.n_rows - 1);
-  }
-  __syncthreads();
-  if (last) {  // every row sum is loaded at once, then added in row order
-    __threadfence();
-    for (int r = threadIdx.x; r < b.n_rows; r += blockDim.x) hs[r] = __builtin_nontemporal_load(rowsum + r);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float s = 0.f;
-      for (int r = 0; r < b.n_rows; ++r) s += hs[r];
-      *loss = s / (float)b.n_rows;
-    }
-  }
 }
 
 int launch_score_fused(const float* uf, const float* f, const dcue_batch* b, int d, float margin,
-                       float* scores, float* cosv, float* norms, float* rowsum, float* loss,
-                       float* du, float* dfcopy, unsigned int* ticket, hipStream_t s) {
+                       float* scores, float* cosv, float* norms, float* rowsum, float* du,
+                       float* dfcopy, hipStream_t s) {
   if (d > 256 || b->n_neg > 1024 || b->n_rows > 1024) return DCUE_ERR_UNSUPPORTED;
-  DCUE_LAUNCH(k_score_fused, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, margin, scores, cosv,
-                     norms, rowsum, loss, du, dfcopy, ticket);
+  if (b->n_neg + 1 <= 16)
+    DCUE_LAUNCH(k_score_fused<4>, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, margin, scores, cosv,
+                norms, rowsum, du, dfcopy);
+  else if (b->n_neg + 1 <= 32)
+    DCUE_LAUNCH(k_score_fused<8>, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, margin, scores, cosv,
+                norms, rowsum, du, dfcopy);
+  else
+    DCUE_LAUNCH(k_score_fused<0>, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, margin, scores, cosv,
+                norms, rowsum, du, dfcopy);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
@@ -469,30 +509,72 @@ int launch_score_bwd(const float* uf, const float* f, const dcue_batch* b, int d
 
 constexpr int kItemGradCap = 4096;  // copies per item (B*N + 1 in gather layout)
 
-// df[i] = sum over item i's copies. One workgroup per item: wave 0 lists the item's copies in
-// (positive, (b,j) row-major) order with ballots over neg_item (loads batched ahead of the ballots);
-// the four waves then each sum a contiguous quarter of the list with all its row loads in flight,
-// and the quarters are added in wave order (deterministic). With `fc` set the fc input gradient of
-// the item follows in the same workgroup -- g5[i][n] = sum_k df[i][k] W[k][n] (k in order) -- with
-// its share of BN5's backward sums (sum g5, sum g5*xhat5) into the accumulators.
+// df[i] = sum over item i's copies. One workgroup per item: the four waves scan contiguous
+// quarters of neg_item with ballots and their hit lists are laid end to end in wave order, which
+// lists the copies in (positive, (b,j) row-major) order; each wave then sums a contiguous quarter of
+// the list with all its row loads in flight, and the quarters are added in wave order
+// (deterministic). With `fc` set the fc input gradient of the item follows in the same workgroup --
+// g5[i][n] = sum_k df[i][k] W[k][n] (k in order, the two k halves added) -- with its share of BN5's
+// backward sums (sum g5, sum g5*xhat5) into the accumulators. Everything the block reads that does
+// not depend on the scan (W into LDS when d <= 128, the item's y5 row, the BN5 stats, the row sums
+// for the loss) is loaded up front, so the block waits on memory about three times, not eight.
 struct ItemGradFc {
+  const float* rowsum;     // nullable: the fused score's per-row hinge sums -> loss (block 0)
+  float* loss;
   const float* W;          // fc.weight [d][d] (null: df only)
   float* g5;               // [M][d]
   unsigned long long* acc; // BN5 backward accumulators [2][d]
   const float *y5, *mean5, *invstd5;
 };
 
+constexpr int kItemGradWLds = 128;  // W staged in LDS up to d = 128 (64 KB)
+
+template <bool WLDS>
 __global__ __launch_bounds__(256) void k_item_grad(const float* __restrict__ dfcopy, dcue_batch b, int d,
                                                    float* df, ItemGradFc fc) {
   constexpr int kCap = kItemGradCap;
-  __shared__ int list[kCap];
-  __shared__ int s_len;
+  __shared__ int list[kCap];      // per-wave hit lists, kCap / 4 each
+  __shared__ int lst[kCap + 1];   // the item's copies in order
+  __shared__ int s_len, wlen[4], wofs[4];
   __shared__ float part[4][256];
   __shared__ float dfs[256];
+  __shared__ float rs[1024];
+  extern __shared__ __attribute__((aligned(16))) float wl[];  // [d][d] when WLDS
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = blockIdx.x;
   const int N = b.n_neg, B = b.n_rows;
-  if (b.layout == DCUE_LAYOUT_CATALOGUE) {
+  const bool gather = b.layout != DCUE_LAYOUT_CATALOGUE;
+
+  // ---- up-front loads
+  const int nneg = B * N;
+  const int e_lo = (int)(((long)nneg * wave) / 4), e_hi = (int)(((long)nneg * (wave + 1)) / 4);
+  constexpr int kBatch = 8;
+  int32_t nv[kBatch];
+  if (gather) {
+#pragma unroll
+    for (int q = 0; q < kBatch; ++q) {
+      const int e = e_lo + 64 * q + lane;
+      nv[q] = e < e_hi ? b.neg_item[e] : -1;
+    }
+  }
+  if constexpr (WLDS) {
+    if (fc.W) {
+      const int n4 = d * d / 4;
+      for (int q = threadIdx.x; q < n4; q += blockDim.x)
+        reinterpret_cast<float4*>(wl)[q] = reinterpret_cast<const float4*>(fc.W)[q];
+    }
+  }
+  float y5v = 0.f, mu5 = 0.f, is5 = 0.f;
+  const bool col = fc.W && threadIdx.x < d;
+  if (col) {
+    y5v = fc.y5[(long)i * d + threadIdx.x];
+    mu5 = fc.mean5[threadIdx.x];
+    is5 = fc.invstd5[threadIdx.x];
+  }
+  if (fc.rowsum && i == 0)
+    for (int r = threadIdx.x; r < B; r += blockDim.x) rs[r] = fc.rowsum[r];
+
+  if (!gather) {
     const long cidx = i < B ? (long)i * (N + 1) : (long)((i - B) / N) * (N + 1) + 1 + (i - B) % N;
     for (int k = threadIdx.x; k < d; k += blockDim.x) {
       const float v = dfcopy[cidx * d + k];
@@ -500,35 +582,46 @@ __global__ __launch_bounds__(256) void k_item_grad(const float* __restrict__ dfc
       dfs[k] = v;
     }
   } else {
-    if (wave == 0) {
+    {  // scan: this wave's quarter of the negatives (the first batch is already loaded)
       int len = 0;
-      if (i < B) {
-        if (lane == 0) list[0] = i * (N + 1);
-        len = 1;
-      }
-      const int nneg = B * N;
-      constexpr int kBatch = 16;
-      for (int e0 = 0; e0 < nneg; e0 += 64 * kBatch) {
-        int32_t v[kBatch];
+      for (int e0 = e_lo; e0 < e_hi; e0 += 64 * kBatch) {
+        if (e0 != e_lo) {
 #pragma unroll
-        for (int q = 0; q < kBatch; ++q) {
-          const int e = e0 + 64 * q + lane;
-          v[q] = e < nneg ? b.neg_item[e] : -1;
+          for (int q = 0; q < kBatch; ++q) {
+            const int e = e0 + 64 * q + lane;
+            nv[q] = e < e_hi ? b.neg_item[e] : -1;
+          }
         }
 #pragma unroll
         for (int q = 0; q < kBatch; ++q) {
           const int e = e0 + 64 * q + lane;
-          const bool hit = v[q] == i;
+          const bool hit = nv[q] == i;
           const unsigned long long bal = __ballot(hit);
           const int pos = len + __popcll(bal & ((1ull << lane) - 1ull));
-          if (hit && pos < kCap) {
+          if (hit && pos < kCap / 4) {
             const int row = e / N;
-            list[pos] = row * (N + 1) + 1 + (e - row * N);
+            list[wave * (kCap / 4) + pos] = row * (N + 1) + 1 + (e - row * N);
           }
           len += __popcll(bal);
         }
       }
-      if (lane == 0) s_len = len < kCap ? len : kCap;
+      if (lane == 0) wlen[wave] = len;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // compact: positive, then the quarters in order
+      int n = 0;
+      if (i < B) lst[n++] = i * (N + 1);
+      for (int w = 0; w < 4; ++w) {
+        const int m = wlen[w] < kCap / 4 ? wlen[w] : kCap / 4;
+        wofs[w] = n;
+        n += m;
+      }
+      s_len = n;
+    }
+    __syncthreads();
+    for (int w = 0; w < 4; ++w) {
+      const int m = wlen[w] < kCap / 4 ? wlen[w] : kCap / 4;
+      for (int q = threadIdx.x; q < m; q += blockDim.x) lst[wofs[w] + q] = list[w * (kCap / 4) + q];
     }
     __syncthreads();
     const int len = s_len;
@@ -543,7 +636,7 @@ __global__ __launch_bounds__(256) void k_item_grad(const float* __restrict__ dfc
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int k = lane + 64 * e;
-          v[r][e] = (qb + r < q1 && e < per && k < d) ? dfcopy[(long)list[qb + r] * d + k] : 0.f;
+          v[r][e] = (qb + r < q1 && e < per && k < d) ? dfcopy[(long)lst[qb + r] * d + k] : 0.f;
         }
 #pragma unroll
       for (int r = 0; r < kRows; ++r)
@@ -562,25 +655,68 @@ __global__ __launch_bounds__(256) void k_item_grad(const float* __restrict__ dfc
       dfs[k] = v;
     }
   }
-  if (!fc.W) return;
-  __syncthreads();
-  for (int n = threadIdx.x; n < d; n += blockDim.x) {
-    float g = 0.f;
-    for (int k = 0; k < d; ++k) g += dfs[k] * fc.W[(long)k * d + n];
-    fc.g5[(long)i * d + n] = g;
-    const float xh = (fc.y5[(long)i * d + n] - fc.mean5[n]) * fc.invstd5[n];
-    acc128_add(acc_at(fc.acc, d, 0, n), g);
-    acc128_add(acc_at(fc.acc, d, 1, n), g * xh);
+  if (fc.W) {
+    __syncthreads();
+    // g5[i][n] = sum_k df[i][k] W[k][n]: the k range split in halves over the block's two thread
+    // halves (first half + second half, fixed order)
+    const int hk = (d + 1) / 2;
+    for (int t = threadIdx.x; t < 2 * d; t += blockDim.x) {
+      const int n = t % d, h = t / d;
+      const int k0 = h * hk, k1 = h ? d : hk;
+      float g = 0.f;
+      if constexpr (WLDS) {
+        for (int k = k0; k < k1; ++k) g += dfs[k] * wl[k * d + n];
+      } else {
+        for (int k = k0; k < k1; k += 16) {  // sixteen weight loads in flight, then the ordered sum
+          float wv[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) wv[q] = k + q < k1 ? fc.W[(long)(k + q) * d + n] : 0.f;
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            if (k + q < k1) g += dfs[k + q] * wv[q];
+        }
+      }
+      part[h][n] = g;
+    }
+    __syncthreads();
+    if (col) {
+      const int n = threadIdx.x;
+      const float g = part[0][n] + part[1][n];
+      fc.g5[(long)i * d + n] = g;
+      const float xh = (y5v - mu5) * is5;
+      acc128_add(acc_at(fc.acc, d, 0, n), g);
+      acc128_add(acc_at(fc.acc, d, 1, n), g * xh);
+    }
+  }
+  if (fc.rowsum && i == 0) {  // loss = mean of the row sums in row order (k_loss_mean's sums)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float s = 0.f;
+      for (int r = 0; r < B; ++r) s += rs[r];
+      *fc.loss = s / (float)B;
+    }
   }
 }
 
 int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df, const float* fcW, float* g5,
                      unsigned long long* acc5, const float* y5, const float* mean5, const float* invstd5,
-                     hipStream_t s) {
-  if (d > 256) return DCUE_ERR_UNSUPPORTED;
+                     const float* rowsum, float* loss, hipStream_t s) {
+  if (d > 256 || (rowsum && b->n_rows > 1024)) return DCUE_ERR_UNSUPPORTED;
   if (b->layout == DCUE_LAYOUT_GATHER && (long)b->n_rows * b->n_neg + 1 > kItemGradCap) return DCUE_ERR_UNSUPPORTED;
-  const ItemGradFc fc = {fcW, g5, acc5, y5, mean5, invstd5};
-  DCUE_LAUNCH(k_item_grad, dim3(b->n_items), dim3(256), 0, s, dfcopy, *b, d, df, fc);
+  const ItemGradFc fc = {rowsum, loss, fcW, g5, acc5, y5, mean5, invstd5};
+  if (fcW && d <= kItemGradWLds && d % 4 == 0) {
+    const size_t lds = sizeof(float) * d * d;
+    static bool attr = false;
+    if (!attr) {
+      DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_item_grad<true>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)(sizeof(float) * kItemGradWLds * kItemGradWLds)));
+      attr = true;
+    }
+    DCUE_LAUNCH(k_item_grad<true>, dim3(b->n_items), dim3(256), lds, s, dfcopy, *b, d, df, fc);
+  } else {
+    DCUE_LAUNCH(k_item_grad<false>, dim3(b->n_items), dim3(256), 0, s, dfcopy, *b, d, df, fc);
+  }
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }

@@ -6,6 +6,11 @@
 // replay is timed. Single host thread per process (the
 // library's usage model: one process per GPU).
 #include <stdio.h>
+#include <stdlib.h>
+
+#include <chrono>
+#include <map>
+#include <string>
 
 #include <utility>
 #include <vector>
@@ -104,6 +109,46 @@ void timer_release(hipEvent_t e) {
 
 namespace {
 char g_last_error[512] = "";
+
+struct HostProfile {
+  bool on = false;
+  std::chrono::steady_clock::time_point last;
+  std::map<std::string, std::pair<double, long>> acc;
+  std::vector<std::string> order;
+  HostProfile() {
+    const char* e = getenv("DCUE_HOST_PROFILE");
+    on = e && e[0] == '1';
+    last = std::chrono::steady_clock::now();
+  }
+  ~HostProfile() {
+    if (!on) return;
+    for (auto& k : order) {
+      auto& v = acc[k];
+      fprintf(stderr, "[dcue host] %-28s %8.2f us  x%ld\n", k.c_str(), v.first / (v.second ? v.second : 1),
+              v.second);
+    }
+  }
+};
+HostProfile& hp() {
+  static HostProfile p;
+  return p;
+}
+}  // namespace
+
+bool host_profile_on() { return hp().on; }
+
+void host_profile_mark(const char* label) {
+  HostProfile& p = hp();
+  const auto now = std::chrono::steady_clock::now();
+  const double us = std::chrono::duration<double, std::micro>(now - p.last).count();
+  p.last = now;
+  auto it = p.acc.find(label);
+  if (it == p.acc.end()) {
+    p.order.push_back(label);
+    it = p.acc.emplace(label, std::make_pair(0.0, 0L)).first;
+  }
+  it->second.first += us;
+  it->second.second += 1;
 }
 
 void set_last_error(const char* expr, hipError_t e, const char* file, int line) {
