@@ -79,7 +79,8 @@ class PlanConfig(ctypes.Structure):
 
 MT_STATE_BYTES = 624 * 4 + 16
 MAX_LOG_CAP = 256
-ABI_VERSION = 2
+ABI_VERSION = 3
+RANK_SPLIT, RANK_SINGLE = 0, 1
 
 _P = ctypes.c_void_p
 _SIGS = {
@@ -121,6 +122,11 @@ _SIGS = {
     "dcue_timer_enable": ([ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
     "dcue_timer_read": ([ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)],
                         ctypes.c_int),
+    "dcue_rank_workspace_bytes": ([ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                   ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "dcue_rank_metrics": ([_P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int32, _P, ctypes.c_int32, _P, _P,
+                           _P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_size_t, _P, _P, _P, _P], ctypes.c_int),
+    "dcue_factor_repeat_mean": ([_P, ctypes.c_int64, ctypes.c_int32, _P], ctypes.c_int),
 }
 
 _lib = None

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DCUE_ABI_VERSION 2
+#define DCUE_ABI_VERSION 3
 #define DCUE_N_MELS 128
 #define DCUE_N_FRAMES 131
 #define DCUE_N_BN 6
@@ -264,6 +264,42 @@ int dcue_plan_destroy(dcue_plan* plan);
 #define DCUE_N_TIMED 4
 int dcue_timer_enable(int32_t kernel, int32_t enable);
 int dcue_timer_read(int32_t kernel, double* total_ms_host, int64_t* launches_host);
+
+/* ------------------------------------------------------------------------ evaluation metrics */
+/* Ranking metrics of DCUE's evaluation for a batch of queries (users for DCUE.score, songs for
+ * DCUE.score_song), replacing the per-query predict() loops and sklearn calls of nn/dcue.py:380-476
+ * and the candidate lists of datasets/dcuepredset.py:39-131.
+ *   query_feat [n_query_rows][d], cand_feat [n_cand][d]: factors (DCUE.user_factors / item_factors,
+ *     nn/dcue.py:629-668); scores are nn.CosineSimilarity(dim=1) of a query row and a candidate row.
+ *   queries[n_queries]: query row of each evaluated query (a sample; repeats allowed, :413/:420).
+ *   pos_ptr[n_query_rows+1], pos_idx: CSR over query rows of the candidates the query interacted
+ *     with in ANY split (datasets/dcuedataset.py:74-89 item_user matrix), each row sorted, no repeats.
+ *   cand_class[n_cand]: bit 0 = the candidate is in the pred list (the pred split's songs/users),
+ *     bit 1 = in the truth list; 0 = in neither.
+ *   DCUE_RANK_SPLIT (DCUE.score, :399-447): AUC weighted over {pred positives + truth negatives} and
+ *     {pred negatives + truth positives}, AP over both; has_pos = the query has pred positives (the
+ *     reference stops its user loop at the first query without, :393-394).
+ *   DCUE_RANK_SINGLE (DCUE.score_song, :463-474): targets = 1 for the query's positives among the
+ *     candidates with bit 1, 0 for EVERY candidate with bit 0 -- positives included: the reference's
+ *     non-user list (dcuepredset.py:53-62) takes `getrow(i).nonzero()[0]`, the row indices (all 0),
+ *     so it only drops user index 0 and keeps the song's own users as negatives too; callers set
+ *     bit 0 on the split's users except user 0 and bit 1 on the split's users. AUC / AP over that
+ *     list, 1/1 if every target is 1, 0/0 if none; has_pos = 0 marks a query the reference skips.
+ * Exact tie-aware AUC (Mann-Whitney, ties 1/2) and step-wise AP from integer rank counts, fp64.
+ * At most 4096 positives per query inside the lists (else DCUE_ERR_UNSUPPORTED). query_batch
+ * queries are scored per pass; the workspace holds their [query_batch][n_cand] score rows.
+ * Synchronises `stream` before returning. */
+#define DCUE_RANK_SPLIT 0
+#define DCUE_RANK_SINGLE 1
+int dcue_rank_workspace_bytes(int64_t n_cand, int32_t d, int32_t query_batch, size_t* bytes_host);
+int dcue_rank_metrics(const float* query_feat, int64_t n_query_rows, const float* cand_feat,
+                      int64_t n_cand, int32_t d, const int32_t* queries, int32_t n_queries,
+                      const int64_t* pos_ptr, const int32_t* pos_idx, const uint8_t* cand_class,
+                      int32_t mode, int32_t query_batch, void* ws, size_t ws_bytes, double* auc,
+                      double* ap, int32_t* has_pos, void* stream);
+/* DCUE._item_factors' averaging (nn/dcue.py:655-668): f <- (f + f + ... n_iter times) / n_iter in
+ * fp32, for 131-frame tracks whose n_iter eval passes are identical (no random crop). */
+int dcue_factor_repeat_mean(float* f, int64_t n, int32_t n_iter, void* stream);
 
 #ifdef __cplusplus
 }

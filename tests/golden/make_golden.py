@@ -18,6 +18,8 @@ Which reference code produced what:
 * scheduler.npz -- CyclicLRWithRestarts (optim/cyclic_scheduler.py:49-215) driven the way
                    DCUE.fit/_train_epoch drive it (nn/dcue.py:338-341, 209-210).
 * train5.npz    -- five DCUE train steps (nn/dcue.py:202-210) with Adam + scheduler.
+* eval.npz      -- the evaluation path end to end: DCUE._user_factors / _item_factors over
+                   DCUEItemset, DCUE.score (val and train splits, DCUEPredset) and score_song.
 * metrics.npz   -- DCUE.score's split-weighted AUC / mAP arithmetic (nn/dcue.py:399-449) and
                    score_song's (nn/dcue.py:463-476), on fixed score vectors.
 """
@@ -304,13 +306,96 @@ def metrics_fixture():
     _save("metrics.npz", **out)
 
 
+def eval_fixture():
+    """DCUE's evaluation path end to end (nn/dcue.py:380-476, 629-668; datasets/dcuepredset.py,
+    dcueitemset.py): factors from a small eval-mode model over torch.save'd spectrograms, then
+    per-user split-weighted AUC / mAP (val and train) and per-song AUC / AP."""
+    import tempfile
+    from torch.utils.data import DataLoader
+    from dcrecommend.datasets.dcuepredset import DCUEPredset  # reference
+    from dcrecommend.datasets.dcueitemset import DCUEItemset  # reference
+    n_users, n_tracks, n_pairs, H, d = 30, 48, 420, 32, 32
+    trip = _synthetic_triplets(n_users, n_tracks, n_pairs, 11)
+    songs = sorted(set(trip["song_id"]))
+    # metadata rows in a shuffled order: metadata index != item (category) index
+    meta_order = np.random.RandomState(5).permutation(len(songs))
+    meta_songs = [songs[i] for i in meta_order]
+    gen = torch.Generator().manual_seed(21)
+    spec = _spectros(gen, len(songs), 128, 131)
+    # two tracks share one spectrogram: identical factors -> exact score ties across items
+    spec[7] = spec[3]
+    tmp = tempfile.mkdtemp()
+    paths = []
+    for k in range(len(songs)):
+        p = os.path.join(tmp, "t%03d.pt" % k)
+        torch.save(spec[k].clone(), p)
+        paths.append(p)
+    meta = pd.DataFrame({"idx": np.arange(len(songs)), "song_id": meta_songs, "data_mel": paths})
+    train = DCUEPredset(trip.copy(), meta, split="train")
+    val = DCUEPredset(trip.copy(), meta, split="val")
+    items = DCUEItemset(trip.copy(), meta)
+    torch.manual_seed(4)
+    tr = DCUE(feature_dim=d, conv_hidden=H, batch_size=8)
+    tr.n_users, tr.n_items = len(train.user_index), len(train.item_index)
+    tr.epoch_size = 64
+    tr._init_nn()
+    sd = tr.model.state_dict()
+    g2 = torch.Generator().manual_seed(9)
+    for k in list(sd):
+        if k.endswith("running_mean"):
+            sd[k] = 0.3 * torch.randn(sd[k].shape, generator=g2)
+        elif k.endswith("running_var"):
+            sd[k] = 0.5 + torch.rand(sd[k].shape, generator=g2)
+        elif k.endswith("num_batches_tracked"):
+            sd[k] = torch.tensor(7)
+    tr.model.load_state_dict(sd)
+    tr._user_factors(items)
+    tr._item_factors(items)
+
+    def loader(ds):
+        return DataLoader(ds, batch_size=1024, shuffle=False, num_workers=0)
+    val_users = sorted(set(train.uniq_users).intersection(set(val.uniq_users)))
+    train_users = sorted(train.uniq_users)
+    val_auc, val_ap, tr_auc, tr_ap = [], [], [], []
+    for u in val_users:
+        a, m = tr.score([u], loader(val), loader(train))
+        val_auc.append(a)
+        val_ap.append(m)
+    for u in train_users:
+        a, m = tr.score([u], loader(train), loader(train))
+        tr_auc.append(a)
+        tr_ap.append(m)
+    val_songs = sorted(val.uniq_songs)
+    song_auc, song_ap = [], []
+    for s in val_songs:
+        a, m = tr.score_song([s], loader(val))
+        song_auc.append(a)
+        song_ap.append(m)
+    mean_val = tr.score(val_users[:9], loader(val), loader(train))
+    _save("eval.npz", raw_users=trip["user_id"].to_numpy().astype(str),
+          raw_songs=trip["song_id"].to_numpy().astype(str), raw_score=trip["score"].to_numpy(),
+          meta_songs=np.array(meta_songs).astype(str), spec=spec.half(), H=H, d=d,
+          **{"sd." + k: v for k, v in tr.model.state_dict().items()},
+          user_factors=tr.user_factors, item_factors=tr.item_factors,
+          val_users=np.array(val_users).astype(str), val_auc=np.array(val_auc), val_ap=np.array(val_ap),
+          train_users=np.array(train_users).astype(str), train_auc=np.array(tr_auc),
+          train_ap=np.array(tr_ap), val_songs=np.array(val_songs).astype(str),
+          song_auc=np.array(song_auc), song_ap=np.array(song_ap),
+          mean9_auc=mean_val[0], mean9_ap=mean_val[1],
+          user_categories=np.array(list(train.user_index.keys())).astype(str),
+          song_categories=np.array(list(train.item_index.keys())).astype(str),
+          train_split_items=np.array(sorted(train.uniq_song_idxs), dtype=np.int64),
+          val_split_items=np.array(sorted(val.uniq_song_idxs), dtype=np.int64))
+
+
 if __name__ == "__main__":
-    model_fixture("model_tiny.npz", H=32, d=32, n_users=10, B=4, N=3)
-    model_fixture("model_h128.npz", H=128, d=128, n_users=10, B=2, N=2, store_init=False,
-                  store_steps=False)
-    inbatch_fixtures()
-    catalogue_fixture()
-    batches_fixture()
-    scheduler_fixture()
-    train5_fixture()
-    metrics_fixture()
+    jobs = {
+        "model": lambda: (model_fixture("model_tiny.npz", H=32, d=32, n_users=10, B=4, N=3),
+                          model_fixture("model_h128.npz", H=128, d=128, n_users=10, B=2, N=2,
+                                        store_init=False, store_steps=False)),
+        "inbatch": inbatch_fixtures, "catalogue": catalogue_fixture, "batches": batches_fixture,
+        "scheduler": scheduler_fixture, "train5": train5_fixture, "metrics": metrics_fixture,
+        "eval": eval_fixture,
+    }
+    for name in (sys.argv[1:] or list(jobs)):  # e.g. `make_golden.py eval` regenerates one fixture
+        jobs[name]()
