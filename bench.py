@@ -44,6 +44,8 @@ def parse():
                          "bit-identical replay")
     ap.add_argument("--flush-every", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-eval", action="store_true", help="skip AUC@val after the timed steps")
+    ap.add_argument("--eval-pct", type=float, default=0.025, help="users sampled for AUC@val (eval_pct)")
     ap.add_argument("--gpu-only", action="store_true",
                     help="diagnostic: hold the stream behind a sleep kernel while the steps are "
                          "enqueued, then report the GPU's own time for them (no host in the loop)")
@@ -59,6 +61,83 @@ def synthetic_tracks(n, device, seed):
         e = min(n, s + step)
         table[s:e] = torch.randn((e - s, 131, 128), generator=gen, device=device).half()
     return table
+
+
+def song_split(n_tracks):
+    """Split code per track (0 train, 1 val, 2 test) by the reference's song split
+    (datasets/dcuedataset.py:146-164): two masks drawn right after seeding with 10."""
+    rs = np.random.RandomState(10)
+    in_train = rs.rand(n_tracks) < 0.80
+    rs = np.random.RandomState(10)
+    in_val = rs.rand(int(in_train.sum())) < 0.1 / 0.8
+    code = np.full(n_tracks, 2, dtype=np.int8)
+    train_ids = np.nonzero(in_train)[0]
+    code[train_ids] = 0
+    code[train_ids[in_val]] = 1
+    return code
+
+
+def evaluate_val(args, net, tracks, pair_user, pair_track, split, n_users, dev):
+    """Item factors of every track (eval tower), user factors of every user, then the split-weighted
+    AUC / mAP of DCUE.score for an eval_pct sample of the users with train and val interactions."""
+    import ctypes
+    from dcrecommend import _native as nat
+    from dcrecommend.nn import rank
+    t0 = time.perf_counter()
+    net.sync_user_table()
+    net.eval()
+    d = args.feature_dim
+    n_tracks = tracks.shape[0]
+    model = net._model_struct()
+    tr = nat.Tracks(tracks.data_ptr(), n_tracks, 0 if tracks.dtype == torch.float16 else 1, 0)
+    item_f = torch.empty((n_tracks, d), device=dev)
+    step = 8192
+    ws = torch.empty(nat.workspace_bytes(net._flat["dims"], step, 0, step), dtype=torch.uint8, device=dev)
+    for s in range(0, n_tracks, step):
+        n = min(step, n_tracks - s)
+        it = torch.arange(s, s + n, dtype=torch.int32, device=dev)
+        nat.check(nat.lib().dcue_item_tower_eval(ctypes.byref(model), ctypes.byref(tr), nat.ptr(it), n, nat.ptr(ws),
+                                                 ws.numel(), nat.ptr(item_f[s:s + n]), nat.stream_handle()),
+                  "dcue_item_tower_eval")
+    nat.check(nat.lib().dcue_factor_repeat_mean(nat.ptr(item_f), item_f.numel(), 10, nat.stream_handle()),
+              "dcue_factor_repeat_mean")
+    torch.cuda.synchronize()
+    t_items = time.perf_counter() - t0
+    user_f = torch.empty((n_users, d), device=dev)
+    for s in range(0, n_users, step):
+        n = min(step, n_users - s)
+        u = torch.arange(s, s + n, dtype=torch.int64, device=dev)
+        nat.check(nat.lib().dcue_user_tower(ctypes.byref(model), nat.ptr(u), n, nat.ptr(ws), ws.numel(),
+                                            nat.ptr(user_f[s:s + n]), nat.stream_handle()), "dcue_user_tower")
+    torch.cuda.synchronize()
+    t_factors = time.perf_counter() - t0
+    # all-split interaction CSR over users (duplicate pairs collapse, as the reference's csr_matrix)
+    pu, pt = pair_user.cpu().numpy(), pair_track.cpu().numpy()
+    key = np.unique(pu * np.int64(n_tracks) + pt)
+    u_of, t_of = key // n_tracks, (key % n_tracks).astype(np.int32)
+    ptr = np.zeros(n_users + 1, np.int64)
+    np.add.at(ptr, u_of + 1, 1)
+    ptr = np.cumsum(ptr)
+    cls = np.where(split == 1, rank.LIST_PRED, 0).astype(np.uint8) | np.where(split == 0, rank.LIST_TRUTH, 0).astype(np.uint8)
+    sp = split[t_of]
+    has_train = np.zeros(n_users, bool)
+    has_val = np.zeros(n_users, bool)
+    has_train[u_of[sp == 0]] = True
+    has_val[u_of[sp == 1]] = True
+    users = np.nonzero(has_train & has_val)[0]
+    sample = np.random.RandomState(0).choice(users, int(len(users) * args.eval_pct))
+    t1 = time.perf_counter()
+    ev = rank.RankEvaluator({"pos_ptr": ptr, "pos_idx": t_of, "cand_class": cls}, dev)
+    auc, ap, ok = ev.metrics(user_f, item_f, sample, nat.RANK_SPLIT)
+    t_rank = time.perf_counter() - t1
+    net.train()
+    H = args.hidden
+    # eval item tower FLOPs per track at full conv lengths (SURVEY 8(d): 23.2 MFLOP at H=d=128)
+    flops = 2 * (128 * 4 * H * 132 + H * 4 * H * 34 + H * 4 * H * 9 + H * 2 * H * 3 + H * d + d * d)
+    return {"auc": rank.mean_until_missing(auc, ok), "map_val": rank.mean_until_missing(ap, ok),
+            "users": int(len(sample)), "candidates": int(n_tracks), "factors_s": t_factors, "rank_s": t_rank,
+            "item_tower_s": t_items, "item_tower_tflops": flops * n_tracks / t_items / 1e12,
+            "note": "random-init model after the bench steps on synthetic data: AUC ~0.5 is expected"}
 
 
 def cpu_baseline(args, n_users_local):
@@ -127,6 +206,11 @@ def main():
     defer = not args.dense_embedding_adam
     opt = NativeAdam(net.parameters(), 1e-5, (0.9, 0.99), 1e-8, 0, defer_embedding=defer,
                      flush_every=args.flush_every)
+    # song split of the reference (datasets/dcuedataset.py:146-164): 80% train of which 1/8 is val,
+    # the rest test; training batches draw only train-split interactions, AUC@val ranks val songs
+    split = song_split(args.tracks)
+    split_d = torch.from_numpy(split).to(dev)
+    train_pairs = torch.nonzero(split_d[pair_track] == 0).squeeze(1)
     epoch_size = (int(math.ceil(n_pairs / 10)) // B) * B
     sched = CyclicLRWithRestarts(opt, B, epoch_size=epoch_size, restart_period=30, t_mult=2, policy="cosine")
     sched.step()
@@ -134,7 +218,7 @@ def main():
     # batch composition (DataLoader shuffle over the interaction rows) is prepared ahead, like the
     # reference's worker processes; the step consumes HBM-resident index vectors
     total = args.warmup + args.steps
-    perm = torch.randperm(n_pairs, generator=gen, device=dev)[: total * B].view(total, B)
+    perm = train_pairs[torch.randperm(train_pairs.numel(), generator=gen, device=dev)[: total * B]].view(total, B)
     users_b = pair_user[perm].contiguous()
     items_b = pair_track[perm].to(torch.int32).contiguous()
     mt = torch.empty(nat.MT_STATE_BYTES, dtype=torch.uint8, device=dev)
@@ -232,6 +316,12 @@ def main():
                      "achieved": achieved, "peak": 157.3, "unit": "TFLOP/s", "frac": achieved / 157.3,
                      "traffic": traffic, "avg_ms": wg_ms, "launches": wg_n, "algorithmic_flops": wg_flops},
     }
+    if rank == 0 and not args.no_eval:
+        # AUC@val of the trained model (outside the timed region): DCUE.score over an eval_pct
+        # sample of this rank's users (nn/dcue.py:380-449, 580-603) on the GPU evaluator
+        ev = evaluate_val(args, net, tracks, pair_user, pair_track, split, n_users_local, dev)
+        result["auc_val"] = ev.pop("auc")
+        result["eval"] = ev
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, n_users_local)
     if rank == 0:
