@@ -169,7 +169,7 @@ __device__ __forceinline__ AdamScalars* log_hist(dcue_emb_log* hdr) {
 
 // Bring users' rows current to step_done (before a forward reads them). One workgroup per listed
 // user; a row listed twice is claimed by one workgroup (CAS on its clock; INT_MIN = in progress).
-__global__ __launch_bounds__(256) void k_emb_sync(float* __restrict__ p, float* __restrict__ m,
+__global__ __launch_bounds__(1024) void k_emb_sync(float* __restrict__ p, float* __restrict__ m,
                                                   float* __restrict__ v, dcue_emb_log* hdr,
                                                   int32_t* emb_step, const int64_t* users, int E,
                                                   float gz) {
@@ -192,24 +192,12 @@ __global__ __launch_bounds__(256) void k_emb_sync(float* __restrict__ p, float* 
   float* pr = p + u * E;
   float* mr = m + u * E;
   float* vr = v + u * E;
-  if ((E & 3) == 0) {  // four independent chains per thread (the replay is a long dependent chain)
-    for (int k4 = threadIdx.x; k4 < (E >> 2); k4 += blockDim.x) {
-      float4 pp = ld4(pr + 4 * k4), mm = ld4(mr + 4 * k4), vv = ld4(vr + 4 * k4);
-      for (int j = from + 1; j <= T; ++j) {
-        const AdamScalars s = hs[j % cap];
-        adam_replay(pp.x, mm.x, vv.x, s, gz);
-        adam_replay(pp.y, mm.y, vv.y, s, gz);
-        adam_replay(pp.z, mm.z, vv.z, s, gz);
-        adam_replay(pp.w, mm.w, vv.w, s, gz);
-      }
-      st4(pr + 4 * k4, pp); st4(mr + 4 * k4, mm); st4(vr + 4 * k4, vv);
-    }
-  } else {
-    for (int k = threadIdx.x; k < E; k += blockDim.x) {
-      float pp = pr[k], mm = mr[k], vv = vr[k];
-      for (int j = from + 1; j <= T; ++j) adam_replay(pp, mm, vv, hs[j % cap], gz);
-      pr[k] = pp; mr[k] = mm; vr[k] = vv;
-    }
+  // one element per thread: each element's replay is a dependent chain of VALU-bound steps, so the
+  // row is spread over as many lanes as it has elements (launch: blockDim >= E)
+  for (int k = threadIdx.x; k < E; k += blockDim.x) {
+    float pp = pr[k], mm = mr[k], vv = vr[k];
+    for (int j = from + 1; j <= T; ++j) adam_replay(pp, mm, vv, hs[j % cap], gz);
+    pr[k] = pp; mr[k] = mm; vr[k] = vv;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -379,7 +367,9 @@ int launch_emb_log_init(const dcue_model* md, int cap, int step, hipStream_t s) 
 
 int launch_emb_sync(const dcue_model* md, const int64_t* users, int n, hipStream_t s) {
   if (n <= 0) return DCUE_OK;
-  DCUE_LAUNCH(k_emb_sync, dim3((unsigned)n), dim3(256), 0, s, md->emb, md->emb_exp_avg,
+  const int E = md->dims.user_embdim;
+  const int threads = E <= 64 ? 64 : (E >= 1024 ? 1024 : (E + 63) / 64 * 64);
+  DCUE_LAUNCH(k_emb_sync, dim3((unsigned)n), dim3(threads), 0, s, md->emb, md->emb_exp_avg,
                      md->emb_exp_avg_sq, md->emb_log, md->emb_step, users, md->dims.user_embdim, 0.f);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
@@ -402,7 +392,8 @@ int launch_emb_flush(const dcue_model* md, hipStream_t s) {
   return DCUE_OK;
 }
 
-int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* poff, hipStream_t s) {
+int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* poff, hipStream_t s,
+                bool flush_slice) {
   const double bc1 = 1.0 - pow((double)a->beta1, (double)a->step);
   const double bc2 = 1.0 - pow((double)a->beta2, (double)a->step);
   AdamScalars sc;
@@ -426,7 +417,8 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
                        md->emb_exp_avg_sq, md->emb_grad, md->emb_rows, md->emb_step, md->emb_log,
                        md->dims.user_embdim, a->step, sc, 0.f);
     DCUE_LAUNCH_CHECK();
-    return launch_emb_flush_rows(md, a->step, s);  // this step's slice of the rolling flush
+    // this step's slice of the rolling flush (or the caller issues it later: StepOpts)
+    return flush_slice ? launch_emb_flush_rows(md, a->step, s) : DCUE_OK;
   } else if ((parts & DCUE_ADAM_EMBEDDING) && md->dims.n_users > 0) {
     long blocks = (md->dims.n_users + 3) / 4;
     if (blocks > 8192) blocks = 8192;

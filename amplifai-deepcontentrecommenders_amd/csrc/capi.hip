@@ -517,6 +517,7 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
     TRY(fk.done());
     HPROF("capi:8");
   }
+  if (o.flush_slice_step >= 0 && m->emb_step) TRY(launch_emb_flush_rows(m, o.flush_slice_step, su));
   TRY(wait_point(s, ev_uf));
   HPROF("capi:9");
   if (o.fuse_score) {
@@ -738,7 +739,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(fk.done());
     HPROF("capi:31");
   }
-  if (o.emb_adam) TRY(launch_adam(m, o.emb_adam, c.poff, su));
+  if (o.emb_adam) TRY(launch_adam(m, o.emb_adam, c.poff, su, !o.defer_flush_slice));
   HPROF("capi:32");
 
   // the join: wgrad stream 0 collects the user stream's and wgrad stream 1's tails, and the caller's

@@ -729,11 +729,299 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
   }
 }
 
+
+// Layer-1 weight gradient (the step's largest MFMA kernel), warp-specialised. The GEMM is
+// dW1[o][kc] = sum over conv-1 rows (item, t) of dz1[row][o] * xhat0[row + tap][c]: K = M*132 rows.
+// Workgroup = a 64 (o) x 64 (kc) output tile x one chunk of rows, 8 waves: waves 0-3 run the MFMAs
+// (a 32x32 quarter each, 2x2 v_mfma_f32_16x16x4 tiles) on one LDS buffer while waves 4-7 build the
+// next step's dz (BN1 backward through relu + max-pool) and xhat0 tiles into the other buffer from
+// registers loaded two steps ahead. Producer work per row is kept to the arithmetic itself (row
+// cursors advance incrementally, the chunk's item table sits in LDS); in the bias workgroups
+// (kc tile 0) the MFMA waves also sum dz per channel -- all rows and the four edge positions --
+// from the LDS tile. With 64x64 tiles the split-K partials are a quarter of a 128x128 tiling's.
+constexpr int kW1Tile = 64, kW1Rch = 64, kW1Pw = 64 + 16;  // pitch == 16 (mod 32): rows r, r+1 on disjoint banks
+constexpr int kW1Items = 128;                               // items per chunk staged in LDS
+
+// One producer thread = one max-pool window (4 conv rows) x one channel quad per step: the BN1
+// backward of the window's pooled gradient is computed once and routed to its argmax row (the
+// other three rows of the window get zeros), and the window's four xhat0 rows are converted.
+struct W1Set {
+  float4 g, y;
+  float4 x[4];
+  uint32_t id;
+  int ii, w;  // item (relative to the chunk's first) and pool window of the thread's rows
+};
+
+template <int SRCX>
+__global__ __launch_bounds__(512) void k_conv1_wgrad(WgradArgs a) {
+  constexpr int PAD = 2, LIN = kFrames, R = 132, LP = 33, CIN = kMels, KS = 4, NB = 5;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  __shared__ float bsum[4][NB][kW1Tile];
+  __shared__ const char* s_xrow[kW1Items];  // track row base of each item of the chunk
+  __shared__ float s_cnt[kW1Items];
+  __shared__ int s_t[2][kW1Rch];  // conv position of each LDS row (-1: past the chunk)
+  const int tid = threadIdx.x;
+  const int cout = a.cout, kcn = KS * CIN;
+  const int obase = blockIdx.y * kW1Tile, kbase = blockIdx.x * kW1Tile;
+  const int total = a.M * R;
+  const int r_begin = blockIdx.z * a.rows_per_chunk;  // multiple of 4: chunks start on a window
+  const int r_end = min(r_begin + a.rows_per_chunk, total);
+  const int nsteps = r_end > r_begin ? (r_end - r_begin + kW1Rch - 1) / kW1Rch : 0;
+  const bool do_bias = blockIdx.x == 0;
+  const bool producer = tid >= 256;
+  const int i_first = r_begin / R, t_first = r_begin - i_first * R;
+  for (int k = tid; k < kW1Items; k += 512) {
+    const int ii = min(i_first + k, a.M - 1);
+    s_xrow[k] = reinterpret_cast<const char*>(a.xsrc) +
+                (size_t)a.item_track[ii] * kFrames * kMels * (SRCX == SRC_TRACK_F16 ? 2 : 4);
+    s_cnt[k] = a.counts ? a.counts[ii] : 1.f;
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && tid < cout) {
+    a.dbeta[tid] = (float)acc_sum(a.dz_acc, cout, 0, tid);
+    a.dgamma[tid] = (float)acc_sum(a.dz_acc, cout, 1, tid);
+  }
+  __syncthreads();
+
+  // ---- producers: channel quad q (o = obase+4q, kc = kbase+4q) of window wslot of every step
+  const int p = tid & 255;
+  const int q = p & 15, wslot = p >> 4;
+  const int o = obase + 4 * q;
+  const bool o_ok = o < cout;
+  const int oc = o_ok ? o : 0;
+  const int kc = kbase + 4 * q;
+  const int kx = kc / CIN, cx = kc - kx * CIN;
+  float4 mean4 = {}, inv4 = {}, a4 = {}, sD4 = {}, sDx4 = {}, xmu = {}, xsc = {};
+  if (producer) {
+    mean4 = ld4(a.mean_l + oc); inv4 = ld4(a.invstd_l + oc); a4 = ld4(a.a_l + oc);
+    float sd[4], sdx[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sd[s] = (float)acc_sum(a.dz_acc, cout, 0, oc + s);
+      sdx[s] = (float)acc_sum(a.dz_acc, cout, 1, oc + s);
+    }
+    sD4 = make_float4(sd[0], sd[1], sd[2], sd[3]);
+    sDx4 = make_float4(sdx[0], sdx[1], sdx[2], sdx[3]);
+    xmu = ld4(a.x_mean + cx); xsc = ld4(a.x_a + cx);
+  }
+  // settle every load so far: the loop's wait counts then only track the step prefetches (a load
+  // still pending at the loop entry makes each iteration wait for all of them)
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0), expcnt/lgkmcnt untouched
+  // issue cursor: window (r_begin + 64*step)/4 + wslot as (item offset, window), 16 windows a step
+  int cur_i = 0, cur_w = t_first / 4 + wslot;
+  if (cur_w >= LP) { cur_w -= LP; cur_i = 1; }
+  auto issue = [&](W1Set& st) {
+    st.ii = cur_i;
+    st.w = cur_w;
+    const int base = ((i_first + min(cur_i, a.M - 1 - i_first)) * LP + cur_w) * cout + oc;  // < 2^31
+    st.g = ld4(a.g_l + base);
+    st.y = ld4(a.y_l + base);
+    st.id = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
+    const char* xrow = s_xrow[min(cur_i, kW1Items - 1)];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int pp = 4 * cur_w + r + kx - PAD;
+      pp = pp < 0 ? 0 : (pp >= LIN ? LIN - 1 : pp);
+      const int xo = pp * kMels + cx;
+      if constexpr (SRCX == SRC_TRACK_F16) {
+        const uint2 raw = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(xrow) + xo);
+        st.x[r] = make_float4(__uint_as_float(raw.x), __uint_as_float(raw.y), 0.f, 0.f);
+      } else {
+        st.x[r] = ld4(reinterpret_cast<const float*>(xrow) + xo);
+      }
+    }
+    cur_w += kW1Rch / 4;
+    if (cur_w >= LP) { cur_w -= LP; ++cur_i; }
+  };
+  // branch-free: the loads' wait counts stay exact (a divergent branch makes the compiler wait for
+  // every outstanding load, including the next step's prefetch)
+  auto fill = [&](const W1Set& st, int step, int buf) {
+    float* dzs = lds + buf * 2 * kW1Rch * kW1Pw;
+    float* xs = dzs + kW1Rch * kW1Pw;
+    const int r0 = 4 * wslot;
+    const bool valid = r_begin + step * kW1Rch + r0 < r_end;  // a window is wholly in or out
+    const float kD = s_cnt[min(st.ii, kW1Items - 1)] * a.invN;
+    const float gv[4] = {st.g.x, st.g.y, st.g.z, st.g.w};
+    const float yv[4] = {st.y.x, st.y.y, st.y.z, st.y.w};
+    const float mu[4] = {mean4.x, mean4.y, mean4.z, mean4.w}, iv[4] = {inv4.x, inv4.y, inv4.z, inv4.w};
+    const float av[4] = {a4.x, a4.y, a4.z, a4.w}, sd[4] = {sD4.x, sD4.y, sD4.z, sD4.w};
+    const float sdx[4] = {sDx4.x, sDx4.y, sDx4.z, sDx4.w};
+    float dxv[4];
+    uint32_t arg[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float xh = (yv[s] - mu[s]) * iv[s];
+      const float dx = av[s] * (gv[s] - kD * sd[s] - kD * xh * sdx[s]);
+      dxv[s] = (valid & o_ok & (yv[s] > 0.f)) ? dx : 0.f;
+      arg[s] = (st.id >> (8 * s)) & 0xff;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = 4 * st.w + r;
+      const int pp = t + kx - PAD;
+      const bool x_ok = valid & (pp >= 0) & (pp < LIN);
+      st4(&dzs[(r0 + r) * kW1Pw + 4 * q],
+          make_float4(arg[0] == (uint32_t)r ? dxv[0] : 0.f, arg[1] == (uint32_t)r ? dxv[1] : 0.f,
+                      arg[2] == (uint32_t)r ? dxv[2] : 0.f, arg[3] == (uint32_t)r ? dxv[3] : 0.f));
+      float x[4];
+      if constexpr (SRCX == SRC_TRACK_F16) {
+        const uint32_t lo = __float_as_uint(st.x[r].x), hi = __float_as_uint(st.x[r].y);
+        const __half2 h0 = *reinterpret_cast<const __half2*>(&lo);
+        const __half2 h1 = *reinterpret_cast<const __half2*>(&hi);
+        x[0] = __low2float(h0); x[1] = __high2float(h0); x[2] = __low2float(h1); x[3] = __high2float(h1);
+      } else {
+        x[0] = st.x[r].x; x[1] = st.x[r].y; x[2] = st.x[r].z; x[3] = st.x[r].w;
+      }
+      st4(&xs[(r0 + r) * kW1Pw + 4 * q],
+          make_float4(x_ok ? (x[0] - xmu.x) * xsc.x : 0.f, x_ok ? (x[1] - xmu.y) * xsc.y : 0.f,
+                      x_ok ? (x[2] - xmu.z) * xsc.z : 0.f, x_ok ? (x[3] - xmu.w) * xsc.w : 0.f));
+      s_t[buf][r0 + r] = valid ? t : -1;  // the 16 threads of a window store the same values
+    }
+  };
+
+  // ---- consumers: wave w owns the (w>>1, w&1) 32x32 quarter of the tile
+  const int lane = tid & 63, w = (tid >> 6) & 3;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int wo = w >> 1, wk = w & 1;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[NB] = {0.f, 0.f, 0.f, 0.f, 0.f};  // bias workgroups: channel tid&63, rows == tid>>6 (mod 4)
+  auto mma = [&](int step, int buf) {
+    const float* dzs = lds + buf * 2 * kW1Rch * kW1Pw;
+    const float* xs = dzs + kW1Rch * kW1Pw;
+    const int nr = min(kW1Rch, r_end - (r_begin + step * kW1Rch));
+    // rows past the chunk end are zero in LDS, so whole groups of 8 rows are safe to read. Two
+    // operand sets alternate: one k-step's reads are issued before the other's MFMAs, so the LDS
+    // latency hides under them (the scheduling barriers keep that order)
+    const float* dr = dzs + g * kW1Pw + 32 * wo + l16;
+    const float* xr = xs + g * kW1Pw + 32 * wk + l16;
+    float a0 = dr[0], a1 = dr[16], b0 = xr[0], b1 = xr[16];
+    const int n8 = (nr + 7) & ~7;
+    for (int r0 = 0; r0 < n8; r0 += 8) {
+      const int o1 = (r0 + 4) * kW1Pw;
+      const float c0 = dr[o1], c1 = dr[o1 + 16], e0 = xr[o1], e1 = xr[o1 + 16];
+      __builtin_amdgcn_sched_barrier(0);
+      acc[0][0] = mfma4(a0, b0, acc[0][0]);
+      acc[0][1] = mfma4(a0, b1, acc[0][1]);
+      acc[1][0] = mfma4(a1, b0, acc[1][0]);
+      acc[1][1] = mfma4(a1, b1, acc[1][1]);
+      __builtin_amdgcn_sched_barrier(0);
+      const int o2 = (r0 + 8 < kW1Rch ? r0 + 8 : 0) * kW1Pw;
+      a0 = dr[o2]; a1 = dr[o2 + 16]; b0 = xr[o2]; b1 = xr[o2 + 16];
+      __builtin_amdgcn_sched_barrier(0);
+      acc[0][0] = mfma4(c0, e0, acc[0][0]);
+      acc[0][1] = mfma4(c0, e1, acc[0][1]);
+      acc[1][0] = mfma4(c1, e0, acc[1][0]);
+      acc[1][1] = mfma4(c1, e1, acc[1][1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (do_bias) {
+      const int ch = tid & 63;
+      for (int r = tid >> 6; r < nr; r += 4) {
+        const float v = dzs[r * kW1Pw + ch];
+        const int t = s_t[buf][r];
+        bacc[0] += v;
+        bacc[1] += t == 0 ? v : 0.f;
+        bacc[2] += t == 1 ? v : 0.f;
+        bacc[3] += t == R - 2 ? v : 0.f;
+        bacc[4] += t == R - 1 ? v : 0.f;
+      }
+    }
+  };
+
+  // Producers fill and prefetch unconditionally (steps past the chunk read clamped, in-bounds rows
+  // and fill an LDS buffer nobody consumes): with no conditional load the compiler's wait counts
+  // wait for exactly the set being filled, never for the prefetch behind it.
+  W1Set sa, sb;
+  if (producer) {
+    issue(sa);
+    issue(sb);
+    fill(sa, 0, 0);
+    issue(sa);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; s += 2) {
+    if (!producer) {
+      mma(s, 0);
+    } else {
+      fill(sb, s + 1, 1);
+      issue(sb);
+    }
+    __syncthreads();
+    if (s + 1 >= nsteps) break;
+    if (!producer) {
+      mma(s + 1, 1);
+    } else {
+      fill(sa, s + 2, 0);
+      issue(sa);
+    }
+    __syncthreads();
+  }
+
+  if (!producer) {  // partial tile -> wpart[z][o][kc]; D lane map: o = 4g + reg, kc = l16
+    float* wp = a.wpart + (size_t)blockIdx.z * cout * kcn;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int kk = kbase + 32 * wk + 16 * n + l16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int oo = obase + 32 * wo + 16 * m + 4 * g + j;
+          if (oo < cout) wp[(size_t)oo * kcn + kk] = acc[m][n][j];
+        }
+      }
+    if (do_bias) {
+#pragma unroll
+      for (int e = 0; e < NB; ++e) bsum[tid >> 6][e][tid & 63] = bacc[e];
+    }
+  }
+  if (do_bias) {
+    __syncthreads();
+    if (tid < kW1Tile && obase + tid < cout) {
+#pragma unroll
+      for (int e = 0; e < NB; ++e) {
+        const float v = ((bsum[0][e][tid] + bsum[1][e][tid]) + bsum[2][e][tid]) + bsum[3][e][tid];
+        a.bpart[((size_t)blockIdx.z * NB + e) * cout + obase + tid] = v;
+      }
+    }
+  }
+}
+
+template <int SRCX>
+static int conv1_wgrad(const WgradArgs& a0, int nchunk, hipStream_t s) {
+  constexpr size_t LDS = (size_t)2 * 2 * kW1Rch * kW1Pw * sizeof(float);
+  auto kern = k_conv1_wgrad<SRCX>;
+  static bool attr = false;
+  if (!attr) {
+    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS));
+    attr = true;
+  }
+  WgradArgs a = a0;
+  const long rows = (long)a.M * 132;
+  a.rows_per_chunk = (int)(4 * ((rows + 4L * nchunk - 1) / (4L * nchunk)));  // whole pool windows
+  dim3 grid((unsigned)(4 * kMels / kW1Tile), (unsigned)((a.cout + kW1Tile - 1) / kW1Tile), (unsigned)nchunk);
+  DCUE_LAUNCH(kern, grid, dim3(512), LDS, s, a);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
 int wgrad_nchunk(int layer, int M, int cout, int cin) {
   // one workgroup per CU (LDS-bound): at most 256 / tiles chunks, each of >= 64 rows; partial
   // blocks cost a write + a read of cout*ks*cin floats per chunk
   const LayerGeom gm = layer_geom(layer);
   const long rows = (long)M * gm.lp * gm.pool;
+  if (layer == 1) {  // k_conv1_wgrad: 64x64 tiles, >= 4 row steps per chunk, <= ~256 workgroups,
+                     // and few enough items per chunk for its LDS item table
+    const long tiles1 = (4L * kMels / kW1Tile) * ((cout + kW1Tile - 1) / kW1Tile);
+    long n = 256 / tiles1;
+    if (n > (rows + 4 * kW1Rch - 1) / (4 * kW1Rch)) n = (rows + 4 * kW1Rch - 1) / (4 * kW1Rch);
+    const long need = (M + kW1Items - 3) / (kW1Items - 2);
+    if (n < need) n = need;
+    return (int)(n < 1 ? 1 : n);
+  }
   const long tiles = ((gm.ks * cin + 127) / 128) * ((cout + 127) / 128);
   long n = 256 / tiles;
   if (n > (rows + 63) / 64) n = (rows + 63) / 64;
@@ -767,8 +1055,8 @@ static int wgrad_layer(const WgradArgs& a0, int nchunk, hipStream_t s) {
 
 int launch_conv_wgrad(int layer, int src, const WgradArgs& a, int nchunk, hipStream_t s) {
   switch (layer) {
-    case 1: return src == SRC_TRACK_F16 ? wgrad_layer<1, SRC_TRACK_F16>(a, nchunk, s)
-                                        : wgrad_layer<1, SRC_TRACK_F32>(a, nchunk, s);
+    case 1: return src == SRC_TRACK_F16 ? conv1_wgrad<SRC_TRACK_F16>(a, nchunk, s)
+                                        : conv1_wgrad<SRC_TRACK_F32>(a, nchunk, s);
     case 2: return wgrad_layer<2, SRC_ACT>(a, nchunk, s);
     case 3: return wgrad_layer<3, SRC_ACT>(a, nchunk, s);
     case 4: return wgrad_layer<4, SRC_ACT>(a, nchunk, s);

@@ -189,7 +189,11 @@ int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df,
 int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float scale,
                     float* emb_grad, int32_t* slot, int64_t* emb_rows, dcue_emb_log* log,
                     hipStream_t s);
-int launch_adam(const dcue_model* m, const dcue_adam_args* a, const int64_t* poff, hipStream_t s);
+// flush_slice = false: the user-table part leaves this step's rolling-flush slice to the caller
+// (plans issue it during the next step, after that step's user tower: launch_emb_flush_rows)
+int launch_adam(const dcue_model* m, const dcue_adam_args* a, const int64_t* poff, hipStream_t s,
+                bool flush_slice = true);
+int launch_emb_flush_rows(const dcue_model* m, int step, hipStream_t s);
 int launch_emb_log_init(const dcue_model* m, int cap, int step, hipStream_t s);
 int launch_emb_sync(const dcue_model* m, const int64_t* users, int n, hipStream_t s);
 int launch_emb_flush(const dcue_model* m, hipStream_t s);
@@ -269,6 +273,11 @@ struct StepOpts {
   // the workspace's own
   const float* counts = nullptr;
   unsigned long long* acc = nullptr;
+  // deferred rolling flush (plans): the backward's user-table Adam skips its flush slice, and the
+  // next forward issues the slice of step flush_slice_step on the user stream right after the user
+  // tower -- same stream order relative to every Adam step, but off the next step's user-tower path
+  bool defer_flush_slice = false;
+  int flush_slice_step = -1;
 };
 // words of the per-step accumulator block (BN sums) cleared before each step
 long step_acc_words(const dcue_dims* d, int B, int N, int M);

@@ -40,6 +40,7 @@ struct dcue_plan {
   dcue_mt_state* mt_ahead = nullptr;
   long launches = 0;
   hipEvent_t tails[2] = {};       // the last launched step's end (StepOpts::tails)
+  int pending_flush = -1;         // step whose rolling-flush slice the next launch issues
 };
 
 namespace {
@@ -132,10 +133,15 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   hipEvent_t score_done = nullptr;
   o.score_done = &score_done;
   o.tails = p->tails;
+  // the previous step's rolling-flush slice runs after this step's user tower (StepOpts)
+  const bool deferred = p->model.emb_step != nullptr;
+  o.flush_slice_step = deferred ? p->pending_flush : -1;
+  o.defer_flush_slice = deferred && emb_adam != nullptr;
   TRY(forward_impl(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, 1, p->cfg.margin, o, s));
   HPROF("plan:4");
   TRY(backward_impl(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, nullptr, p->cfg.emb_grad_scale, o, s));
   HPROF("plan:5");
+  p->pending_flush = o.defer_flush_slice ? emb_adam->step : -1;
   ++p->launches;
   return DCUE_OK;
 }

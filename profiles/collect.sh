@@ -16,8 +16,8 @@ BENCH="$ROOT/bench.py --no-cpu-baseline --steps 200 --warmup 20"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/stats" -o run -- python3 $BENCH \
   > "$OUT/stats.log" 2>&1
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 180 rocprofv3 --pmc $c --kernel-include-regex 'k_conv_wgrad<0' -f csv \
-    -d "$OUT/pmc_$c" -o run -- python3 $ROOT/bench.py --no-cpu-baseline --steps 40 --warmup 5 \
+  timeout -s KILL 180 rocprofv3 --pmc $c --kernel-include-regex 'k_conv1_wgrad' -f csv \
+    -d "$OUT/pmc_$c" -o run -- python3 $ROOT/bench.py --no-cpu-baseline --no-eval --steps 40 --warmup 5 \
     > "$OUT/pmc_$c.log" 2>&1
 done
 python3 "$ROOT/profiles/summarize_pmc.py" "$OUT" "$TAG"

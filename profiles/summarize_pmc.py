@@ -47,7 +47,7 @@ def main():
     if fetch_kb is not None and write_kb is not None:
         rd = 2.0 * fetch_kb * 1024.0
         wr = write_kb * 1024.0
-        out = {"kernel": "k_conv_wgrad<0,...> (conv layer 1 weight gradient)",
+        out = {"kernel": "k_conv1_wgrad (conv layer 1 weight gradient)",
                "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
                "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                "hbm_bytes_per_launch": rd + wr, "dispatches": [n_f, n_w],
