@@ -762,12 +762,16 @@ __global__ __launch_bounds__(512) void k_conv1_wgrad(WgradArgs a) {
   __shared__ int s_t[2][kW1Rch];  // conv position of each LDS row (-1: past the chunk)
   const int tid = threadIdx.x;
   const int cout = a.cout, kcn = KS * CIN;
-  const int obase = blockIdx.y * kW1Tile, kbase = blockIdx.x * kW1Tile;
+  // grid (chunk, kc tile, o tile): consecutive workgroup ids -- dispatched round-robin over the 8
+  // XCDs -- are different chunks, so all tiles of one chunk share an XCD and its L2 serves their
+  // re-reads of the chunk's rows (8 kc tiles read the same dz inputs, 2 o tiles the same tracks)
+  const int chunk = blockIdx.x, ktile = blockIdx.y, otile = blockIdx.z;
+  const int obase = otile * kW1Tile, kbase = ktile * kW1Tile;
   const int total = a.M * R;
-  const int r_begin = blockIdx.z * a.rows_per_chunk;  // multiple of 4: chunks start on a window
+  const int r_begin = chunk * a.rows_per_chunk;  // multiple of 4: chunks start on a window
   const int r_end = min(r_begin + a.rows_per_chunk, total);
   const int nsteps = r_end > r_begin ? (r_end - r_begin + kW1Rch - 1) / kW1Rch : 0;
-  const bool do_bias = blockIdx.x == 0;
+  const bool do_bias = ktile == 0;
   const bool producer = tid >= 256;
   const int i_first = r_begin / R, t_first = r_begin - i_first * R;
   for (int k = tid; k < kW1Items; k += 512) {
@@ -776,7 +780,7 @@ __global__ __launch_bounds__(512) void k_conv1_wgrad(WgradArgs a) {
                 (size_t)a.item_track[ii] * kFrames * kMels * (SRCX == SRC_TRACK_F16 ? 2 : 4);
     s_cnt[k] = a.counts ? a.counts[ii] : 1.f;
   }
-  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && tid < cout) {
+  if (chunk == 0 && ktile == 0 && otile == 0 && tid < cout) {
     a.dbeta[tid] = (float)acc_sum(a.dz_acc, cout, 0, tid);
     a.dgamma[tid] = (float)acc_sum(a.dz_acc, cout, 1, tid);
   }
@@ -961,7 +965,7 @@ __global__ __launch_bounds__(512) void k_conv1_wgrad(WgradArgs a) {
   }
 
   if (!producer) {  // partial tile -> wpart[z][o][kc]; D lane map: o = 4g + reg, kc = l16
-    float* wp = a.wpart + (size_t)blockIdx.z * cout * kcn;
+    float* wp = a.wpart + (size_t)chunk * cout * kcn;
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -984,7 +988,7 @@ __global__ __launch_bounds__(512) void k_conv1_wgrad(WgradArgs a) {
 #pragma unroll
       for (int e = 0; e < NB; ++e) {
         const float v = ((bsum[0][e][tid] + bsum[1][e][tid]) + bsum[2][e][tid]) + bsum[3][e][tid];
-        a.bpart[((size_t)blockIdx.z * NB + e) * cout + obase + tid] = v;
+        a.bpart[((size_t)chunk * NB + e) * cout + obase + tid] = v;
       }
     }
   }
@@ -1002,7 +1006,7 @@ static int conv1_wgrad(const WgradArgs& a0, int nchunk, hipStream_t s) {
   WgradArgs a = a0;
   const long rows = (long)a.M * 132;
   a.rows_per_chunk = (int)(4 * ((rows + 4L * nchunk - 1) / (4L * nchunk)));  // whole pool windows
-  dim3 grid((unsigned)(4 * kMels / kW1Tile), (unsigned)((a.cout + kW1Tile - 1) / kW1Tile), (unsigned)nchunk);
+  dim3 grid((unsigned)nchunk, (unsigned)(4 * kMels / kW1Tile), (unsigned)((a.cout + kW1Tile - 1) / kW1Tile));
   DCUE_LAUNCH(kern, grid, dim3(512), LDS, s, a);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
