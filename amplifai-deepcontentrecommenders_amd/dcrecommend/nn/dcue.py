@@ -150,6 +150,7 @@ class DCUE(Trainer):
         self._tracks = None       # [n_items][131][128] HBM table, item-index order
         self._item_meta = None    # metadata index of every item index
         self._plan = None
+        self._plan_n = None
         self._evals = {}
 
     # ------------------------------------------------------------------ model / optimizer
@@ -189,13 +190,19 @@ class DCUE(Trainer):
         self._item_meta = meta
         self._tracks_src = item_dataset
 
-    def _train_plan(self):
-        if self._plan is None:
-            self._plan = TrainPlan(self.model, self._tracks, self.batch_size, self.neg_batch_size,
+    def _n_neg(self, ds):
+        """Negatives per row: the dataset's neg_samples, as in the reference, where the trainer's
+        neg_batch_size is never read (datasets/dcuedataset.py:18,219)."""
+        return int(getattr(ds, "neg_samples", self.neg_batch_size))
+
+    def _train_plan(self, N):
+        if self._plan is None or self._plan_n != N:
+            self._plan = TrainPlan(self.model, self._tracks, self.batch_size, N,
                                    margin=self.margin, optimizer=self.optimizer)
+            self._plan_n = N
             fl = self.model._flat
-            M = self.batch_size * (1 + self.neg_batch_size)
-            off = nat.workspace_outputs(fl["dims"], self.batch_size, self.neg_batch_size, M)
+            M = self.batch_size * (1 + N)
+            off = nat.workspace_outputs(fl["dims"], self.batch_size, N, M)
             self._plan_loss = self._plan.ws[off[3]:off[3] + 4].view(torch.float32)
         return self._plan
 
@@ -205,8 +212,8 @@ class DCUE(Trainer):
         self.model.train()
         ds = loader.dataset if hasattr(loader, "dataset") else self.train_data
         neg = self._negatives(ds)
-        plan = self._train_plan()
-        B, N = self.batch_size, self.neg_batch_size
+        B, N = self.batch_size, self._n_neg(ds)
+        plan = self._train_plan(N)
         users_all, items_all = self._rows(ds)
         mt = _mt_from_numpy(self.device)
         negs = torch.empty((B, N), dtype=torch.int64, device=self.device)
@@ -234,7 +241,7 @@ class DCUE(Trainer):
         ds = _dataset(loader)
         neg = self._negatives(ds)
         users_all, items_all = self._rows(ds)
-        B, N = self.batch_size, self.neg_batch_size
+        B, N = self.batch_size, self._n_neg(ds)
         mt = _mt_from_numpy(self.device)
         loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
         n = users_all.numel()

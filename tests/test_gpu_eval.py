@@ -197,3 +197,15 @@ def test_trainer_fit_and_checkpoint(golden, tmp_path):
     assert tr2.nn_epoch == ep + 1 and tr2.feature_dim == 32
     assert torch.equal(tr2.model.conv.fc.weight.cpu(),
                        torch.load(str(sub / files[0]), weights_only=True)["model"]["conv.fc.weight"])
+
+
+def test_train_dcue_driver_synthetic(tmp_path):
+    """train_dcue.py (the reference README's train_* driver) end to end on synthetic files."""
+    import train_dcue
+    dcue = train_dcue.main(["--synthetic", "--synthetic-users", "24", "--synthetic-tracks", "40",
+                            "--synthetic-pairs", "300", "--feature-dim", "32", "--conv-hidden", "32",
+                            "--batch-size", "8", "--neg-batch-size", "3", "--num-epochs", "1",
+                            "--eval-pct", "1.0", "--lr", "1e-3", "--save-dir", str(tmp_path)])
+    assert dcue._plan_n == 3 and dcue.nn_epoch >= 9
+    assert 0.0 <= dcue.best_val_auc <= 1.0
+    assert os.listdir(tmp_path)
