@@ -15,7 +15,10 @@ What runs where:
 * AUC / mAP through dcue_rank_metrics (dcrecommend.nn.rank) instead of per-user pandas frames
   and sklearn calls.
 The only host work per batch is the index permutation (torch RandomSampler, as the reference's
-DataLoader(shuffle=True)) and the kernel launches.
+DataLoader(shuffle=True)) and the kernel launches. numpy's and torch's global random streams are
+consumed as the reference consumes them with num_workers=0 loaders (negative draws continue numpy's
+stream on the GPU; every DataLoader iteration's torch draws are mirrored), so a seeded fit follows
+the reference's trajectory: tests/golden/fit.npz.
 """
 import ctypes
 import os
@@ -39,9 +42,18 @@ def _dataset(x):
     return getattr(x, "dataset", x)
 
 
+def _loader_draws(n):
+    """The draws n DataLoader iterations take from torch's global RNG: each iterator draws a base
+    seed (torch/utils/data/dataloader.py _BaseDataLoaderIter), so torch's stream -- and with it every
+    later RandomSampler permutation -- stays where the reference's trainer leaves it."""
+    for _ in range(n):
+        torch.empty((), dtype=torch.int64).random_()
+
+
 class _IndexBatches:
     """One sub-epoch loader (nn/dcue.py:711-721): the rows of a get_batches chunk in
-    RandomSampler order (DataLoader(shuffle=True)), cut into batches, drop_last."""
+    RandomSampler order (DataLoader(shuffle=True)), cut into batches, drop_last. Iterating takes the
+    same two draws from torch's global RNG as the DataLoader: its base seed, then the sampler's."""
 
     def __init__(self, rows, batch_size):
         self.rows = np.asarray(rows, dtype=np.int64)
@@ -51,6 +63,7 @@ class _IndexBatches:
         return len(self.rows) // self.batch_size
 
     def __iter__(self):
+        _loader_draws(1)
         order = np.fromiter(iter(RandomSampler(range(len(self.rows)))), dtype=np.int64, count=len(self.rows))
         rows = self.rows[order]
         B = self.batch_size
@@ -237,6 +250,7 @@ class DCUE(Trainer):
 
     def _eval_epoch(self, loader):
         """nn/dcue.py:220-262: eval-mode loss over the val set in order (last batch partial)."""
+        _loader_draws(1)  # DataLoader(shuffle=False): its iterator's base seed
         self.model.eval()
         ds = _dataset(loader)
         neg = self._negatives(ds)
@@ -365,6 +379,7 @@ class DCUE(Trainer):
         return self._factors_over(_dataset(loader), n_iter)
 
     def _factors_over(self, item_data, n_iter):
+        _loader_draws(n_iter)  # the reference iterates its item loader n_iter times
         self._bind_items(item_data)
         self.model.eval()
         self.model._require_device()
@@ -416,6 +431,11 @@ class DCUE(Trainer):
         pred, truth = _dataset(pred_loader), _dataset(truth_loader)
         idx = np.array([pred.user_index[u] for u in users], dtype=np.int64)
         auc, ap, ok = self.score_users(idx, pred, truth)
+        # torch-RNG parity: the reference iterates a shuffling loader per predict() call that finds
+        # songs (base seed + sampler seed), for every user up to and including the one it stops at
+        in_pred, in_truth = set(pred.triplets['user_id']), set(truth.triplets['user_id'])
+        stop = int(np.argmin(ok)) + 1 if not ok.all() else len(users)
+        _loader_draws(sum(2 * ((u in in_pred) + (u in in_truth)) for u in list(users)[:stop]))
         return rank.mean_until_missing(auc, ok), rank.mean_until_missing(ap, ok)
 
     def score_song(self, songs, pred_loader, k=10000):
@@ -426,6 +446,7 @@ class DCUE(Trainer):
         idx = np.array([pred.item_index[s] for s in songs], dtype=np.int64)
         ev = self._evaluator("song", pred)
         auc, ap, ok = ev.metrics(self._item_feat_by_index(), self.user_factors, idx, nat.RANK_SINGLE)
+        _loader_draws(2 * int(ok.sum()))  # one shuffling loader pass per song with users
         return float(np.mean(auc[ok])), float(np.mean(ap[ok]))
 
     def predict(self, user, loader):

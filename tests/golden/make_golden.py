@@ -18,6 +18,8 @@ Which reference code produced what:
 * scheduler.npz -- CyclicLRWithRestarts (optim/cyclic_scheduler.py:49-215) driven the way
                    DCUE.fit/_train_epoch drive it (nn/dcue.py:338-341, 209-210).
 * train5.npz    -- five DCUE train steps (nn/dcue.py:202-210) with Adam + scheduler.
+* fit.npz       -- DCUE.fit for one epoch (10 sub-epochs) with num_workers=0 loaders: per sub-epoch
+                   train / val loss and AUC / mAP, final parameters.
 * eval.npz      -- the evaluation path end to end: DCUE._user_factors / _item_factors over
                    DCUEItemset, DCUE.score (val and train splits, DCUEPredset) and score_song.
 * metrics.npz   -- DCUE.score's split-weighted AUC / mAP arithmetic (nn/dcue.py:399-449) and
@@ -388,6 +390,77 @@ def eval_fixture():
           val_split_items=np.array(sorted(val.uniq_song_idxs), dtype=np.int64))
 
 
+class _RecDCUE(DCUE):
+    """The reference trainer, recording what fit() computes (methods on the class: fit's checkpoint
+    pickles the instance __dict__)."""
+    rec = {"train": [], "update": [], "scores": [], "song": []}
+
+    def _train_epoch(self, loader):
+        out = DCUE._train_epoch(self, loader)
+        self.rec["train"].append(out)
+        return out
+
+    def _update_best(self, val_map, val_auc, val_loss):
+        self.rec["update"].append((val_map, val_auc, val_loss))
+        return DCUE._update_best(self, val_map, val_auc, val_loss)
+
+    def _compute_scores(self, split, *a, **k):
+        out = DCUE._compute_scores(self, split, *a, **k)
+        self.rec["scores"].append((0 if split == "val" else 1,) + tuple(out))
+        return out
+
+    def _compute_scores_song(self, *a, **k):
+        out = DCUE._compute_scores_song(self, *a, **k)
+        self.rec["song"].append(out)
+        return out
+
+
+def fit_fixture():
+    """DCUE.fit end to end (nn/dcue.py:264-378) for one epoch (10 sub-epochs) on the eval fixture's
+    data, with every DataLoader forced to num_workers=0: the protocol under which negative draws and
+    shuffles follow the global numpy / torch streams (multi-worker loaders reseed per worker).
+    Records each sub-epoch's train loss, val loss, AUC / mAP numbers and the final parameters."""
+    import tempfile
+    import torch.utils.data as tud
+    import dcrecommend.nn.dcue as refnn  # reference
+    from dcrecommend.datasets.dcuepredset import DCUEPredset  # reference
+    from dcrecommend.datasets.dcueitemset import DCUEItemset  # reference
+    g = np.load(os.path.join(HERE, "eval.npz"), allow_pickle=False)
+    trip = pd.DataFrame({"user_id": g["raw_users"], "song_id": g["raw_songs"], "score": g["raw_score"]})
+    tmp = tempfile.mkdtemp()
+    paths = []
+    for k in range(len(g["meta_songs"])):
+        pth = os.path.join(tmp, "m%03d.pt" % k)
+        torch.save(torch.from_numpy(g["spec"][k].astype(np.float32)), pth)
+        paths.append(pth)
+    meta = pd.DataFrame({"idx": np.arange(len(g["meta_songs"])), "song_id": g["meta_songs"], "data_mel": paths})
+    N, B = 4, 8
+    train = DCUEDataset(trip.copy(), meta, neg_samples=N, split="train")
+    val = DCUEDataset(trip.copy(), meta, neg_samples=N, split="val")
+    test = DCUEDataset(trip.copy(), meta, neg_samples=N, split="test")
+    pred = DCUEPredset(trip.copy(), meta, split="val")
+    truth = DCUEPredset(trip.copy(), meta, split="train")
+    items = DCUEItemset(trip.copy(), meta)
+    orig = tud.DataLoader
+
+    def loader0(*a, **k):
+        k["num_workers"] = 0
+        return orig(*a, **k)
+    refnn.DataLoader = loader0
+    rec = _RecDCUE.rec
+    tr = _RecDCUE(feature_dim=32, conv_hidden=32, batch_size=B, neg_batch_size=N, lr=1e-3, num_epochs=1,
+                  eval_pct=1.0)
+    np.random.seed(31)
+    torch.manual_seed(32)
+    tr.fit(train, val, test, pred, truth, items, len(train.user_index), len(train.item_index), "t", "m",
+           tempfile.mkdtemp())
+    refnn.DataLoader = orig
+    _save("fit.npz", N=N, B=B, np_seed=31, torch_seed=32,
+          train=np.array(rec["train"], dtype=np.float64), update=np.array(rec["update"], dtype=np.float64),
+          scores=np.array(rec["scores"], dtype=np.float64), song=np.array(rec["song"], dtype=np.float64),
+          **{"final." + k: v for k, v in tr.model.state_dict().items()})
+
+
 if __name__ == "__main__":
     jobs = {
         "model": lambda: (model_fixture("model_tiny.npz", H=32, d=32, n_users=10, B=4, N=3),
@@ -395,7 +468,7 @@ if __name__ == "__main__":
                                         store_init=False, store_steps=False)),
         "inbatch": inbatch_fixtures, "catalogue": catalogue_fixture, "batches": batches_fixture,
         "scheduler": scheduler_fixture, "train5": train5_fixture, "metrics": metrics_fixture,
-        "eval": eval_fixture,
+        "eval": eval_fixture, "fit": fit_fixture,
     }
     for name in (sys.argv[1:] or list(jobs)):  # e.g. `make_golden.py eval` regenerates one fixture
         jobs[name]()

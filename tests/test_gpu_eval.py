@@ -209,3 +209,79 @@ def test_train_dcue_driver_synthetic(tmp_path):
     assert dcue._plan_n == 3 and dcue.nn_epoch >= 9
     assert 0.0 <= dcue.best_val_auc <= 1.0
     assert os.listdir(tmp_path)
+
+
+def test_trainer_fit_matches_reference(golden, tmp_path):
+    """DCUE.fit against the reference's own fit (tests/golden/fit.npz, num_workers=0 loaders): same
+    seeds -> same chunks, shuffles and negative draws (numpy's stream continued on the GPU, torch's
+    DataLoader draws mirrored), so every sub-epoch's numbers line up. Measured on MI355X: train loss
+    1.1e-6 relative, val loss 1.7e-6, AUC / mAP 1.4e-4 absolute. Tolerances: losses 1e-5 relative
+    (fp32 GPU vs CPU, compounded over the Adam steps), AUC / mAP 5e-4 (a score near-tie resolved
+    differently moves a mean by ~1/(n_pos n_neg n_users)), final parameters 1e-3 of their largest
+    magnitude (lr 1e-3 steps on rounding-level gradient differences)."""
+    from dcrecommend.nn.dcue import DCUE
+    g = golden("eval.npz")
+    f = golden("fit.npz")
+    from dcrecommend.datasets.dcuedataset import DCUEDataset
+    train, val, items = _datasets(g, tmp_path)
+    N, B = int(f["N"]), int(f["B"])
+    trip = pd.DataFrame({"user_id": g["raw_users"], "song_id": g["raw_songs"], "score": g["raw_score"]})
+    meta = items.metadata.copy()
+    meta = pd.DataFrame({"idx": np.arange(len(g["meta_songs"])), "song_id": g["meta_songs"],
+                         "data_mel": [os.path.join(str(tmp_path), "m%03d.pt" % k) for k in range(len(g["meta_songs"]))]})
+    from dcrecommend.datasets.dcuepredset import DCUEPredset
+    from dcrecommend.datasets.dcueitemset import DCUEItemset
+    tr_ds = DCUEDataset(trip.copy(), meta, neg_samples=N, split="train")
+    va_ds = DCUEDataset(trip.copy(), meta, neg_samples=N, split="val")
+    te_ds = DCUEDataset(trip.copy(), meta, neg_samples=N, split="test")
+    pred = DCUEPredset(trip.copy(), meta, split="val")
+    truth = DCUEPredset(trip.copy(), meta, split="train")
+    it_ds = DCUEItemset(trip.copy(), meta)
+
+    rec = {"train": [], "update": [], "scores": [], "song": []}
+
+    class Rec(DCUE):
+        def _train_epoch(self, loader):
+            out = DCUE._train_epoch(self, loader)
+            rec["train"].append(out)
+            return out
+
+        def _update_best(self, val_map, val_auc, val_loss):
+            rec["update"].append((val_map, val_auc, val_loss))
+            return DCUE._update_best(self, val_map, val_auc, val_loss)
+
+        def _compute_scores(self, split, *a, **k):
+            out = DCUE._compute_scores(self, split, *a, **k)
+            rec["scores"].append((0 if split == "val" else 1,) + tuple(out))
+            return out
+
+        def _compute_scores_song(self, *a, **k):
+            out = DCUE._compute_scores_song(self, *a, **k)
+            rec["song"].append(out)
+            return out
+
+    tr = Rec(feature_dim=32, conv_hidden=32, batch_size=B, neg_batch_size=N, lr=1e-3, num_epochs=1, eval_pct=1.0,
+             device=DEV)
+    np.random.seed(int(f["np_seed"]))
+    torch.manual_seed(int(f["torch_seed"]))
+    tr.fit(tr_ds, va_ds, te_ds, pred, truth, it_ds, len(tr_ds.user_index), len(tr_ds.item_index), "t", "m",
+           str(tmp_path / "ck"))
+    got = {k: np.array(v, dtype=np.float64) for k, v in rec.items()}
+    assert got["train"].shape == f["train"].shape
+    print("fit vs reference: train loss rel %.2e, val loss rel %.2e, AUC/mAP abs %.2e / %.2e / %.2e" % (
+        float(np.abs(got["train"][:, 1] / f["train"][:, 1] - 1).max()),
+        float(np.abs(got["update"][:, 2] / f["update"][:, 2] - 1).max()),
+        float(np.abs(got["update"][:, :2] - f["update"][:, :2]).max()),
+        float(np.abs(got["scores"] - f["scores"]).max()), float(np.abs(got["song"] - f["song"]).max())))
+    np.testing.assert_array_equal(got["train"][:, 0], f["train"][:, 0])
+    np.testing.assert_allclose(got["train"][:, 1], f["train"][:, 1], rtol=1e-5)
+    np.testing.assert_allclose(got["update"][:, 2], f["update"][:, 2], rtol=1e-5)   # val loss
+    np.testing.assert_allclose(got["update"][:, :2], f["update"][:, :2], atol=5e-4)  # val mAP, AUC
+    np.testing.assert_allclose(got["scores"], f["scores"], atol=5e-4)
+    np.testing.assert_allclose(got["song"], f["song"], atol=5e-4)
+    sd = tr.model.state_dict()
+    for k in f.files:
+        if k.startswith("final.") and "num_batches" not in k:
+            want = torch.from_numpy(np.array(f[k])).double()
+            diff = float((sd[k[6:]].cpu().double() - want).abs().max())
+            assert diff <= 1e-3 * max(float(want.abs().max()), 1.0), (k, diff)
