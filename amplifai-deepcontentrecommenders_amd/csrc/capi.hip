@@ -199,6 +199,8 @@ struct Ws {
   float* g[6];
   float *dh1, *de;
   float *wpart[3], *bpart[3], *G, *S;  // wgrad partials: one set per wgrad stream
+  float* xhat0;          // [M][kXp][128] bn0-normalised, zero-padded input: conv-1 wgrad's X operand
+  float* dx1;            // [M][33][H] BN1 backward at the pooled positions: conv-1 wgrad's dz operand
 };
 
 // the accumulator block's parts: [6][2][Cmax][2] forward sums, then the same for the backward
@@ -260,6 +262,8 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   }
   w->G = ar.take<float>((long)H * 4 * kMels);
   w->S = ar.take<float>(5L * H);  // the five layer-1 bias partial sums E[5][H]
+  w->xhat0 = ar.take<float>((long)(M + 1) * kXp * kMels);  // + a zero item
+  w->dx1 = ar.take<float>((long)M * layer_geom(1).lp * H);
   return ar.used + 256;
 }
 
@@ -597,6 +601,16 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   else
     TRY(fork_point(sp, s, &ev_score));
     HPROF("capi:14");
+  // the conv-1 weight gradient's X operand, bn0(x) without gamma/beta, materialised once beside the
+  // backward chain (it needs only the forward's input statistics); waited for just before that kernel
+  hipEvent_t ev_x0 = nullptr;
+  {
+    TRY(wait_point(sw[1], ev_score));
+    ForkAfter fk(sp, sw[1], &ev_x0);
+    TRY(launch_xhat0(src, t->data, b->item_track, M, bn_acc(w.bnacc, w.cmax, 0), copies * kFrames, w.xhat0,
+                     sw[1]));
+    TRY(fk.done());
+  }
   {  // per-item feature gradients df, then (same kernel) the fc input gradient g5 = df W and BN5's sums
     ForkAfter fk(sp, s, &ev_layer[5]);
     TRY(launch_item_grad(w.dfcopy, b, D, w.df, c.P(SEG_FC_W), w.g[5], bn_acc(w.bnbacc, w.cmax, 5),
@@ -633,7 +647,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     if (so != s) TRY(wait_point(so, ev_layer[l]));
     HPROF("capi:18");
     WgradArgs wa = {};
-    wa.xsrc = l == 1 ? t->data : (const void*)w.y[l - 1];
+    wa.xsrc = l == 1 ? (const void*)w.xhat0 : (const void*)w.y[l - 1];
     wa.item_track = b->item_track;
     wa.x_mean = w.mean[l - 1];
     wa.x_a = l == 1 ? w.invstd[0] : w.a[l - 1];
@@ -645,6 +659,10 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     wa.M = M; wa.cout = C; wa.cin = cin;
     wa.wpart = w.wpart[ps]; wa.bpart = w.bpart[ps];
     const int nch = wgrad_nchunk(l, M, C, cin);
+    if (l == 1) {  // the GEMM reads the pooled BN1 backward, expanded to rows at MFMA time
+      TRY(launch_conv1_dx(wa, w.dx1, so));
+      wa.g_l = w.dx1;
+    }
     TimerScope tsc;
     TRY(timer_begin(&tsc, l == 1 ? DCUE_TIMED_CONV1_WGRAD : -1, so));
     HPROF("capi:19");
@@ -668,6 +686,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   };
   hipEvent_t tail[4] = {};  // caller's stream, user stream, wgrad streams 0 and 1
   // layer 1 (the step's tail) follows the chain on the caller's stream, issued right away
+  TRY(wait_point(s, ev_x0));
   TRY(issue_wgrad(1, s, 2, &tail[0]));
   HPROF("capi:22");
 

@@ -730,284 +730,309 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
 }
 
 
-// Layer-1 weight gradient (the step's largest MFMA kernel), warp-specialised. The GEMM is
-// dW1[o][kc] = sum over conv-1 rows (item, t) of dz1[row][o] * xhat0[row + tap][c]: K = M*132 rows.
-// Workgroup = a 64 (o) x 64 (kc) output tile x one chunk of rows, 8 waves: waves 0-3 run the MFMAs
-// (a 32x32 quarter each, 2x2 v_mfma_f32_16x16x4 tiles) on one LDS buffer while waves 4-7 build the
-// next step's dz (BN1 backward through relu + max-pool) and xhat0 tiles into the other buffer from
-// registers loaded two steps ahead. Producer work per row is kept to the arithmetic itself (row
-// cursors advance incrementally, the chunk's item table sits in LDS); in the bias workgroups
-// (kc tile 0) the MFMA waves also sum dz per channel -- all rows and the four edge positions --
-// from the LDS tile. With 64x64 tiles the split-K partials are a quarter of a 128x128 tiling's.
-constexpr int kW1Tile = 64, kW1Rch = 64, kW1Pw = 64 + 16;  // pitch == 16 (mod 32): rows r, r+1 on disjoint banks
-constexpr int kW1Items = 128;                               // items per chunk staged in LDS
+// Layer-1 weight gradient (the step's largest MFMA kernel). The GEMM is
+// dW1[o][kc] = sum over conv-1 rows (item, t) of dz1[row][o] * xhat0[item][t + kx - 2][c], K = M*132
+// rows, kc = kx*128 + c. dz1 is BN1's backward through relu + max-pool: of each pool window's four
+// rows only the argmax row carries the window's gradient dx1[window][o]. The operands therefore stay
+// compact in HBM -- xhat0 (k_xhat0, zero-padded so every tap row exists) and the pooled dx1
+// (k_conv1_dx) plus the pool argmax bytes -- and the dz1 fragment is expanded at MFMA time:
+// a = (argmax[window][o] == row & 3) ? dx1[window][o] : 0.
+// Workgroup = a 64 (o) x 64 (kc) output tile x one chunk of pool windows, 8 waves: wave w owns the
+// (w>>1 & 1, w & 1) 32x32 quarter over half of each step's 32 windows (w >> 2), two
+// v_mfma_f32_32x32x2_f32 per window. The three LDS stages are filled by global_load_lds_dwordx4
+// (no register staging): step s+2's loads are issued behind step s's first MFMAs and retired by a
+// counted vmcnt before the raw barrier that ends step s+1; a window's LDS operands are read one
+// window ahead of its MFMAs. In the bias workgroups (kc tile 0) the waves also sum dx1 per channel
+// -- all rows and the four edge positions t = 0, 1, 130, 131.
+constexpr int kW1Tile = 64;                      // 64 (o) x 64 (kc) output tile
+constexpr int kW1Win = 32;                       // pool windows (128 conv rows) per step
+constexpr int kW1XF = kW1Win * 4 * kW1Tile;      // x stage: [128 rows][64 kc] floats, quad-swizzled
+constexpr int kW1DF = kW1Win * kW1Tile;          // dx1 stage: [32 windows][64 o]
+constexpr int kW1AF = kW1Win * kW1Tile / 4;      // argmax stage: [32 windows][64 o] bytes
+constexpr int kW1StageF = kW1XF + kW1DF + kW1AF; // 10752 floats = 42 KB
+constexpr int kW1Stages = 3;
 
-// One producer thread = one max-pool window (4 conv rows) x one channel quad per step: the BN1
-// backward of the window's pooled gradient is computed once and routed to its argmax row (the
-// other three rows of the window get zeros), and the window's four xhat0 rows are converted.
-struct W1Set {
-  float4 g, y;
-  float4 x[4];
-  uint32_t id;
-  int ii, w;  // item (relative to the chunk's first) and pool window of the thread's rows
-};
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-template <int SRCX>
+__device__ __forceinline__ void glds16(const void* g, float* l) {
+  __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)l, 16, 0, 0);
+}
+
 __global__ __launch_bounds__(512) void k_conv1_wgrad(WgradArgs a) {
-  constexpr int PAD = 2, LIN = kFrames, R = 132, LP = 33, CIN = kMels, KS = 4, NB = 5;
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  __shared__ float bsum[4][NB][kW1Tile];
-  __shared__ const char* s_xrow[kW1Items];  // track row base of each item of the chunk
-  __shared__ float s_cnt[kW1Items];
-  __shared__ int s_t[2][kW1Rch];  // conv position of each LDS row (-1: past the chunk)
-  const int tid = threadIdx.x;
-  const int cout = a.cout, kcn = KS * CIN;
+  constexpr int R = 132, LP = 33, NB = 5;
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // the only LDS object: a second
+                                                                // one makes hipcc drain the loads
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int cout = a.cout, kcn = 4 * kMels;
   // grid (chunk, kc tile, o tile): consecutive workgroup ids -- dispatched round-robin over the 8
   // XCDs -- are different chunks, so all tiles of one chunk share an XCD and its L2 serves their
-  // re-reads of the chunk's rows (8 kc tiles read the same dz inputs, 2 o tiles the same tracks)
+  // re-reads of the chunk's rows (8 kc tiles read the same dx1, 2 o tiles the same xhat0 rows)
   const int chunk = blockIdx.x, ktile = blockIdx.y, otile = blockIdx.z;
   const int obase = otile * kW1Tile, kbase = ktile * kW1Tile;
-  const int total = a.M * R;
-  const int r_begin = chunk * a.rows_per_chunk;  // multiple of 4: chunks start on a window
-  const int r_end = min(r_begin + a.rows_per_chunk, total);
-  const int nsteps = r_end > r_begin ? (r_end - r_begin + kW1Rch - 1) / kW1Rch : 0;
+  const int kx = kbase / kMels, cbase = kbase - kx * kMels;
+  const int nwin = a.M * LP;
+  const int w_begin = min(chunk * (a.rows_per_chunk / 4), nwin);
+  const int w_end = min(w_begin + a.rows_per_chunk / 4, nwin);
+  const int nsteps = (w_end - w_begin + kW1Win - 1) / kW1Win;
   const bool do_bias = ktile == 0;
-  const bool producer = tid >= 256;
-  const int i_first = r_begin / R, t_first = r_begin - i_first * R;
-  for (int k = tid; k < kW1Items; k += 512) {
-    const int ii = min(i_first + k, a.M - 1);
-    s_xrow[k] = reinterpret_cast<const char*>(a.xsrc) +
-                (size_t)a.item_track[ii] * kFrames * kMels * (SRCX == SRC_TRACK_F16 ? 2 : 4);
-    s_cnt[k] = a.counts ? a.counts[ii] : 1.f;
+  const float* xp = reinterpret_cast<const float*>(a.xsrc);  // [M + 1][kXp][128], zero pads
+  const float* dx1 = a.g_l;                                   // [M*33][cout]
+  const uint8_t* arg = a.idx_l;                               // [M*33][cout]
+
+  // ---- stage loads: per step every wave issues 4 x pieces (rows 16w + 4h .. +3), 1 dx1 piece
+  // (windows 4w .. 4w+3) and waves 0-1 one argmax piece (windows 16w .. 16w+15): 1 KB each
+  const int nload = w < 2 ? 6 : 5;
+  int xi[4], xt[4];  // row cursors (item, frame) of the lane's four x pieces; rows past the end
+                     // read the next chunk's rows or the zero item M (their dx1 is zero)
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const int r = 4 * w_begin + 16 * w + 4 * h + (lane >> 4);
+    xi[h] = r / R;
+    xt[h] = r - xi[h] * R;
   }
-  if (chunk == 0 && ktile == 0 && otile == 0 && tid < cout) {
+  const int xq = (lane & 15) ^ ((lane >> 4 & 1) << 3);  // row-parity quad swizzle (32-lane reads)
+  auto issue = [&](int step) {
+    float* st = lds + (step % kW1Stages) * kW1StageF;
+    const int win0 = w_begin + step * kW1Win;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      glds16(xp + ((size_t)(xi[h] * kXp + xt[h] + kx) * kMels + cbase + 4 * xq), st + (4 * w + h) * 256);
+      xt[h] += 4 * kW1Win;
+      if (xt[h] >= R) { xt[h] -= R; ++xi[h]; }
+    }
+    {
+      const int wl = win0 + 4 * w + (lane >> 4), o = obase + 4 * (lane & 15);
+      const bool ok = wl < w_end && o < cout;  // else xhat0's zero pad row
+      glds16(ok ? (const void*)(dx1 + (size_t)wl * cout + o) : (const void*)(xp + 4 * (lane & 15)),
+             st + kW1XF + w * 256);
+    }
+    if (w < 2) {
+      const int wl = min(win0 + 16 * w + (lane >> 2), nwin - 1);
+      const int ob = min(obase + 16 * (lane & 3), cout - 16);
+      glds16(arg + (size_t)wl * cout + ob, st + kW1XF + kW1DF + w * 256);
+    }
+  };
+  auto wait_stage = [&](bool one_in_flight) {  // retire all but the newest step's loads
+    if (!one_in_flight) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (nload == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  };
+  auto barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+
+  if (chunk == 0 && ktile == 0 && otile == 0 && tid < cout) {  // BN1's gamma/beta gradients
     a.dbeta[tid] = (float)acc_sum(a.dz_acc, cout, 0, tid);
     a.dgamma[tid] = (float)acc_sum(a.dz_acc, cout, 1, tid);
   }
-  __syncthreads();
 
-  // ---- producers: channel quad q (o = obase+4q, kc = kbase+4q) of window wslot of every step
-  const int p = tid & 255;
-  const int q = p & 15, wslot = p >> 4;
-  const int o = obase + 4 * q;
-  const bool o_ok = o < cout;
-  const int oc = o_ok ? o : 0;
-  const int kc = kbase + 4 * q;
-  const int kx = kc / CIN, cx = kc - kx * CIN;
-  float4 mean4 = {}, inv4 = {}, a4 = {}, sD4 = {}, sDx4 = {}, xmu = {}, xsc = {};
-  if (producer) {
-    mean4 = ld4(a.mean_l + oc); inv4 = ld4(a.invstd_l + oc); a4 = ld4(a.a_l + oc);
-    float sd[4], sdx[4];
+  // ---- MFMA: lane (hl = lane >> 5, l32) holds A[o = l32][row 2h + hl] and B[row 2h + hl][kc = l32]
+  const int hl = lane >> 5, l32 = lane & 31;
+  const int wo = (w >> 1) & 1, wk = w & 1, hk = w >> 2;
+  f32x16 acc;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      sd[s] = (float)acc_sum(a.dz_acc, cout, 0, oc + s);
-      sdx[s] = (float)acc_sum(a.dz_acc, cout, 1, oc + s);
-    }
-    sD4 = make_float4(sd[0], sd[1], sd[2], sd[3]);
-    sDx4 = make_float4(sdx[0], sdx[1], sdx[2], sdx[3]);
-    xmu = ld4(a.x_mean + cx); xsc = ld4(a.x_a + cx);
-  }
-  // settle every load so far: the loop's wait counts then only track the step prefetches (a load
-  // still pending at the loop entry makes each iteration wait for all of them)
-  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0), expcnt/lgkmcnt untouched
-  // issue cursor: window (r_begin + 64*step)/4 + wslot as (item offset, window), 16 windows a step
-  int cur_i = 0, cur_w = t_first / 4 + wslot;
-  if (cur_w >= LP) { cur_w -= LP; cur_i = 1; }
-  auto issue = [&](W1Set& st) {
-    st.ii = cur_i;
-    st.w = cur_w;
-    const int base = ((i_first + min(cur_i, a.M - 1 - i_first)) * LP + cur_w) * cout + oc;  // < 2^31
-    st.g = ld4(a.g_l + base);
-    st.y = ld4(a.y_l + base);
-    st.id = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
-    const char* xrow = s_xrow[min(cur_i, kW1Items - 1)];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      int pp = 4 * cur_w + r + kx - PAD;
-      pp = pp < 0 ? 0 : (pp >= LIN ? LIN - 1 : pp);
-      const int xo = pp * kMels + cx;
-      if constexpr (SRCX == SRC_TRACK_F16) {
-        const uint2 raw = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(xrow) + xo);
-        st.x[r] = make_float4(__uint_as_float(raw.x), __uint_as_float(raw.y), 0.f, 0.f);
-      } else {
-        st.x[r] = ld4(reinterpret_cast<const float*>(xrow) + xo);
-      }
-    }
-    cur_w += kW1Rch / 4;
-    if (cur_w >= LP) { cur_w -= LP; ++cur_i; }
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  float bacc[NB] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  const int ao = 32 * wo + l32;                                    // A element's channel in the tile
+  const int bx0 = hl * kW1Tile + 4 * ((8 * wk + (l32 >> 2)) ^ (hl << 3)) + (l32 & 3);  // row 2h + hl
+  struct Ops { float d, b0, b1; int g; };
+  auto ops = [&](const float* st, int kk) {
+    const float* dxs = st + kW1XF;
+    const uint8_t* ags = reinterpret_cast<const uint8_t*>(st + kW1XF + kW1DF);
+    const float* xr = st + 4 * kk * kW1Tile + bx0;
+    return Ops{dxs[kk * kW1Tile + ao], xr[0], xr[2 * kW1Tile], (int)ags[kk * kW1Tile + ao]};
   };
-  // branch-free: the loads' wait counts stay exact (a divergent branch makes the compiler wait for
-  // every outstanding load, including the next step's prefetch)
-  auto fill = [&](const W1Set& st, int step, int buf) {
-    float* dzs = lds + buf * 2 * kW1Rch * kW1Pw;
-    float* xs = dzs + kW1Rch * kW1Pw;
-    const int r0 = 4 * wslot;
-    const bool valid = r_begin + step * kW1Rch + r0 < r_end;  // a window is wholly in or out
-    const float kD = s_cnt[min(st.ii, kW1Items - 1)] * a.invN;
-    const float gv[4] = {st.g.x, st.g.y, st.g.z, st.g.w};
-    const float yv[4] = {st.y.x, st.y.y, st.y.z, st.y.w};
-    const float mu[4] = {mean4.x, mean4.y, mean4.z, mean4.w}, iv[4] = {inv4.x, inv4.y, inv4.z, inv4.w};
-    const float av[4] = {a4.x, a4.y, a4.z, a4.w}, sd[4] = {sD4.x, sD4.y, sD4.z, sD4.w};
-    const float sdx[4] = {sDx4.x, sDx4.y, sDx4.z, sDx4.w};
-    float dxv[4];
-    uint32_t arg[4];
+  auto mma2 = [&](const Ops& p) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(p.g == hl ? p.d : 0.f, p.b0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(p.g == 2 + hl ? p.d : 0.f, p.b1, acc, 0, 0, 0);
+  };
+  auto bias = [&](const float* st, int win0, int nw) {  // channel tid & 63 of windows w + 8u
+    const float* dxs = st + kW1XF;
+    const uint8_t* ags = reinterpret_cast<const uint8_t*>(st + kW1XF + kW1DF);
+    const int ch = tid & 63;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const float xh = (yv[s] - mu[s]) * iv[s];
-      const float dx = av[s] * (gv[s] - kD * sd[s] - kD * xh * sdx[s]);
-      dxv[s] = (valid & o_ok & (yv[s] > 0.f)) ? dx : 0.f;
-      arg[s] = (st.id >> (8 * s)) & 0xff;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = 4 * st.w + r;
-      const int pp = t + kx - PAD;
-      const bool x_ok = valid & (pp >= 0) & (pp < LIN);
-      st4(&dzs[(r0 + r) * kW1Pw + 4 * q],
-          make_float4(arg[0] == (uint32_t)r ? dxv[0] : 0.f, arg[1] == (uint32_t)r ? dxv[1] : 0.f,
-                      arg[2] == (uint32_t)r ? dxv[2] : 0.f, arg[3] == (uint32_t)r ? dxv[3] : 0.f));
-      float x[4];
-      if constexpr (SRCX == SRC_TRACK_F16) {
-        const uint32_t lo = __float_as_uint(st.x[r].x), hi = __float_as_uint(st.x[r].y);
-        const __half2 h0 = *reinterpret_cast<const __half2*>(&lo);
-        const __half2 h1 = *reinterpret_cast<const __half2*>(&hi);
-        x[0] = __low2float(h0); x[1] = __high2float(h0); x[2] = __low2float(h1); x[3] = __high2float(h1);
-      } else {
-        x[0] = st.x[r].x; x[1] = st.x[r].y; x[2] = st.x[r].z; x[3] = st.x[r].w;
-      }
-      st4(&xs[(r0 + r) * kW1Pw + 4 * q],
-          make_float4(x_ok ? (x[0] - xmu.x) * xsc.x : 0.f, x_ok ? (x[1] - xmu.y) * xsc.y : 0.f,
-                      x_ok ? (x[2] - xmu.z) * xsc.z : 0.f, x_ok ? (x[3] - xmu.w) * xsc.w : 0.f));
-      s_t[buf][r0 + r] = valid ? t : -1;  // the 16 threads of a window store the same values
+    for (int u = 0; u < kW1Win / 8; ++u) {
+      const int kk = w + 8 * u;
+      if (kk >= nw) break;
+      const float v = dxs[kk * kW1Tile + ch];
+      const int t = 4 * ((win0 + kk) % LP) + ags[kk * kW1Tile + ch];
+      bacc[0] += v;
+      bacc[1] += t == 0 ? v : 0.f;
+      bacc[2] += t == 1 ? v : 0.f;
+      bacc[3] += t == R - 2 ? v : 0.f;
+      bacc[4] += t == R - 1 ? v : 0.f;
     }
   };
 
-  // ---- consumers: wave w owns the (w>>1, w&1) 32x32 quarter of the tile
-  const int lane = tid & 63, w = (tid >> 6) & 3;
-  const int g = lane >> 4, l16 = lane & 15;
-  const int wo = w >> 1, wk = w & 1;
-  f32x4 acc[2][2];
+  // Pipeline over stages step % 3: step s+2 goes into the stage step s-1 read (every wave's reads
+  // of it retired before the barrier that ended step s-1); the wait ending step s retires step
+  // s+1's loads (each wave its own, the barrier then publishes them to all).
+  if (nsteps > 0) issue(0);
+  if (nsteps > 1) issue(1);
+  wait_stage(nsteps > 1);
+  barrier();
+  for (int s = 0; s < nsteps; ++s) {
+    const float* st = lds + (s % kW1Stages) * kW1StageF;
+    const bool more = s + 2 < nsteps;
+    const int win0 = w_begin + s * kW1Win;
+    const int nw = min(kW1Win, w_end - win0);
+    const int kn = min(max(nw - 16 * hk, 0), 16);  // this wave's windows 16hk .. 16hk+kn-1
+    if (kn == 16) {  // every step but a chunk's last: unrolled, operands read ahead freely
+      // two windows of read-ahead, pinned: a window's LDS reads are issued two MFMA pairs
+      // (256 pipe cycles) before their use
+      Ops q0 = ops(st, 16 * hk), q1 = ops(st, 16 * hk + 1);
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bacc[NB] = {0.f, 0.f, 0.f, 0.f, 0.f};  // bias workgroups: channel tid&63, rows == tid>>6 (mod 4)
-  auto mma = [&](int step, int buf) {
-    const float* dzs = lds + buf * 2 * kW1Rch * kW1Pw;
-    const float* xs = dzs + kW1Rch * kW1Pw;
-    const int nr = min(kW1Rch, r_end - (r_begin + step * kW1Rch));
-    // rows past the chunk end are zero in LDS, so whole groups of 8 rows are safe to read. Two
-    // operand sets alternate: one k-step's reads are issued before the other's MFMAs, so the LDS
-    // latency hides under them (the scheduling barriers keep that order)
-    const float* dr = dzs + g * kW1Pw + 32 * wo + l16;
-    const float* xr = xs + g * kW1Pw + 32 * wk + l16;
-    float a0 = dr[0], a1 = dr[16], b0 = xr[0], b1 = xr[16];
-    const int n8 = (nr + 7) & ~7;
-    for (int r0 = 0; r0 < n8; r0 += 8) {
-      const int o1 = (r0 + 4) * kW1Pw;
-      const float c0 = dr[o1], c1 = dr[o1 + 16], e0 = xr[o1], e1 = xr[o1 + 16];
-      __builtin_amdgcn_sched_barrier(0);
-      acc[0][0] = mfma4(a0, b0, acc[0][0]);
-      acc[0][1] = mfma4(a0, b1, acc[0][1]);
-      acc[1][0] = mfma4(a1, b0, acc[1][0]);
-      acc[1][1] = mfma4(a1, b1, acc[1][1]);
-      __builtin_amdgcn_sched_barrier(0);
-      const int o2 = (r0 + 8 < kW1Rch ? r0 + 8 : 0) * kW1Pw;
-      a0 = dr[o2]; a1 = dr[o2 + 16]; b0 = xr[o2]; b1 = xr[o2 + 16];
-      __builtin_amdgcn_sched_barrier(0);
-      acc[0][0] = mfma4(c0, e0, acc[0][0]);
-      acc[0][1] = mfma4(c0, e1, acc[0][1]);
-      acc[1][0] = mfma4(c1, e0, acc[1][0]);
-      acc[1][1] = mfma4(c1, e1, acc[1][1]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (do_bias) {
-      const int ch = tid & 63;
-      for (int r = tid >> 6; r < nr; r += 4) {
-        const float v = dzs[r * kW1Pw + ch];
-        const int t = s_t[buf][r];
-        bacc[0] += v;
-        bacc[1] += t == 0 ? v : 0.f;
-        bacc[2] += t == 1 ? v : 0.f;
-        bacc[3] += t == R - 2 ? v : 0.f;
-        bacc[4] += t == R - 1 ? v : 0.f;
+      for (int k = 0; k < 16; ++k) {
+        const Ops q2 = ops(st, 16 * hk + (k < 14 ? k + 2 : 15));
+        __builtin_amdgcn_sched_barrier(0);
+        mma2(q0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (k == 0 && more) issue(s + 2);  // behind the first MFMAs: the pipe stays fed
+        q0 = q1;
+        q1 = q2;
       }
+    } else {  // a chunk's last step (never followed by loads)
+      for (int k = 0; k < kn; ++k) mma2(ops(st, 16 * hk + k));
     }
-  };
-
-  // Producers fill and prefetch unconditionally (steps past the chunk read clamped, in-bounds rows
-  // and fill an LDS buffer nobody consumes): with no conditional load the compiler's wait counts
-  // wait for exactly the set being filled, never for the prefetch behind it.
-  W1Set sa, sb;
-  if (producer) {
-    issue(sa);
-    issue(sb);
-    fill(sa, 0, 0);
-    issue(sa);
-  }
-  __syncthreads();
-  for (int s = 0; s < nsteps; s += 2) {
-    if (!producer) {
-      mma(s, 0);
-    } else {
-      fill(sb, s + 1, 1);
-      issue(sb);
-    }
-    __syncthreads();
-    if (s + 1 >= nsteps) break;
-    if (!producer) {
-      mma(s + 1, 1);
-    } else {
-      fill(sa, s + 2, 0);
-      issue(sa);
-    }
-    __syncthreads();
+    if (do_bias) bias(st, win0, nw);
+    wait_stage(more);
+    barrier();
   }
 
-  if (!producer) {  // partial tile -> wpart[z][o][kc]; D lane map: o = 4g + reg, kc = l16
-    float* wp = a.wpart + (size_t)chunk * cout * kcn;
+  // ---- epilogue: k-halves summed through LDS (the stages are free: no load in flight)
+  float* red = lds;                          // [64 o][64 kc] of waves 4-7
+  float* bsum = lds + kW1Tile * kW1Tile;     // [8 waves][NB][64]
+  // D lane map (32x32): o = (j & 3) + 8 (j >> 2) + 4 hl, kc = l32
+  if (hk == 1) {
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const int kk = kbase + 32 * wk + 16 * n + l16;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int oo = obase + 32 * wo + 16 * m + 4 * g + j;
-          if (oo < cout) wp[(size_t)oo * kcn + kk] = acc[m][n][j];
-        }
-      }
-    if (do_bias) {
-#pragma unroll
-      for (int e = 0; e < NB; ++e) bsum[tid >> 6][e][tid & 63] = bacc[e];
-    }
+    for (int j = 0; j < 16; ++j)
+      red[(32 * wo + (j & 3) + 8 * (j >> 2) + 4 * hl) * kW1Tile + 32 * wk + l32] = acc[j];
   }
   if (do_bias) {
-    __syncthreads();
-    if (tid < kW1Tile && obase + tid < cout) {
 #pragma unroll
-      for (int e = 0; e < NB; ++e) {
-        const float v = ((bsum[0][e][tid] + bsum[1][e][tid]) + bsum[2][e][tid]) + bsum[3][e][tid];
-        a.bpart[((size_t)chunk * NB + e) * cout + obase + tid] = v;
-      }
+    for (int e = 0; e < NB; ++e) bsum[(w * NB + e) * kW1Tile + (tid & 63)] = bacc[e];
+  }
+  __syncthreads();
+  if (hk == 0) {
+    float* wp = a.wpart + (size_t)chunk * cout * kcn;
+    const int kl = 32 * wk + l32;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int ol = 32 * wo + (j & 3) + 8 * (j >> 2) + 4 * hl;
+      if (obase + ol < cout) wp[(size_t)(obase + ol) * kcn + kbase + kl] = acc[j] + red[ol * kW1Tile + kl];
+    }
+  }
+  if (do_bias && tid < kW1Tile && obase + tid < cout) {
+#pragma unroll
+    for (int e = 0; e < NB; ++e) {
+      float v = 0.f;
+      for (int sl = 0; sl < 8; ++sl) v += bsum[(sl * NB + e) * kW1Tile + tid];
+      a.bpart[((size_t)chunk * NB + e) * cout + obase + tid] = v;
     }
   }
 }
 
-template <int SRCX>
 static int conv1_wgrad(const WgradArgs& a0, int nchunk, hipStream_t s) {
-  constexpr size_t LDS = (size_t)2 * 2 * kW1Rch * kW1Pw * sizeof(float);
-  auto kern = k_conv1_wgrad<SRCX>;
+  constexpr size_t LDS = (size_t)kW1Stages * kW1StageF * sizeof(float);
   static bool attr = false;
   if (!attr) {
-    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS));
+    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_conv1_wgrad, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)LDS));
     attr = true;
   }
+  if (a0.cout % 16 != 0) return DCUE_ERR_UNSUPPORTED;  // argmax rows are loaded 16 channels at a time
   WgradArgs a = a0;
-  const long rows = (long)a.M * 132;
-  a.rows_per_chunk = (int)(4 * ((rows + 4L * nchunk - 1) / (4L * nchunk)));  // whole pool windows
+  const long wins = (long)a.M * 33;
+  a.rows_per_chunk = (int)(4L * ((wins + nchunk - 1) / nchunk));  // whole pool windows
   dim3 grid((unsigned)nchunk, (unsigned)(4 * kMels / kW1Tile), (unsigned)((a.cout + kW1Tile - 1) / kW1Tile));
-  DCUE_LAUNCH(kern, grid, dim3(512), LDS, s, a);
+  DCUE_LAUNCH(k_conv1_wgrad, grid, dim3(512), LDS, s, a);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+// BN1's backward through relu at the pooled positions: dx1[window][o] = a_o (g - kD sum_g - kD xhat
+// sum_gxhat), zero where the pooled activation is not positive; kD = copies(item) / N. One thread
+// per channel quad of a window.
+__global__ __launch_bounds__(256) void k_conv1_dx(WgradArgs a, float* __restrict__ dx1) {
+  constexpr int LP = 33;
+  const int cq = a.cout / 4;
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)a.M * LP * cq) return;
+  const int o = 4 * (int)(e % cq);
+  const long win = e / cq;
+  const int item = (int)(win / LP);
+  const float kD = (a.counts ? a.counts[item] : 1.f) * a.invN;
+  const float4 g = ld4(a.g_l + win * a.cout + o), y = ld4(a.y_l + win * a.cout + o);
+  const float4 mu = ld4(a.mean_l + o), iv = ld4(a.invstd_l + o), av = ld4(a.a_l + o);
+  const float gv[4] = {g.x, g.y, g.z, g.w}, yv[4] = {y.x, y.y, y.z, y.w};
+  const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, i4[4] = {iv.x, iv.y, iv.z, iv.w}, a4[4] = {av.x, av.y, av.z, av.w};
+  float d[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const float sd = (float)acc_sum(a.dz_acc, a.cout, 0, o + s), sdx = (float)acc_sum(a.dz_acc, a.cout, 1, o + s);
+    const float xh = (yv[s] - m4[s]) * i4[s];
+    const float dx = a4[s] * (gv[s] - kD * sd - kD * xh * sdx);
+    d[s] = yv[s] > 0.f ? dx : 0.f;
+  }
+  st4(dx1 + win * a.cout + o, make_float4(d[0], d[1], d[2], d[3]));
+}
+
+int launch_conv1_dx(const WgradArgs& a, float* dx1, hipStream_t s) {
+  const long n = (long)a.M * 33 * (a.cout / 4);
+  DCUE_LAUNCH(k_conv1_dx, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, dx1);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+// bn0(x) without its affine, zero-padded for the conv-1 taps: xhat0[i][p][c] for p = t + 2 (t the
+// frame), rows p < 2 and p > 132 zero. One thread per channel quad of a padded row.
+template <int SRC>
+__global__ __launch_bounds__(256) void k_xhat0(const void* __restrict__ tracks, const int32_t* __restrict__ item_track,
+                                               int M, const unsigned long long* acc0, double count,
+                                               double inv_count, float* __restrict__ xhat0) {
+  __shared__ float s_mu[kMels], s_is[kMels];
+  if (threadIdx.x < kMels) {
+    const BnChan st = bn_chan_train(acc0, kMels, threadIdx.x, count, inv_count);
+    s_mu[threadIdx.x] = st.mean;
+    s_is[threadIdx.x] = st.invstd;
+  }
+  __syncthreads();
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;  // float4 index
+  const long n4 = (long)(M + 1) * kXp * (kMels / 4);  // item M: zeros
+  if (e >= n4) return;
+  const int c = 4 * (int)(e % (kMels / 4));
+  const long row = e / (kMels / 4);  // item * kXp + p
+  const long i = row / kXp;
+  const int t = (int)(row - i * kXp) - 2;
+  float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t >= 0 && t < kFrames && i < M) {
+    const long src = ((long)item_track[i] * kFrames + t) * kMels + c;
+    float x[4];
+    if constexpr (SRC == SRC_TRACK_F16) {
+      const uint2 raw = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(tracks) + src);
+      const __half2 h0 = *reinterpret_cast<const __half2*>(&raw.x);
+      const __half2 h1 = *reinterpret_cast<const __half2*>(&raw.y);
+      x[0] = __low2float(h0); x[1] = __high2float(h0); x[2] = __low2float(h1); x[3] = __high2float(h1);
+    } else {
+      const float4 v = ld4(reinterpret_cast<const float*>(tracks) + src);
+      x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+    }
+    out = make_float4((x[0] - s_mu[c]) * s_is[c], (x[1] - s_mu[c + 1]) * s_is[c + 1],
+                      (x[2] - s_mu[c + 2]) * s_is[c + 2], (x[3] - s_mu[c + 3]) * s_is[c + 3]);
+  }
+  st4(xhat0 + 4 * e, out);
+}
+
+int launch_xhat0(int src, const void* tracks, const int32_t* item_track, int M, const unsigned long long* acc0,
+                 double count, float* xhat0, hipStream_t s) {
+  const long n4 = (long)(M + 1) * kXp * (kMels / 4);
+  const dim3 grid((unsigned)((n4 + 255) / 256));
+  if (src == SRC_TRACK_F16)
+    DCUE_LAUNCH(k_xhat0<SRC_TRACK_F16>, grid, dim3(256), 0, s, tracks, item_track, M, acc0, count, 1.0 / count, xhat0);
+  else
+    DCUE_LAUNCH(k_xhat0<SRC_TRACK_F32>, grid, dim3(256), 0, s, tracks, item_track, M, acc0, count, 1.0 / count, xhat0);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
@@ -1017,13 +1042,11 @@ int wgrad_nchunk(int layer, int M, int cout, int cin) {
   // blocks cost a write + a read of cout*ks*cin floats per chunk
   const LayerGeom gm = layer_geom(layer);
   const long rows = (long)M * gm.lp * gm.pool;
-  if (layer == 1) {  // k_conv1_wgrad: 64x64 tiles, >= 4 row steps per chunk, <= ~256 workgroups,
-                     // and few enough items per chunk for its LDS item table
+  if (layer == 1) {  // k_conv1_wgrad: 64x64 tiles, >= 4 steps (64 windows) per chunk, <= ~256 workgroups
     const long tiles1 = (4L * kMels / kW1Tile) * ((cout + kW1Tile - 1) / kW1Tile);
     long n = 256 / tiles1;
-    if (n > (rows + 4 * kW1Rch - 1) / (4 * kW1Rch)) n = (rows + 4 * kW1Rch - 1) / (4 * kW1Rch);
-    const long need = (M + kW1Items - 3) / (kW1Items - 2);
-    if (n < need) n = need;
+    const long wins = (long)M * gm.lp;
+    if (n > (wins + 4 * kW1Win - 1) / (4 * kW1Win)) n = (wins + 4 * kW1Win - 1) / (4 * kW1Win);
     return (int)(n < 1 ? 1 : n);
   }
   const long tiles = ((gm.ks * cin + 127) / 128) * ((cout + 127) / 128);
@@ -1059,8 +1082,7 @@ static int wgrad_layer(const WgradArgs& a0, int nchunk, hipStream_t s) {
 
 int launch_conv_wgrad(int layer, int src, const WgradArgs& a, int nchunk, hipStream_t s) {
   switch (layer) {
-    case 1: return src == SRC_TRACK_F16 ? conv1_wgrad<SRC_TRACK_F16>(a, nchunk, s)
-                                        : conv1_wgrad<SRC_TRACK_F32>(a, nchunk, s);
+    case 1: (void)src; return conv1_wgrad(a, nchunk, s);  // X = xhat0 (k_xhat0), whatever the table dtype
     case 2: return wgrad_layer<2, SRC_ACT>(a, nchunk, s);
     case 3: return wgrad_layer<3, SRC_ACT>(a, nchunk, s);
     case 4: return wgrad_layer<4, SRC_ACT>(a, nchunk, s);

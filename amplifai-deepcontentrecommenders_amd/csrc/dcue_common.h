@@ -58,6 +58,7 @@ namespace dcue {
 
 constexpr int kMels = DCUE_N_MELS;     // 128, truedcuemel1dbn.py:24
 constexpr int kFrames = DCUE_N_FRAMES; // 131, datasets/dcuedataset.py:235
+constexpr int kXp = kFrames + 5;        // zero-padded xhat0 rows per item: every conv-1 tap row exists
 constexpr int kWave = 64;
 
 // Per-layer geometry of the default item tower (truedcuemel1dbn.py:25-61).

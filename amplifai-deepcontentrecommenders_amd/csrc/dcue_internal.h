@@ -89,7 +89,14 @@ struct WgradArgs {
 int launch_conv_fwd(int layer, int kc, int src, const RowsArgs& a, hipStream_t s);
 int launch_conv_dgrad(int layer, int kc, const RowsArgs& a, hipStream_t s);
 int launch_conv_wgrad(int layer, int src, const WgradArgs& a, int nchunk, hipStream_t s);
+// xhat0[i][t + 2][c] = (x[track_i][t][c] - mean0[c]) * invstd0[c] in a [M][kXp][128] zero-padded
+// layout, bn0's batch statistics finalized from its accumulators (layer 1's wgrad reads it from `xsrc`)
+int launch_xhat0(int src, const void* tracks, const int32_t* item_track, int M, const unsigned long long* acc0,
+                 double count, float* xhat0, hipStream_t s);
 int wgrad_nchunk(int layer, int M, int cout, int cin);
+// layer 1: the pooled BN1 backward dx1[M*33][cout] that k_conv1_wgrad reads from `g_l` (the
+// WgradArgs of the same call, with g_l the pooled gradient)
+int launch_conv1_dx(const WgradArgs& a, float* dx1, hipStream_t s);
 int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int nchunk, int cout,
                         int cin, float* dW, float* db, float* G_tmp, float* E_tmp, hipStream_t s);
 int launch_bn0_grads(const float* G, const float* E, const float* W1, const float* gamma0,

@@ -227,22 +227,48 @@ def main():
     TIMED = nat.TIMED_CONV1_WGRAD  # the roofline kernel, timed live by HIP events in the library
     TIMER_STRIDE = 8
 
-    if args.mode == "catalogue":
-        raise SystemExit("catalogue mode bench: use --mode inbatch (config 2); catalogue runs in tests")
+    catalogue = args.mode == "catalogue"
+    if catalogue:
+        # the reference's live sampler (datasets/dcuedataset.py:207-220): N negatives per row drawn
+        # from the train split's songs the user never interacted with; the conv runs on all
+        # M = B(1+N) distinct items. The user -> split-rank CSR covers every interaction.
+        from dcrecommend.datasets.csr import user_split_ranks
+        split_items = np.nonzero(split == 0)[0].astype(np.int64)
+        indptr, ranks = user_split_ranks(pair_user.cpu().numpy(), pair_track.cpu().numpy(), n_users_local,
+                                         split_items)
+        split_d64 = torch.from_numpy(split_items).to(dev)
+        indptr_d = torch.from_numpy(indptr).to(dev)
+        ranks_d = torch.from_numpy(ranks).to(dev)
+        items_b64 = items_b.long()
+        negs = torch.empty((B, N), dtype=torch.int64, device=dev)
 
     # The roofline kernel's timer is on before the plan is built. It binds a HIP event pair to every
     # TIMER_STRIDE-th launch of the kernel (its own dispatch's start and end, on the stream it runs
     # on); a timed launch costs the stream a few microseconds, so a sample is timed, not every step.
     nat.timer_enable(TIMED, TIMER_STRIDE)
-    plan = TrainPlan(net, tracks, B, N, mt_state=mt, emb_grad_scale=1.0 / world, optimizer=opt)
+    plan = TrainPlan(net, tracks, B, N, mt_state=None if catalogue else mt, emb_grad_scale=1.0 / world,
+                     optimizer=opt)
+
+    def sample_catalogue(s):
+        nat.check(nat.lib().dcue_sample_catalogue(nat.ptr(mt), 0, 0, nat.ptr(split_d64), split_d64.numel(),
+                                                  nat.ptr(indptr_d), nat.ptr(ranks_d), nat.ptr(users_b[s]), B, N,
+                                                  nat.ptr(negs), nat.stream_handle()), "dcue_sample_catalogue")
+        nat.check(nat.lib().dcue_build_catalogue_batch(nat.ptr(items_b64[s]), nat.ptr(negs), B, N,
+                                                       nat.ptr(plan.item_track), nat.stream_handle()),
+                  "dcue_build_catalogue_batch")
 
     def step(s):
+        if catalogue:
+            sample_catalogue(s)
+            src = (users_b[s], None)
+        else:
+            src = (users_b[s], items_b[s])
         if world > 1:
-            plan.launch(users_b[s], items_b[s])
+            plan.launch(*src)
             D.allreduce_mean_(G)  # RCCL: the one exchange of the step (1.57 MB)
             opt.step()
         else:
-            plan.step(users_b[s], items_b[s])  # sample + forward + backward + Adam, one host call
+            plan.step(*src)  # sample + forward + backward + Adam, one host call
         sched.batch_step()
 
     for s in range(args.warmup):
@@ -279,11 +305,12 @@ def main():
     # algorithmic FLOPs of one conv-1 weight-gradient launch: dW1[o][c][k] summed over every conv-1
     # output row (item, position) of the batch's distinct items -- B items x 132 positions (131
     # frames, kernel 4, padding 2) x 128 mel inputs x 4 taps x H outputs, 2 FLOP per product
-    wg_flops = 2.0 * args.hidden * 128 * 4 * (B * 132)
+    M_items = B * (1 + N) if catalogue else B
+    wg_flops = 2.0 * args.hidden * 128 * 4 * (M_items * 132)
     achieved = wg_flops / (wg_ms * 1e-3) / 1e12
     traffic = None
     tf_path = os.path.join(ROOT, "profiles", "pmc_conv1_wgrad.json")
-    if os.path.exists(tf_path):
+    if os.path.exists(tf_path) and not catalogue:  # collected on the default (in-batch) workload
         try:
             traffic = json.load(open(tf_path)).get("hbm_bytes_per_launch")
         except (ValueError, OSError):
@@ -307,9 +334,9 @@ def main():
         "rows_per_s": rows,
         "auc_val": None,
         "config": {"workload": "DCUE truedcuemel1dbn d=%d H=%d E=%d, %d users x %d tracks (fp16 table), "
-                               "%d interactions, in-batch negatives N=%d"
+                               "%d interactions, %s negatives N=%d"
                                % (args.feature_dim, args.hidden, E, args.users, args.tracks,
-                                  args.interactions, N),
+                                  args.interactions, "catalogue" if catalogue else "in-batch", N),
                    "batch_per_gpu": B, "global_batch": B * world, "neg": N,
                    "parallelism": "dp%d (users sharded, dense grads all-reduced)" % world},
         "roofline": {"kernel": "k_conv1_wgrad (conv layer 1 weight gradient, f32 MFMA 16x16x4)", "bound": "mfma",
