@@ -745,11 +745,15 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
 // window ahead of its MFMAs. In the bias workgroups (kc tile 0) the waves also sum dx1 per channel
 // -- all rows and the four edge positions t = 0, 1, 130, 131.
 constexpr int kW1Tile = 64;                      // 64 (o) x 64 (kc) output tile
-constexpr int kW1Win = 32;                       // pool windows (128 conv rows) per step
+constexpr int kW1Win = 16;                       // pool windows (64 conv rows) per step
+constexpr int kW1Half = kW1Win / 2;              // windows per wave per step (two k halves)
+constexpr int kW1XPW = kW1Win / 8;               // x pieces (4 rows, 1 KB) per wave per step
+constexpr int kW1DW = kW1Win / 4;                // waves loading a dx1 piece (4 windows)
+constexpr int kW1AW = kW1Win / 16;               // waves loading an argmax piece (16 windows)
 constexpr int kW1XF = kW1Win * 4 * kW1Tile;      // x stage: [128 rows][64 kc] floats, quad-swizzled
 constexpr int kW1DF = kW1Win * kW1Tile;          // dx1 stage: [32 windows][64 o]
 constexpr int kW1AF = kW1Win * kW1Tile / 4;      // argmax stage: [32 windows][64 o] bytes
-constexpr int kW1StageF = kW1XF + kW1DF + kW1AF; // 10752 floats = 42 KB
+constexpr int kW1StageF = kW1XF + kW1DF + kW1AF; // 5376 floats = 21 KB: two workgroups per CU
 constexpr int kW1Stages = 3;
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -759,8 +763,9 @@ __device__ __forceinline__ void glds16(const void* g, float* l) {
   __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)l, 16, 0, 0);
 }
 
-__global__ __launch_bounds__(512) void k_conv1_wgrad(WgradArgs a) {
+__global__ __launch_bounds__(512, 2) void k_conv1_wgrad(WgradArgs a) {
   constexpr int R = 132, LP = 33, NB = 5;
+  static_assert(kW1Win % 16 == 0 && kW1DW + kW1AW <= 8, "load assignment");
   extern __shared__ __attribute__((aligned(16))) float lds[];  // the only LDS object: a second
                                                                 // one makes hipcc drain the loads
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -780,14 +785,16 @@ __global__ __launch_bounds__(512) void k_conv1_wgrad(WgradArgs a) {
   const float* dx1 = a.g_l;                                   // [M*33][cout]
   const uint8_t* arg = a.idx_l;                               // [M*33][cout]
 
-  // ---- stage loads: per step every wave issues 4 x pieces (rows 16w + 4h .. +3), 1 dx1 piece
-  // (windows 4w .. 4w+3) and waves 0-1 one argmax piece (windows 16w .. 16w+15): 1 KB each
-  const int nload = w < 2 ? 6 : 5;
-  int xi[4], xt[4];  // row cursors (item, frame) of the lane's four x pieces; rows past the end
-                     // read the next chunk's rows or the zero item M (their dx1 is zero)
+  // ---- stage loads (1 KB pieces): per step every wave issues kW1XPW x pieces (rows
+  // 4 kW1XPW w + 4h .. +3), waves 0 .. kW1DW-1 one dx1 piece (windows 4w .. 4w+3) and the next
+  // kW1AW waves one argmax piece (16 windows)
+  const bool dxw = w < kW1DW, agw = w >= kW1DW && w < kW1DW + kW1AW;
+  const int nload = kW1XPW + (dxw ? 1 : 0) + (agw ? 1 : 0);
+  int xi[kW1XPW], xt[kW1XPW];  // row cursors (item, frame) of the lane's x pieces; rows past the
+                               // end read the next chunk's rows or the zero item M (unused)
 #pragma unroll
-  for (int h = 0; h < 4; ++h) {
-    const int r = 4 * w_begin + 16 * w + 4 * h + (lane >> 4);
+  for (int h = 0; h < kW1XPW; ++h) {
+    const int r = 4 * w_begin + 4 * kW1XPW * w + 4 * h + (lane >> 4);
     xi[h] = r / R;
     xt[h] = r - xi[h] * R;
   }
@@ -796,27 +803,28 @@ __global__ __launch_bounds__(512) void k_conv1_wgrad(WgradArgs a) {
     float* st = lds + (step % kW1Stages) * kW1StageF;
     const int win0 = w_begin + step * kW1Win;
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      glds16(xp + ((size_t)(xi[h] * kXp + xt[h] + kx) * kMels + cbase + 4 * xq), st + (4 * w + h) * 256);
+    for (int h = 0; h < kW1XPW; ++h) {
+      glds16(xp + ((size_t)(xi[h] * kXp + xt[h] + kx) * kMels + cbase + 4 * xq), st + (kW1XPW * w + h) * 256);
       xt[h] += 4 * kW1Win;
       if (xt[h] >= R) { xt[h] -= R; ++xi[h]; }
     }
-    {
+    if (dxw) {
       const int wl = win0 + 4 * w + (lane >> 4), o = obase + 4 * (lane & 15);
       const bool ok = wl < w_end && o < cout;  // else xhat0's zero pad row
       glds16(ok ? (const void*)(dx1 + (size_t)wl * cout + o) : (const void*)(xp + 4 * (lane & 15)),
              st + kW1XF + w * 256);
     }
-    if (w < 2) {
-      const int wl = min(win0 + 16 * w + (lane >> 2), nwin - 1);
+    if (agw) {
+      const int wa = w - kW1DW;
+      const int wl = min(win0 + 16 * wa + (lane >> 2), nwin - 1);
       const int ob = min(obase + 16 * (lane & 3), cout - 16);
-      glds16(arg + (size_t)wl * cout + ob, st + kW1XF + kW1DF + w * 256);
+      glds16(arg + (size_t)wl * cout + ob, st + kW1XF + kW1DF + wa * 256);
     }
   };
   auto wait_stage = [&](bool one_in_flight) {  // retire all but the newest step's loads
     if (!one_in_flight) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (nload == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if (nload == kW1XPW + 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(kW1XPW + 1) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(kW1XPW) : "memory");
   };
   auto barrier = [&]() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -878,14 +886,14 @@ __global__ __launch_bounds__(512) void k_conv1_wgrad(WgradArgs a) {
     const bool more = s + 2 < nsteps;
     const int win0 = w_begin + s * kW1Win;
     const int nw = min(kW1Win, w_end - win0);
-    const int kn = min(max(nw - 16 * hk, 0), 16);  // this wave's windows 16hk .. 16hk+kn-1
-    if (kn == 16) {  // every step but a chunk's last: unrolled, operands read ahead freely
+    const int kn = min(max(nw - kW1Half * hk, 0), kW1Half);  // this wave's windows
+    if (kn == kW1Half) {  // every step but a chunk's last: unrolled, operands read ahead freely
       // two windows of read-ahead, pinned: a window's LDS reads are issued two MFMA pairs
       // (256 pipe cycles) before their use
-      Ops q0 = ops(st, 16 * hk), q1 = ops(st, 16 * hk + 1);
+      Ops q0 = ops(st, kW1Half * hk), q1 = ops(st, kW1Half * hk + 1);
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const Ops q2 = ops(st, 16 * hk + (k < 14 ? k + 2 : 15));
+      for (int k = 0; k < kW1Half; ++k) {
+        const Ops q2 = ops(st, kW1Half * hk + (k < kW1Half - 2 ? k + 2 : kW1Half - 1));
         __builtin_amdgcn_sched_barrier(0);
         mma2(q0);
         __builtin_amdgcn_sched_barrier(0);
@@ -894,7 +902,7 @@ __global__ __launch_bounds__(512) void k_conv1_wgrad(WgradArgs a) {
         q1 = q2;
       }
     } else {  // a chunk's last step (never followed by loads)
-      for (int k = 0; k < kn; ++k) mma2(ops(st, 16 * hk + k));
+      for (int k = 0; k < kn; ++k) mma2(ops(st, kW1Half * hk + k));
     }
     if (do_bias) bias(st, win0, nw);
     wait_stage(more);
@@ -924,13 +932,13 @@ __global__ __launch_bounds__(512) void k_conv1_wgrad(WgradArgs a) {
       if (obase + ol < cout) wp[(size_t)(obase + ol) * kcn + kbase + kl] = acc[j] + red[ol * kW1Tile + kl];
     }
   }
-  if (do_bias && tid < kW1Tile && obase + tid < cout) {
+  if (do_bias && tid < NB * kW1Tile) {  // one (sum, channel) per thread, its 8 wave slots
+    const int e = tid / kW1Tile, c = tid - e * kW1Tile;
+    float v[8];
 #pragma unroll
-    for (int e = 0; e < NB; ++e) {
-      float v = 0.f;
-      for (int sl = 0; sl < 8; ++sl) v += bsum[(sl * NB + e) * kW1Tile + tid];
-      a.bpart[((size_t)chunk * NB + e) * cout + obase + tid] = v;
-    }
+    for (int sl = 0; sl < 8; ++sl) v[sl] = bsum[(sl * NB + e) * kW1Tile + c];
+    const float sum = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+    if (obase + c < cout) a.bpart[((size_t)chunk * NB + e) * cout + obase + c] = sum;
   }
 }
 
@@ -953,35 +961,44 @@ static int conv1_wgrad(const WgradArgs& a0, int nchunk, hipStream_t s) {
 }
 
 // BN1's backward through relu at the pooled positions: dx1[window][o] = a_o (g - kD sum_g - kD xhat
-// sum_gxhat), zero where the pooled activation is not positive; kD = copies(item) / N. One thread
-// per channel quad of a window.
+// sum_gxhat), zero where the pooled activation is not positive; kD = copies(item) / N. Grid-stride
+// over channel quads of windows; each block finalizes the per-channel sums once, into LDS.
 __global__ __launch_bounds__(256) void k_conv1_dx(WgradArgs a, float* __restrict__ dx1) {
   constexpr int LP = 33;
-  const int cq = a.cout / 4;
-  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (long)a.M * LP * cq) return;
-  const int o = 4 * (int)(e % cq);
-  const long win = e / cq;
-  const int item = (int)(win / LP);
-  const float kD = (a.counts ? a.counts[item] : 1.f) * a.invN;
-  const float4 g = ld4(a.g_l + win * a.cout + o), y = ld4(a.y_l + win * a.cout + o);
-  const float4 mu = ld4(a.mean_l + o), iv = ld4(a.invstd_l + o), av = ld4(a.a_l + o);
-  const float gv[4] = {g.x, g.y, g.z, g.w}, yv[4] = {y.x, y.y, y.z, y.w};
-  const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, i4[4] = {iv.x, iv.y, iv.z, iv.w}, a4[4] = {av.x, av.y, av.z, av.w};
-  float d[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const float sd = (float)acc_sum(a.dz_acc, a.cout, 0, o + s), sdx = (float)acc_sum(a.dz_acc, a.cout, 1, o + s);
-    const float xh = (yv[s] - m4[s]) * i4[s];
-    const float dx = a4[s] * (gv[s] - kD * sd - kD * xh * sdx);
-    d[s] = yv[s] > 0.f ? dx : 0.f;
+  __shared__ float s_sd[256], s_sdx[256];
+  for (int c = threadIdx.x; c < a.cout; c += blockDim.x) {
+    s_sd[c] = (float)acc_sum(a.dz_acc, a.cout, 0, c);
+    s_sdx[c] = (float)acc_sum(a.dz_acc, a.cout, 1, c);
   }
-  st4(dx1 + win * a.cout + o, make_float4(d[0], d[1], d[2], d[3]));
+  __syncthreads();
+  const int cq = a.cout / 4;
+  const long n = (long)a.M * LP * cq;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int o = 4 * (int)(e % cq);
+    const long win = e / cq;
+    const int item = (int)(win / LP);
+    const float kD = (a.counts ? a.counts[item] : 1.f) * a.invN;
+    const float4 g = ld4(a.g_l + win * a.cout + o), y = ld4(a.y_l + win * a.cout + o);
+    const float4 mu = ld4(a.mean_l + o), iv = ld4(a.invstd_l + o), av = ld4(a.a_l + o);
+    const float gv[4] = {g.x, g.y, g.z, g.w}, yv[4] = {y.x, y.y, y.z, y.w};
+    const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, i4[4] = {iv.x, iv.y, iv.z, iv.w};
+    const float a4[4] = {av.x, av.y, av.z, av.w};
+    float d[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float xh = (yv[s] - m4[s]) * i4[s];
+      const float dx = a4[s] * (gv[s] - kD * s_sd[o + s] - kD * xh * s_sdx[o + s]);
+      d[s] = yv[s] > 0.f ? dx : 0.f;
+    }
+    st4(dx1 + win * a.cout + o, make_float4(d[0], d[1], d[2], d[3]));
+  }
 }
 
 int launch_conv1_dx(const WgradArgs& a, float* dx1, hipStream_t s) {
+  if (a.cout > 256 || a.cout % 4) return DCUE_ERR_UNSUPPORTED;
   const long n = (long)a.M * 33 * (a.cout / 4);
-  DCUE_LAUNCH(k_conv1_dx, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, dx1);
+  const long blocks = (n + 255) / 256;
+  DCUE_LAUNCH(k_conv1_dx, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, s, a, dx1);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
@@ -999,36 +1016,37 @@ __global__ __launch_bounds__(256) void k_xhat0(const void* __restrict__ tracks, 
     s_is[threadIdx.x] = st.invstd;
   }
   __syncthreads();
-  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;  // float4 index
   const long n4 = (long)(M + 1) * kXp * (kMels / 4);  // item M: zeros
-  if (e >= n4) return;
-  const int c = 4 * (int)(e % (kMels / 4));
-  const long row = e / (kMels / 4);  // item * kXp + p
-  const long i = row / kXp;
-  const int t = (int)(row - i * kXp) - 2;
-  float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (t >= 0 && t < kFrames && i < M) {
-    const long src = ((long)item_track[i] * kFrames + t) * kMels + c;
-    float x[4];
-    if constexpr (SRC == SRC_TRACK_F16) {
-      const uint2 raw = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(tracks) + src);
-      const __half2 h0 = *reinterpret_cast<const __half2*>(&raw.x);
-      const __half2 h1 = *reinterpret_cast<const __half2*>(&raw.y);
-      x[0] = __low2float(h0); x[1] = __high2float(h0); x[2] = __low2float(h1); x[3] = __high2float(h1);
-    } else {
-      const float4 v = ld4(reinterpret_cast<const float*>(tracks) + src);
-      x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += (long)gridDim.x * blockDim.x) {
+    const int c = 4 * (int)(e % (kMels / 4));
+    const long row = e / (kMels / 4);  // item * kXp + p
+    const long i = row / kXp;
+    const int t = (int)(row - i * kXp) - 2;
+    float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t >= 0 && t < kFrames && i < M) {
+      const long src = ((long)item_track[i] * kFrames + t) * kMels + c;
+      float x[4];
+      if constexpr (SRC == SRC_TRACK_F16) {
+        const uint2 raw = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(tracks) + src);
+        const __half2 h0 = *reinterpret_cast<const __half2*>(&raw.x);
+        const __half2 h1 = *reinterpret_cast<const __half2*>(&raw.y);
+        x[0] = __low2float(h0); x[1] = __high2float(h0); x[2] = __low2float(h1); x[3] = __high2float(h1);
+      } else {
+        const float4 v = ld4(reinterpret_cast<const float*>(tracks) + src);
+        x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+      }
+      out = make_float4((x[0] - s_mu[c]) * s_is[c], (x[1] - s_mu[c + 1]) * s_is[c + 1],
+                        (x[2] - s_mu[c + 2]) * s_is[c + 2], (x[3] - s_mu[c + 3]) * s_is[c + 3]);
     }
-    out = make_float4((x[0] - s_mu[c]) * s_is[c], (x[1] - s_mu[c + 1]) * s_is[c + 1],
-                      (x[2] - s_mu[c + 2]) * s_is[c + 2], (x[3] - s_mu[c + 3]) * s_is[c + 3]);
+    st4(xhat0 + 4 * e, out);
   }
-  st4(xhat0 + 4 * e, out);
 }
 
 int launch_xhat0(int src, const void* tracks, const int32_t* item_track, int M, const unsigned long long* acc0,
                  double count, float* xhat0, hipStream_t s) {
   const long n4 = (long)(M + 1) * kXp * (kMels / 4);
-  const dim3 grid((unsigned)((n4 + 255) / 256));
+  const long blocks = (n4 + 255) / 256;
+  const dim3 grid((unsigned)(blocks < 2048 ? blocks : 2048));
   if (src == SRC_TRACK_F16)
     DCUE_LAUNCH(k_xhat0<SRC_TRACK_F16>, grid, dim3(256), 0, s, tracks, item_track, M, acc0, count, 1.0 / count, xhat0);
   else
@@ -1042,9 +1060,9 @@ int wgrad_nchunk(int layer, int M, int cout, int cin) {
   // blocks cost a write + a read of cout*ks*cin floats per chunk
   const LayerGeom gm = layer_geom(layer);
   const long rows = (long)M * gm.lp * gm.pool;
-  if (layer == 1) {  // k_conv1_wgrad: 64x64 tiles, >= 4 steps (64 windows) per chunk, <= ~256 workgroups
+  if (layer == 1) {  // k_conv1_wgrad: 64x64 tiles, >= 4 steps per chunk, <= ~512 workgroups (2 per CU)
     const long tiles1 = (4L * kMels / kW1Tile) * ((cout + kW1Tile - 1) / kW1Tile);
-    long n = 256 / tiles1;
+    long n = 512 / tiles1;
     const long wins = (long)M * gm.lp;
     if (n > (wins + 4 * kW1Win - 1) / (4 * kW1Win)) n = (wins + 4 * kW1Win - 1) / (4 * kW1Win);
     return (int)(n < 1 ? 1 : n);
