@@ -339,7 +339,7 @@ def main():
                                   args.interactions, "catalogue" if catalogue else "in-batch", N),
                    "batch_per_gpu": B, "global_batch": B * world, "neg": N,
                    "parallelism": "dp%d (users sharded, dense grads all-reduced)" % world},
-        "roofline": {"kernel": "k_conv1_wgrad (conv layer 1 weight gradient, f32 MFMA 16x16x4)", "bound": "mfma",
+        "roofline": {"kernel": "k_conv1_wgrad (conv layer 1 weight gradient, f32 MFMA 32x32x2)", "bound": "mfma",
                      "achieved": achieved, "peak": 157.3, "unit": "TFLOP/s", "frac": achieved / 157.3,
                      "traffic": traffic, "avg_ms": wg_ms, "launches": wg_n, "algorithmic_flops": wg_flops},
     }
