@@ -12,6 +12,7 @@ template <int SRC>
 __global__ __launch_bounds__(256) void k_input_stats(const void* tracks, const int32_t* item_track,
                                                      const float* counts, int M, int rows_per_blk,
                                                      unsigned long long* acc) {
+  critical_path_priority();
   __shared__ float red[8][2][kMels];
   const int q = threadIdx.x & 31, slot = threadIdx.x >> 5;
   const long rows = (long)M * kFrames;

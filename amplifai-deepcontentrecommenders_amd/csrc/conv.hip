@@ -155,6 +155,7 @@ constexpr int kRowsWaves = 8, kRowsThreads = 64 * kRowsWaves, kRowsCT = 128 / (1
 template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,
           int POOLL>
 __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
+  critical_path_priority();
   constexpr int RX = R + KS - 1;
   constexpr int ROWS = TW * 16;
   constexpr int MAXI = (ROWS + R - 1) / R + 1;
@@ -764,6 +765,7 @@ __device__ __forceinline__ void glds16(const void* g, float* l) {
 }
 
 __global__ __launch_bounds__(512, 2) void k_conv1_wgrad(WgradArgs a) {
+  critical_path_priority();
   constexpr int R = 132, LP = 33, NB = 5;
   static_assert(kW1Win % 16 == 0 && kW1DW + kW1AW <= 8, "load assignment");
   extern __shared__ __attribute__((aligned(16))) float lds[];  // the only LDS object: a second
@@ -964,6 +966,7 @@ static int conv1_wgrad(const WgradArgs& a0, int nchunk, hipStream_t s) {
 // sum_gxhat), zero where the pooled activation is not positive; kD = copies(item) / N. Grid-stride
 // over channel quads of windows; each block finalizes the per-channel sums once, into LDS.
 __global__ __launch_bounds__(256) void k_conv1_dx(WgradArgs a, float* __restrict__ dx1) {
+  critical_path_priority();
   constexpr int LP = 33;
   __shared__ float s_sd[256], s_sdx[256];
   for (int c = threadIdx.x; c < a.cout; c += blockDim.x) {
@@ -1149,6 +1152,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
                                                       const float* __restrict__ bpart, int nchunk,
                                                       int cout, int cin, int ks, int nb, float* dW,
                                                       float* db, float* G, float* S) {
+  critical_path_priority();
   __shared__ float4 red[kRedGroups][32];
   const int col = threadIdx.x & 31, grp = threadIdx.x >> 5;
   const long kcn = (long)ks * cin;
@@ -1199,6 +1203,7 @@ __global__ __launch_bounds__(256) void k_bn0_grads(const float* __restrict__ G, 
                                                    const float* __restrict__ W1, const float* gamma0,
                                                    const float* beta0, int H, float* dW1,
                                                    float* dgamma0, float* dbeta0, float* db1) {
+  critical_path_priority();
   // E = the five layer-1 bias-partial sums [5][H]: sum dz1 and its parts at t = 0, 1, R-2, R-1.
   // Tap k of conv row t reads input t+k-2 (zero padding at t+k-2 < 0 or > 130), so
   //   S[0] = e0-e1-e2, S[1] = e0-e1, S[2] = e0-e4, S[3] = e0-e3-e4;  db1 = e0.

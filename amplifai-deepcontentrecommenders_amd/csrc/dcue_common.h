@@ -77,6 +77,11 @@ __host__ __device__ constexpr LayerGeom layer_geom(int l) {
 
 // v_mfma_f32_16x16x4_f32: A lane l = A[l&15][l>>4], B lane l = B[l>>4][l&15],
 // D lane l, reg r = D[4*(l>>4)+r][l&15]. Exact f32 products, k-ordered f32 accumulation.
+// Critical-path kernels raise their waves' issue priority: the off-path work that shares the CUs
+// with them (the user table's rolling Adam flush, side-stream weight gradients, next-step draws)
+// then takes the issue slots they leave, instead of stretching the step's chain.
+__device__ __forceinline__ void critical_path_priority() { __builtin_amdgcn_s_setprio(2); }
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }

@@ -60,6 +60,7 @@ constexpr int kTgKC = 128;
 // unconditionally (no per-element branch), row gathers resolved before the data loads.
 template <int TA, int TB, int AKF, int BNF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_tgemm(TGemmArgs g) {
+  critical_path_priority();
   __shared__ float As[kTgKC][16];
   __shared__ float Bs[kTgKC][80];
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
@@ -298,6 +299,7 @@ __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ u
                                                      float margin, float* scores, float* cosv,
                                                      float* norms, float* rowsum, float* dU,
                                                      float* dfcopy) {
+  critical_path_priority();
   constexpr int CMAX = CPW > 0 ? 4 * CPW : 1025;
   __shared__ float cs[CMAX], dcs[CMAX], hs[CMAX];
   __shared__ float gus[4][256];
@@ -532,6 +534,7 @@ constexpr int kItemGradWLds = 128;  // W staged in LDS up to d = 128 (64 KB)
 template <bool WLDS>
 __global__ __launch_bounds__(256) void k_item_grad(const float* __restrict__ dfcopy, dcue_batch b, int d,
                                                    float* df, ItemGradFc fc) {
+  critical_path_priority();
   constexpr int kCap = kItemGradCap;
   __shared__ int list[kCap];      // per-wave hit lists, kCap / 4 each
   __shared__ int lst[kCap + 1];   // the item's copies in order
