@@ -740,8 +740,8 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
 // a = (argmax[window][o] == row & 3) ? dx1[window][o] : 0.
 // Workgroup = a 64 (o) x 64 (kc) output tile x one chunk of pool windows, 8 waves: wave w owns the
 // (w>>1 & 1, w & 1) 32x32 quarter over half of each step's 32 windows (w >> 2), two
-// v_mfma_f32_32x32x2_f32 per window. The three LDS stages are filled by global_load_lds_dwordx4
-// (no register staging): step s+2's loads are issued behind step s's first MFMAs and retired by a
+// v_mfma_f32_32x32x2_f32 per window. The LDS stages are filled by global_load_lds_dwordx4
+// (no register staging): step s+PD's loads are issued behind step s's first MFMAs and retired by a
 // counted vmcnt before the raw barrier that ends step s+1; a window's LDS operands are read one
 // window ahead of its MFMAs. In the bias workgroups (kc tile 0) the waves also sum dx1 per channel
 // -- all rows and the four edge positions t = 0, 1, 130, 131.
@@ -755,7 +755,18 @@ constexpr int kW1XF = kW1Win * 4 * kW1Tile;      // x stage: [128 rows][64 kc] f
 constexpr int kW1DF = kW1Win * kW1Tile;          // dx1 stage: [32 windows][64 o]
 constexpr int kW1AF = kW1Win * kW1Tile / 4;      // argmax stage: [32 windows][64 o] bytes
 constexpr int kW1StageF = kW1XF + kW1DF + kW1AF; // 5376 floats = 21 KB: two workgroups per CU
-constexpr int kW1Stages = 3;
+#ifndef DCUE_W1_STAGES
+#define DCUE_W1_STAGES 2
+#endif
+#ifndef DCUE_W1_WGS
+#define DCUE_W1_WGS 2
+#endif
+// LDS stages; loads run kW1Stages - 1 steps ahead. Measured at two workgroups per CU, two stages
+// (42 KB) match three (catalogue 271 vs 277 us, in-batch 22.6 vs 25.1 us) and leave LDS to the
+// kernels that run beside it; workgroup counts of 768 or 1024 gain nothing over 512.
+constexpr int kW1Stages = DCUE_W1_STAGES;
+constexpr int kW1PD = kW1Stages - 1;
+static_assert(kW1PD >= 1 && kW1PD <= 2, "wait_stage counts one or two steps in flight");
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -764,7 +775,7 @@ __device__ __forceinline__ void glds16(const void* g, float* l) {
   __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)l, 16, 0, 0);
 }
 
-__global__ __launch_bounds__(512, 2) void k_conv1_wgrad(WgradArgs a) {
+__global__ __launch_bounds__(512, DCUE_W1_WGS) void k_conv1_wgrad(WgradArgs a) {
   critical_path_priority();
   constexpr int R = 132, LP = 33, NB = 5;
   static_assert(kW1Win % 16 == 0 && kW1DW + kW1AW <= 8, "load assignment");
@@ -876,16 +887,16 @@ __global__ __launch_bounds__(512, 2) void k_conv1_wgrad(WgradArgs a) {
     }
   };
 
-  // Pipeline over stages step % 3: step s+2 goes into the stage step s-1 read (every wave's reads
-  // of it retired before the barrier that ended step s-1); the wait ending step s retires step
-  // s+1's loads (each wave its own, the barrier then publishes them to all).
-  if (nsteps > 0) issue(0);
-  if (nsteps > 1) issue(1);
-  wait_stage(nsteps > 1);
+  // Pipeline over stages step % kW1Stages, PD = kW1Stages - 1 steps ahead: step s+PD goes into the
+  // stage step s-1 read (every wave's reads of it retired before the barrier that ended step s-1);
+  // the wait ending step s retires step s+1's loads (each wave its own, the barrier then publishes
+  // them to all).
+  for (int q = 0; q < kW1PD && q < nsteps; ++q) issue(q);
+  wait_stage(kW1PD > 1 && nsteps > 1);
   barrier();
   for (int s = 0; s < nsteps; ++s) {
     const float* st = lds + (s % kW1Stages) * kW1StageF;
-    const bool more = s + 2 < nsteps;
+    const bool more = s + kW1PD < nsteps;
     const int win0 = w_begin + s * kW1Win;
     const int nw = min(kW1Win, w_end - win0);
     const int kn = min(max(nw - kW1Half * hk, 0), kW1Half);  // this wave's windows
@@ -899,7 +910,7 @@ __global__ __launch_bounds__(512, 2) void k_conv1_wgrad(WgradArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         mma2(q0);
         __builtin_amdgcn_sched_barrier(0);
-        if (k == 0 && more) issue(s + 2);  // behind the first MFMAs: the pipe stays fed
+        if (k == 0 && more) issue(s + kW1PD);  // behind the first MFMAs: the pipe stays fed
         q0 = q1;
         q1 = q2;
       }
@@ -907,7 +918,7 @@ __global__ __launch_bounds__(512, 2) void k_conv1_wgrad(WgradArgs a) {
       for (int k = 0; k < kn; ++k) mma2(ops(st, kW1Half * hk + k));
     }
     if (do_bias) bias(st, win0, nw);
-    wait_stage(more);
+    wait_stage(kW1PD > 1 && more);
     barrier();
   }
 
