@@ -248,3 +248,49 @@ def test_catalogue_sampler(golden):
                                               nat.ptr(rk), nat.ptr(us), us.numel(), N, nat.ptr(out),
                                               nat.stream_handle()), "catalogue stream")
     assert np.array_equal(out.cpu().numpy(), g["stream"])
+
+
+def test_catalogue_sampler_groups_and_long_lists():
+    """The global-stream sampler stages rank lists in LDS per group of samples: cover several
+    groups, a list longer than the LDS stage (scanned in global memory), a user with one candidate
+    (bounded draw over [0, 0]) and users with no split items, against the C MT19937 oracle
+    (the algorithm of datasets/dcuedataset.py:207-220 on numpy's stream)."""
+    from dcrecommend import _native as nat
+    from dcrecommend.datasets.csr import user_split_ranks
+    from oracle import mt19937 as MT
+    rs = np.random.RandomState(5)
+    n_songs, n_users, N = 12000, 300, 20
+    split = np.sort(rs.choice(n_songs, 10000, replace=False)).astype(np.int64)
+    pairs = [(0, int(x)) for x in rs.choice(split, 9000, replace=False)]  # > the 8192-rank stage
+    pairs += [(1, int(x)) for x in split[1:]]                              # one candidate left
+    for u in range(3, n_users):                                            # user 2: none
+        pairs += [(u, int(x)) for x in rs.choice(n_songs, rs.randint(0, 60), replace=False)]
+    uidx = np.array([p[0] for p in pairs], dtype=np.int64)
+    sidx = np.array([p[1] for p in pairs], dtype=np.int64)
+    order = np.lexsort((sidx, uidx))
+    uidx, sidx = uidx[order], sidx[order]
+    indptr_items = np.zeros(n_users + 1, dtype=np.int64)
+    np.add.at(indptr_items, uidx + 1, 1)
+    indptr_items = np.cumsum(indptr_items)
+    users_seq = rs.randint(0, n_users, 700).astype(np.int64)
+    users_seq[[3, 250, 251, 600]] = [0, 1, 0, 2]
+    want = MT.catalogue(77, False, split, indptr_items, sidx, users_seq, N)
+    indptr, ranks = user_split_ranks(uidx, sidx, n_users, split)
+    dev = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dt).to(DEV)  # noqa: E731
+    sp, ip, rk, us = (dev(split, torch.int64), dev(indptr, torch.int64), dev(ranks, torch.int32),
+                      dev(users_seq, torch.int64))
+    st = _mt_state(77)
+    out = torch.empty((len(users_seq), N), dtype=torch.int64, device=DEV)
+    nat.check(nat.lib().dcue_sample_catalogue(nat.ptr(st), 0, 0, nat.ptr(sp), sp.numel(), nat.ptr(ip),
+                                              nat.ptr(rk), nat.ptr(us), us.numel(), N, nat.ptr(out),
+                                              nat.stream_handle()), "catalogue stream")
+    assert np.array_equal(out.cpu().numpy(), want)
+    # the stream continues where the oracle's does: the next call equals its next samples
+    nxt = rs.randint(3, n_users, 50).astype(np.int64)
+    both = MT.catalogue(77, False, split, indptr_items, sidx, np.concatenate([users_seq, nxt]), N)
+    us2 = dev(nxt, torch.int64)
+    out2 = torch.empty((len(nxt), N), dtype=torch.int64, device=DEV)
+    nat.check(nat.lib().dcue_sample_catalogue(nat.ptr(st), 0, 0, nat.ptr(sp), sp.numel(), nat.ptr(ip),
+                                              nat.ptr(rk), nat.ptr(us2), us2.numel(), N, nat.ptr(out2),
+                                              nat.stream_handle()), "catalogue stream 2")
+    assert np.array_equal(out2.cpu().numpy(), both[len(users_seq):])
