@@ -20,4 +20,9 @@ for c in FETCH_SIZE WRITE_SIZE; do
     -d "$OUT/pmc_$c" -o run -- python3 $ROOT/bench.py --no-cpu-baseline --no-eval --steps 40 --warmup 5 \
     > "$OUT/pmc_$c.log" 2>&1
 done
+# catalogue mode (M = B(1+N) distinct items per step): kernel stats only
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/stats_cat" -o run -- python3 $ROOT/bench.py \
+  --mode catalogue --no-cpu-baseline --no-eval --steps 40 --warmup 5 > "$OUT/stats_cat.log" 2>&1
+cp "$OUT/stats_cat/run_kernel_stats.csv" "$OUT/${TAG}_cat_kernel_stats.csv"
+grep '^{' "$OUT/stats_cat.log" | tail -n 1 > "$OUT/${TAG}_cat_bench.json"
 python3 "$ROOT/profiles/summarize_pmc.py" "$OUT" "$TAG"
