@@ -303,6 +303,13 @@ extern "C" int dcue_plan_step(dcue_plan* p, const int64_t* users_src, const int3
   return r;
 }
 
+extern "C" int dcue_plan_wait_side(dcue_plan* p, void* stream) {
+  if (!p || p->exec || p->launches == 0 || !p->tails[1]) return DCUE_ERR_INVALID;
+  // tails[1]: wgrad stream 0 after it joined the user stream's and wgrad stream 1's tails
+  DCUE_HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream, p->tails[1], 0));
+  return DCUE_OK;
+}
+
 extern "C" int dcue_plan_destroy(dcue_plan* p) {
   if (!p) return DCUE_OK;
   if (p->exec) (void)hipGraphExecDestroy(p->exec);

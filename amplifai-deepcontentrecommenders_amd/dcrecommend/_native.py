@@ -16,6 +16,7 @@ N_MELS = 128
 N_FRAMES = 131
 N_BN = 6
 N_DENSE_SEGMENTS = 28
+SEG_LATE = 6  # DCUE_SEG_LATE: bn0, conv layer 1, bn1 come first in the flat layout
 LAYOUT_CATALOGUE = 0
 LAYOUT_GATHER = 1
 
@@ -79,7 +80,7 @@ class PlanConfig(ctypes.Structure):
 
 MT_STATE_BYTES = 624 * 4 + 16
 MAX_LOG_CAP = 256
-ABI_VERSION = 3
+ABI_VERSION = 4
 RANK_SPLIT, RANK_SINGLE = 0, 1
 
 _P = ctypes.c_void_p
@@ -119,6 +120,7 @@ _SIGS = {
     "dcue_plan_launch": ([_P, _P, _P, _P], ctypes.c_int),
     "dcue_plan_destroy": ([_P], ctypes.c_int),
     "dcue_plan_step": ([_P, _P, _P, ctypes.POINTER(AdamArgs), _P], ctypes.c_int),
+    "dcue_plan_wait_side": ([_P, _P], ctypes.c_int),
     "dcue_timer_enable": ([ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
     "dcue_timer_read": ([ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)],
                         ctypes.c_int),

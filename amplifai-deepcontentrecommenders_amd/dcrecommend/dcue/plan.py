@@ -114,6 +114,15 @@ class TrainPlan:
         if st != 0:
             nat.check(st, "dcue_plan_step")
 
+    def wait_side(self, stream):
+        """`stream` (a torch.cuda.Stream or raw handle) waits until the side-stream part of the last
+        launched step is in: the flat gradient is then final past its first SEG_LATE segments
+        (include/dcue.h dcue_plan_wait_side)."""
+        if self._handle is None:
+            raise RuntimeError("TrainPlan was closed")
+        h = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        nat.check(self._lib.dcue_plan_wait_side(self._handle, h), "dcue_plan_wait_side")
+
     def close(self):
         if getattr(self, "_handle", None) is not None:
             torch.cuda.synchronize()

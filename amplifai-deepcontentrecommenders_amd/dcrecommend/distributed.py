@@ -41,6 +41,47 @@ def allreduce_mean_(grad, group=None):
     return grad
 
 
+def late_grad_floats(net):
+    """Floats at the head of the flat gradient that the step's end writes (bn0, conv layer 1, bn1:
+    segments [0, SEG_LATE) of the reference order); everything after is final once the plan's side
+    streams are in."""
+    from . import _native as nat
+    dims = nat.make_dims(net.conv_hidden, net.feature_dim, net.user_embdim, net.user_count)
+    return nat.param_layout(dims)[nat.SEG_LATE]
+
+
+_COMM_STREAMS = {}
+
+
+def allreduce_mean_overlapped_(plan, grad, late, group=None):
+    """In-place mean over the ranks of the flat gradient of the step `plan` last launched, in two
+    buckets. grad[late:] -- every gradient but bn0/conv1/bn1 -- is all-reduced as soon as the
+    plan's side streams are in, from a stream of its own, so it overlaps the step's conv-1 weight
+    gradient on the caller's stream; grad[:late] follows after the step's end. The caller's stream
+    then waits for both (RCCL runs them in issue order on the process group's stream). On CPU
+    tensors (gloo tests) the buckets run in order."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return grad
+    if grad.is_cuda:
+        dev = grad.device
+        comm = _COMM_STREAMS.get(dev)
+        if comm is None:
+            comm = _COMM_STREAMS[dev] = torch.cuda.Stream(device=dev)
+        plan.wait_side(comm)
+        with torch.cuda.stream(comm):
+            w_early = dist.all_reduce(grad[late:], group=group, async_op=True)
+        w_late = dist.all_reduce(grad[:late], group=group, async_op=True)
+        w_early.wait()
+        w_late.wait()
+    else:
+        plan.wait_side(None)
+        dist.all_reduce(grad[late:], group=group)
+        dist.all_reduce(grad[:late], group=group)
+    grad.div_(world)
+    return grad
+
+
 def max_over_ranks(value, device, group=None):
     """Max of a host scalar over the ranks (bench timing: the slowest rank defines the step)."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:

@@ -176,10 +176,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; DCUE_DIST_BACKEND=gloo rehearses the N>1 path with several ranks on one
+    # GPU (local ranks wrap over the visible devices), RCCL ("nccl") otherwise
+    backend = os.environ.get("DCUE_DIST_BACKEND", "nccl")
+    local = local % torch.cuda.device_count() if backend != "nccl" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from dcrecommend import _native as nat
     from dcrecommend import distributed as D
@@ -224,6 +231,7 @@ def main():
     mt = torch.empty(nat.MT_STATE_BYTES, dtype=torch.uint8, device=dev)
     nat.check(nat.lib().dcue_mt_seed(nat.ptr(mt), 10 + rank, nat.stream_handle()), "mt_seed")
     G = net._flat["G"]
+    G_late = D.late_grad_floats(net)
     TIMED = nat.TIMED_CONV1_WGRAD  # the roofline kernel, timed live by HIP events in the library
     TIMER_STRIDE = 8
 
@@ -265,7 +273,9 @@ def main():
             src = (users_b[s], items_b[s])
         if world > 1:
             plan.launch(*src)
-            D.allreduce_mean_(G)  # RCCL: the one exchange of the step (1.57 MB)
+            # RCCL: the one exchange of the step (1.57 MB), in two buckets; the larger one overlaps
+            # the conv-1 weight gradient
+            D.allreduce_mean_overlapped_(plan, G, G_late)
             opt.step()
         else:
             plan.step(*src)  # sample + forward + backward + Adam, one host call

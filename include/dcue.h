@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DCUE_ABI_VERSION 3
+#define DCUE_ABI_VERSION 4
 #define DCUE_N_MELS 128
 #define DCUE_N_FRAMES 131
 #define DCUE_N_BN 6
@@ -250,6 +250,14 @@ int dcue_plan_launch(dcue_plan* plan, const int64_t* users_src, const int32_t* i
  * so launch and dcue_adam_step are issued separately). */
 int dcue_plan_step(dcue_plan* plan, const int64_t* users_src, const int32_t* item_track_src,
                    const dcue_adam_args* adam, void* stream);
+/* Data-parallel overlap (row e): `stream` waits until every side-stream part of the plan's last
+ * launched step is in. From then on the flat gradient buffer is final except its first
+ * DCUE_SEG_LATE segments (bn0, conv layer 1, bn1: written by the caller's stream at the step's end),
+ * so an all-reduce of the rest issued on `stream` overlaps the conv-1 weight gradient. Eager plans
+ * only (DCUE_ERR_INVALID for a graph plan or before the first launch). Replaces the single
+ * post-backward all-reduce of the DDP-style loop (nn/dcue.py:208-209 under data parallelism). */
+#define DCUE_SEG_LATE 6
+int dcue_plan_wait_side(dcue_plan* plan, void* stream);
 int dcue_plan_destroy(dcue_plan* plan);
 
 /* ------------------------------------------------------------------- live kernel timing */

@@ -38,6 +38,15 @@ def _worker(rank, world, port, out_dir):
         # replicated dense grad: every rank holds its own, the mean comes back everywhere
         g = torch.arange(8, dtype=torch.float32) * (rank + 1)
         D.allreduce_mean_(g)
+        # the bucketed exchange (CPU branch: buckets in order) gives the same mean
+        class _Plan:
+            waits = 0
+
+            def wait_side(self, stream):
+                _Plan.waits += 1
+        g2 = torch.arange(8, dtype=torch.float32) * (rank + 1)
+        D.allreduce_mean_overlapped_(_Plan(), g2, 3)
+        assert torch.equal(g2, g) and _Plan.waits == 1
         t = D.max_over_ranks(1.5 + rank, torch.device("cpu"))
         torch.save({"glob": glob, "items": li, "g": g, "t": t}, os.path.join(out_dir, "r%d.pt" % rank))
     finally:
