@@ -13,6 +13,9 @@ mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 BENCH="$ROOT/bench.py --no-cpu-baseline --steps 200 --warmup 20"
+# the same command without the profiler: its live roofline timing is the one bench.py reports
+(cd "$ROOT" && timeout -k 10 240 python3 $BENCH > "$OUT/plain.log" 2>&1)
+grep '^{' "$OUT/plain.log" | tail -n 1 > "$OUT/${TAG}_bench_plain.json"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/stats" -o run -- python3 $BENCH \
   > "$OUT/stats.log" 2>&1
 for c in FETCH_SIZE WRITE_SIZE; do
