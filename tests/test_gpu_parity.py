@@ -112,6 +112,45 @@ def test_module_forward_backward(golden, name):
     _check_params_after_adam(net, g, "step2.", 2 * lr, skip_rows=np.unique(g["u"]))
 
 
+@pytest.mark.parametrize("H,d", [(64, 64), (256, 128), (128, 256)])
+def test_widths_against_oracle(H, d):
+    """conv_hidden / feature_dim the golden fixtures do not cover (they hold 32 and 128): one train
+    step's scores, loss and every dense gradient against the CPU oracle (oracle/dcue_oracle.py, the
+    reference step restated). Covers the conv-1 weight gradient's output tiling (one, two or four
+    64-channel o tiles) and the 256-wide fc/score paths. Tolerance as test_module_forward_backward."""
+    from dcrecommend.dcue.dcue import DCUENet
+    from oracle import dcue_oracle as O
+    n_users, B, N = 7, 4, 3
+    torch.manual_seed(1)
+    net = DCUENet({"feature_dim": d, "conv_hidden": H, "user_embdim": 40, "user_count": n_users,
+                   "model_type": "truedcuemel1dbn"})
+    torch.manual_seed(1)
+    p, b = O.init_params(d, H, 40, n_users)
+    net = net.to(DEV).train()
+    gen = torch.Generator().manual_seed(4)
+    u = torch.randint(0, n_users, (B,), generator=gen)
+    pos = torch.randn(B, 128, 131, generator=gen).half().float()
+    neg = torch.randn(B, N, 128, 131, generator=gen).half().float()
+    scores, _, _, _ = net(u.to(DEV), pos.to(DEV), neg.to(DEV))
+    loss = torch.max(torch.zeros_like(scores), 0.2 - scores).sum(dim=1).mean()
+    loss.backward()
+    torch.cuda.synchronize()
+    ref_loss, grads, (rs, _, _, _) = O.loss_and_grads(p, b, u, pos, neg)
+    assert float((scores.detach().cpu() - rs).abs().max()) <= 1e-4 * float(rs.abs().max()) + 1e-6
+    assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-4 * abs(float(ref_loss)) + 1e-7
+    named = dict(net.named_parameters())
+    for k, g_ref in grads.items():
+        if k not in named or named[k].grad is None:
+            continue
+        g = named[k].grad.detach().cpu()
+        scale = float(g_ref.abs().max())
+        if scale == 0.0:
+            assert float(g.abs().max()) < 1e-6, k
+            continue
+        assert float((g - g_ref).abs().max()) <= 1e-3 * scale, "%s: %.3e" % (
+            k, float((g - g_ref).abs().max()) / scale)
+
+
 def test_eval_forward(golden):
     g = golden("model_tiny.npz")
     net = _net(g, int(g["seed"]))
