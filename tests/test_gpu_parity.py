@@ -289,7 +289,8 @@ def test_catalogue_sampler(golden):
     assert np.array_equal(out.cpu().numpy(), g["stream"])
 
 
-def test_catalogue_sampler_groups_and_long_lists():
+@pytest.mark.parametrize("N", [20, 1, 300])
+def test_catalogue_sampler_groups_and_long_lists(N):
     """The global-stream sampler stages rank lists in LDS per group of samples: cover several
     groups, a list longer than the LDS stage (scanned in global memory), a user with one candidate
     (bounded draw over [0, 0]) and users with no split items, against the C MT19937 oracle
@@ -298,7 +299,7 @@ def test_catalogue_sampler_groups_and_long_lists():
     from dcrecommend.datasets.csr import user_split_ranks
     from oracle import mt19937 as MT
     rs = np.random.RandomState(5)
-    n_songs, n_users, N = 12000, 300, 20
+    n_songs, n_users = 12000, 300
     split = np.sort(rs.choice(n_songs, 10000, replace=False)).astype(np.int64)
     pairs = [(0, int(x)) for x in rs.choice(split, 9000, replace=False)]  # > the 8192-rank stage
     pairs += [(1, int(x)) for x in split[1:]]                              # one candidate left
