@@ -55,6 +55,25 @@ __device__ __forceinline__ void adam_replay(float& p, float& m, float& v, const 
     adam_elem(p, gz, m, v, s);
 }
 
+// (m, v) = (+0, +0) is a fixed point of the zero-gradient step without weight decay (adam_zero_elem:
+// m - w*0 = +0, v*b2 = +0, sqrt(0)/bc2 = 0, denom = eps, p + (-lr_bc1)*(0/eps) = p + (-0) = p,
+// signed zeros included): a user row never in a batch needs no replay, bit for bit what the dense
+// sweep computes. The replay kernels skip such elements (no loads of p, no stores).
+__device__ __forceinline__ bool idle_moments(float m, float v) {
+  return (__float_as_uint(m) | __float_as_uint(v)) == 0u;
+}
+__device__ __forceinline__ bool idle_moments4(const float4& m, const float4& v) {
+  return (__float_as_uint(m.x) | __float_as_uint(m.y) | __float_as_uint(m.z) | __float_as_uint(m.w) |
+          __float_as_uint(v.x) | __float_as_uint(v.y) | __float_as_uint(v.z) | __float_as_uint(v.w)) == 0u;
+}
+// whether every replayed step of [j0, j1] (history slots j % cap, or j - base) is free of weight decay
+__device__ __forceinline__ bool no_decay(const AdamScalars* hs, int j0, int j1, int cap, float gz, int base) {
+  if (gz != 0.f) return false;
+  for (int j = j0; j <= j1; ++j)
+    if (hs[base >= 0 ? j - base : j % cap].wd != 0.f) return false;
+  return true;
+}
+
 struct PackSeg {
   long src, fwd, bwd;  // floats: W in params; forward pack; dgrad pack (-1: none)
   int cout, cin, ks;
@@ -189,13 +208,16 @@ __global__ __launch_bounds__(1024) void k_emb_sync(float* __restrict__ p, float*
   const AdamScalars* hist = log_hist(hdr);
   for (int j = from + 1 + (int)threadIdx.x; j <= T; j += blockDim.x) hs[j % cap] = hist[j % cap];
   __syncthreads();
+  const bool nd = no_decay(hs, from + 1, T, cap, gz, -1);
   float* pr = p + u * E;
   float* mr = m + u * E;
   float* vr = v + u * E;
   // one element per thread: each element's replay is a dependent chain of VALU-bound steps, so the
   // row is spread over as many lanes as it has elements (launch: blockDim >= E)
   for (int k = threadIdx.x; k < E; k += blockDim.x) {
-    float pp = pr[k], mm = mr[k], vv = vr[k];
+    float mm = mr[k], vv = vr[k];
+    if (nd && idle_moments(mm, vv)) continue;  // fixed point (idle_moments)
+    float pp = pr[k];
     for (int j = from + 1; j <= T; ++j) adam_replay(pp, mm, vv, hs[j % cap], gz);
     pr[k] = pp; mr[k] = mm; vr[k] = vv;
   }
@@ -218,13 +240,16 @@ __global__ __launch_bounds__(256) void k_emb_flush(float* __restrict__ p, float*
   const AdamScalars* hist = log_hist(const_cast<dcue_emb_log*>(hdr));
   for (int j = F + 1 + (int)threadIdx.x; j <= T; j += blockDim.x) hs[j - F - 1] = hist[j % cap];
   __syncthreads();
+  const bool nd = no_decay(hs, F + 1, T, cap, gz, F + 1);
   const long stride = (long)gridDim.x * blockDim.x;
   if ((E & 3) == 0) {
     const int E4 = E >> 2;
     const long n4 = n_rows * E4;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
       const int from = max(emb_step[i / E4], F);
-      float4 pp = ld4(p + 4 * i), mm = ld4(m + 4 * i), vv = ld4(v + 4 * i);
+      float4 mm = ld4(m + 4 * i), vv = ld4(v + 4 * i);
+      if (nd && idle_moments4(mm, vv)) continue;  // fixed point (idle_moments)
+      float4 pp = ld4(p + 4 * i);
       for (int j = F + 1; j <= T; ++j) {
         if (j <= from) continue;
         const AdamScalars s = hs[j - F - 1];
@@ -239,7 +264,9 @@ __global__ __launch_bounds__(256) void k_emb_flush(float* __restrict__ p, float*
     const long n = n_rows * E;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
       const int from = max(emb_step[i / E], F);
-      float pp = p[i], mm = m[i], vv = v[i];
+      float mm = m[i], vv = v[i];
+      if (nd && idle_moments(mm, vv)) continue;
+      float pp = p[i];
       for (int j = F + 1; j <= T; ++j)
         if (j > from) adam_replay(pp, mm, vv, hs[j - F - 1], gz);
       p[i] = pp; m[i] = mm; v[i] = vv;
@@ -268,12 +295,15 @@ __global__ __launch_bounds__(256) void k_emb_flush_rows(float* __restrict__ p, f
   for (int j = lo + (int)threadIdx.x; j <= T; j += blockDim.x) hs[j % cap] = hist[j % cap];
   for (int i = threadIdx.x; i < nr; i += blockDim.x) from_s[i] = max(emb_step[rb + i], F);
   __syncthreads();
+  const bool nd = no_decay(hs, lo, T, cap, gz, -1);
   if ((E & 3) == 0) {
     const int E4 = E >> 2;
     for (int e = threadIdx.x; e < nr * E4; e += blockDim.x) {
       const int i = e / E4;
       const long off = (rb + i) * E + 4 * (e - i * E4);
-      float4 pp = ld4(p + off), mm = ld4(m + off), vv = ld4(v + off);
+      float4 mm = ld4(m + off), vv = ld4(v + off);
+      if (nd && idle_moments4(mm, vv)) continue;  // fixed point (idle_moments)
+      float4 pp = ld4(p + off);
       for (int j = from_s[i] + 1; j <= T; ++j) {
         const AdamScalars s = hs[j % cap];
         adam_replay(pp.x, mm.x, vv.x, s, gz);
@@ -287,7 +317,9 @@ __global__ __launch_bounds__(256) void k_emb_flush_rows(float* __restrict__ p, f
     for (int e = threadIdx.x; e < nr * E; e += blockDim.x) {
       const int i = e / E;
       const long off = (rb + i) * E + (e - i * E);
-      float pp = p[off], mm = m[off], vv = v[off];
+      float mm = m[off], vv = v[off];
+      if (nd && idle_moments(mm, vv)) continue;
+      float pp = p[off];
       for (int j = from_s[i] + 1; j <= T; ++j) adam_replay(pp, mm, vv, hs[j % cap], gz);
       p[off] = pp; m[off] = mm; v[off] = vv;
     }
