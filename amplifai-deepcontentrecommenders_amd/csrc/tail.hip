@@ -83,8 +83,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   }
   // B columns: BNF -> column t&63 (fixed), k = (t>>6)+4j; else columns (t>>7)+2j, k = t&127 (fixed)
   const long bcol0 = (long)min(nb0 + (BNF ? (t & 63) : (t >> 7)), g.N - 1) * g.sbn;
-  for (int k0 = 0; k0 < g.K; k0 += kTgKC) {
-    float ra[NA], rb[NB];
+  // register-staged K chunks: chunk k0 + kTgKC's loads are issued right after chunk k0 is in LDS,
+  // so they fly during its MFMAs (one load latency per GEMM instead of one per chunk)
+  float ra[NA], rb[NB];
+  auto load = [&](int k0) {
     long brk[BNF ? NB : 1];
 #pragma unroll
     for (int j = 0; j < (BNF ? NB : 1); ++j) {
@@ -107,33 +109,62 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         rb[j] = bp[(long)nc * g.sbn];
       }
     }
+  };
+  load(0);
+  for (int k0 = 0; k0 < g.K; k0 += kTgKC) {
+    // TA == 2 / TB == 2 affine operands, per column: gathered before the conversion loops (their
+    // loads issued together; the acc-finalize branch is uniform, hoisted out of the loop)
+    constexpr int NAC = TA == 2 ? NA : 1, NBC = TB == 2 ? NB : 1;
+    float amu[NAC], asc[NAC], abt[NAC], bmu[NBC], bsc[NBC], bbt[NBC];
+    if constexpr (TA == 2) {
+      int kcs[NA];
+#pragma unroll
+      for (int j = 0; j < NA; ++j) kcs[j] = min(k0 + (AKF ? (t & 127) : (t >> 4) + 16 * j), g.K - 1);
+      if (g.abn.acc) {  // train: BatchNorm of A's columns finalized from its accumulators
+#pragma unroll
+        for (int j = 0; j < NA; ++j) {
+          const BnChan st = bn_chan_train(g.abn.acc, g.K, kcs[j], g.abn.count, g.abn.inv_count);
+          amu[j] = st.mean;
+          asc[j] = g.abn.gamma[kcs[j]] * st.invstd;
+          abt[j] = g.abn.beta[kcs[j]];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < NA; ++j) {
+          amu[j] = g.amean[kcs[j]];
+          asc[j] = g.aa[kcs[j]];
+          abt[j] = g.abeta[kcs[j]];
+        }
+      }
+    }
+    if constexpr (TB == 2) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int nc = min(nb0 + (BNF ? (t & 63) : (t >> 7) + 2 * j), g.N - 1);
+        bmu[j] = g.bmean[nc];
+        bsc[j] = g.ba[nc];
+        bbt[j] = g.bbeta[nc];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       const int kk = AKF ? (t & 127) : (t >> 4) + 16 * j, mm = AKF ? (t >> 7) + 2 * j : (t & 15);
       const int k = k0 + kk;
       float a = ra[j];
       if constexpr (TA == 1) a = a > 0.f ? a : 0.f;
-      if constexpr (TA == 2) {
-        const int kc = min(k, g.K - 1);
-        if (g.abn.acc) {  // train: BatchNorm of A's columns finalized from its accumulators
-          const BnChan st = bn_chan_train(g.abn.acc, g.K, kc, g.abn.count, g.abn.inv_count);
-          a = (a - st.mean) * (g.abn.gamma[kc] * st.invstd) + g.abn.beta[kc];
-        } else {
-          a = (a - g.amean[kc]) * g.aa[kc] + g.abeta[kc];
-        }
-      }
+      if constexpr (TA == 2) a = (a - amu[j]) * asc[j] + abt[j];
       As[kk][mm] = k < g.K ? a : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int kk = BNF ? (t >> 6) + 4 * j : (t & 127), nn = BNF ? (t & 63) : (t >> 7) + 2 * j;
-      const int nc = min(nb0 + nn, g.N - 1);
       float b = rb[j];
       if constexpr (TB == 1) b = b > 0.f ? b : 0.f;
-      if constexpr (TB == 2) b = (b - g.bmean[nc]) * g.ba[nc] + g.bbeta[nc];
+      if constexpr (TB == 2) b = (b - bmu[j]) * bsc[j] + bbt[j];
       Bs[kk][nn] = b;
     }
     __syncthreads();
+    if (k0 + kTgKC < g.K) load(k0 + kTgKC);
     const int kn = min(kTgKC, g.K - k0);
     for (int kk = 0; kk < kn; kk += 4) {
       const float a = As[kk + kq][l16];
@@ -151,18 +182,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     rsum += __shfl_xor(rsum, 32, 64);
     if (kq == 0 && mok) g.rowsum[m] = rsum;
   }
+  // epilogue operands: every load issued (at clamped, in-bounds indices) before any is used -- a
+  // per-element conditional load makes hipcc wait for each one in turn
   float cs = 0.f, csx = 0.f;
-  const float xmu = g.colacc && nok ? g.xmean[n] : 0.f, xis = g.colacc && nok ? g.xinvstd[n] : 0.f;
+  const int nc = min(n, g.N - 1);
+  float bn = 0.f, xmu = 0.f, xis = 0.f;
+  float cmv[4] = {1.f, 1.f, 1.f, 1.f}, xyv[4] = {0.f, 0.f, 0.f, 0.f};
+  int mrow[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) mrow[j] = min(m0 + 4 * kq + j, g.M - 1);
+  if (g.bias) bn = g.bias[nc];
+  if (g.cmask) {
+    long cr[4];
+    if (g.cmrow) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cr[j] = g.cmrow[mrow[j]];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cr[j] = mrow[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cmv[j] = g.cmask[cr[j] * g.smm + (long)nc * g.smn];
+  }
+  if (g.colacc) {
+    xmu = g.xmean[nc];
+    xis = g.xinvstd[nc];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xyv[j] = g.xy[(long)mrow[j] * g.N + nc];
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int mm = m0 + 4 * kq + j;
     if (mm < g.M && nok) {
-      float v = acc[j] + (g.bias ? g.bias[n] : 0.f);
-      if (g.cmask && !(g.cmask[(g.cmrow ? g.cmrow[mm] : mm) * g.smm + (long)n * g.smn] > 0.f)) v = 0.f;
+      float v = acc[j] + bn;
+      if (g.cmask && !(cmv[j] > 0.f)) v = 0.f;
       g.C[(long)mm * g.scm + (long)n * g.scn] = v;
       if (g.colacc) {
         cs += v;
-        csx += v * ((g.xy[(long)mm * g.N + n] - xmu) * xis);
+        csx += v * ((xyv[j] - xmu) * xis);
       }
     }
   }
