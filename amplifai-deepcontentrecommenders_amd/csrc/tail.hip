@@ -61,8 +61,8 @@ constexpr int kTgKC = 128;
 template <int TA, int TB, int AKF, int BNF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_tgemm(TGemmArgs g) {
   critical_path_priority();
-  __shared__ float As[kTgKC][16];
-  __shared__ float Bs[kTgKC][80];
+  __shared__ float As[kTgKC][17];  // odd pitches: the k-major staging stores hit 64 distinct banks
+  __shared__ float Bs[kTgKC][81];
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int m0 = blockIdx.x * 16, nb0 = blockIdx.y * 64, n0 = nb0 + 16 * wave;
   const int l16 = lane & 15, kq = lane >> 4;
