@@ -4,37 +4,46 @@
 
 namespace dcue {
 
-// torch.optim.Adam, foreach=False/fused=False (the CPU reference path), per element:
-//   g += wd*p (wd != 0);  m.lerp_(g, 1-b1);  v = v*b2 + (1-b2)*g*g;
-//   p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
+// torch.optim.Adam, foreach=False/fused=False, per element, as torch 2.10's CPU kernels round it
+// (torch/optim/adam.py _single_tensor_adam; each form below was matched bit for bit against those
+// kernels on random inputs, tests/test_adam_cpu.py):
+//   g = fma(p, wd, g)                      grad.add(param, alpha=wd)
+//   m = fma(c, g - m, base)                exp_avg.lerp_(grad, 1-b1): c = w, base = m (w < 0.5),
+//                                          else c = w - 1, base = g (the vectorised lerp)
+//   v = fma((1-b2)*g, g, v*b2)             exp_avg_sq.mul_(b2).addcmul_(grad, grad, value=1-b2)
+//   d = sqrt(v) / bc2_sqrt + eps           (exp_avg_sq.sqrt() / bias_correction2_sqrt).add_(eps)
+//   p = p + (step * m) / d                 param.addcdiv_(exp_avg, denom, value=-step_size)
+// The one place this cannot be bit-identical is sqrt: the CPU kernel's vectorised sqrt is not
+// correctly rounded (1 ulp off on ~0.6% of inputs, tests/test_adam_cpu.py); here it is. (It must be
+// __builtin_sqrtf: hipcc lowers it to v_sqrt_f32 plus the two-fma correction, while __fsqrt_rn
+// compiles to the bare 1-ulp v_sqrt_f32.)
 struct AdamScalars {
-  float lr_bc1, one_m_b1, b2, one_m_b2, bc2_sqrt, eps, wd;
+  float neg_step, lerp_c, b2, one_m_b2, bc2_sqrt, eps, wd;  // neg_step = -(lr / bc1)
   float inv_bc2_sqrt;  // RN(1 / bc2_sqrt): Markstein division by the per-step constant
 };
 static_assert(sizeof(AdamScalars) == 32, "history entry is [8] floats");
 
-// Every operation rounded on its own (fp contraction off: no fma fusion) so that the dense sweep,
-// the deferred replay and the touched-row step produce identical bits whatever code the compiler
-// schedules around them; the order follows torch's CPU kernels: lerp (w < 0.5) m + w*(g-m);
-// mul_(b2).addcmul_(g, g, 1-b2); denom = sqrt(v)/bc2_sqrt + eps; addcdiv_(m, denom, -lr/bc1).
+// Every operation rounded on its own unless written as an fma (fp contraction off for this file)
+// so that the dense sweep, the deferred replay and the touched-row step produce identical bits.
+// lerp_c < 0: the lerp weight is >= 0.5 (beta1 <= 0.5), so the blend base is g.
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamScalars& s) {
 #pragma clang fp contract(off)
-  if (s.wd != 0.f) g = __fadd_rn(g, __fmul_rn(s.wd, p));
-  m = __fadd_rn(m, __fmul_rn(s.one_m_b1, __fsub_rn(g, m)));
-  v = __fadd_rn(__fmul_rn(v, s.b2), __fmul_rn(__fmul_rn(s.one_m_b2, g), g));
-  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), s.bc2_sqrt), s.eps);
-  p = __fadd_rn(p, __fmul_rn(-s.lr_bc1, __fdiv_rn(m, denom)));
+  if (s.wd != 0.f) g = __fmaf_rn(p, s.wd, g);
+  m = __fmaf_rn(s.lerp_c, __fsub_rn(g, m), s.lerp_c < 0.f ? g : m);
+  v = __fmaf_rn(__fmul_rn(s.one_m_b2, g), g, __fmul_rn(v, s.b2));
+  const float denom = __fadd_rn(__fdiv_rn(__builtin_sqrtf(v), s.bc2_sqrt), s.eps);
+  p = __fadd_rn(p, __fdiv_rn(__fmul_rn(s.neg_step, m), denom));
 }
 
-// The zero-gradient step (a row outside the batch, wd == 0), bit-identical to adam_elem(p, +0, m, v, s):
-//   m + w*(0 - m) == m - w*m (signed zeros included), v*b2 + w2*0*0 == v*b2 (v >= 0), and
-//   sqrt(v)/bc2_sqrt by Markstein's correction with r = RN(1/bc2_sqrt): q = RN(a r),
-//   q' = RN(q + RN?(a - q bc2)*r) is the correctly rounded quotient for a >= 2^-100 (below it the
-//   plain division runs). This is the deferred replay's inner loop (VALU-bound).
+// The zero-gradient step (a row outside the batch, wd == 0, lerp weight < 0.5), bit-identical to
+// adam_elem(p, +0, m, v, s): fma((1-b2)*0, 0, v*b2) == v*b2 (v >= 0), and sqrt(v)/bc2_sqrt by
+// Markstein's correction with r = RN(1/bc2_sqrt): q = RN(a r), q' = RN(q + RN?(a - q bc2)*r) is the
+// correctly rounded quotient for a >= 2^-100 (below it the plain division runs). This is the
+// deferred replay's inner loop (VALU-bound).
 __device__ __forceinline__ void adam_zero_elem(float& p, float& m, float& v, const AdamScalars& s) {
-  m = __fsub_rn(m, __fmul_rn(s.one_m_b1, m));
+  m = __fmaf_rn(s.lerp_c, __fsub_rn(0.f, m), m);
   v = __fmul_rn(v, s.b2);
-  const float sq = __fsqrt_rn(v);
+  const float sq = __builtin_sqrtf(v);
   float t;
   if (sq >= 0x1p-100f) {
     const float q = __fmul_rn(sq, s.inv_bc2_sqrt);
@@ -44,12 +53,12 @@ __device__ __forceinline__ void adam_zero_elem(float& p, float& m, float& v, con
     t = __fdiv_rn(sq, s.bc2_sqrt);
   }
   const float denom = __fadd_rn(t, s.eps);
-  p = __fadd_rn(p, __fmul_rn(-s.lr_bc1, __fdiv_rn(m, denom)));
+  p = __fadd_rn(p, __fdiv_rn(__fmul_rn(s.neg_step, m), denom));
 }
 
 // replay of a zero-gradient step: the fast form when no weight decay touches g
 __device__ __forceinline__ void adam_replay(float& p, float& m, float& v, const AdamScalars& s, float gz) {
-  if (s.wd == 0.f)
+  if (s.wd == 0.f && s.lerp_c < 0.5f)
     adam_zero_elem(p, m, v, s);
   else
     adam_elem(p, gz, m, v, s);
@@ -66,11 +75,11 @@ __device__ __forceinline__ bool idle_moments4(const float4& m, const float4& v) 
   return (__float_as_uint(m.x) | __float_as_uint(m.y) | __float_as_uint(m.z) | __float_as_uint(m.w) |
           __float_as_uint(v.x) | __float_as_uint(v.y) | __float_as_uint(v.z) | __float_as_uint(v.w)) == 0u;
 }
-// whether every replayed step of [j0, j1] (history slots j % cap, or j - base) is free of weight decay
-__device__ __forceinline__ bool no_decay(const AdamScalars* hs, int j0, int j1, int cap, float gz, int base) {
+// whether every replayed step of [j0, j1] (history slots j % cap) is free of weight decay
+__device__ __forceinline__ bool no_decay(const AdamScalars* hs, int j0, int j1, int cap, float gz) {
   if (gz != 0.f) return false;
   for (int j = j0; j <= j1; ++j)
-    if (hs[base >= 0 ? j - base : j % cap].wd != 0.f) return false;
+    if (hs[j % cap].wd != 0.f) return false;
   return true;
 }
 
@@ -100,13 +109,20 @@ __device__ __forceinline__ void pack_store(const PackSeg& sg, long e, float w, f
 
 // Adam over the flat dense buffer with the conv-weight repack fused in: a float4 that lies in a
 // conv weight segment (segments are 4-float aligned) also writes its four packed copies.
-__global__ __launch_bounds__(256) void k_adam_dense_pack(float* __restrict__ p, const float* __restrict__ g,
+// gdiv > 0: the gradient is an all-reduced sum over gdiv ranks; it becomes the mean first (stored
+// back, as grad.div_(world) leaves it) -- DDP's averaging fused into the sweep.
+__global__ __launch_bounds__(256) void k_adam_dense_pack(float* __restrict__ p, float* __restrict__ g,
                                                          float* __restrict__ m, float* __restrict__ v,
                                                          long n, AdamScalars s, PackArgs pa,
-                                                         float* __restrict__ wpack) {
+                                                         float* __restrict__ wpack, float gdiv) {
   const long n4 = n / 4;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     float4 pp = ld4(p + 4 * i), gg = ld4(g + 4 * i), mm = ld4(m + 4 * i), vv = ld4(v + 4 * i);
+    if (gdiv > 0.f) {
+      gg.x = __fdiv_rn(gg.x, gdiv); gg.y = __fdiv_rn(gg.y, gdiv);
+      gg.z = __fdiv_rn(gg.z, gdiv); gg.w = __fdiv_rn(gg.w, gdiv);
+      st4(g + 4 * i, gg);
+    }
     adam_elem(pp.x, gg.x, mm.x, vv.x, s);
     adam_elem(pp.y, gg.y, mm.y, vv.y, s);
     adam_elem(pp.z, gg.z, mm.z, vv.z, s);
@@ -126,24 +142,11 @@ __global__ __launch_bounds__(256) void k_adam_dense_pack(float* __restrict__ p, 
       }
     }
   }
-  for (long i = 4 * n4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    adam_elem(p[i], g[i], m[i], v[i], s);  // tail past the last float4: never a conv weight
-}
-
-__global__ __launch_bounds__(256) void k_adam_dense(float* __restrict__ p, const float* __restrict__ g,
-                                                    float* __restrict__ m, float* __restrict__ v,
-                                                    long n, AdamScalars s) {
-  const long n4 = n / 4;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
-    float4 pp = ld4(p + 4 * i), gg = ld4(g + 4 * i), mm = ld4(m + 4 * i), vv = ld4(v + 4 * i);
-    adam_elem(pp.x, gg.x, mm.x, vv.x, s);
-    adam_elem(pp.y, gg.y, mm.y, vv.y, s);
-    adam_elem(pp.z, gg.z, mm.z, vv.z, s);
-    adam_elem(pp.w, gg.w, mm.w, vv.w, s);
-    st4(p + 4 * i, pp); st4(m + 4 * i, mm); st4(v + 4 * i, vv);
+  for (long i = 4 * n4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float gi = g[i];  // tail past the last float4: never a conv weight
+    if (gdiv > 0.f) g[i] = gi = __fdiv_rn(gi, gdiv);
+    adam_elem(p[i], gi, m[i], v[i], s);
   }
-  for (long i = 4 * n4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    adam_elem(p[i], g[i], m[i], v[i], s);
 }
 
 // User table: one wave per row; rows without a gradient this step get g = 0 (the reference's dense
@@ -208,7 +211,7 @@ __global__ __launch_bounds__(1024) void k_emb_sync(float* __restrict__ p, float*
   const AdamScalars* hist = log_hist(hdr);
   for (int j = from + 1 + (int)threadIdx.x; j <= T; j += blockDim.x) hs[j % cap] = hist[j % cap];
   __syncthreads();
-  const bool nd = no_decay(hs, from + 1, T, cap, gz, -1);
+  const bool nd = no_decay(hs, from + 1, T, cap, gz);
   float* pr = p + u * E;
   float* mr = m + u * E;
   float* vr = v + u * E;
@@ -238,9 +241,13 @@ __global__ __launch_bounds__(256) void k_emb_flush(float* __restrict__ p, float*
   const int T = hdr->step_done, F = hdr->flush_step, cap = hdr->cap;
   if (T <= F) return;
   const AdamScalars* hist = log_hist(const_cast<dcue_emb_log*>(hdr));
-  for (int j = F + 1 + (int)threadIdx.x; j <= T; j += blockDim.x) hs[j - F - 1] = hist[j % cap];
+  // Only the ring's live window [lo, T] is staged (slot j % cap): the full flush may come thousands
+  // of steps after the previous one, but the rolling slices keep every row within `cap` steps of T,
+  // so no row needs an entry older than lo.
+  const int lo = max(F + 1, T - cap + 1);
+  for (int j = lo + (int)threadIdx.x; j <= T; j += blockDim.x) hs[j % cap] = hist[j % cap];
   __syncthreads();
-  const bool nd = no_decay(hs, F + 1, T, cap, gz, F + 1);
+  const bool nd = no_decay(hs, lo, T, cap, gz);
   const long stride = (long)gridDim.x * blockDim.x;
   if ((E & 3) == 0) {
     const int E4 = E >> 2;
@@ -250,9 +257,8 @@ __global__ __launch_bounds__(256) void k_emb_flush(float* __restrict__ p, float*
       float4 mm = ld4(m + 4 * i), vv = ld4(v + 4 * i);
       if (nd && idle_moments4(mm, vv)) continue;  // fixed point (idle_moments)
       float4 pp = ld4(p + 4 * i);
-      for (int j = F + 1; j <= T; ++j) {
-        if (j <= from) continue;
-        const AdamScalars s = hs[j - F - 1];
+      for (int j = max(from + 1, lo); j <= T; ++j) {
+        const AdamScalars s = hs[j % cap];
         adam_replay(pp.x, mm.x, vv.x, s, gz);
         adam_replay(pp.y, mm.y, vv.y, s, gz);
         adam_replay(pp.z, mm.z, vv.z, s, gz);
@@ -267,8 +273,7 @@ __global__ __launch_bounds__(256) void k_emb_flush(float* __restrict__ p, float*
       float mm = m[i], vv = v[i];
       if (nd && idle_moments(mm, vv)) continue;
       float pp = p[i];
-      for (int j = F + 1; j <= T; ++j)
-        if (j > from) adam_replay(pp, mm, vv, hs[j - F - 1], gz);
+      for (int j = max(from + 1, lo); j <= T; ++j) adam_replay(pp, mm, vv, hs[j % cap], gz);
       p[i] = pp; m[i] = mm; v[i] = vv;
     }
   }
@@ -295,7 +300,7 @@ __global__ __launch_bounds__(256) void k_emb_flush_rows(float* __restrict__ p, f
   for (int j = lo + (int)threadIdx.x; j <= T; j += blockDim.x) hs[j % cap] = hist[j % cap];
   for (int i = threadIdx.x; i < nr; i += blockDim.x) from_s[i] = max(emb_step[rb + i], F);
   __syncthreads();
-  const bool nd = no_decay(hs, lo, T, cap, gz, -1);
+  const bool nd = no_decay(hs, lo, T, cap, gz);
   if ((E & 3) == 0) {
     const int E4 = E >> 2;
     for (int e = threadIdx.x; e < nr * E4; e += blockDim.x) {
@@ -426,22 +431,26 @@ int launch_emb_flush(const dcue_model* md, hipStream_t s) {
 
 int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* poff, hipStream_t s,
                 bool flush_slice) {
-  const double bc1 = 1.0 - pow((double)a->beta1, (double)a->step);
-  const double bc2 = 1.0 - pow((double)a->beta2, (double)a->step);
+  // host scalars as torch.optim.Adam forms them from Python floats (double), each rounded once to
+  // float where the CPU kernel takes it as a float scalar
+  const double bc1 = 1.0 - pow(a->beta1, (double)a->step);
+  const double bc2 = 1.0 - pow(a->beta2, (double)a->step);
+  const double w = 1.0 - a->beta1;
   AdamScalars sc;
-  sc.lr_bc1 = (float)((double)a->lr / bc1);
-  sc.one_m_b1 = (float)(1.0 - (double)a->beta1);
-  sc.b2 = a->beta2;
-  sc.one_m_b2 = (float)(1.0 - (double)a->beta2);
-  sc.bc2_sqrt = (float)sqrt(bc2);
-  sc.eps = a->eps;
-  sc.wd = a->weight_decay;
+  sc.neg_step = (float)(-(a->lr / bc1));
+  sc.lerp_c = w < 0.5 ? (float)w : (float)w - 1.0f;
+  sc.b2 = (float)a->beta2;
+  sc.one_m_b2 = (float)(1.0 - a->beta2);
+  sc.bc2_sqrt = (float)pow(bc2, 0.5);  // bias_correction2 ** 0.5
+  sc.eps = (float)a->eps;
+  sc.wd = (float)a->weight_decay;
   sc.inv_bc2_sqrt = 1.0f / sc.bc2_sqrt;  // IEEE single division on the host: RN(1/bc2_sqrt)
+  const float gdiv = a->grad_div > 1.0 ? (float)a->grad_div : 0.f;
   const int parts = a->parts ? a->parts : (DCUE_ADAM_DENSE | DCUE_ADAM_EMBEDDING);
   const long n = poff[DCUE_N_DENSE_SEGMENTS];
   if (parts & DCUE_ADAM_DENSE) {  // Adam + the conv-weight repack in one sweep
     DCUE_LAUNCH(k_adam_dense_pack, dim3(512), dim3(256), 0, s, md->params, md->grads, md->exp_avg,
-                       md->exp_avg_sq, n, sc, pack_args(md, poff), md->wpack);
+                       md->exp_avg_sq, n, sc, pack_args(md, poff), md->wpack, gdiv);
     DCUE_LAUNCH_CHECK();
   }
   if ((parts & DCUE_ADAM_EMBEDDING) && md->emb_step) {

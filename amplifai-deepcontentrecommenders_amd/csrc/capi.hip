@@ -450,6 +450,19 @@ int dcue_workspace_outputs(const dcue_dims* dims, int32_t B, int32_t N, int32_t 
   return DCUE_OK;
 }
 
+int dcue_workspace_activations(const dcue_dims* dims, int32_t B, int32_t N, int32_t M,
+                               size_t* offsets_host) {
+  TRY(check_dims(dims));
+  if (!offsets_host || B <= 0 || N < 0 || M <= 0) return DCUE_ERR_INVALID;
+  Ws w;
+  carve(dims, B, N, M, nullptr, &w);
+  for (int l = 1; l <= 5; ++l) {
+    offsets_host[2 * (l - 1)] = (size_t)w.y[l];
+    offsets_host[2 * (l - 1) + 1] = (size_t)w.idx[l];
+  }
+  return DCUE_OK;
+}
+
 int dcue_pack_weights(const dcue_model* m, void* stream) {
   Ctx c;
   TRY(init_ctx(&c, m));

@@ -168,6 +168,9 @@ extern "C" int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const 
     return DCUE_ERR_INVALID;
   if (!dcue::side_pool()) return DCUE_ERR_HIP;  // side streams exist before capture starts
   if (!(cfg->flags & DCUE_PLAN_GRAPH)) {
+    // the eager replay prepares step t+1's copy counts during launch t from the negatives it drew
+    // itself; caller-written gather negatives would be read before the caller refreshed them
+    if (b->layout == DCUE_LAYOUT_GATHER && !(cfg->flags & DCUE_PLAN_SAMPLE_INBATCH)) return DCUE_ERR_UNSUPPORTED;
     // eager plan: validate once by issuing nothing but the checks the calls make themselves
     const int B = b->n_rows, N = b->n_neg, M = b->n_items;
     const long nneg = (cfg->flags & DCUE_PLAN_SAMPLE_INBATCH) ? (long)B * N : 0;

@@ -843,7 +843,10 @@ __global__ void k_build_catalogue(const int64_t* pos, const int64_t* neg, int B,
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long tot = (long)B * (1 + N);
   if (e >= tot) return;
-  item_track[e] = (int32_t)(e < B ? pos[e] : neg[e - B]);
+  // a -1 from the catalogue sampler (a user with no candidate negative; the host raises the
+  // reference's ValueError before such a batch is sampled) never becomes an out-of-table read
+  const int64_t id = e < B ? pos[e] : neg[e - B];
+  item_track[e] = (int32_t)(id < 0 ? 0 : id);
 }
 
 }  // namespace dcue

@@ -56,9 +56,9 @@ class Tracks(ctypes.Structure):
 
 
 class AdamArgs(ctypes.Structure):
-    _fields_ = [("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
-                ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float), ("step", ctypes.c_int32),
-                ("parts", ctypes.c_int32)]
+    _fields_ = [("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
+                ("eps", ctypes.c_double), ("weight_decay", ctypes.c_double), ("step", ctypes.c_int32),
+                ("parts", ctypes.c_int32), ("grad_div", ctypes.c_double)]
 
 
 ADAM_DENSE = 1
@@ -80,7 +80,7 @@ class PlanConfig(ctypes.Structure):
 
 MT_STATE_BYTES = 624 * 4 + 16
 MAX_LOG_CAP = 256
-ABI_VERSION = 4
+ABI_VERSION = 5
 RANK_SPLIT, RANK_SINGLE = 0, 1
 
 _P = ctypes.c_void_p
@@ -94,6 +94,8 @@ _SIGS = {
                               ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "dcue_workspace_outputs": ([ctypes.POINTER(Dims), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                 ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "dcue_workspace_activations": ([ctypes.POINTER(Dims), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "dcue_pack_weights": ([ctypes.POINTER(Model), _P], ctypes.c_int),
     "dcue_forward": ([ctypes.POINTER(Model), ctypes.POINTER(Batch), ctypes.POINTER(Tracks), _P,
                       ctypes.c_size_t, ctypes.c_int32, ctypes.c_float, _P, _P, _P, _P, _P], ctypes.c_int),
@@ -200,6 +202,13 @@ def workspace_outputs(dims, B, N, M):
     off = (ctypes.c_size_t * 4)()
     check(lib().dcue_workspace_outputs(ctypes.byref(dims), B, N, M, off), "dcue_workspace_outputs")
     return list(off)
+
+
+def workspace_activations(dims, B, N, M):
+    """Byte offsets of (y_l, argmax_l) for conv layers l = 1..5 inside a (B, N, M) workspace."""
+    off = (ctypes.c_size_t * 10)()
+    check(lib().dcue_workspace_activations(ctypes.byref(dims), B, N, M, off), "dcue_workspace_activations")
+    return [(off[2 * i], off[2 * i + 1]) for i in range(5)]
 
 
 def timer_enable(kernel, enable=True):

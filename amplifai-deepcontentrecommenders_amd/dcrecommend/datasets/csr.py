@@ -20,5 +20,19 @@ def user_split_ranks(user_idx, item_idx, n_users, split_items):
     key = np.unique(user_idx[inside] * (n + 1) + pos[inside])
     u, r = key // (n + 1), key % (n + 1)
     indptr = np.zeros(n_users + 1, dtype=np.int64)
-    np.add.at(indptr, u + 1, 1)
-    return np.cumsum(indptr), r.astype(np.int32)
+    indptr[1:] = np.cumsum(np.bincount(u, minlength=n_users)[:n_users])
+    return indptr, r.astype(np.int32)
+
+
+def saturated_users(indptr, n_split):
+    """Users who interacted with every song of the split: the reference's
+    np.random.choice(nonitems, N) raises ValueError for them (datasets/dcuedataset.py:219, an empty
+    `nonitems`). The GPU sampler writes -1 for such a row; callers check batches against this set
+    on the host first and raise as the reference does."""
+    return np.nonzero(np.diff(np.asarray(indptr, dtype=np.int64)) >= int(n_split))[0]
+
+
+def check_catalogue_users(users, saturated):
+    """Raise numpy's ValueError if a batch row's user has no candidate negative."""
+    if len(saturated) and np.isin(np.asarray(users), saturated).any():
+        raise ValueError("a cannot be empty unless no samples are taken")

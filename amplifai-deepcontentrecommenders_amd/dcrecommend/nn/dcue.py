@@ -28,7 +28,7 @@ import torch
 from torch.utils.data import RandomSampler
 
 from dcrecommend import _native as nat
-from dcrecommend.datasets.csr import user_split_ranks
+from dcrecommend.datasets.csr import check_catalogue_users, saturated_users, user_split_ranks
 from dcrecommend.dcue.dcue import DCUENet
 from dcrecommend.dcue.plan import TrainPlan
 from dcrecommend.nn import rank
@@ -86,6 +86,12 @@ class _Negatives:
         self.ranks = torch.from_numpy(ranks if len(ranks) else np.zeros(1, np.int32)).to(device)
         self.reseed = ds.random_seed is not None
         self.seed = int(ds.random_seed) if self.reseed else 0
+        self.saturated = saturated_users(indptr, len(split))  # usually empty
+
+    def check(self, users):
+        """ValueError (numpy's) before a batch whose user has no candidate negative is sampled."""
+        if len(self.saturated):
+            check_catalogue_users(users.cpu().numpy() if torch.is_tensor(users) else users, self.saturated)
 
     def draw(self, mt, users, N, out):
         nat.check(nat.lib().dcue_sample_catalogue(
@@ -236,6 +242,7 @@ class DCUE(Trainer):
             r = torch.from_numpy(rows).to(self.device, non_blocking=True)
             users = users_all.index_select(0, r)
             pos = items_all.index_select(0, r)
+            neg.check(users)
             neg.draw(mt, users, N, negs)
             plan.users.copy_(users)
             nat.check(nat.lib().dcue_build_catalogue_batch(nat.ptr(pos), nat.ptr(negs), B, N,
@@ -263,6 +270,7 @@ class DCUE(Trainer):
             users = users_all[s:s + B].contiguous()
             b = users.numel()
             negs = torch.empty((b, N), dtype=torch.int64, device=self.device)
+            neg.check(users)
             neg.draw(mt, users, N, negs)
             track = torch.empty(b * (1 + N), dtype=torch.int32, device=self.device)
             nat.check(nat.lib().dcue_build_catalogue_batch(nat.ptr(items_all[s:s + B].contiguous()), nat.ptr(negs),

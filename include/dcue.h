@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DCUE_ABI_VERSION 4
+#define DCUE_ABI_VERSION 5
 #define DCUE_N_MELS 128
 #define DCUE_N_FRAMES 131
 #define DCUE_N_BN 6
@@ -123,9 +123,13 @@ typedef struct dcue_tracks {
 #define DCUE_ADAM_EMBEDDING 2 /* the user table */
 
 typedef struct dcue_adam_args {
-  float lr, beta1, beta2, eps, weight_decay; /* param_group values set by CyclicLRWithRestarts */
+  /* param_group values set by CyclicLRWithRestarts, as the Python floats torch.optim.Adam reads
+   * (double: 1 - beta1 etc. are formed in double and rounded once, as torch does) */
+  double lr, beta1, beta2, eps, weight_decay;
   int32_t step;                              /* Adam step count AFTER increment (1 on first step) */
   int32_t parts;                             /* DCUE_ADAM_* mask; 0 = both */
+  double grad_div; /* > 1: the dense gradient is first divided by it in place (DDP's mean over
+                      grad_div ranks of an all-reduced sum); 0 or 1: used as is */
 } dcue_adam_args;
 
 /* ---------------------------------------------------------------------------------- layout */
@@ -144,6 +148,12 @@ int dcue_workspace_bytes(const dcue_dims* dims, int32_t max_rows, int32_t max_ne
  * [3] loss (one float). Valid until the next call on the same workspace. */
 int dcue_workspace_outputs(const dcue_dims* dims, int32_t B, int32_t N, int32_t M,
                            size_t* offsets_host);
+/* Inspection (tests): byte offsets of the train forward's per-layer activations in the same
+ * workspace. offsets[2(l-1)] = y_l, float [M][Lp_l][C_l] = relu(max-pooled conv + bias), before
+ * BN; offsets[2(l-1)+1] = its uint8 [M][Lp_l][C_l] window argmax (0..pool-1, first maximum), for
+ * conv layers l = 1..5 (Lp = 33, 8, 2, 1, 1; C = H, H, H, H, d). */
+int dcue_workspace_activations(const dcue_dims* dims, int32_t B, int32_t N, int32_t M,
+                               size_t* offsets_host);
 
 /* ------------------------------------------------------------------------- hot-path entries */
 /* Refresh wpack from params (after any host-side write of conv weights and after every Adam step). */
@@ -215,7 +225,10 @@ int dcue_sample_inbatch(dcue_mt_state* state, int32_t B, int32_t N, int32_t* neg
  * the split (split_items sorted; user_split_rank = CSR over users of the ranks, inside split_items,
  * of the user's split items, sorted), N draws with replacement. reseed != 0: every sample draws from
  * a fresh stream seeded with `seed` (random_seed mode); else all samples share `state` in order.
- * Writes item ids (values of split_items). */
+ * Writes item ids (values of split_items). A user with no non-item in the split (numpy raises
+ * ValueError there) gets a row of -1 and consumes no draw: callers check for such users on the host
+ * (their CSR row length >= n_split) and raise before sampling them; dcue_build_catalogue_batch
+ * maps a -1 to item 0 so it never reads outside the track table. */
 int dcue_sample_catalogue(dcue_mt_state* state, int32_t reseed, uint32_t seed,
                           const int64_t* split_items, int64_t n_split, const int64_t* user_indptr,
                           const int32_t* user_split_rank, const int64_t* users, int32_t n_samples,

@@ -104,15 +104,42 @@ def _bn(x, p, b, l, train):
     return out
 
 
-def item_tower(p, b, X, train=True):
-    """X [M,128,131] fp32 -> [M,d] (truedcuemel1dbn.py:77-101)."""
+def _pool_relu(h, pool, route):
+    """max_pool1d then relu (truedcuemel1dbn.py:80-82 order), or -- with route = (argmax [M,C,Lp],
+    live [M,C,Lp]) -- the same pooling with the window argmax and the relu mask given (tests pass
+    the GPU's own choices here, so the rest of the step is compared without max-pool near-ties,
+    whose routing any 1-ulp difference can flip)."""
+    if route is None:
+        if pool > 1:
+            h = F.max_pool1d(h, pool)
+        return F.relu(h)
+    idx, live = route
+    if pool > 1:
+        L = idx.shape[2] * pool
+        h = h[:, :, :L].reshape(h.shape[0], h.shape[1], -1, pool).gather(3, idx.unsqueeze(3)).squeeze(3)
+    return h * live.to(h.dtype)
+
+
+def item_tower(p, b, X, train=True, route=None):
+    """X [M,128,131] fp32 -> [M,d] (truedcuemel1dbn.py:77-101). route: {layer: (argmax, live)}."""
     h = _bn(X, p, b, 0, train)
     for l, (k, pad, pool) in enumerate(CONV_SPECS, start=1):
         h = F.conv1d(h, p["conv.layer%d.weight" % l], p["conv.layer%d.bias" % l], padding=pad)
-        if pool > 1:
-            h = F.max_pool1d(h, pool)
-        h = _bn(F.relu(h), p, b, l, train)
+        h = _bn(_pool_relu(h, pool, None if route is None else route[l]), p, b, l, train)
     return F.linear(h.permute(0, 2, 1), p["conv.fc.weight"], p["conv.fc.bias"]).squeeze()
+
+
+def conv_trace(p, b, X):
+    """Train-mode item tower returning each conv layer's pre-pool output [M,C,L] (BN running stats
+    in `b` are left untouched): the inputs of the max-pool decisions."""
+    b = {k: v.clone() for k, v in b.items()}
+    out = []
+    h = _bn(X, p, b, 0, True)
+    for l, (k, pad, pool) in enumerate(CONV_SPECS, start=1):
+        h = F.conv1d(h, p["conv.layer%d.weight" % l], p["conv.layer%d.bias" % l], padding=pad)
+        out.append(h)
+        h = _bn(_pool_relu(h, pool, None), p, b, l, True)
+    return out
 
 
 def user_tower(p, u):
@@ -121,11 +148,11 @@ def user_tower(p, u):
     return F.linear(h, p["user_embd.linear2.weight"], p["user_embd.linear2.bias"])
 
 
-def forward(p, b, u, pos, neg, train=True):
+def forward(p, b, u, pos, neg, train=True, route=None):
     """dcue/dcue.py:70-108: one conv pass over cat([pos, neg.view(B*N,...)])."""
     B, N = neg.shape[0], neg.shape[1]
     uf = user_tower(p, u)
-    feats = item_tower(p, b, torch.cat([pos, neg.reshape(B * N, N_MELS, -1)], 0), train)
+    feats = item_tower(p, b, torch.cat([pos, neg.reshape(B * N, N_MELS, -1)], 0), train, route)
     pf, nf = feats[:B], feats[B:].reshape(B, N, -1)
     pos_cos = F.cosine_similarity(uf, pf, dim=1)
     neg_cos = F.cosine_similarity(uf.unsqueeze(2), nf.permute(0, 2, 1), dim=1)
@@ -136,9 +163,9 @@ def hinge_loss(scores, margin=0.2):
     return torch.maximum(torch.zeros_like(scores), margin - scores).sum(dim=1).mean()
 
 
-def loss_and_grads(p, b, u, pos, neg, margin=0.2):
+def loss_and_grads(p, b, u, pos, neg, margin=0.2, route=None):
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
-    scores, uf, pf, nf = forward(leaves, b, u, pos, neg, train=True)
+    scores, uf, pf, nf = forward(leaves, b, u, pos, neg, train=True, route=route)
     loss = hinge_loss(scores, margin)
     loss.backward()
     grads = {k: v.grad.detach().clone() for k, v in leaves.items()}

@@ -1,0 +1,183 @@
+"""Parity at the shape bench.py runs (BASELINE.json config 2: B=64, N=20, d=H=128, E=300).
+
+The benchmarked step is a TrainPlan replay (dcue_plan_*) -- in the compact in-batch layout (the
+tower runs once per positive, M = 64 items, BN statistics copy-weighted) and in the catalogue
+layout (M = B(1+N) = 1,344 distinct items). Its kernels choose their tilings, split-K partitions
+and grids from M, so this test runs exactly that plan at exactly those shapes and checks it
+against the CPU oracle (oracle/dcue_oracle.py) on the reference's literal [pos; neg] stack
+(dcue/dcue.py:70-108, nn/dcue.py:167-170, 202-210, 698-709):
+
+  step 0 (plan.launch): scores, loss, user/item features within 1e-4 of max (north_star);
+          in-batch draws bit-exact with numpy's RandomState; the GPU's max-pool argmax and relu
+          decisions equal the fp64 oracle's wherever they are not near-ties (1e-5 of the layer's
+          scale); every dense gradient and the embedding rows within 1e-4 (abs floor 1e-4 of max)
+          of the fp64 oracle run with the GPU's decisions;
+  steps 1-3 (plan.step: launch + fused NativeAdam, deferred user table, as bench.py): loss 1e-4,
+          draws bit-exact; after the steps every parameter and BN buffer within 2 x the summed lr
+          (+1e-4 of max) of the oracle's torch.optim.Adam trajectory.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+B, N, D, H, E = 64, 20, 128, 128, 300
+N_USERS, N_TRACKS = 400, 700
+LRS = [1e-4, 2e-4, 1e-4, 5e-5]
+
+
+def _close(got, ref, rtol, afrac, what):
+    got = torch.as_tensor(got).double().cpu()
+    ref = torch.as_tensor(ref).double().cpu()
+    atol = afrac * max(float(ref.abs().max()), 1e-30)
+    err = (got - ref).abs()
+    bad = err > atol + rtol * ref.abs()
+    assert not bool(bad.any()), "%s: max err %.3e of max %.3e" % (what, float(err.max()), float(ref.abs().max()))
+
+
+LP = (33, 8, 2, 1, 1)
+
+
+def _gpu_route(net, nat, B, N, M, rows):
+    """The step's max-pool argmax and relu-live masks as the GPU computed them (workspace, layout
+    [M][Lp][C]), as oracle routes [rows, C, Lp] over the literal [pos; neg] stack."""
+    route = {}
+    for l, (yo, io) in enumerate(nat.workspace_activations(net._flat["dims"], B, N, M), start=1):
+        C = D if l == 5 else H
+        n = M * LP[l - 1] * C
+        y = net._ws[yo:yo + 4 * n].view(torch.float32).view(M, LP[l - 1], C).permute(0, 2, 1).cpu()
+        ix = net._ws[io:io + n].view(M, LP[l - 1], C).permute(0, 2, 1).long().cpu()
+        route[l] = (ix[rows].contiguous(), (y > 0)[rows].contiguous())
+    return route
+
+
+def _check_decisions(pre, route, tie=1e-5):
+    """GPU argmax / relu decisions against the fp64 pre-pool conv outputs: equal wherever the
+    decision is robust (top-two gap, or distance of the max from 0, above `tie` of the layer's
+    scale). Returns the number of near-tie windows decided differently, per layer."""
+    flips = {}
+    for l, (k, pad, pool) in enumerate(((4, 2, 4), (4, 2, 4), (4, 2, 4), (2, 1, 2), (1, 0, 1)), start=1):
+        c = pre[l - 1]
+        ix, live = route[l]
+        scale = float(c.abs().max())
+        Lp = ix.shape[2]
+        w = c[:, :, :Lp * pool].reshape(c.shape[0], c.shape[1], Lp, pool)
+        top = w.topk(min(2, pool), dim=3)
+        mx = top.values[..., 0]
+        firm_relu = mx.abs() > tie * scale
+        assert bool(((mx > 0) == live)[firm_relu].all()), "layer %d: relu decision differs" % l
+        if pool == 1:
+            flips[l] = int(((mx > 0) != live).sum())
+            continue
+        gap = top.values[..., 0] - top.values[..., 1]
+        firm = live & (mx > 0) & (gap > tie * scale)
+        ref_idx = top.indices[..., 0]
+        assert bool((ref_idx == ix)[firm].all()), "layer %d: argmax differs off near-ties" % l
+        flips[l] = int(((ref_idx != ix) & live & (mx > 0)).sum())
+    return flips
+
+
+@pytest.mark.parametrize("mode", ["inbatch", "catalogue"])
+def test_plan_at_bench_shape_against_oracle(mode):
+    from dcrecommend import _native as nat
+    from dcrecommend.dcue.dcue import DCUENet
+    from dcrecommend.dcue.plan import TrainPlan
+    from dcrecommend.optim import NativeAdam
+    from oracle import dcue_oracle as O
+    inbatch = mode == "inbatch"
+    torch.manual_seed(0)
+    net = DCUENet({"feature_dim": D, "conv_hidden": H, "user_embdim": E, "user_count": N_USERS,
+                   "model_type": "truedcuemel1dbn"}).to(DEV).train()
+    torch.manual_seed(0)
+    p, b = O.init_params(D, H, E, N_USERS)
+    adam = O.AdamState(p)
+    p0 = {k: v.clone() for k, v in p.items()}
+    b0 = {k: v.clone() for k, v in b.items()}
+    opt = NativeAdam(net.parameters(), LRS[0], (0.9, 0.99), 1e-8, 0, defer_embedding=True, flush_every=64)
+
+    gen = torch.Generator().manual_seed(5)
+    X = torch.randn(N_TRACKS, 128, 131, generator=gen).half().float()  # fp16-exact, as bench's table
+    table = X.half().transpose(1, 2).contiguous().to(DEV)              # [n][131][128] fp16 rows
+    seed = 17
+    mt = torch.empty(nat.MT_STATE_BYTES, dtype=torch.uint8, device=DEV)
+    nat.check(nat.lib().dcue_mt_seed(nat.ptr(mt), seed, nat.stream_handle()), "mt_seed")
+    rs = np.random.RandomState(seed)
+    plan = TrainPlan(net, table, B, N, mt_state=mt if inbatch else None, optimizer=opt)
+    M = B if inbatch else B * (1 + N)
+    off = nat.workspace_outputs(net._flat["dims"], B, N, M)
+
+    def ws_view(o, n, shape):
+        return net._ws[o:o + 4 * n].view(torch.float32).view(shape)
+
+    for step, lr in enumerate(LRS):
+        u = torch.randint(0, N_USERS, (B,), generator=gen)
+        pos_items = torch.randint(0, N_TRACKS, (B,), generator=gen)
+        if inbatch:
+            r = torch.from_numpy(O.inbatch_negatives(rs, B, N))
+            neg_items = pos_items[r.reshape(-1)].reshape(B, N)
+            items = pos_items
+        else:
+            neg_items = torch.randint(0, N_TRACKS, (B, N), generator=gen)
+            items = torch.cat([pos_items, neg_items.reshape(-1)])
+        u_d = u.to(DEV)
+        items_d = items.to(torch.int32).to(DEV)
+        pos, neg = X[pos_items], X[neg_items.reshape(-1)].reshape(B, N, 128, 131)
+        opt.param_groups[0]["lr"] = lr
+        if step == 0:
+            plan.launch(u_d, items_d)
+            torch.cuda.synchronize()
+            ref_loss, grads, (rs_, ruf, rpf, rnf) = O.loss_and_grads(p, b, u, pos, neg)
+            if inbatch:
+                assert torch.equal(plan.neg_item.cpu().long(), r), "in-batch draws differ from numpy"
+            _close(ws_view(off[0], B * N, (B, N)), rs_, 1e-4, 1e-4, "scores")
+            _close(ws_view(off[1], B * D, (B, D)), ruf, 1e-4, 1e-4, "user feats")
+            feats = ws_view(off[2], M * D, (M, D)).cpu()
+            _close(feats[:B], rpf, 1e-4, 1e-4, "positive feats")
+            if not inbatch:
+                _close(feats[B:].reshape(B, N, D), rnf, 1e-4, 1e-4, "negative feats")
+            _close(ws_view(off[3], 1, ()), ref_loss, 1e-4, 1e-4, "loss")
+            for k, v in net.state_dict().items():  # BN running stats after one train forward
+                if "running" in k:
+                    _close(v, b[k], 1e-4, 1e-4, k)
+            # Gradients. Max-pool routes each window's gradient to its first maximum; at M = 1,344
+            # items some windows hold two candidates within ~1e-6 of each other, and any 1-ulp
+            # difference in the conv sums (CPU oneDNN vs f32 MFMA) may pick the other one. So:
+            # (1) the GPU's argmax and relu decisions must equal the fp64 oracle's wherever the
+            #     decision is not such a near-tie;
+            # (2) the gradients are compared with the fp64 oracle run on the GPU's decisions.
+            rows = torch.cat([torch.arange(B), r.reshape(-1)]) if inbatch else torch.arange(M)
+            route = _gpu_route(net, nat, B, N, M, rows)
+            p64 = {k: v.double() for k, v in p0.items()}
+            b64 = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in b0.items()}
+            lit = torch.cat([pos, neg.reshape(B * N, 128, 131)]).double()
+            flips = _check_decisions(O.conv_trace(p64, b64, lit), route)
+            _, g64, _ = O.loss_and_grads(p64, b64, u, pos.double(), neg.double(), route=route)
+            named = dict(net.named_parameters())
+            for k, g_ref in g64.items():
+                got = net.embedding_grad_dense() if k == "user_embd.embeddings.weight" else named[k].grad
+                _close(got, g_ref, 1e-4, 1e-4, "grad %s (near-tie flips: %s)" % (k, flips))
+            opt.step()
+            adam.step(p, grads, lr)
+        else:
+            plan.step(u_d, items_d)
+            torch.cuda.synchronize()
+            ref_loss = O.train_step(p, b, adam, u, pos, neg, lr)
+            if inbatch:
+                assert torch.equal(plan.neg_item.cpu().long(), r), "step %d: in-batch draws differ" % step
+            _close(ws_view(off[3], 1, ()), ref_loss, 1e-4, 1e-4, "step %d loss" % step)
+    opt.flush()
+    torch.cuda.synchronize()
+    budget = 2 * sum(LRS)
+    sd = net.state_dict()
+    for k, ref in list(p.items()) + list(b.items()):
+        got = sd[k].detach().double().cpu()
+        ref = ref.detach().double()
+        if k.endswith("num_batches_tracked"):
+            assert int(got) == int(ref), k
+            continue
+        tol = budget + 1e-4 * float(ref.abs().max()) if k in p else 1e-4 * float(ref.abs().max()) + 1e-6
+        assert float((got - ref).abs().max()) <= tol, "%s after %d steps: %.3e" % (
+            k, len(LRS), float((got - ref).abs().max()))
+    plan.close()

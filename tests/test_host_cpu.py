@@ -32,3 +32,25 @@ def test_scheduler_sequence(golden, tag):
     except StopIteration:
         raised = 1
     assert raised == int(g[tag + "_raised"])
+
+
+class _Len:
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+
+@pytest.mark.parametrize("n,seed", [(95, 0), (100, 1), (1003, 2), (7, 3)])
+def test_get_batches_matches_reference(golden, n, seed):
+    """DCUEDataset.get_batches against the reference's own output (batches.npz): np.random.shuffle
+    of the row order, chunks of ceil(len/k), the last chunk dropped when len % k != 0 -- including
+    n = 7 with k = 10, where every chunk holds one row and the seventh is dropped
+    (datasets/dcuedataset.py:189-201)."""
+    from dcrecommend.datasets.dcuedataset import DCUEDataset
+    g = golden("batches.npz")
+    np.random.seed(seed)
+    chunks = DCUEDataset.get_batches(_Len(n), k=10)
+    assert np.array_equal(np.array([len(c) for c in chunks]), g["n%d_lens" % n])
+    assert np.array_equal(np.array([x for c in chunks for x in c], dtype=np.int64), g["n%d_flat" % n])
