@@ -343,10 +343,13 @@ int launch_emb_flush_rows(const dcue_model* md, int step, hipStream_t s) {
   if (rpb < 1) rpb = 1;
   if (rpb > 256) rpb = 256;
   const long blocks = (r1 - r0 + rpb - 1) / rpb;
+  TimerScope tsc;
+  int st = timer_begin(&tsc, DCUE_TIMED_EMB_SLICE, s);
+  if (st) return st;
   DCUE_LAUNCH(k_emb_flush_rows, dim3((unsigned)blocks), dim3(256), 0, s, md->emb, md->emb_exp_avg,
                      md->emb_exp_avg_sq, md->emb_log, md->emb_step, r0, r1, E, rpb, 0.f);
   DCUE_LAUNCH_CHECK();
-  return DCUE_OK;
+  return timer_end(&tsc);
 }
 
 

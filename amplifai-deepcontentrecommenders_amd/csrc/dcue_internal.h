@@ -226,6 +226,13 @@ int timer_end(TimerScope* sc);
 hipEvent_t timer_event();
 void timer_release(hipEvent_t e);
 void timer_add_recorded(int cls, hipEvent_t a, hipEvent_t b);
+// RCCL exchange of a plan step (comm.hip): bucket grad[late:n) once `side_done`, then grad[0:late)
+// after the caller's stream `s`; `s` then waits for both
+int comm_exchange_step(dcue_comm* c, float* grad, long late, long n, hipEvent_t side_done, hipStream_t s);
+int comm_world(const dcue_comm* c);
+// whether this occurrence of a timed class is one to time (every stride-th; for intervals timed by
+// event records rather than a bound launch, e.g. the RCCL exchange)
+bool timer_take_turn(int cls);
 std::vector<CapturedTimer> timer_take_captured();
 
 // side streams (capi.hip): three per device, plus a ring of fork/join events

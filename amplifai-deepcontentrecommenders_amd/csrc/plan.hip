@@ -41,6 +41,10 @@ struct dcue_plan {
   long launches = 0;
   hipEvent_t tails[2] = {};       // the last launched step's end (StepOpts::tails)
   int pending_flush = -1;         // step whose rolling-flush slice the next launch issues
+  hipStream_t last_stream = nullptr;  // the caller's stream of the last launch
+  dcue_comm* comm = nullptr;      // data-parallel exchange between backward and Adam (plan_step)
+  long late = 0, n_dense = 0;     // flat-gradient floats: end of bn0/conv1/bn1, total
+  int comm_world = 1;
 };
 
 namespace {
@@ -142,6 +146,7 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   TRY(backward_impl(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, nullptr, p->cfg.emb_grad_scale, o, s));
   HPROF("plan:5");
   p->pending_flush = o.defer_flush_slice ? emb_adam->step : -1;
+  p->last_stream = s;
   ++p->launches;
   return DCUE_OK;
 }
@@ -301,9 +306,28 @@ extern "C" int dcue_plan_step(dcue_plan* p, const int64_t* users_src, const int3
   const int st = issue_eager(p, users_src, item_track_src, (hipStream_t)stream, &emb);
   if (st) return st;
   HPROF("plan_step:issue");
+  if (p->comm) {  // the DDP mean of the dense gradient: RCCL sum here, the divide inside Adam
+    TRY(dcue::comm_exchange_step(p->comm, p->model.grads, p->late, p->n_dense, p->tails[1],
+                                 (hipStream_t)stream));
+    dense.grad_div = p->comm_world;
+    HPROF("plan_step:exchange");
+  }
   const int r = dcue_adam_step(&p->model, &dense, stream);
   HPROF("plan_step:adam");
   return r;
+}
+
+extern "C" int dcue_plan_set_comm(dcue_plan* p, dcue_comm* comm) {
+  if (!p || p->exec) return DCUE_ERR_INVALID;  // eager plans only
+  p->comm = comm;
+  p->comm_world = 1;
+  if (!comm) return DCUE_OK;
+  int64_t off[DCUE_N_DENSE_SEGMENTS + 1];
+  TRY(dcue_param_layout(&p->model.dims, off));
+  p->late = off[DCUE_SEG_LATE];
+  p->n_dense = off[DCUE_N_DENSE_SEGMENTS];
+  p->comm_world = dcue::comm_world(comm);
+  return DCUE_OK;
 }
 
 extern "C" int dcue_plan_wait_side(dcue_plan* p, void* stream) {
@@ -315,6 +339,12 @@ extern "C" int dcue_plan_wait_side(dcue_plan* p, void* stream) {
 
 extern "C" int dcue_plan_destroy(dcue_plan* p) {
   if (!p) return DCUE_OK;
+  // a rolling-flush slice deferred to the next launch must still run: every row has to be replayed
+  // within `cap` steps of the current one, or the history ring it needs is overwritten
+  if (p->pending_flush >= 0 && p->model.emb_step) {
+    (void)dcue::launch_emb_flush_rows(&p->model, p->pending_flush, p->last_stream);
+    (void)hipStreamSynchronize(p->last_stream);
+  }
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->graph) (void)hipGraphDestroy(p->graph);
   for (hipEvent_t e : p->placeholders) dcue::timer_release(e);

@@ -47,6 +47,11 @@ hipEvent_t timer_event() {
 
 void timer_add_recorded(int cls, hipEvent_t a, hipEvent_t b) { ts().recorded[cls].emplace_back(a, b); }
 
+bool timer_take_turn(int cls) {
+  if (cls < 0 || cls >= DCUE_N_TIMED || !ts().stride[cls]) return false;
+  return ts().seen[cls]++ % ts().stride[cls] == 0;
+}
+
 int timer_begin(TimerScope* sc, int cls, hipStream_t s) {
   sc->cls = cls;
   sc->s = s;

@@ -71,6 +71,9 @@ TIMED_CONV1_WGRAD = 0
 TIMED_CONV1_FWD = 1
 TIMED_EMB_FLUSH = 2
 TIMED_ADAM_EMBED = 3
+TIMED_ALLREDUCE = 4
+TIMED_EMB_SLICE = 5
+COMM_ID_BYTES = 128
 
 
 class PlanConfig(ctypes.Structure):
@@ -123,6 +126,11 @@ _SIGS = {
     "dcue_plan_destroy": ([_P], ctypes.c_int),
     "dcue_plan_step": ([_P, _P, _P, ctypes.POINTER(AdamArgs), _P], ctypes.c_int),
     "dcue_plan_wait_side": ([_P, _P], ctypes.c_int),
+    "dcue_comm_unique_id": ([_P], ctypes.c_int),
+    "dcue_comm_create": ([_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "dcue_comm_destroy": ([_P], ctypes.c_int),
+    "dcue_comm_allreduce_mean": ([_P, _P, ctypes.c_int64, _P], ctypes.c_int),
+    "dcue_plan_set_comm": ([_P, _P], ctypes.c_int),
     "dcue_timer_enable": ([ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
     "dcue_timer_read": ([ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)],
                         ctypes.c_int),

@@ -114,6 +114,17 @@ class TrainPlan:
         if st != 0:
             nat.check(st, "dcue_plan_step")
 
+    def set_comm(self, comm):
+        """Data parallelism inside step(): with a distributed.NativeComm bound, each step() also
+        all-reduces the dense gradient over RCCL between the backward and Adam (two buckets, the
+        larger overlapping the conv-1 weight gradient) and Adam averages it -- one host call per
+        step, as on one GPU. Build the plan with emb_grad_scale = 1/world. None unbinds."""
+        if self._handle is None:
+            raise RuntimeError("TrainPlan was closed")
+        nat.check(self._lib.dcue_plan_set_comm(self._handle, None if comm is None else comm.handle),
+                  "dcue_plan_set_comm")
+        self._comm = comm  # keep the communicator alive while bound
+
     def wait_side(self, stream):
         """`stream` (a torch.cuda.Stream or raw handle) waits until the side-stream part of the last
         launched step is in: the flat gradient is then final past its first SEG_LATE segments

@@ -6,7 +6,21 @@ its optimizer state never cross xGMI), and the per-rank user-table Adam work is 
 is replicated. The one exchange per step is the all-reduce (sum, then / W) of the replicated dense
 gradient -- the flat buffer DCUENet keeps (393,276 fp32 at d=H=128) -- which together with
 emb_grad_scale = 1/W on the local rows reproduces DDP's mean-over-ranks gradient.
+
+Two ways to run the exchange:
+* NativeComm + TrainPlan.set_comm (the production path): libdcue_hip owns an RCCL communicator and
+  the whole data-parallel step -- sample, forward, backward, the two-bucket all-reduce overlapped
+  with the conv-1 weight gradient, Adam with the divide by W fused in -- stays ONE host call
+  (TrainPlan.step), exactly as the single-GPU step.
+* allreduce_mean_overlapped_ over a torch.distributed group: the same buckets from Python (gloo
+  on CPU tests, or several ranks sharing one GPU, which RCCL does not allow).
+
+BatchNorm running statistics are per replica during training, as under DDP without SyncBN; DDP's
+default broadcast_buffers makes every rank use rank 0's buffers, which broadcast_buffers_ does
+before evaluation or a checkpoint.
 """
+import ctypes
+
 import torch
 import torch.distributed as dist
 
@@ -89,3 +103,55 @@ def max_over_ranks(value, device, group=None):
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
+
+
+def broadcast_buffers_(net, group=None, src=0):
+    """Every rank takes rank `src`'s BN running statistics and batch counters (DDP's
+    broadcast_buffers semantics), e.g. before evaluation or saving on rank 0."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return net
+    for _, b in net.named_buffers():
+        dist.broadcast(b.data, src=src, group=group)
+    return net
+
+
+class NativeComm:
+    """An RCCL communicator owned by libdcue_hip (include/dcue.h dcue_comm_*) over the ranks of a
+    torch.distributed group, which only carries the unique id from rank 0."""
+
+    def __init__(self, group=None):
+        from . import _native as nat
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        obj = [None]
+        if self.rank == 0:
+            buf = (ctypes.c_ubyte * nat.COMM_ID_BYTES)()
+            nat.check(nat.lib().dcue_comm_unique_id(buf), "dcue_comm_unique_id")
+            obj[0] = bytes(buf)
+        dist.broadcast_object_list(obj, src=0, group=group)
+        buf = (ctypes.c_ubyte * nat.COMM_ID_BYTES).from_buffer_copy(obj[0])
+        handle = ctypes.c_void_p()
+        nat.check(nat.lib().dcue_comm_create(buf, self.world, self.rank, ctypes.byref(handle)),
+                  "dcue_comm_create")
+        self.handle = handle
+        self._lib = nat.lib()
+
+    def allreduce_mean_(self, t):
+        """In place: the mean of a GPU float32 tensor over the ranks (ordered on the current stream)."""
+        from . import _native as nat
+        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("allreduce_mean_ needs a contiguous float32 GPU tensor")
+        nat.check(self._lib.dcue_comm_allreduce_mean(self.handle, nat.ptr(t), t.numel(), nat.stream_handle()),
+                  "dcue_comm_allreduce_mean")
+        return t
+
+    def close(self):
+        if getattr(self, "handle", None) is not None:
+            self._lib.dcue_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

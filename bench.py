@@ -1,18 +1,30 @@
 #!/usr/bin/env python
 """DCUE training-step throughput on MI355X (BASELINE.json config 2; weak scaling over GPUs).
 
-One step = the reference's per-batch hot loop (nn/dcue.py:202-210) on one batch of synthetic
-input already resident in HBM: in-batch negative draws (MT19937, bit-exact with numpy) ->
-forward (item ConvNet over the batch's tracks, user tower, cosine scores, hinge loss) -> backward ->
-[RCCL all-reduce of the dense gradient when N>1] -> Adam over every parameter incl. the whole user
-table -> cyclic LR schedule. Prints ONE JSON line on rank 0.
+One step = the reference's per-batch hot loop (nn/dcue.py:202-210) on one batch of synthetic input
+already resident in HBM: negative draws (MT19937, bit-exact with numpy) -> forward (item ConvNet,
+user tower, cosine scores, hinge loss) -> backward -> [N>1: RCCL all-reduce of the dense gradient,
+overlapped with the conv-1 weight gradient] -> Adam over every parameter incl. the whole user table
+-> cyclic LR schedule. The whole step, exchange included, is one host call (TrainPlan.step).
 
-  python bench.py [--gpus N --steps K --warmup W]         (N>1: torch.distributed.run, one rank/GPU)
+Phases, each W untimed warm-up steps then EXACTLY K timed steps between barrier + synchronize:
+  1. in-batch negatives, cold user table (a fresh optimizer: most user rows have zero moments);
+  2. in-batch negatives after a pass over every local user (steady state: every row's Adam
+     moments are live) -- `value` and `ms_per_step`;
+  3. catalogue negatives (the reference's live sampler, datasets/dcuedataset.py:207-256: M =
+     B(1+N) distinct items per step) -- the `catalogue` object.
+Rank 0 prints ONE JSON line.
+
+  python bench.py [--gpus N --steps K --warmup W]
+N>1 runs one process per GPU: under torch.distributed.run (RANK/WORLD_SIZE set) or, when started
+directly, bench.py launches the N ranks itself before touching any GPU.
 """
 import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -23,13 +35,17 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+F32_PEAK_TFLOPS = 157.3   # MI355X dense FP32 (matrix and vector), MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--mode", choices=["inbatch", "catalogue"], default="inbatch")
+    ap.add_argument("--modes", default="inbatch,catalogue",
+                    help="comma list of phases after the cold one: inbatch (warm), catalogue")
     ap.add_argument("--users", type=int, default=100_000)
     ap.add_argument("--tracks", type=int, default=200_000)
     ap.add_argument("--interactions", type=int, default=5_000_000)
@@ -38,7 +54,7 @@ def parse():
     ap.add_argument("--feature-dim", type=int, default=128)
     ap.add_argument("--hidden", type=int, default=128)
     ap.add_argument("--user-embdim", type=int, default=300)
-    ap.add_argument("--cpu-steps", type=int, default=6)
+    ap.add_argument("--cpu-steps", type=int, default=10)
     ap.add_argument("--dense-embedding-adam", action="store_true",
                     help="step every user row every step (the literal sweep) instead of the deferred, "
                          "bit-identical replay")
@@ -46,12 +62,45 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-eval", action="store_true", help="skip AUC@val after the timed steps")
     ap.add_argument("--eval-pct", type=float, default=0.025, help="users sampled for AUC@val (eval_pct)")
+    ap.add_argument("--timer-stride", type=int, default=8,
+                    help="time every n-th launch of the roofline kernels live (HIP events)")
     ap.add_argument("--gpu-only", action="store_true",
-                    help="diagnostic: hold the stream behind a sleep kernel while the steps are "
-                         "enqueued, then report the GPU's own time for them (no host in the loop)")
+                    help="diagnostic: hold the stream behind a sleep kernel while the warm in-batch "
+                         "steps are enqueued, then report the GPU's own time for them")
+    ap.add_argument("--py-exchange", action="store_true",
+                    help="N>1: all-reduce from Python over torch.distributed instead of the plan's RCCL")
     return ap.parse_args()
 
 
+# ----------------------------------------------------------------------------------- launching
+def spawn_ranks(n):
+    """`bench.py --gpus N` started directly: one child process per GPU with the torch.distributed
+    env (rendezvous on 127.0.0.1), before this process touches a GPU; rank 0 prints the line."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        for p in procs:
+            r = p.wait()
+            rc = rc or r
+            if r:  # one rank failed: the others would wait in a collective forever
+                for q in procs:
+                    if q.poll() is None:
+                        q.terminate()
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+    return rc
+
+
+# ------------------------------------------------------------------------------ synthetic data
 def synthetic_tracks(n, device, seed):
     """[n][131][128] fp16 spectrograms (randn rounded to fp16: lossless in the fp16 table)."""
     gen = torch.Generator(device=device).manual_seed(seed)
@@ -77,6 +126,19 @@ def song_split(n_tracks):
     return code
 
 
+def item_flops(H, d):
+    """Forward FLOPs of the item tower per spectrogram at full conv lengths (23.2 MFLOP at H=d=128)."""
+    return 2 * (128 * 4 * H * 132 + H * 4 * H * 34 + H * 4 * H * 9 + H * 2 * H * 3 + H * d + d * d)
+
+
+def row_flops(args, items_per_row):
+    """SURVEY §8(d) canonical work per row: 3 x forward (fwd + bwd) of the item tower over the
+    row's items plus the user tower (1.462 GFLOP catalogue, 70.4 MFLOP compact in-batch)."""
+    E, d = args.user_embdim, args.feature_dim
+    return 3 * item_flops(args.hidden, d) * items_per_row + 3 * 2 * (E * E + E * d)
+
+
+# --------------------------------------------------------------------------------- evaluation
 def evaluate_val(args, net, tracks, pair_user, pair_track, split, n_users, dev):
     """Item factors of every track (eval tower), user factors of every user, then the split-weighted
     AUC / mAP of DCUE.score for an eval_pct sample of the users with train and val interactions."""
@@ -116,8 +178,7 @@ def evaluate_val(args, net, tracks, pair_user, pair_track, split, n_users, dev):
     key = np.unique(pu * np.int64(n_tracks) + pt)
     u_of, t_of = key // n_tracks, (key % n_tracks).astype(np.int32)
     ptr = np.zeros(n_users + 1, np.int64)
-    np.add.at(ptr, u_of + 1, 1)
-    ptr = np.cumsum(ptr)
+    ptr[1:] = np.cumsum(np.bincount(u_of, minlength=n_users))
     cls = np.where(split == 1, rank.LIST_PRED, 0).astype(np.uint8) | np.where(split == 0, rank.LIST_TRUTH, 0).astype(np.uint8)
     sp = split[t_of]
     has_train = np.zeros(n_users, bool)
@@ -131,53 +192,71 @@ def evaluate_val(args, net, tracks, pair_user, pair_track, split, n_users, dev):
     auc, ap, ok = ev.metrics(user_f, item_f, sample, nat.RANK_SPLIT)
     t_rank = time.perf_counter() - t1
     net.train()
-    H = args.hidden
-    # eval item tower FLOPs per track at full conv lengths (23.2 MFLOP at H=d=128)
-    flops = 2 * (128 * 4 * H * 132 + H * 4 * H * 34 + H * 4 * H * 9 + H * 2 * H * 3 + H * d + d * d)
+    flops = item_flops(args.hidden, d)
     return {"auc": rank.mean_until_missing(auc, ok), "map_val": rank.mean_until_missing(ap, ok),
             "users": int(len(sample)), "candidates": int(n_tracks), "factors_s": t_factors, "rank_s": t_rank,
             "item_tower_s": t_items, "item_tower_tflops": flops * n_tracks / t_items / 1e12,
             "note": "random-init model after the bench steps on synthetic data: AUC ~0.5 is expected"}
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, n_users_local):
-    """The oracle (torch-CPU restatement of the reference step) on a bounded sample of the same
-    workload: in-batch negatives are copies of positives run through the tower, as the reference's
-    in-batch sampler builds them (nn/dcue.py:698-709)."""
+    """The oracle (torch-CPU restatement of the reference step, pinned to the reference's golden
+    vectors) on the host cores: warm-up 2 steps, then the median of --cpu-steps steps (SURVEY
+    §8(d)). Like the reference, it runs the item tower over the literal [pos; neg] stack of
+    B(1+N) spectrograms, in-batch negatives being copies of positives (nn/dcue.py:698-709) --
+    the GPU's compact in-batch layout runs the tower once per distinct item (B = 64), so part of
+    the in-batch GPU/CPU ratio is that 21x reuse; catalogue mode does the same work on both."""
     from oracle import dcue_oracle as O
+    affinity = len(os.sched_getaffinity(0))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
+    threads = max(1, min(threads, affinity))
+    torch.set_num_threads(threads)
     torch.manual_seed(0)
     B, N = args.batch, args.neg
     p, b = O.init_params(args.feature_dim, args.hidden, args.user_embdim, n_users_local)
     adam = O.AdamState(p)
     rs = np.random.RandomState(0)
     gen = torch.Generator().manual_seed(1)
-    batches = []
-    for _ in range(args.cpu_steps + 2):
+    times = []
+    for s in range(args.cpu_steps + 2):
         u = torch.randint(0, n_users_local, (B,), generator=gen)
         pos = torch.randn(B, 128, 131, generator=gen).half().float()
         r = torch.from_numpy(O.inbatch_negatives(rs, B, N))
-        batches.append((u, pos, pos[r.reshape(-1)].reshape(B, N, 128, 131)))
-    for u, pos, neg in batches[:2]:
+        neg = pos[r.reshape(-1)].reshape(B, N, 128, 131)
+        t0 = time.perf_counter()
         O.train_step(p, b, adam, u, pos, neg, 1e-5)
-    t0 = time.perf_counter()
-    for u, pos, neg in batches[2:]:
-        O.train_step(p, b, adam, u, pos, neg, 1e-5)
-    dt = time.perf_counter() - t0
-    rows = B * args.cpu_steps / dt
-    return {"value": rows * N, "unit": "triplets/s", "rows_per_s": rows, "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": "%d oracle train steps (after 2 warm-up) at B=%d, N=%d in-batch, d=%d, H=%d, "
-                      "%d users, torch-CPU fp32, %.1f s" % (args.cpu_steps, B, N, args.feature_dim,
-                                                            args.hidden, n_users_local, dt)}
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times[2:]))
+    rows = B / med
+    return {"value": rows * N, "unit": "triplets/s", "rows_per_s": rows, "cores": threads, "kind": "port",
+            "host_cpus_visible": affinity, "cpu_model": cpu_model(),
+            "sample": "median of %d oracle train steps (after 2 warm-up) at B=%d, N=%d, d=%d, H=%d, %d users, "
+                      "torch-CPU fp32 on %d threads; the reference-literal %d-item [pos; neg] stack per step "
+                      "(the GPU's in-batch step runs the compact %d-item tower)"
+                      % (args.cpu_steps, B, N, args.feature_dim, args.hidden, n_users_local, threads, B * (1 + N), B),
+            "ms_per_step_median": med * 1e3}
 
 
+# ---------------------------------------------------------------------------------------- main
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; DCUE_DIST_BACKEND=gloo rehearses the N>1 path with several ranks on one
-    # GPU (local ranks wrap over the visible devices), RCCL ("nccl") otherwise
+    # GPU (local ranks wrap over the visible devices; the exchange then runs from Python)
     backend = os.environ.get("DCUE_DIST_BACKEND", "nccl")
     local = local % torch.cuda.device_count() if backend != "nccl" else local
     torch.cuda.set_device(local)
@@ -196,6 +275,7 @@ def main():
     from dcrecommend.dcue.plan import TrainPlan
 
     B, N = args.batch, args.neg
+    modes = [m for m in args.modes.split(",") if m]
     # users are sharded across ranks (row u of rank r = global user u*world + r): each rank owns its
     # users' embedding rows + Adam moments; the track table is replicated
     n_users_local = D.local_user_count(args.users, rank, world)
@@ -222,137 +302,253 @@ def main():
     sched = CyclicLRWithRestarts(opt, B, epoch_size=epoch_size, restart_period=30, t_mult=2, policy="cosine")
     sched.step()
 
+    def sched_step():
+        try:
+            sched.batch_step()
+        except StopIteration:  # the sub-epoch's batch count is spent: the trainer's next sched.step()
+            sched.step()
+            sched.batch_step()
+
     # batch composition (DataLoader shuffle over the interaction rows) is prepared ahead, like the
-    # reference's worker processes; the step consumes HBM-resident index vectors
-    total = args.warmup + args.steps
-    perm = train_pairs[torch.randperm(train_pairs.numel(), generator=gen, device=dev)[: total * B]].view(total, B)
-    users_b = pair_user[perm].contiguous()
-    items_b = pair_track[perm].to(torch.int32).contiguous()
+    # reference's worker processes; every step consumes HBM-resident index vectors
+    def batches(n_steps):
+        perm = train_pairs[torch.randint(0, train_pairs.numel(), (n_steps * B,), generator=gen, device=dev)]
+        return pair_user[perm].view(n_steps, B).contiguous(), pair_track[perm].to(torch.int32).view(n_steps, B).contiguous()
+
+    # one pass over every local user with a train interaction (the steady state's precondition)
+    u_t = pair_user[train_pairs]
+    order = torch.argsort(u_t, stable=True)
+    first = torch.ones_like(order, dtype=torch.bool)
+    first[1:] = u_t[order][1:] != u_t[order][:-1]
+    cover = train_pairs[order[first]]
+    cover = cover[torch.randperm(cover.numel(), generator=gen, device=dev)]
+    n_cover = cover.numel() // B * B
+    warm_users = pair_user[cover[:n_cover]].view(-1, B).contiguous()
+    warm_items = pair_track[cover[:n_cover]].to(torch.int32).view(-1, B).contiguous()
+
     mt = torch.empty(nat.MT_STATE_BYTES, dtype=torch.uint8, device=dev)
     nat.check(nat.lib().dcue_mt_seed(nat.ptr(mt), 10 + rank, nat.stream_handle()), "mt_seed")
     G = net._flat["G"]
     G_late = D.late_grad_floats(net)
-    TIMED = nat.TIMED_CONV1_WGRAD  # the roofline kernel, timed live by HIP events in the library
-    TIMER_STRIDE = 8
+    native_exchange = world > 1 and backend == "nccl" and not args.py_exchange
+    comm, comm_error = None, None
+    if native_exchange:
+        try:
+            comm = D.NativeComm()
+        except RuntimeError as e:  # reported in the line; the step then all-reduces from Python
+            comm_error = str(e)
 
-    catalogue = args.mode == "catalogue"
-    if catalogue:
-        # the reference's live sampler (datasets/dcuedataset.py:207-220): N negatives per row drawn
-        # from the train split's songs the user never interacted with; the conv runs on all
-        # M = B(1+N) distinct items. The user -> split-rank CSR covers every interaction.
-        from dcrecommend.datasets.csr import user_split_ranks
+    timed = [nat.TIMED_CONV1_WGRAD, nat.TIMED_CONV1_FWD, nat.TIMED_EMB_SLICE, nat.TIMED_ALLREDUCE]
+    # every stride-th launch of each class is timed live (a timed launch costs its stream a few us)
+    stride = max(1, min(args.timer_stride, args.steps // 4))
+
+    def make_plan(catalogue):
+        plan = TrainPlan(net, tracks, B, N, mt_state=None if catalogue else mt, emb_grad_scale=1.0 / world,
+                         optimizer=opt)
+        if comm is not None:
+            plan.set_comm(comm)
+        return plan
+
+    def run(plan, step_fn, n):
+        for s in range(n):
+            step_fn(plan, s)
+
+    def inbatch_step(users_b, items_b):
+        def fn(plan, s):
+            if world > 1 and comm is None:
+                plan.launch(users_b[s], items_b[s])
+                D.allreduce_mean_overlapped_(plan, G, G_late)
+                opt.step()
+            else:
+                plan.step(users_b[s], items_b[s])  # sample + fwd + bwd (+ RCCL) + Adam: one host call
+            sched_step()
+        return fn
+
+    def timed_phase(plan, step_fn, gpu_only=False):
+        """W warm-up steps, then EXACTLY K timed steps between barrier + synchronize on both
+        sides; max over ranks. Returns (seconds, host enqueue seconds, gpu-only ms or None)."""
+        run(plan, step_fn, args.warmup)
+        opt.flush()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        for k in timed:
+            nat.timer_enable(k, stride)  # from the first timed step on (restarts the stride count)
+        ev0 = ev1 = None
+        if gpu_only:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(int(2.4e6 * args.steps))  # ~1 ms of GPU per step (2.4 GHz cycles)
+            ev0.record()
+        t0 = time.perf_counter()
+        run(plan, lambda p, s: step_fn(p, args.warmup + s), args.steps)
+        opt.flush()  # deferred user-table steps still pending are part of the timed work
+        t_enq = time.perf_counter() - t0
+        if gpu_only:
+            ev1.record()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = D.max_over_ranks(time.perf_counter() - t0, dev)
+        kern = {k: nat.timer_read(k) for k in timed}
+        for k in timed:
+            nat.timer_enable(k, False)
+        return dt, t_enq, (ev0.elapsed_time(ev1) / args.steps if gpu_only else None), kern
+
+    def kernel_rooflines(kern, M, steps):
+        """Live HIP-event timing of the candidate kernels: per launch and per step, with each
+        one's algorithmic work against its roofline."""
+        H, E = args.hidden, args.user_embdim
+        conv1 = 2.0 * H * 128 * 4 * (M * 132)
+        rows_slice = n_users_local / args.flush_every
+        spec = {
+            nat.TIMED_CONV1_WGRAD: ("k_conv1_wgrad (conv-1 weight gradient, f32 MFMA 32x32x2)", "mfma", conv1),
+            nat.TIMED_CONV1_FWD: ("k_conv_rows<0,0> layer 1 (conv-1 forward + pool + BN partials, f32 MFMA)",
+                                  "mfma", conv1),
+            nat.TIMED_EMB_SLICE: ("k_emb_flush_rows (deferred user-table Adam, one rolling slice)", "hbm",
+                                  24.0 * rows_slice * E),
+            nat.TIMED_ALLREDUCE: ("RCCL all-reduce of the dense gradient (per bucket)", "xgmi", None),
+        }
+        out = []
+        for k, (ms, n) in kern.items():
+            if n == 0:
+                continue
+            name, bound, work = spec[k]
+            avg = ms / n
+            # launches per step from the timer stride (every stride-th launch is timed)
+            per_step = n * stride / steps
+            ent = {"kernel": name, "bound": bound, "avg_ms": avg, "launches_timed": n,
+                   "ms_per_step": avg * per_step}
+            if bound == "mfma":
+                ent.update(achieved=work / (avg * 1e-3) / 1e12, peak=F32_PEAK_TFLOPS, unit="TFLOP/s",
+                           algorithmic_flops=work)
+                ent["frac"] = ent["achieved"] / F32_PEAK_TFLOPS
+            elif bound == "hbm":
+                ent.update(achieved=work / (avg * 1e-3) / 1e9, peak=HBM_PEAK_GBS, unit="GB/s",
+                           algorithmic_bytes=work)
+                ent["frac"] = ent["achieved"] / HBM_PEAK_GBS
+            out.append(ent)
+        out.sort(key=lambda e: -e["ms_per_step"])
+        return out
+
+    def traffic_for(kernel_name, mode):
+        tag = {"k_conv1_wgrad": "conv1_wgrad"}.get(kernel_name.split(" ")[0])
+        path = os.path.join(ROOT, "profiles", "pmc_%s_%s.json" % (tag, mode)) if tag else None
+        if path and os.path.exists(path):
+            try:
+                return json.load(open(path)).get("hbm_bytes_per_launch")
+            except (ValueError, OSError):
+                return None
+        return None
+
+    def summary(dt, t_enq, kern, M, items_per_row, mode):
+        rows = world * B * args.steps / dt
+        ks = kernel_rooflines(kern, M, args.steps)
+        mf = [k for k in ks if k["bound"] in ("mfma", "hbm")]
+        roof = dict(mf[0]) if mf else {}
+        if roof:
+            roof["traffic"] = traffic_for(roof["kernel"], mode)
+        flops_row = row_flops(args, items_per_row)
+        roof["step_frac"] = rows / world * flops_row / (F32_PEAK_TFLOPS * 1e12)
+        roof["step_flops_per_row"] = flops_row
+        res = {"ms_per_step": dt / args.steps * 1e3, "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
+               "rows_per_s": rows, "triplets_per_s": rows * N, "roofline": roof, "kernels": ks}
+        ar = [k for k in ks if k["bound"] == "xgmi"]
+        if ar:
+            res["allreduce_ms_per_step"] = ar[0]["ms_per_step"]
+        return res
+
+    out = {}
+    # ---- phase 1: in-batch, cold user table
+    plan = make_plan(False)
+    ub, ib = batches(args.warmup + args.steps)
+    dt, t_enq, _, kern = timed_phase(plan, inbatch_step(ub, ib))
+    out["inbatch_cold"] = summary(dt, t_enq, kern, B, 1, "inbatch")
+    # ---- phase 2: every local user once (outside any timed region), then in-batch steady state
+    warm = inbatch_step(warm_users, warm_items)
+    run(plan, warm, warm_users.shape[0])
+    if "inbatch" in modes:
+        ub, ib = batches(args.warmup + args.steps)
+        dt, t_enq, gpu_ms, kern = timed_phase(plan, inbatch_step(ub, ib), gpu_only=args.gpu_only)
+        out["inbatch"] = summary(dt, t_enq, kern, B, 1, "inbatch")
+        if gpu_ms is not None:
+            out["inbatch"]["gpu_only_ms_per_step"] = gpu_ms
+    plan.close()
+    # ---- phase 3: catalogue negatives (the reference's live sampler)
+    if "catalogue" in modes:
+        from dcrecommend.datasets.csr import check_catalogue_users, saturated_users, user_split_ranks
         split_items = np.nonzero(split == 0)[0].astype(np.int64)
-        indptr, ranks = user_split_ranks(pair_user.cpu().numpy(), pair_track.cpu().numpy(), n_users_local,
-                                         split_items)
+        indptr, ranks_ = user_split_ranks(pair_user.cpu().numpy(), pair_track.cpu().numpy(), n_users_local,
+                                          split_items)
+        sat = saturated_users(indptr, len(split_items))
         split_d64 = torch.from_numpy(split_items).to(dev)
         indptr_d = torch.from_numpy(indptr).to(dev)
-        ranks_d = torch.from_numpy(ranks).to(dev)
-        items_b64 = items_b.long()
+        ranks_d = torch.from_numpy(ranks_).to(dev)
         negs = torch.empty((B, N), dtype=torch.int64, device=dev)
+        cplan = make_plan(True)
+        ub, ib = batches(args.warmup + args.steps)
+        check_catalogue_users(ub.cpu().numpy(), sat)
+        ib64 = ib.long()
 
-    # The roofline kernel's timer is on before the plan is built. It binds a HIP event pair to every
-    # TIMER_STRIDE-th launch of the kernel (its own dispatch's start and end, on the stream it runs
-    # on); a timed launch costs the stream a few microseconds, so a sample is timed, not every step.
-    nat.timer_enable(TIMED, TIMER_STRIDE)
-    plan = TrainPlan(net, tracks, B, N, mt_state=None if catalogue else mt, emb_grad_scale=1.0 / world,
-                     optimizer=opt)
-
-    def sample_catalogue(s):
-        nat.check(nat.lib().dcue_sample_catalogue(nat.ptr(mt), 0, 0, nat.ptr(split_d64), split_d64.numel(),
-                                                  nat.ptr(indptr_d), nat.ptr(ranks_d), nat.ptr(users_b[s]), B, N,
-                                                  nat.ptr(negs), nat.stream_handle()), "dcue_sample_catalogue")
-        nat.check(nat.lib().dcue_build_catalogue_batch(nat.ptr(items_b64[s]), nat.ptr(negs), B, N,
-                                                       nat.ptr(plan.item_track), nat.stream_handle()),
-                  "dcue_build_catalogue_batch")
-
-    def step(s):
-        if catalogue:
-            sample_catalogue(s)
-            src = (users_b[s], None)
-        else:
-            src = (users_b[s], items_b[s])
-        if world > 1:
-            plan.launch(*src)
-            # RCCL: the one exchange of the step (1.57 MB), in two buckets; the larger one overlaps
-            # the conv-1 weight gradient
-            D.allreduce_mean_overlapped_(plan, G, G_late)
-            opt.step()
-        else:
-            plan.step(*src)  # sample + forward + backward + Adam, one host call
-        sched.batch_step()
-
-    for s in range(args.warmup):
-        step(s)
-    opt.flush()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    nat.timer_read(TIMED)  # drop the warm-up records
-    if args.gpu_only:
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda._sleep(int(2.4e6 * args.steps))  # ~1 ms of GPU per step (2.4 GHz cycles)
-        ev0.record()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(args.warmup + k)
-    opt.flush()  # deferred user-table steps still pending are part of the timed work
-    t_enq = time.perf_counter() - t0  # host time to enqueue the steps (diagnostic)
-    if args.gpu_only:
-        ev1.record()
-    torch.cuda.synchronize()
-    if args.gpu_only:
-        print(json.dumps({"gpu_only_ms_per_step": ev0.elapsed_time(ev1) / args.steps,
-                          "host_enqueue_ms_per_step": t_enq / args.steps * 1e3}))
-    nat.timer_enable(TIMED, False)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    dt = D.max_over_ranks(dt, dev)
-
-    rows = world * B * args.steps / dt
-    wg_ms, wg_n = nat.timer_read(TIMED)
-    wg_ms = wg_ms / max(wg_n, 1)
-    # algorithmic FLOPs of one conv-1 weight-gradient launch: dW1[o][c][k] summed over every conv-1
-    # output row (item, position) of the batch's distinct items -- B items x 132 positions (131
-    # frames, kernel 4, padding 2) x 128 mel inputs x 4 taps x H outputs, 2 FLOP per product
-    M_items = B * (1 + N) if catalogue else B
-    wg_flops = 2.0 * args.hidden * 128 * 4 * (M_items * 132)
-    achieved = wg_flops / (wg_ms * 1e-3) / 1e12
-    traffic = None
-    tf_path = os.path.join(ROOT, "profiles", "pmc_conv1_wgrad.json")
-    if os.path.exists(tf_path) and not catalogue:  # collected on the default (in-batch) workload
-        try:
-            traffic = json.load(open(tf_path)).get("hbm_bytes_per_launch")
-        except (ValueError, OSError):
-            traffic = None
+        def cat_step(plan, s):
+            nat.check(nat.lib().dcue_sample_catalogue(nat.ptr(mt), 0, 0, nat.ptr(split_d64), split_d64.numel(),
+                                                      nat.ptr(indptr_d), nat.ptr(ranks_d), nat.ptr(ub[s]), B, N,
+                                                      nat.ptr(negs), nat.stream_handle()), "dcue_sample_catalogue")
+            nat.check(nat.lib().dcue_build_catalogue_batch(nat.ptr(ib64[s]), nat.ptr(negs), B, N,
+                                                           nat.ptr(cplan.item_track), nat.stream_handle()),
+                      "dcue_build_catalogue_batch")
+            if world > 1 and comm is None:
+                plan.launch(ub[s], None)
+                D.allreduce_mean_overlapped_(plan, G, G_late)
+                opt.step()
+            else:
+                plan.step(ub[s], None)
+            sched_step()
+        dt, t_enq, _, kern = timed_phase(cplan, cat_step)
+        out["catalogue"] = summary(dt, t_enq, kern, B * (1 + N), 1 + N, "catalogue")
+        cplan.close()
+    head = out.get("inbatch", out["inbatch_cold"])
     E = args.user_embdim
-
     result = {
         "metric": "training triplets/sec (whole node) + AUC@val, DCUE d=128 at 1/2/4/8 MI355X",
-        "value": rows * N,
+        "value": head["triplets_per_s"],
         "unit": "triplets/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": dt / args.steps * 1e3,
-        "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
+        "ms_per_step": head["ms_per_step"],
+        "host_enqueue_ms_per_step": head["host_enqueue_ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
-        "rows_per_s": rows,
+        "rows_per_s": head["rows_per_s"],
         "auc_val": None,
         "config": {"workload": "DCUE truedcuemel1dbn d=%d H=%d E=%d, %d users x %d tracks (fp16 table), "
-                               "%d interactions, %s negatives N=%d"
-                               % (args.feature_dim, args.hidden, E, args.users, args.tracks,
-                                  args.interactions, "catalogue" if catalogue else "in-batch", N),
+                               "%d interactions, in-batch negatives N=%d"
+                               % (args.feature_dim, args.hidden, E, args.users, args.tracks, args.interactions, N),
+                   "regime": ("steady state: every local user's Adam moments live (one pass over all users "
+                              "before the timed steps)") if "inbatch" in out else "cold user table",
                    "batch_per_gpu": B, "global_batch": B * world, "neg": N,
-                   "parallelism": "dp%d (users sharded, dense grads all-reduced)" % world},
-        "roofline": {"kernel": "k_conv1_wgrad (conv layer 1 weight gradient, f32 MFMA 32x32x2)", "bound": "mfma",
-                     "achieved": achieved, "peak": 157.3, "unit": "TFLOP/s", "frac": achieved / 157.3,
-                     "traffic": traffic, "avg_ms": wg_ms, "launches": wg_n, "algorithmic_flops": wg_flops},
+                   "parallelism": "dp%d (users sharded, dense grads all-reduced)" % world,
+                   "exchange": ("RCCL inside the plan step (libdcue_hip)" if comm is not None else
+                                "torch.distributed (%s) from Python%s" % (
+                                    backend, "; native RCCL failed: " + comm_error if comm_error else ""))
+                               if world > 1 else None,
+                   "process_group_world": dist.get_world_size() if world > 1 else 1},
+        "roofline": head["roofline"],
+        "kernels": head["kernels"],
+        "inbatch_cold": {k: out["inbatch_cold"][k] for k in ("ms_per_step", "rows_per_s", "triplets_per_s",
+                                                             "host_enqueue_ms_per_step")},
     }
+    if "allreduce_ms_per_step" in head:
+        result["allreduce_ms_per_step"] = head["allreduce_ms_per_step"]
+    if "gpu_only_ms_per_step" in head:
+        result["gpu_only_ms_per_step"] = head["gpu_only_ms_per_step"]
+    if "catalogue" in out:
+        result["catalogue"] = out["catalogue"]
+    if world > 1:
+        D.broadcast_buffers_(net)  # DDP semantics: evaluate with rank 0's BN statistics
     if rank == 0 and not args.no_eval:
         # AUC@val of the trained model (outside the timed region): DCUE.score over an eval_pct
         # sample of this rank's users (nn/dcue.py:380-449, 580-603) on the GPU evaluator
@@ -363,13 +559,10 @@ def main():
         result["cpu_baseline"] = cpu_baseline(args, n_users_local)
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
-
-
-def ctypes_ref(x):
-    import ctypes
-    return ctypes.byref(x)
 
 
 if __name__ == "__main__":

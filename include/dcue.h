@@ -273,6 +273,27 @@ int dcue_plan_step(dcue_plan* plan, const int64_t* users_src, const int32_t* ite
 int dcue_plan_wait_side(dcue_plan* plan, void* stream);
 int dcue_plan_destroy(dcue_plan* plan);
 
+/* ------------------------------------------------- data-parallel gradient exchange (RCCL) */
+/* One process per GPU; users are sharded over the ranks, so the only exchange of a step is the
+ * mean over ranks of the replicated dense gradient (the flat buffer, dcue_param_layout). The
+ * library drives RCCL itself so that a data-parallel step stays one host call (dcue_plan_step).
+ * The caller ships the unique id from rank 0 to the others (e.g. over torch.distributed). */
+typedef struct dcue_comm dcue_comm;
+#define DCUE_COMM_ID_BYTES 128
+int dcue_comm_unique_id(void* id_host); /* rank 0: DCUE_COMM_ID_BYTES bytes */
+/* A communicator over `world` ranks on the current HIP device (collective: every rank calls it). */
+int dcue_comm_create(const void* id_host, int32_t world, int32_t rank, dcue_comm** comm_host);
+int dcue_comm_destroy(dcue_comm* comm);
+/* In-place mean over the ranks of n floats, ordered on `stream` (sum all-reduce, then / world). */
+int dcue_comm_allreduce_mean(dcue_comm* comm, float* buf, int64_t n, void* stream);
+/* Bind (or, with NULL, unbind) a communicator to an eager plan. dcue_plan_step then exchanges the
+ * dense gradient between the backward and Adam, in two buckets on the communicator's stream: the
+ * gradients the side streams finish (everything after DCUE_SEG_LATE) as soon as they are in,
+ * overlapping the conv-1 weight gradient on the caller's stream, then bn0/conv-1/bn1 once the step
+ * ends; Adam then divides by the world size (dcue_adam_args.grad_div) in its sweep. Collective
+ * order is the same on every rank. The plan must have been created with emb_grad_scale = 1/world. */
+int dcue_plan_set_comm(dcue_plan* plan, dcue_comm* comm);
+
 /* ------------------------------------------------------------------- live kernel timing */
 /* enable = n > 0: every n-th launch of the kernel class (also inside plans created afterwards)
  * gets a HIP event pair bound to the launch itself (its dispatch's start and end); 0 disables.
@@ -282,7 +303,9 @@ int dcue_plan_destroy(dcue_plan* plan);
 #define DCUE_TIMED_CONV1_FWD 1   /* conv layer-1 forward */
 #define DCUE_TIMED_EMB_FLUSH 2   /* deferred user-table Adam: full-table flush */
 #define DCUE_TIMED_ADAM_EMBED 3  /* dense user-table Adam sweep */
-#define DCUE_N_TIMED 4
+#define DCUE_TIMED_ALLREDUCE 4    /* a plan's RCCL gradient exchange (each bucket's all-reduce) */
+#define DCUE_TIMED_EMB_SLICE 5    /* deferred user-table Adam: one step's rolling-flush slice */
+#define DCUE_N_TIMED 6
 int dcue_timer_enable(int32_t kernel, int32_t enable);
 int dcue_timer_read(int32_t kernel, double* total_ms_host, int64_t* launches_host);
 

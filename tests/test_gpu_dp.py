@@ -47,3 +47,125 @@ def test_overlapped_allreduce_matches_plain(tmp_path):
     parts = [torch.load(os.path.join(tmp_path, "r%d.pt" % r), weights_only=True) for r in range(world)]
     assert torch.equal(parts[0]["G"], parts[1]["G"])  # the mean is the same on every rank
     assert 0 < parts[0]["late"] < parts[0]["G"].numel()
+
+
+def _pair_nets(n_users=40, E=40):
+    from dcrecommend.dcue.dcue import DCUENet
+    nets = []
+    for _ in range(2):
+        torch.manual_seed(5)
+        nets.append(DCUENet({"feature_dim": 32, "conv_hidden": 32, "user_embdim": E, "user_count": n_users,
+                             "model_type": "truedcuemel1dbn"}).cuda().train())
+    return nets
+
+
+def _full_state(net, opt):
+    out = {k: v.detach().clone() for k, v in net.state_dict().items()}
+    st = opt._adam_state()
+    for k in ("m", "v", "em", "ev"):
+        out["adam." + k] = st[k].clone()
+    out["grad"] = net._flat["G"].clone()
+    return out
+
+
+def test_native_exchange_in_plan_step_world1():
+    """The plan's own RCCL exchange (dcue_plan_set_comm) on a one-rank communicator: the step with
+    the exchange bound (events, comm stream, both buckets, Adam's divide) is bit-exact with the step
+    without it. (RCCL refuses two ranks on one GPU, so the multi-rank numbers come from the 8-GPU
+    bench; the bucket arithmetic itself is covered by test_overlapped_allreduce_matches_plain.)"""
+    import torch.distributed as dist
+    from dcrecommend import distributed as D
+    from dcrecommend.dcue.plan import TrainPlan
+    from dcrecommend.optim import NativeAdam
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1)
+    try:
+        comm = D.NativeComm()
+        assert comm.world == 1 and comm.rank == 0
+        a, b = _pair_nets()
+        gen = torch.Generator(device="cuda:0").manual_seed(11)
+        tracks = torch.randn((48, 131, 128), generator=gen, device="cuda:0").half()
+        opts = [NativeAdam(n.parameters(), 1e-3, (0.9, 0.99), 1e-8, 0, defer_embedding=True, flush_every=4)
+                for n in (a, b)]
+        B, N = 8, 3
+        plans = [TrainPlan(n, tracks, B, N, mt_state=None, optimizer=o) for n, o in zip((a, b), opts)]
+        plans[0].set_comm(comm)
+        for _ in range(6):
+            users = torch.randint(0, 40, (B,), generator=gen, device="cuda:0")
+            items = torch.randint(0, 48, (B * (1 + N),), generator=gen, device="cuda:0").to(torch.int32)
+            for p in plans:
+                p.step(users, items)
+        for o in opts:
+            o.flush()
+        torch.cuda.synchronize()
+        sa, sb = _full_state(a, opts[0]), _full_state(b, opts[1])
+        for k in sa:
+            assert torch.equal(sa[k], sb[k]), k
+        t = torch.arange(1000, dtype=torch.float32, device="cuda:0")
+        comm.allreduce_mean_(t)
+        assert torch.equal(t.cpu(), torch.arange(1000, dtype=torch.float32))
+        for p in plans:
+            p.close()
+        comm.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_adam_grad_div_is_the_ddp_mean():
+    """dcue_adam_args.grad_div = W on a summed gradient == the step on the mean (W a power of two:
+    both exact), and the gradient buffer holds the mean afterwards (grad.div_(world) semantics)."""
+    import ctypes
+    from dcrecommend import _native as nat
+    from dcrecommend.optim import NativeAdam
+    a, b = _pair_nets()
+    gen = torch.Generator(device="cuda:0").manual_seed(3)
+    tracks = torch.randn((48, 131, 128), generator=gen, device="cuda:0").half()
+    users = torch.randint(0, 40, (8,), generator=gen, device="cuda:0")
+    items = torch.randint(0, 48, (32,), generator=gen, device="cuda:0").to(torch.int32)
+    opts = []
+    for n in (a, b):
+        n.native_forward(users, tracks, items, 3, nat.LAYOUT_CATALOGUE, None, train=True)
+        n.native_backward(None)
+        opts.append(NativeAdam(n.parameters(), 1e-3, (0.9, 0.99), 1e-8, 0))
+    a._flat["G"].mul_(4.0)  # as if 4 ranks had summed this rank's gradient
+    for n, o, div in ((a, opts[0], 4.0), (b, opts[1], 0.0)):
+        st = o._adam_state()
+        args = nat.AdamArgs(1e-3, 0.9, 0.99, 1e-8, 0.0, 1, nat.ADAM_DENSE, div)
+        nat.check(nat.lib().dcue_adam_step(ctypes.byref(n._model_struct(st)), ctypes.byref(args),
+                                           nat.stream_handle()), "dcue_adam_step")
+    torch.cuda.synchronize()
+    assert torch.equal(a._flat["G"], b._flat["G"])
+    assert torch.equal(a._flat["P"], b._flat["P"])
+
+
+def _bench(args, env=None, timeout=240):
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                         timeout=timeout, env=dict(os.environ, **(env or {})))
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    import json
+    return json.loads(lines[0])
+
+
+SMALL = ["--steps", "3", "--warmup", "1", "--no-eval", "--no-cpu-baseline", "--users", "3000", "--tracks",
+         "4000", "--interactions", "60000"]
+
+
+def test_bench_single_gpu_line():
+    """The bench line's contract fields at a small workload: the steady-state in-batch value, the
+    cold in-batch and the catalogue phases, kernel rooflines with the step-level fraction."""
+    r = _bench(SMALL)
+    assert r["n_gpus"] == 1 and r["value"] > 0 and r["unit"] == "triplets/s"
+    assert r["catalogue"]["rows_per_s"] > 0 and r["inbatch_cold"]["rows_per_s"] > 0
+    assert 0 < r["roofline"]["step_frac"] < 1
+    assert r["kernels"] and all(k["avg_ms"] > 0 for k in r["kernels"])
+
+
+def test_bench_launches_its_own_ranks():
+    """`bench.py --gpus 2` started directly (no torch.distributed.run) spawns two ranks before any
+    GPU call; here both share the one GPU over gloo with the Python exchange (RCCL needs a GPU per
+    rank); rank 0 prints the single line with the whole-job numbers."""
+    r = _bench(["--gpus", "2"] + SMALL, env={"DCUE_DIST_BACKEND": "gloo"})
+    assert r["n_gpus"] == 2 and r["config"]["process_group_world"] == 2
+    assert r["config"]["global_batch"] == 2 * r["config"]["batch_per_gpu"]
+    assert r["value"] > 0 and r["catalogue"]["rows_per_s"] > 0

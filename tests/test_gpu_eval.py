@@ -202,13 +202,25 @@ def test_trainer_fit_and_checkpoint(golden, tmp_path):
 def test_train_dcue_driver_synthetic(tmp_path):
     """train_dcue.py (the reference README's train_* driver) end to end on synthetic files."""
     import train_dcue
-    dcue = train_dcue.main(["--synthetic", "--synthetic-users", "24", "--synthetic-tracks", "40",
+    dcue = train_dcue.main(["--synthetic", "--synthetic-users", "24", "--synthetic-tracks", "80",
                             "--synthetic-pairs", "300", "--feature-dim", "32", "--conv-hidden", "32",
                             "--batch-size", "8", "--neg-batch-size", "3", "--num-epochs", "1",
                             "--eval-pct", "1.0", "--lr", "1e-3", "--save-dir", str(tmp_path)])
     assert dcue._plan_n == 3 and dcue.nn_epoch >= 9
     assert 0.0 <= dcue.best_val_auc <= 1.0
     assert os.listdir(tmp_path)
+
+
+def test_saturated_user_raises_like_numpy(tmp_path):
+    """40 tracks: the val split holds 3 songs and one user has all of them, so the reference's
+    np.random.choice over that user's (empty) non-items raises ValueError
+    (datasets/dcuedataset.py:219); the GPU sampler's host check raises the same error."""
+    import train_dcue
+    with pytest.raises(ValueError, match="cannot be empty"):
+        train_dcue.main(["--synthetic", "--synthetic-users", "24", "--synthetic-tracks", "40",
+                         "--synthetic-pairs", "300", "--feature-dim", "32", "--conv-hidden", "32",
+                         "--batch-size", "8", "--neg-batch-size", "3", "--num-epochs", "1",
+                         "--eval-pct", "1.0", "--lr", "1e-3", "--save-dir", str(tmp_path)])
 
 
 def test_trainer_fit_matches_reference(golden, tmp_path):
