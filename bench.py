@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--gpu-only", action="store_true",
                     help="diagnostic: hold the stream behind a sleep kernel while the warm in-batch "
                          "steps are enqueued, then report the GPU's own time for them")
+    ap.add_argument("--profile-phase", choices=["inbatch_cold", "inbatch", "catalogue"],
+                    help="under `rocprofv3 --kernel-trace`: bracket this phase's timed steps with a "
+                         "marker kernel (profiles/summarize_pmc.py keeps what lies between)")
     ap.add_argument("--py-exchange", action="store_true",
                     help="N>1: all-reduce from Python over torch.distributed instead of the plan's RCCL")
     return ap.parse_args()
@@ -364,7 +367,15 @@ def main():
             sched_step()
         return fn
 
-    def timed_phase(plan, step_fn, gpu_only=False):
+    def profile_mark():
+        """--profile-phase: a short sleep kernel (torch's spin_kernel) that brackets the phase's
+        timed steps in a rocprofv3 kernel trace; profiles/summarize_pmc.py keeps the dispatches
+        between the two marks."""
+        torch.cuda.synchronize()
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
+
+    def timed_phase(name, plan, step_fn, gpu_only=False):
         """W warm-up steps, then EXACTLY K timed steps between barrier + synchronize on both
         sides; max over ranks. Returns (seconds, host enqueue seconds, gpu-only ms or None)."""
         run(plan, step_fn, args.warmup)
@@ -374,6 +385,9 @@ def main():
         torch.cuda.synchronize()
         for k in timed:
             nat.timer_enable(k, stride)  # from the first timed step on (restarts the stride count)
+        profiled = args.profile_phase == name
+        if profiled:
+            profile_mark()
         ev0 = ev1 = None
         if gpu_only:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -386,6 +400,8 @@ def main():
         if gpu_only:
             ev1.record()
         torch.cuda.synchronize()
+        if profiled:
+            profile_mark()
         if world > 1:
             dist.barrier()
         dt = D.max_over_ranks(time.perf_counter() - t0, dev)
@@ -431,7 +447,7 @@ def main():
         return out
 
     def traffic_for(kernel_name, mode):
-        tag = {"k_conv1_wgrad": "conv1_wgrad"}.get(kernel_name.split(" ")[0])
+        tag = {"k_conv1_wgrad": "conv1_wgrad", "k_emb_flush_rows": "emb_flush_rows"}.get(kernel_name.split(" ")[0])
         path = os.path.join(ROOT, "profiles", "pmc_%s_%s.json" % (tag, mode)) if tag else None
         if path and os.path.exists(path):
             try:
@@ -461,14 +477,14 @@ def main():
     # ---- phase 1: in-batch, cold user table
     plan = make_plan(False)
     ub, ib = batches(args.warmup + args.steps)
-    dt, t_enq, _, kern = timed_phase(plan, inbatch_step(ub, ib))
+    dt, t_enq, _, kern = timed_phase("inbatch_cold", plan, inbatch_step(ub, ib))
     out["inbatch_cold"] = summary(dt, t_enq, kern, B, 1, "inbatch")
     # ---- phase 2: every local user once (outside any timed region), then in-batch steady state
     warm = inbatch_step(warm_users, warm_items)
     run(plan, warm, warm_users.shape[0])
     if "inbatch" in modes:
         ub, ib = batches(args.warmup + args.steps)
-        dt, t_enq, gpu_ms, kern = timed_phase(plan, inbatch_step(ub, ib), gpu_only=args.gpu_only)
+        dt, t_enq, gpu_ms, kern = timed_phase("inbatch", plan, inbatch_step(ub, ib), gpu_only=args.gpu_only)
         out["inbatch"] = summary(dt, t_enq, kern, B, 1, "inbatch")
         if gpu_ms is not None:
             out["inbatch"]["gpu_only_ms_per_step"] = gpu_ms
@@ -503,7 +519,7 @@ def main():
             else:
                 plan.step(ub[s], None)
             sched_step()
-        dt, t_enq, _, kern = timed_phase(cplan, cat_step)
+        dt, t_enq, _, kern = timed_phase("catalogue", cplan, cat_step)
         out["catalogue"] = summary(dt, t_enq, kern, B * (1 + N), 1 + N, "catalogue")
         cplan.close()
     head = out.get("inbatch", out["inbatch_cold"])

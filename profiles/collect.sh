@@ -1,31 +1,34 @@
 #!/bin/bash
 # Round profile collection, run on the GPU box from the repo root:
-#   gpurun -- 'bash profiles/collect.sh r01_c'
-# 1. rocprofv3 --kernel-trace --stats of the default bench command (csv kernel stats)
-# 2. two --pmc passes (FETCH_SIZE, then WRITE_SIZE: they do not fit one TCC pass) restricted to the
-#    roofline kernel, summarised (gfx950 FETCH_SIZE x2 correction, KB -> B) by summarize_pmc.py into
-#    profiles/pmc_conv1_wgrad.json, which bench.py reports as roofline.traffic.
+#   gpurun -- 'bash profiles/collect.sh r02_a'
+# 1. the bench command without the profiler (its live HIP-event kernel timings are what the bench
+#    line reports; compared against 2.)
+# 2. per timed phase (cold in-batch, steady-state in-batch, catalogue): rocprofv3 --kernel-trace
+#    --stats; bench.py --profile-phase brackets that phase's timed steps with a marker kernel and
+#    summarize_pmc.py keeps only the dispatches between the marks (<tag>_<phase>_kernel_stats.csv)
+# 3. per mode, two --pmc passes (FETCH_SIZE, then WRITE_SIZE: they do not fit one TCC pass) over
+#    the conv-1 weight gradient and the rolling user-table flush (+ the marker), summarised by
+#    summarize_pmc.py (gfx950 FETCH_SIZE x2 correction, KB -> B) into pmc_<kernel>_<mode>.json
 set -euo pipefail
 TAG=${1:-rNN}
+STEPS=${2:-200}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
-BENCH="$ROOT/bench.py --no-cpu-baseline --steps 200 --warmup 20"
-# the same command without the profiler: its live roofline timing is the one bench.py reports
-(cd "$ROOT" && timeout -k 10 240 python3 $BENCH > "$OUT/plain.log" 2>&1)
+BENCH="$ROOT/bench.py --no-cpu-baseline --no-eval --steps $STEPS --warmup 20"
+(cd "$ROOT" && timeout -k 10 300 python3 $BENCH > "$OUT/plain.log" 2>&1)
 grep '^{' "$OUT/plain.log" | tail -n 1 > "$OUT/${TAG}_bench_plain.json"
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/stats" -o run -- python3 $BENCH \
-  > "$OUT/stats.log" 2>&1
-for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 180 rocprofv3 --pmc $c --kernel-include-regex 'k_conv1_wgrad' -f csv \
-    -d "$OUT/pmc_$c" -o run -- python3 $ROOT/bench.py --no-cpu-baseline --no-eval --steps 40 --warmup 5 \
-    > "$OUT/pmc_$c.log" 2>&1
+for PH in inbatch catalogue inbatch_cold; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/stats_$PH" -o run \
+    -- python3 $BENCH --profile-phase $PH > "$OUT/stats_$PH.log" 2>&1
 done
-# catalogue mode (M = B(1+N) distinct items per step): kernel stats only
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/stats_cat" -o run -- python3 $ROOT/bench.py \
-  --mode catalogue --no-cpu-baseline --no-eval --steps 40 --warmup 5 > "$OUT/stats_cat.log" 2>&1
-cp "$OUT/stats_cat/run_kernel_stats.csv" "$OUT/${TAG}_cat_kernel_stats.csv"
-grep '^{' "$OUT/stats_cat.log" | tail -n 1 > "$OUT/${TAG}_cat_bench.json"
+for PH in inbatch catalogue; do
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 180 rocprofv3 --pmc $C --kernel-include-regex 'k_conv1_wgrad|k_emb_flush_rows|spin_kernel' \
+      -f csv -d "$OUT/pmc_${PH}_$C" -o run -- python3 $ROOT/bench.py --no-cpu-baseline --no-eval --steps 40 \
+      --warmup 5 --profile-phase $PH > "$OUT/pmc_${PH}_$C.log" 2>&1
+  done
+done
 python3 "$ROOT/profiles/summarize_pmc.py" "$OUT" "$TAG"

@@ -1,11 +1,16 @@
-"""Summarise one collect.sh run into committed profile files.
+"""Summarise one collect.sh run into profile files (copied into profiles/ after review).
 
   python3 profiles/summarize_pmc.py <collect output dir> <tag>
 
-Writes (under gpurun_out/<dir>, copied into profiles/ by hand after review):
-  <tag>_kernel_stats.csv     rocprofv3 --stats kernel summary of the bench command
-  <tag>_bench.json           the bench JSON line printed under the profiler
-  pmc_conv1_wgrad.json       per-launch HBM bytes of the roofline kernel (k_conv_wgrad layer 1)
+bench.py --profile-phase <phase> brackets that phase's timed steps with two marker kernels
+(torch's spin_kernel); only the dispatches between the marks count here.
+
+Writes
+  <tag>_<phase>_kernel_stats.csv  per kernel: calls, total/avg/min/max ns inside the phase window
+                                  (rocprofv3's own --stats cover the whole process)
+  <tag>_kernels_per_step.json     each kernel's time per timed step, per phase
+  pmc_<kernel>_<mode>.json        per-launch HBM bytes of the kernels the bench line reports a
+                                  roofline for (bench.py reads roofline.traffic from them)
 
 HBM bytes follow MI355X_MICROARCH.md "HBM [CDNA4]": FETCH_SIZE / WRITE_SIZE are in KB; on gfx950
 FETCH_SIZE reports half the bytes of a wide coalesced read, so it is doubled; WRITE_SIZE is exact.
@@ -16,24 +21,55 @@ import json
 import os
 import sys
 
+KERNELS = {"conv1_wgrad": "k_conv1_wgrad", "emb_flush_rows": "k_emb_flush_rows"}
+MARK = "spin_kernel"
 
-def _counter_rows(d):
-    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+
+def _rows(d, pattern):
     rows = []
-    for f in files:
+    for f in glob.glob(os.path.join(d, "**", pattern), recursive=True):
         with open(f) as fh:
             rows += list(csv.DictReader(fh))
     return rows
 
 
-def per_dispatch(d, counter):
-    """mean over dispatches of the counter's value (summed over its dimensions per dispatch)"""
-    by = {}
-    for r in _counter_rows(d):
-        if r.get("Counter_Name") != counter:
+def _window_by_dispatch(rows):
+    """(first, last) dispatch ids strictly between the two marker kernels, or None."""
+    ids = sorted({int(r["Dispatch_Id"]) for r in rows if MARK in r.get("Kernel_Name", "")})
+    return (ids[0], ids[-1]) if len(ids) >= 2 else None
+
+
+def phase_stats(d):
+    rows = _rows(d, "*kernel_trace.csv")
+    marks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows if MARK in r["Kernel_Name"])
+    if len(marks) < 2:
+        return None
+    lo, hi = marks[0][1], marks[-1][0]
+    agg = {}
+    for r in rows:
+        if MARK in r["Kernel_Name"]:
             continue
-        key = r.get("Dispatch_Id") or r.get("Correlation_Id")
-        by[key] = by.get(key, 0.0) + float(r["Counter_Value"])
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if s < lo or e > hi:
+            continue
+        a = agg.setdefault(r["Kernel_Name"], [])
+        a.append(e - s)
+    return agg
+
+
+def per_dispatch(d, counter, kernel):
+    """mean over the kernel's dispatches inside the marker window of the counter's value (summed
+    over its dimensions per dispatch)"""
+    rows = _rows(d, "*counter_collection.csv")
+    win = _window_by_dispatch(rows)
+    by = {}
+    for r in rows:
+        if r.get("Counter_Name") != counter or kernel not in r.get("Kernel_Name", ""):
+            continue
+        did = int(r["Dispatch_Id"])
+        if win and not (win[0] < did < win[1]):
+            continue
+        by[did] = by.get(did, 0.0) + float(r["Counter_Value"])
     if not by:
         return None, 0
     return sum(by.values()) / len(by), len(by)
@@ -42,28 +78,43 @@ def per_dispatch(d, counter):
 def main():
     d, tag = sys.argv[1], sys.argv[2]
     out = {}
-    fetch_kb, n_f = per_dispatch(os.path.join(d, "pmc_FETCH_SIZE"), "FETCH_SIZE")
-    write_kb, n_w = per_dispatch(os.path.join(d, "pmc_WRITE_SIZE"), "WRITE_SIZE")
-    if fetch_kb is not None and write_kb is not None:
-        rd = 2.0 * fetch_kb * 1024.0
-        wr = write_kb * 1024.0
-        out = {"kernel": "k_conv1_wgrad (conv layer 1 weight gradient)",
-               "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
-               "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
-               "hbm_bytes_per_launch": rd + wr, "dispatches": [n_f, n_w],
-               "correction": "FETCH_SIZE x2 (gfx950 half-count on wide reads), KB x1024"}
-        with open(os.path.join(d, "pmc_conv1_wgrad.json"), "w") as fh:
-            json.dump(out, fh, indent=1)
-    stats = glob.glob(os.path.join(d, "stats", "**", "*kernel_stats.csv"), recursive=True)
-    if stats:
-        with open(stats[0]) as src, open(os.path.join(d, "%s_kernel_stats.csv" % tag), "w") as dst:
-            dst.write(src.read())
-    log = os.path.join(d, "stats.log")
-    if os.path.exists(log):
-        lines = [ln for ln in open(log) if ln.startswith("{")]
-        if lines:
-            with open(os.path.join(d, "%s_bench.json" % tag), "w") as fh:
-                fh.write(lines[-1])
+    for mode in ("inbatch", "catalogue"):
+        for short, kname in KERNELS.items():
+            fetch_kb, n_f = per_dispatch(os.path.join(d, "pmc_%s_FETCH_SIZE" % mode), "FETCH_SIZE", kname)
+            write_kb, n_w = per_dispatch(os.path.join(d, "pmc_%s_WRITE_SIZE" % mode), "WRITE_SIZE", kname)
+            if fetch_kb is None or write_kb is None:
+                continue
+            rd, wr = 2.0 * fetch_kb * 1024.0, write_kb * 1024.0
+            rec = {"kernel": kname, "mode": mode, "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
+                   "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+                   "hbm_bytes_per_launch": rd + wr, "dispatches": [n_f, n_w], "tag": tag,
+                   "correction": "FETCH_SIZE x2 (gfx950 half-count on wide reads), KB x1024"}
+            name = "pmc_%s_%s.json" % (short, mode)
+            with open(os.path.join(d, name), "w") as fh:
+                json.dump(rec, fh, indent=1)
+            out[name] = rec["hbm_bytes_per_launch"]
+    steps = None
+    plain = os.path.join(d, "%s_bench_plain.json" % tag)
+    if os.path.exists(plain):
+        steps = json.load(open(plain)).get("steps")
+    per_step = {}
+    for ph in ("inbatch", "catalogue", "inbatch_cold"):
+        agg = phase_stats(os.path.join(d, "stats_%s" % ph))
+        if not agg or not steps:
+            continue
+        tot = sum(sum(v) for v in agg.values())
+        rows = sorted(agg.items(), key=lambda kv: -sum(kv[1]))
+        with open(os.path.join(d, "%s_%s_kernel_stats.csv" % (tag, ph)), "w", newline="") as fh:
+            w = csv.writer(fh)
+            w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs"])
+            for k, v in rows:
+                w.writerow([k, len(v), sum(v), sum(v) / len(v), 100.0 * sum(v) / tot, min(v), max(v)])
+        per_step[ph] = {"steps": steps, "kernel_ms_per_step": tot / steps / 1e6,
+                        "kernels": [{"name": k.split("(")[0][:120], "calls_per_step": len(v) / steps,
+                                     "avg_us": sum(v) / len(v) / 1e3, "us_per_step": sum(v) / steps / 1e3}
+                                    for k, v in rows]}
+    with open(os.path.join(d, "%s_kernels_per_step.json" % tag), "w") as fh:
+        json.dump(per_step, fh, indent=1)
     print(json.dumps(out))
 
 
