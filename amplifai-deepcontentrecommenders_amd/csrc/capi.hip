@@ -813,6 +813,25 @@ int dcue_adam_step(const dcue_model* m, const dcue_adam_args* a, void* stream) {
   return DCUE_OK;
 }
 
+int dcue_optimizer_step(const dcue_model* m, const dcue_opt_args* a, const dcue_opt_state* st, void* stream) {
+  Ctx c;
+  TRY(init_ctx(&c, m));
+  if (!a || !st || a->step < 1 || !m->grads || !m->emb || !m->emb_slot) return DCUE_ERR_INVALID;
+  if (m->dims.n_users > 0 && !m->emb_grad) return DCUE_ERR_INVALID;
+  if (a->kind == DCUE_OPT_SGD) {
+    if (!st->dense_a || !st->emb_a) return DCUE_ERR_INVALID;
+  } else if (a->kind == DCUE_OPT_RANGER) {
+    if (!st->dense_a || !st->dense_b || !st->dense_c || !st->emb_a || !st->emb_b || !st->emb_c || a->k < 1)
+      return DCUE_ERR_INVALID;
+  } else {
+    return DCUE_ERR_INVALID;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  TRY(join_user_stream(s));
+  TRY(launch_opt(m, a, st, c.poff[kSeg], s));
+  return launch_pack(m, c.poff, s);
+}
+
 int dcue_item_tower_eval(const dcue_model* m, const dcue_tracks* t, const int32_t* item_track,
                          int32_t n_items, void* ws, size_t ws_bytes, float* item_feat,
                          void* stream) {

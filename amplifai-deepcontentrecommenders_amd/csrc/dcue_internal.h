@@ -201,6 +201,9 @@ int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float s
 int launch_adam(const dcue_model* m, const dcue_adam_args* a, const int64_t* poff, hipStream_t s,
                 bool flush_slice = true);
 int launch_emb_flush_rows(const dcue_model* m, int step, hipStream_t s);
+// SGD / Ranger over the dense buffer and the user table (optim.hip)
+int launch_opt(const dcue_model* m, const dcue_opt_args* a, const dcue_opt_state* st, long n_dense,
+               hipStream_t s);
 int launch_emb_log_init(const dcue_model* m, int cap, int step, hipStream_t s);
 int launch_emb_sync(const dcue_model* m, const int64_t* users, int n, hipStream_t s);
 int launch_emb_flush(const dcue_model* m, hipStream_t s);

@@ -61,6 +61,20 @@ class AdamArgs(ctypes.Structure):
                 ("parts", ctypes.c_int32), ("grad_div", ctypes.c_double)]
 
 
+class OptArgs(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("step", ctypes.c_int32), ("lr", ctypes.c_double),
+                ("beta1", ctypes.c_double), ("beta2", ctypes.c_double), ("eps", ctypes.c_double),
+                ("weight_decay", ctypes.c_double), ("alpha", ctypes.c_double), ("k", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("n_sma_threshold", ctypes.c_double), ("grad_div", ctypes.c_double)]
+
+
+class OptState(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("dense_a", "dense_b", "dense_c", "emb_a", "emb_b", "emb_c")]
+
+
+OPT_SGD = 1
+OPT_RANGER = 2
+
 ADAM_DENSE = 1
 ADAM_EMBEDDING = 2
 
@@ -105,6 +119,8 @@ _SIGS = {
     "dcue_train_backward": ([ctypes.POINTER(Model), ctypes.POINTER(Batch), ctypes.POINTER(Tracks), _P,
                              ctypes.c_size_t, _P, ctypes.c_float, _P], ctypes.c_int),
     "dcue_adam_step": ([ctypes.POINTER(Model), ctypes.POINTER(AdamArgs), _P], ctypes.c_int),
+    "dcue_optimizer_step": ([ctypes.POINTER(Model), ctypes.POINTER(OptArgs), ctypes.POINTER(OptState), _P],
+                            ctypes.c_int),
     "dcue_item_tower_eval": ([ctypes.POINTER(Model), ctypes.POINTER(Tracks), _P, ctypes.c_int32, _P,
                               ctypes.c_size_t, _P, _P], ctypes.c_int),
     "dcue_user_tower": ([ctypes.POINTER(Model), _P, ctypes.c_int32, _P, ctypes.c_size_t, _P, _P],

@@ -40,7 +40,8 @@ class TrainPlan:
         self.ws = net._workspace(B, N, M)
         self.optimizer = optimizer
         # with an optimizer the plan also owns the Adam step (step()); the struct then carries its state
-        model = net._model_struct(optimizer._adam_state() if optimizer is not None else None)
+        self._fused_adam = optimizer is not None and hasattr(optimizer, "_adam_state")
+        model = net._model_struct(optimizer._adam_state() if self._fused_adam else None)
         opt = net._deferred_opt() if getattr(net, "_deferred_opt", None) is not None else None
         self._bound = (fl, self.ws, fl["emb_grad"], opt._moments if opt is not None else None)
         self._keep = (fl["emb_grad"], fl["emb_rows"])
@@ -99,6 +100,10 @@ class TrainPlan:
         opt = self.optimizer
         if opt is None:
             raise RuntimeError("TrainPlan.step needs the plan built with optimizer=...")
+        if not self._fused_adam:  # NativeSGD / NativeRanger: the replay, then their own sweep
+            self.launch(users, item_track, stream)
+            opt.step()
+            return
         if self._handle is None:
             raise RuntimeError("TrainPlan was closed")
         self._check_bound()

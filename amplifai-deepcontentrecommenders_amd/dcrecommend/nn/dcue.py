@@ -33,7 +33,7 @@ from dcrecommend.dcue.dcue import DCUENet
 from dcrecommend.dcue.plan import TrainPlan
 from dcrecommend.nn import rank
 from dcrecommend.nn.trainer import Trainer
-from dcrecommend.optim import NativeAdam
+from dcrecommend.optim import NativeAdam, NativeRanger, NativeSGD
 from dcrecommend.optim.cyclic_scheduler import CyclicLRWithRestarts
 
 
@@ -183,11 +183,22 @@ class DCUE(Trainer):
             sd.update(audio_model)
             self.model.load_state_dict(sd)
         self.model = self.model.to(self.device)
-        if self.optimize != 'adam':
-            raise NotImplementedError("optimize=%r: only 'adam' (the reference default, nn/dcue.py:143-147) "
-                                      "runs on MI355X so far" % self.optimize)
-        self.optimizer = NativeAdam(self.model.parameters(), self.lr, (self.beta_one, self.beta_two), self.eps,
-                                    self.weight_decay, defer_embedding=self.defer_embedding)
+        if self.optimize == 'adam':
+            self.optimizer = NativeAdam(self.model.parameters(), self.lr, (self.beta_one, self.beta_two), self.eps,
+                                        self.weight_decay, defer_embedding=self.defer_embedding)
+        elif self.optimize == 'sgd':
+            # nn/dcue.py:148-152; its StepLR(optimizer, 1, 1 - 1e-6) is replaced by the cyclic schedule
+            # right after (:159) and never stepped, so it changes nothing
+            self.optimizer = NativeSGD(self.model.parameters(), self.lr, self.beta_one,
+                                       weight_decay=self.weight_decay, nesterov=True)
+        elif self.optimize == 'ranger':
+            self.optimizer = NativeRanger(self.model.parameters(), lr=self.lr, alpha=0.5, k=6, N_sma_threshhold=5,
+                                          betas=(self.beta_one, self.beta_two), eps=1e-5,
+                                          weight_decay=self.weight_decay)
+        else:
+            # the reference leaves self.optimizer None and its scheduler raises TypeError
+            # (nn/dcue.py:159-162, optim/cyclic_scheduler.py)
+            self.optimizer = None
         self.scheduler = CyclicLRWithRestarts(self.optimizer, self.batch_size, epoch_size=self.epoch_size,
                                               restart_period=self.restart_period, t_mult=self.t_mult,
                                               policy='cosine')

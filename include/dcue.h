@@ -183,6 +183,32 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
  * must then be consecutive (a->step == step_done + 1). */
 int dcue_adam_step(const dcue_model* m, const dcue_adam_args* a, void* stream);
 
+/* The trainer's other optimizers, DCUE(optimize='sgd' | 'ranger') (nn/dcue.py:148-157): one step
+ * over the dense flat buffer and every user-table row (the dense embedding gradient: rows outside
+ * the batch step with g = 0), then the conv-weight repack. Per-element arithmetic as torch's CPU
+ * kernels round it (oracle/optim_oracle.py), sqrt correctly rounded. */
+#define DCUE_OPT_SGD 1    /* torch.optim.SGD(lr, momentum=beta1, weight_decay, nesterov=True) */
+#define DCUE_OPT_RANGER 2 /* optim/ranger.py:26-165: RAdam + Lookahead */
+typedef struct dcue_opt_args {
+  int32_t kind;           /* DCUE_OPT_* */
+  int32_t step;           /* step count after increment (1 on the first step) */
+  double lr, beta1, beta2, eps, weight_decay; /* SGD: beta1 = momentum; beta2, eps unused */
+  double alpha;           /* Ranger: lookahead interpolation (0.5 in the trainer) */
+  int32_t k;              /* Ranger: lookahead period (6) */
+  int32_t reserved;
+  double n_sma_threshold; /* Ranger: RAdam rectification threshold (5) */
+  double grad_div;        /* as dcue_adam_args.grad_div */
+} dcue_opt_args;
+/* Optimizer state, caller-owned, zero-initialised before the first step except the lookahead
+ * buffers, which start as copies of the parameters (optim/ranger.py:113-114).
+ *   SGD: a = momentum buffer.   Ranger: a = exp_avg, b = exp_avg_sq, c = slow (lookahead) weights.
+ * dense_*: [n_dense] like params; emb_*: [n_users][E] like the user table. */
+typedef struct dcue_opt_state {
+  float *dense_a, *dense_b, *dense_c;
+  float *emb_a, *emb_b, *emb_c;
+} dcue_opt_state;
+int dcue_optimizer_step(const dcue_model* m, const dcue_opt_args* a, const dcue_opt_state* st, void* stream);
+
 /* Deferred user-table Adam: log size for a `cap`-step history; (re)initialise the log and row
  * clocks at Adam step `step` (table and moments current to it); bring `users`' rows current;
  * bring every row current (the state then equals the dense sweep's bit for bit). */

@@ -24,6 +24,10 @@ Which reference code produced what:
                    DCUEItemset, DCUE.score (val and train splits, DCUEPredset) and score_song.
 * metrics.npz   -- DCUE.score's split-weighted AUC / mAP arithmetic (nn/dcue.py:399-449) and
                    score_song's (nn/dcue.py:463-476), on fixed score vectors.
+* optim.npz     -- the trainer's other optimizers as DCUE._init_nn builds them (nn/dcue.py:148-157):
+                   the reference's Ranger (optim/ranger.py:26-165, RAdam + Lookahead, k=6, alpha=0.5,
+                   N_sma_threshhold=5, eps=1e-5) and torch.optim.SGD(momentum=beta_one, nesterov=True),
+                   13 steps on fixed gradients with a changing lr, every step's parameters and state.
 """
 import os
 import sys
@@ -461,6 +465,48 @@ def fit_fixture():
           **{"final." + k: v for k, v in tr.model.state_dict().items()})
 
 
+def optim_fixture():
+    from dcrecommend.optim.ranger import Ranger  # reference
+    shapes = [(37, 5), (64,), (3, 4, 2)]
+    gen = torch.Generator().manual_seed(77)
+    init = [torch.randn(*s, generator=gen) * 0.1 for s in shapes]
+    steps = 13
+    grads = []
+    for t in range(steps):
+        gs = []
+        for s in shapes:
+            g = torch.randn(*s, generator=gen) * (10.0 ** torch.empty(s).uniform_(-6, 0, generator=gen))
+            g.view(-1)[:: 7 + t] = 0.0  # rows without a gradient, as the dense embedding gradient has
+            gs.append(g)
+        grads.append(gs)
+    lrs = [1e-3 * (1.0 - 0.05 * t) for t in range(steps)]
+    out = {"init.%d" % i: v for i, v in enumerate(init)}
+    out.update({"grad.%d.%d" % (t, i): g for t in range(steps) for i, g in enumerate(grads[t])})
+    out["lr"] = np.array(lrs)
+    cfgs = {"ranger_a": ("ranger", (0.9, 0.99), 0.0), "ranger_b": ("ranger", (0.95, 0.999), 1e-2),
+            "sgd_a": ("sgd", 0.9, 0.0), "sgd_b": ("sgd", 0.5, 1e-2)}
+    for tag, (kind, beta, wd) in cfgs.items():
+        ps = [torch.nn.Parameter(v.clone()) for v in init]
+        if kind == "ranger":
+            opt = Ranger(ps, lr=lrs[0], alpha=0.5, k=6, N_sma_threshhold=5, betas=beta, eps=1e-5, weight_decay=wd)
+        else:
+            opt = torch.optim.SGD(ps, lrs[0], beta, weight_decay=wd, nesterov=True)
+        for t in range(steps):
+            for p_, g in zip(ps, grads[t]):
+                p_.grad = g.clone()
+            opt.param_groups[0]["lr"] = lrs[t]
+            opt.step()
+            for i, p_ in enumerate(ps):
+                out["%s.p.%d.%d" % (tag, t, i)] = p_.detach().clone()
+                st = opt.state[p_]
+                for k in ("exp_avg", "exp_avg_sq", "slow_buffer", "momentum_buffer"):
+                    if k in st:
+                        out["%s.%s.%d.%d" % (tag, k, t, i)] = st[k].clone()
+        out["%s.cfg" % tag] = np.array([beta[0] if kind == "ranger" else beta,
+                                        beta[1] if kind == "ranger" else 0.0, wd])
+    _save("optim.npz", **out)
+
+
 if __name__ == "__main__":
     jobs = {
         "model": lambda: (model_fixture("model_tiny.npz", H=32, d=32, n_users=10, B=4, N=3),
@@ -468,7 +514,7 @@ if __name__ == "__main__":
                                         store_init=False, store_steps=False)),
         "inbatch": inbatch_fixtures, "catalogue": catalogue_fixture, "batches": batches_fixture,
         "scheduler": scheduler_fixture, "train5": train5_fixture, "metrics": metrics_fixture,
-        "eval": eval_fixture, "fit": fit_fixture,
+        "eval": eval_fixture, "fit": fit_fixture, "optim": optim_fixture,
     }
     for name in (sys.argv[1:] or list(jobs)):  # e.g. `make_golden.py eval` regenerates one fixture
         jobs[name]()

@@ -1,4 +1,4 @@
-"""Pins oracle/adam_oracle.py -- the per-element restatement NativeAdam implements -- against the
+"""Pins oracle/optim_oracle.py -- the per-element restatement NativeAdam implements -- against the
 reference's optimizer itself: torch.optim.Adam (nn/dcue.py:143-147, foreach=False, CPU float32).
 
 Bar: BIT-EXACT over several steps, with and without weight decay, for both lerp branches, when the
@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from oracle import adam_oracle as A
+from oracle import optim_oracle as A
 
 
 def _inputs(n, steps, seed):
@@ -54,3 +54,35 @@ def test_torch_cpu_sqrt_is_not_correctly_rounded():
     diff = A.torch_cpu_sqrt(x) != A.exact_sqrt(x)
     ulps = np.abs(A.torch_cpu_sqrt(x).view(np.int32)[diff] - A.exact_sqrt(x).view(np.int32)[diff])
     assert ulps.size == 0 or ulps.max() == 1
+
+
+def _optim_case(g, tag, kind):
+    steps, n_par = len(g["lr"]), 3
+    beta_a, beta_b, wd = (float(x) for x in g[tag + ".cfg"])
+    ps = [np.array(g["init.%d" % i]).reshape(-1) for i in range(n_par)]
+    state = [dict(m=np.zeros_like(p), v=np.zeros_like(p), slow=p.copy(), buf=np.zeros_like(p)) for p in ps]
+    for t in range(steps):
+        lr = float(g["lr"][t])
+        for i in range(n_par):
+            grad = np.array(g["grad.%d.%d" % (t, i)]).reshape(-1)
+            st = state[i]
+            if kind == "ranger":
+                ps[i], st["m"], st["v"], st["slow"] = A.ranger_elementwise(
+                    ps[i], grad, st["m"], st["v"], st["slow"], lr, beta_a, beta_b, 1e-5, wd, t + 1, sqrt=A.torch_cpu_sqrt)
+            else:
+                ps[i], st["buf"] = A.sgd_elementwise(ps[i], grad, st["buf"], lr, beta_a, wd, t + 1)
+            want = np.array(g["%s.p.%d.%d" % (tag, t, i)]).reshape(-1)
+            assert np.array_equal(ps[i].view(np.int32), want.view(np.int32)), "%s step %d param %d" % (tag, t + 1, i)
+
+
+@pytest.mark.parametrize("tag", ["ranger_a", "ranger_b"])
+def test_ranger_restatement_matches_reference(golden, tag):
+    """oracle ranger_elementwise == the reference's Ranger (optim/ranger.py), bit for bit, over 13
+    steps: the un-rectified first steps, the RAdam steps, two lookahead syncs (k = 6)."""
+    _optim_case(golden("optim.npz"), tag, "ranger")
+
+
+@pytest.mark.parametrize("tag", ["sgd_a", "sgd_b"])
+def test_sgd_restatement_matches_torch(golden, tag):
+    """oracle sgd_elementwise == torch.optim.SGD(momentum, nesterov=True) as the trainer builds it."""
+    _optim_case(golden("optim.npz"), tag, "sgd")

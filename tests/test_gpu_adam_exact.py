@@ -1,7 +1,7 @@
 """NativeAdam (dcue_adam_step) against torch.optim.Adam's per-element arithmetic on IDENTICAL
 gradients, isolating the optimizer from gradient rounding.
 
-oracle/adam_oracle.py restates torch 2.10's CPU Adam kernels op by op; tests/test_adam_cpu.py pins
+oracle/optim_oracle.py restates torch 2.10's CPU Adam kernels op by op; tests/test_adam_cpu.py pins
 it bit for bit against torch.optim.Adam itself (nn/dcue.py:143-147). The GPU computes the same
 operations with a correctly rounded sqrt, so the bar here is BIT-EXACT against the restatement with
 the exact sqrt -- for the dense buffer and for every user-table row (touched or not), in the dense
@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 import torch
 
-from oracle import adam_oracle as A
+from oracle import optim_oracle as A
 
 pytestmark = pytest.mark.gpu
 

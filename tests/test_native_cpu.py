@@ -36,7 +36,8 @@ def test_ctypes_structs_match_header(tmp_path):
     import subprocess
     from dcrecommend import _native as nat
     structs = {"dcue_dims": nat.Dims, "dcue_model": nat.Model, "dcue_batch": nat.Batch,
-               "dcue_tracks": nat.Tracks, "dcue_adam_args": nat.AdamArgs}
+               "dcue_tracks": nat.Tracks, "dcue_adam_args": nat.AdamArgs, "dcue_opt_args": nat.OptArgs,
+               "dcue_opt_state": nat.OptState}
     src = ["#include <stdio.h>", "#include <stddef.h>", '#include "dcue.h"', "int main(void) {"]
     for cname, py in structs.items():
         src.append('printf("%s %%zu\\n", sizeof(%s));' % (cname, cname))

@@ -41,6 +41,9 @@ def parse(argv=None):
     ap.add_argument("--u-embdim", type=int, default=300)
     ap.add_argument("--margin", type=float, default=0.2)
     ap.add_argument("--lr", type=float, default=1e-5)
+    ap.add_argument("--optimize", choices=["adam", "sgd", "ranger"], default="adam",
+                    help="DCUE(optimize=...): nn/dcue.py:143-157")
+    ap.add_argument("--model-type", default="truedcuemel1dbn", help="DCUE(model_type=...): dcue/dcue.py:49-59")
     ap.add_argument("--weight-decay", type=float, default=0.0)
     ap.add_argument("--num-epochs", type=int, default=90)
     ap.add_argument("--eval-pct", type=float, default=0.025)
@@ -100,7 +103,7 @@ def main(argv=None):
     dcue = DCUE(feature_dim=args.feature_dim, conv_hidden=args.conv_hidden, batch_size=args.batch_size,
                 neg_batch_size=args.neg_batch_size, u_embdim=args.u_embdim, margin=args.margin, lr=args.lr,
                 weight_decay=args.weight_decay, num_epochs=args.num_epochs, eval_pct=args.eval_pct,
-                val_pct=args.val_pct)
+                val_pct=args.val_pct, optimize=args.optimize, model_type=args.model_type)
     dcue.fit(train, val, test, pred, truth, items, len(train.user_index), len(train.item_index),
              triplets_path, metadata_path, args.save_dir)
     return dcue
