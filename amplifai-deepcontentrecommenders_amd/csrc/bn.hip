@@ -106,4 +106,112 @@ int launch_bn_eval(int C, const float* gamma, const float* rmean, const float* r
   return DCUE_OK;
 }
 
+// ----------------------------------------------------------------- tower variants (dcue_dims.tower)
+struct BnIdentity {
+  float* mean[6];
+  float* invstd[6];
+  float* a[6];
+  float *ones, *zeros;
+  int C[6];
+  int cmax;
+};
+
+// truedcuemel1d / truedcuemel1dres have no BatchNorm: every kernel that normalises reads mean 0 and
+// a = invstd = 1 (x = (y - 0) * 1 + 0), and gamma / beta operands read ones / zeros
+__global__ void k_bn_identity(BnIdentity b) {
+  for (int c = threadIdx.x; c < b.cmax; c += blockDim.x) {
+    b.ones[c] = 1.f;
+    b.zeros[c] = 0.f;
+  }
+  for (int l = 0; l < 6; ++l)
+    for (int c = threadIdx.x; c < b.C[l]; c += blockDim.x) {
+      b.mean[l][c] = 0.f;
+      b.invstd[l][c] = 1.f;
+      b.a[l][c] = 1.f;
+    }
+}
+
+int launch_bn_identity(float* const* mean, float* const* invstd, float* const* a, float* ones, float* zeros,
+                       int cmax, int H, int D, hipStream_t s) {
+  BnIdentity b = {};
+  for (int l = 0; l < 6; ++l) {
+    b.mean[l] = mean[l];
+    b.invstd[l] = invstd[l];
+    b.a[l] = a[l];
+    b.C[l] = l == 0 ? kMels : l == 5 ? D : H;
+  }
+  b.ones = ones;
+  b.zeros = zeros;
+  b.cmax = cmax;
+  DCUE_LAUNCH(k_bn_identity, dim3(1), dim3(256), 0, s, b);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+struct TimepoolArgs {
+  const float* y[6];
+  const float* mean[6];
+  const float* a[6];
+  const float* beta[6];  // nullable (0)
+  BnPublish p5;          // train + BN: BN_5 from its accumulators (this kernel is its first consumer)
+  int M, H, D;
+  float* xfc;
+};
+
+// The res towers' fc input, one workgroup per item (truedcuemel1dres.py:86-97, ...resbn.py:82-107):
+// tp_l = AvgPool1d(Lp_l)(bn_l(y_l)) for blocks 1-4 -- each position normalised, then the mean over
+// the block's Lp positions (sum in position order / Lp) -- then bn_5(y_5).
+__global__ __launch_bounds__(256) void k_timepool(TimepoolArgs t) {
+  __shared__ float m5[256], a5[256];
+  const int i = blockIdx.x, H = t.H, D = t.D;
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    if (t.p5.acc) {
+      const BnChan st = bn_chan_train(t.p5.acc, D, c, t.p5.count, t.p5.inv_count);
+      m5[c] = st.mean;
+      a5[c] = t.p5.gamma[c] * st.invstd;
+    } else {
+      m5[c] = t.mean[5][c];
+      a5[c] = t.a[5][c];
+    }
+  }
+  if (i == 0) bn_publish(t.p5, threadIdx.x);
+  __syncthreads();
+  const int FI = 4 * H + D;
+  for (int col = threadIdx.x; col < FI; col += blockDim.x) {
+    float v;
+    if (col < 4 * H) {
+      const int l = col / H + 1, c = col - (l - 1) * H;
+      const int lp = layer_geom(l).lp;
+      const float mu = t.mean[l][c], sc = t.a[l][c], be = t.beta[l] ? t.beta[l][c] : 0.f;
+      const float* yl = t.y[l] + (long)i * lp * H + c;
+      float acc = 0.f;
+      for (int q = 0; q < lp; ++q) acc += (yl[(long)q * H] - mu) * sc + be;
+      v = acc / (float)lp;
+    } else {
+      const int c = col - 4 * H;
+      v = (t.y[5][(long)i * D + c] - m5[c]) * a5[c] + (t.beta[5] ? t.beta[5][c] : 0.f);
+    }
+    t.xfc[(long)i * FI + col] = v;
+  }
+}
+
+int launch_timepool(float* const* y, float* const* mean, float* const* a, const float* beta1, const float* beta2,
+                    const float* beta3, const float* beta4, const float* beta5, const BnPublish& p5, int M, int H,
+                    int D, float* xfc, hipStream_t s) {
+  if (D > 256) return DCUE_ERR_UNSUPPORTED;
+  TimepoolArgs t = {};
+  for (int l = 1; l <= 5; ++l) {
+    t.y[l] = y[l];
+    t.mean[l] = mean[l];
+    t.a[l] = a[l];
+  }
+  t.beta[1] = beta1; t.beta[2] = beta2; t.beta[3] = beta3; t.beta[4] = beta4; t.beta[5] = beta5;
+  t.p5 = p5;
+  t.M = M; t.H = H; t.D = D;
+  t.xfc = xfc;
+  DCUE_LAUNCH(k_timepool, dim3((unsigned)M), dim3(256), 0, s, t);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
 }  // namespace dcue

@@ -126,6 +126,7 @@ int check_dims(const dcue_dims* d) {
     return DCUE_ERR_INVALID;
   if (!pow2_32_256(d->conv_hidden) || !pow2_32_256(d->feature_dim) || d->user_embdim > 1024)
     return DCUE_ERR_UNSUPPORTED;
+  if (d->tower < DCUE_TOWER_BN || d->tower > DCUE_TOWER_RESBN) return DCUE_ERR_INVALID;
   return DCUE_OK;
 }
 
@@ -134,16 +135,17 @@ long al4(long v) { return (v + 3) & ~3L; }
 void param_sizes(const dcue_dims* d, long* sz) {
   const long H = d->conv_hidden, D = d->feature_dim, E = d->user_embdim;
   const long cin[5] = {kMels, H, H, H, H}, cout[5] = {H, H, H, H, D};
+  const long bn = tower_has_bn(d) ? 1 : 0;  // the BN parameters' segments are empty without BN
   int s = 0;
-  sz[s++] = kMels;  // bn0.weight
-  sz[s++] = kMels;  // bn0.bias
+  sz[s++] = bn * kMels;  // bn0.weight
+  sz[s++] = bn * kMels;  // bn0.bias
   for (int l = 1; l <= 5; ++l) {
     sz[s++] = cout[l - 1] * cin[l - 1] * layer_geom(l).ks;  // conv.layer{l}.weight
     sz[s++] = cout[l - 1];                                  // conv.layer{l}.bias
-    sz[s++] = cout[l - 1];                                  // conv.bn{l}.weight
-    sz[s++] = cout[l - 1];                                  // conv.bn{l}.bias
+    sz[s++] = bn * cout[l - 1];                             // conv.bn{l}.weight
+    sz[s++] = bn * cout[l - 1];                             // conv.bn{l}.bias
   }
-  sz[s++] = D * D;  // conv.fc.weight
+  sz[s++] = D * fc_in(d);  // conv.fc.weight [d][d] or, res towers, [d][4H + d]
   sz[s++] = D;      // conv.fc.bias
   sz[s++] = E * E;  // user_embd.linear1.weight
   sz[s++] = E;
@@ -201,6 +203,12 @@ struct Ws {
   float *wpart[3], *bpart[3], *G, *S;  // wgrad partials: one set per wgrad stream
   float* xhat0;          // [M][kXp][128] bn0-normalised, zero-padded input: conv-1 wgrad's X operand
   float* dx1;            // [M][33][H] BN1 backward at the pooled positions: conv-1 wgrad's dz operand
+  // towers without BN: the BN operands every kernel reads become the identity (mean 0, a = invstd
+  // = 1, beta 0) and the BN parameter gradients go to a scratch sink
+  float *ones, *zeros, *sink;
+  // res towers: the fc input [M][4H + d] (time-pooled blocks 1-4, then block 5) and the gradient
+  // of the four time-pooled outputs [M][4H]
+  float *xfc, *dtp;
 };
 
 // the accumulator block's parts: [6][2][Cmax][2] forward sums, then the same for the backward
@@ -264,6 +272,16 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   w->S = ar.take<float>(5L * H);  // the five layer-1 bias partial sums E[5][H]
   w->xhat0 = ar.take<float>((long)(M + 1) * kXp * kMels);  // + a zero item
   w->dx1 = ar.take<float>((long)M * layer_geom(1).lp * H);
+  w->ones = w->zeros = w->sink = w->xfc = w->dtp = nullptr;
+  if (!tower_has_bn(d)) {
+    w->ones = ar.take<float>(w->cmax);
+    w->zeros = ar.take<float>(w->cmax);
+    w->sink = ar.take<float>(2L * w->cmax);
+  }
+  if (tower_res(d)) {
+    w->xfc = ar.take<float>((long)M * fc_in(d));
+    w->dtp = ar.take<float>((long)M * 4 * H);
+  }
   return ar.used + 256;
 }
 
@@ -276,14 +294,26 @@ struct Ctx {
   int64_t poff[kSeg + 1];
   int64_t boff[2 * DCUE_N_BN + 1];
   int H, D, E;
+  bool bn, res;  // tower variant (dcue_dims.tower)
+  int FI;        // fc input width: D, or 4H + D in the res towers
   const float* P(int seg) const { return m->params + poff[seg]; }
   float* Gd(int seg) const { return m->grads + poff[seg]; }
   float* rmean(int l) const { return m->bn_stats + boff[2 * l]; }
   float* rvar(int l) const { return m->bn_stats + boff[2 * l + 1]; }
+  // BN_l's gamma / beta as the kernels read them, and where their gradients go; the identity and a
+  // scratch sink in the towers without BN
+  const float* gamma(const Ws& w, int l) const;
+  const float* beta(const Ws& w, int l) const;
+  float* dgamma(const Ws& w, int l) const;
+  float* dbeta(const Ws& w, int l) const;
 };
 // segment indices
 int seg_bn_w(int l) { return l == 0 ? 0 : 4 + 4 * (l - 1); }
 int seg_bn_b(int l) { return l == 0 ? 1 : 5 + 4 * (l - 1); }
+const float* Ctx::gamma(const Ws& w, int l) const { return bn ? P(seg_bn_w(l)) : w.ones; }
+const float* Ctx::beta(const Ws& w, int l) const { return bn ? P(seg_bn_b(l)) : w.zeros; }
+float* Ctx::dgamma(const Ws& w, int l) const { return bn ? Gd(seg_bn_w(l)) : w.sink; }
+float* Ctx::dbeta(const Ws& w, int l) const { return bn ? Gd(seg_bn_b(l)) : w.sink + w.cmax; }
 int seg_conv_w(int l) { return 2 + 4 * (l - 1); }
 int seg_conv_b(int l) { return 3 + 4 * (l - 1); }
 constexpr int SEG_FC_W = 22, SEG_FC_B = 23, SEG_L1_W = 24, SEG_L1_B = 25, SEG_L2_W = 26, SEG_L2_B = 27;
@@ -302,6 +332,9 @@ int init_ctx(Ctx* c, const dcue_model* m) {
   c->H = m->dims.conv_hidden;
   c->D = m->dims.feature_dim;
   c->E = m->dims.user_embdim;
+  c->bn = tower_has_bn(&m->dims);
+  c->res = tower_res(&m->dims);
+  c->FI = fc_in(&m->dims);
   return DCUE_OK;
 }
 
@@ -315,18 +348,22 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
   // one BN's finalize/publish record for its first consumer (train) -- bnacc.h
   auto bn_of = [&](int l) {
     BnPublish p = {};
-    if (!train) return p;
+    if (!train || !c.bn) return p;  // eval / no BatchNorm: consumers read the mean / a arrays
     p.acc = bn_acc(w.bnacc, w.cmax, l);
     p.count = copies * (l == 0 ? kFrames : layer_geom(l).lp);
     p.inv_count = 1.0 / p.count;
-    p.gamma = c.P(seg_bn_w(l));
-    p.beta = c.P(seg_bn_b(l));
+    p.gamma = c.gamma(w, l);
+    p.beta = c.beta(w, l);
     p.mean = w.mean[l]; p.invstd = w.invstd[l]; p.a = w.a[l];
     p.rmean = c.rmean(l); p.rvar = c.rvar(l); p.nbt = m->bn_batches + l;
     p.C = bn_channels(&m->dims, l);
     return p;
   };
-  if (train) {
+  if (!c.bn) {  // mean 0, invstd = a = 1, beta 0 for every layer: the BN-free towers
+    TRY(launch_bn_identity(w.mean, w.invstd, w.a, w.ones, w.zeros, w.cmax, c.H, c.D, s));
+    if (train && !acc_cleared)  // the epilogues still add their (unused) BN sums
+      DCUE_HIP_CHECK(hipMemsetAsync(w.bnacc, 0, sizeof(unsigned long long) * 6 * 2 * w.cmax * 2, s));
+  } else if (train) {
     if (!acc_cleared)
       DCUE_HIP_CHECK(hipMemsetAsync(w.bnacc, 0, sizeof(unsigned long long) * 6 * 2 * w.cmax * 2, s));
     TRY(launch_input_stats(src, t->data, item_track, counts, M, bn_acc(w.bnacc, w.cmax, 0), s));
@@ -341,7 +378,7 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     a.item_track = item_track;
     a.in_mean = w.mean[l - 1];
     a.in_a = w.a[l - 1];
-    a.in_beta = c.P(seg_bn_b(l - 1));
+    a.in_beta = c.beta(w, l - 1);
     a.in_bn = bn_of(l - 1);
     a.counts = counts;
     a.wpack = m->wpack + wpack_offset(&m->dims, l, false);
@@ -356,11 +393,23 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     TRY(launch_conv_fwd(l, l == 1 ? kMels : c.H, l == 1 ? src : SRC_ACT, a, s));
     TRY(timer_end(&tsc));
   }
+  if (c.res) {  // fc on [tp1, tp2, tp3, tp4, bn5(y5)] (truedcuemel1dres.py:93-97)
+    TRY(launch_timepool(w.y, w.mean, w.a, c.bn ? c.P(seg_bn_b(1)) : nullptr, c.bn ? c.P(seg_bn_b(2)) : nullptr,
+                        c.bn ? c.P(seg_bn_b(3)) : nullptr, c.bn ? c.P(seg_bn_b(4)) : nullptr,
+                        c.bn ? c.P(seg_bn_b(5)) : nullptr, bn_of(5), M, c.H, c.D, w.xfc, s));
+    TGemmArgs g = {};
+    g.M = M; g.N = c.D; g.K = c.FI;
+    g.A = w.xfc; g.sam = c.FI; g.sak = 1;
+    g.B = c.P(SEG_FC_W); g.sbk = 1; g.sbn = c.FI;
+    g.bias = c.P(SEG_FC_B);
+    g.C = f_out ? f_out : w.f; g.scm = c.D; g.scn = 1;
+    return launch_tgemm(0, 0, g, s);
+  }
   // fc on BN5(y5): f = bn5(y5) W^T + b   (truedcuemel1dbn.py:65,101)
   TGemmArgs g = {};
   g.M = M; g.N = c.D; g.K = c.D;
   g.A = w.y[5]; g.sam = c.D; g.sak = 1;
-  g.amean = w.mean[5]; g.aa = w.a[5]; g.abeta = c.P(seg_bn_b(5));
+  g.amean = w.mean[5]; g.aa = w.a[5]; g.abeta = c.beta(w, 5);
   g.abn = bn_of(5);
   g.B = c.P(SEG_FC_W); g.sbk = 1; g.sbn = c.D;
   g.bias = c.P(SEG_FC_B);
@@ -620,11 +669,30 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   {
     TRY(wait_point(sw[1], ev_score));
     ForkAfter fk(sp, sw[1], &ev_x0);
-    TRY(launch_xhat0(src, t->data, b->item_track, M, bn_acc(w.bnacc, w.cmax, 0), copies * kFrames, w.xhat0,
-                     sw[1]));
+    TRY(launch_xhat0(src, t->data, b->item_track, M, c.bn ? bn_acc(w.bnacc, w.cmax, 0) : nullptr,
+                     copies * kFrames, w.xhat0, sw[1]));
     TRY(fk.done());
   }
-  {  // per-item feature gradients df, then (same kernel) the fc input gradient g5 = df W and BN5's sums
+  if (c.res) {  // df; then the fc input gradient split: g5 = df W[:, 4H:] (+ BN5's sums) and the
+                // time-pooled blocks' dtp = df W[:, :4H]
+    TRY(launch_item_grad(w.dfcopy, b, D, w.df, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                         o.fuse_score ? w.rowsum : nullptr, w.loss, s));
+    TGemmArgs g = {};
+    g.M = M; g.N = D; g.K = D;
+    g.A = w.df; g.sam = D; g.sak = 1;
+    g.B = c.P(SEG_FC_W) + 4 * H; g.sbk = c.FI; g.sbn = 1;
+    g.C = w.g[5]; g.scm = D; g.scn = 1;
+    g.colacc = bn_acc(w.bnbacc, w.cmax, 5); g.xy = w.y[5]; g.xmean = w.mean[5]; g.xinvstd = w.invstd[5];
+    TRY(launch_tgemm(0, 0, g, s));
+    g = TGemmArgs{};
+    g.M = M; g.N = 4 * H; g.K = D;
+    g.A = w.df; g.sam = D; g.sak = 1;
+    g.B = c.P(SEG_FC_W); g.sbk = c.FI; g.sbn = 1;
+    g.C = w.dtp; g.scm = 4 * H; g.scn = 1;
+    ForkAfter fk(sp, s, &ev_layer[5]);
+    TRY(launch_tgemm(0, 0, g, s));
+    TRY(fk.done());
+  } else {  // per-item feature gradients df, then (same kernel) the fc input gradient g5 = df W and BN5's sums
     ForkAfter fk(sp, s, &ev_layer[5]);
     TRY(launch_item_grad(w.dfcopy, b, D, w.df, c.P(SEG_FC_W), w.g[5], bn_acc(w.bnbacc, w.cmax, 5),
                          w.y[5], w.mean[5], w.invstd[5], o.fuse_score ? w.rowsum : nullptr, w.loss, s));
@@ -638,7 +706,13 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     ra.src = w.g[l]; ra.y_l = w.y[l]; ra.idx_l = w.idx[l];
     ra.mean_l = w.mean[l]; ra.invstd_l = w.invstd[l]; ra.a_l = w.a[l];
     ra.dz_acc = bn_acc(w.bnbacc, w.cmax, l);
-    ra.invN = (float)(1.0 / (copies * gm.lp)); ra.counts = w.counts;
+    ra.invN = c.bn ? (float)(1.0 / (copies * gm.lp)) : 0.f;  // 0: BN backward is the identity
+    ra.counts = w.counts;
+    if (c.res) {  // + d tp_{l-1} / Lp_{l-1} at every position of block l-1 (AvgPool1d backward)
+      ra.skip = w.dtp + (l - 2) * H;
+      ra.skip_ld = 4 * H;
+      ra.skip_scale = 1.0f / (float)layer_geom(l - 1).lp;
+    }
     ra.wpack = m->wpack + wpack_offset(&m->dims, l, true);
     ra.out = w.g[l - 1];
     ra.out_acc = bn_acc(w.bnbacc, w.cmax, l - 1);
@@ -664,11 +738,12 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     wa.item_track = b->item_track;
     wa.x_mean = w.mean[l - 1];
     wa.x_a = l == 1 ? w.invstd[0] : w.a[l - 1];
-    wa.x_beta = l == 1 ? nullptr : c.P(seg_bn_b(l - 1));
+    wa.x_beta = l == 1 ? nullptr : c.beta(w, l - 1);
     wa.g_l = w.g[l]; wa.y_l = w.y[l]; wa.idx_l = w.idx[l];
     wa.mean_l = w.mean[l]; wa.invstd_l = w.invstd[l]; wa.a_l = w.a[l];
-    wa.dz_acc = bn_acc(w.bnbacc, w.cmax, l); wa.dgamma = c.Gd(seg_bn_w(l)); wa.dbeta = c.Gd(seg_bn_b(l));
-    wa.invN = (float)(1.0 / (copies * gm.lp)); wa.counts = w.counts;
+    wa.dz_acc = bn_acc(w.bnbacc, w.cmax, l); wa.dgamma = c.dgamma(w, l); wa.dbeta = c.dbeta(w, l);
+    wa.invN = c.bn ? (float)(1.0 / (copies * gm.lp)) : 0.f;
+    wa.counts = w.counts;
     wa.M = M; wa.cout = C; wa.cin = cin;
     wa.wpart = w.wpart[ps]; wa.bpart = w.bpart[ps];
     const int nch = wgrad_nchunk(l, M, C, cin);
@@ -692,8 +767,8 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(launch_wgrad_reduce(l, wa.wpart, wa.bpart, nch, C, cin, c.Gd(seg_conv_w(l)),
                             c.Gd(seg_conv_b(l)), w.G, w.S, so));
     ForkAfter fk(sp, so, tail);
-    TRY(launch_bn0_grads(w.G, w.S, c.P(seg_conv_w(1)), c.P(seg_bn_w(0)), c.P(seg_bn_b(0)), H,
-                         c.Gd(seg_conv_w(1)), c.Gd(seg_bn_w(0)), c.Gd(seg_bn_b(0)),
+    TRY(launch_bn0_grads(w.G, w.S, c.P(seg_conv_w(1)), c.gamma(w, 0), c.beta(w, 0), H,
+                         c.Gd(seg_conv_w(1)), c.dgamma(w, 0), c.dbeta(w, 0),
                          c.Gd(seg_conv_b(1)), so));
     return fk.done();
   };
@@ -707,13 +782,18 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(wait_point(sw[0], ev_df));
     HPROF("capi:23");
     TGemmArgs g = {};
-    g.M = D; g.N = D; g.K = M;
+    g.M = D; g.N = c.FI; g.K = M;
     g.A = w.df; g.sam = 1; g.sak = D;
-    g.B = w.y[5]; g.sbk = D; g.sbn = 1;
-    g.bmean = w.mean[5]; g.ba = w.a[5]; g.bbeta = c.P(seg_bn_b(5));
-    g.C = c.Gd(SEG_FC_W); g.scm = D; g.scn = 1;
+    g.C = c.Gd(SEG_FC_W); g.scm = c.FI; g.scn = 1;
     g.rowsum = c.Gd(SEG_FC_B);
-    TRY(launch_tgemm(0, 2, g, sw[0]));
+    if (c.res) {  // dW[n][k] = sum_m df[m][n] xfc[m][k] over the concatenated fc input
+      g.B = w.xfc; g.sbk = c.FI; g.sbn = 1;
+      TRY(launch_tgemm(0, 0, g, sw[0]));
+    } else {
+      g.B = w.y[5]; g.sbk = D; g.sbn = 1;
+      g.bmean = w.mean[5]; g.ba = w.a[5]; g.bbeta = c.beta(w, 5);
+      TRY(launch_tgemm(0, 2, g, sw[0]));
+    }
     HPROF("capi:24");
   }
   // layers 5..2: alternating between the two wgrad streams (each with its own partial set)

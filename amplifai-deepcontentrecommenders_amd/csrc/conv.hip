@@ -305,7 +305,8 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (grb + j < total) {
-            const float gv = acc[r][ct][j];
+            float gv = acc[r][ct][j];
+            if (a.skip) gv += a.skip[((grb + j) / R) * a.skip_ld + o] * a.skip_scale;
             a.out[(grb + j) * nout + o] = gv;
             sg[ct] += gv;
             sgx[ct] += gv * ((yv[j] - mu) * is);
@@ -1025,9 +1026,14 @@ __global__ __launch_bounds__(256) void k_xhat0(const void* __restrict__ tracks, 
                                                double inv_count, float* __restrict__ xhat0) {
   __shared__ float s_mu[kMels], s_is[kMels];
   if (threadIdx.x < kMels) {
-    const BnChan st = bn_chan_train(acc0, kMels, threadIdx.x, count, inv_count);
-    s_mu[threadIdx.x] = st.mean;
-    s_is[threadIdx.x] = st.invstd;
+    if (acc0) {
+      const BnChan st = bn_chan_train(acc0, kMels, threadIdx.x, count, inv_count);
+      s_mu[threadIdx.x] = st.mean;
+      s_is[threadIdx.x] = st.invstd;
+    } else {  // towers without bn0: the raw input
+      s_mu[threadIdx.x] = 0.f;
+      s_is[threadIdx.x] = 1.f;
+    }
   }
   __syncthreads();
   const long n4 = (long)(M + 1) * kXp * (kMels / 4);  // item M: zeros

@@ -61,6 +61,18 @@ constexpr int kFrames = DCUE_N_FRAMES; // 131, datasets/dcuedataset.py:235
 constexpr int kXp = kFrames + 5;        // zero-padded xhat0 rows per item: every conv-1 tap row exists
 constexpr int kWave = 64;
 
+// Tower variant (dcue_dims.tower): BatchNorm present, time-pooled skips into the fc
+__host__ __device__ inline bool tower_has_bn(const dcue_dims* d) {
+  return d->tower == DCUE_TOWER_BN || d->tower == DCUE_TOWER_RESBN;
+}
+__host__ __device__ inline bool tower_res(const dcue_dims* d) {
+  return d->tower == DCUE_TOWER_RES || d->tower == DCUE_TOWER_RESBN;
+}
+// fc input width: d, or 4H + d with the four time-pooled block outputs (truedcuemel1dres.py:63-64)
+__host__ __device__ inline int fc_in(const dcue_dims* d) {
+  return tower_res(d) ? 4 * d->conv_hidden + d->feature_dim : d->feature_dim;
+}
+
 // Per-layer geometry of the default item tower (truedcuemel1dbn.py:25-61).
 //   conv positions Lconv = Lin + 2*pad - ks + 1, pooled Lp = floor(Lconv / pool); only the
 //   R = Lp*pool conv rows that land in a pool window are computed (the reference drops the rest).

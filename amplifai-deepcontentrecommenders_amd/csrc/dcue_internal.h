@@ -61,6 +61,11 @@ struct RowsArgs {
   const float* oinvstd;
   int M;
   int nout;
+  // dgrad, res towers: out[i][t][o] += skip[i * skip_ld + o] * skip_scale (the time-pooled skip's
+  // gradient, AvgPool1d backward), before BN_{l-1}'s backward sums
+  const float* skip;
+  int skip_ld;
+  float skip_scale;
 };
 
 struct WgradArgs {
@@ -201,6 +206,14 @@ int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float s
 int launch_adam(const dcue_model* m, const dcue_adam_args* a, const int64_t* poff, hipStream_t s,
                 bool flush_slice = true);
 int launch_emb_flush_rows(const dcue_model* m, int step, hipStream_t s);
+// BN-free towers: mean 0, invstd = a = 1 for the six BN layers, plus the ones / zeros arrays
+int launch_bn_identity(float* const* mean, float* const* invstd, float* const* a, float* ones, float* zeros,
+                       int cmax, int H, int D, hipStream_t s);
+// res towers: xfc[i] = [mean_t bn_1(y_1), ..., mean_t bn_4(y_4), bn_5(y_5)] (truedcuemel1dres.py:93-97);
+// p5 (train, BN): BN_5 finalized from its accumulators here (block 0 publishes it)
+int launch_timepool(float* const* y, float* const* mean, float* const* a, const float* beta1, const float* beta2,
+                    const float* beta3, const float* beta4, const float* beta5, const BnPublish& p5, int M, int H,
+                    int D, float* xfc, hipStream_t s);
 // SGD / Ranger over the dense buffer and the user table (optim.hip)
 int launch_opt(const dcue_model* m, const dcue_opt_args* a, const dcue_opt_state* st, long n_dense,
                hipStream_t s);

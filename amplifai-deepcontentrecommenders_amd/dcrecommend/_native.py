@@ -33,7 +33,7 @@ DENSE_NAMES = (["conv.bn0.weight", "conv.bn0.bias"]
 
 class Dims(ctypes.Structure):
     _fields_ = [("conv_hidden", ctypes.c_int32), ("feature_dim", ctypes.c_int32),
-                ("user_embdim", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("user_embdim", ctypes.c_int32), ("tower", ctypes.c_int32),
                 ("n_users", ctypes.c_int64)]
 
 
@@ -97,7 +97,7 @@ class PlanConfig(ctypes.Structure):
 
 MT_STATE_BYTES = 624 * 4 + 16
 MAX_LOG_CAP = 256
-ABI_VERSION = 5
+ABI_VERSION = 6
 RANK_SPLIT, RANK_SINGLE = 0, 1
 
 _P = ctypes.c_void_p
@@ -199,8 +199,11 @@ def require_gpu(t, name):
         raise RuntimeError("%s must be a GPU tensor (the DCUE path runs only on the MI355X)" % name)
 
 
-def make_dims(conv_hidden, feature_dim, user_embdim, n_users):
-    return Dims(conv_hidden, feature_dim, user_embdim, 0, n_users)
+TOWERS = {"truedcuemel1dbn": 0, "truedcuemel1d": 1, "truedcuemel1dres": 2, "truedcuemel1dresbn": 3}
+
+
+def make_dims(conv_hidden, feature_dim, user_embdim, n_users, model_type="truedcuemel1dbn"):
+    return Dims(conv_hidden, feature_dim, user_embdim, TOWERS[model_type], n_users)
 
 
 def param_layout(dims):

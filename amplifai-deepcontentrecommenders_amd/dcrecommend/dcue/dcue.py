@@ -16,30 +16,36 @@ from torch import nn
 
 from dcrecommend import _native as nat
 
-SUPPORTED_TYPES = ("truedcuemel1dbn",)
 REFERENCE_TYPES = ("truedcuemel1d", "truedcuemel1dres", "truedcuemel1dbn", "truedcuemel1dresbn")
+SUPPORTED_TYPES = REFERENCE_TYPES
 
-# conv stack of the default tower, truedcuemel1dbn.py:25-61: (kernel, padding) per layer
+# conv stack shared by the towers, truedcuemel1dbn.py:25-61: (kernel, padding) per layer
 _CONV = ((4, 2), (4, 2), (4, 2), (2, 1), (1, 0))
 
 
 class _ItemTower(nn.Module):
-    """Parameter container with the reference's names (conv.bn0..5, conv.layer1..5, conv.fc)."""
+    """Parameter container with the reference's names (conv.bn0..5, conv.layer1..5, conv.fc) for the
+    four towers DCUENet wires (dcue/dcue.py:49-59): truedcuemel1dbn (default), truedcuemel1d (no
+    BatchNorm), truedcuemel1dres / truedcuemel1dresbn (time-pooled skips into fc(4H + d -> d))."""
 
-    def __init__(self, feature_dim, conv_hidden):
+    def __init__(self, feature_dim, conv_hidden, model_type="truedcuemel1dbn"):
         super().__init__()
+        bn = model_type in ("truedcuemel1dbn", "truedcuemel1dresbn")
+        res = model_type in ("truedcuemel1dres", "truedcuemel1dresbn")
         chans = [nat.N_MELS] + [conv_hidden] * 4 + [feature_dim]
-        # construction order = RNG consumption order of the reference constructor
+        # construction order = RNG consumption order of the reference constructors (BN draws nothing)
         for l in range(6):
-            self.add_module("bn%d" % l, nn.BatchNorm1d(chans[l]))
+            if bn:
+                self.add_module("bn%d" % l, nn.BatchNorm1d(chans[l]))
             if l < 5:
                 k, pad = _CONV[l]
                 self.add_module("layer%d" % (l + 1), nn.Conv1d(chans[l], chans[l + 1], k, 1, pad, bias=True))
-        self.fc = nn.Linear(feature_dim, feature_dim)
+        self.fc = nn.Linear(4 * conv_hidden + feature_dim if res else feature_dim, feature_dim)
         for l in range(1, 6):
             nn.init.kaiming_uniform_(getattr(self, "layer%d" % l).weight, nonlinearity="relu")
         nn.init.xavier_uniform_(self.fc.weight)
-        self.outsize = [conv_hidden, 1]
+        if model_type == "truedcuemel1dbn":
+            self.outsize = [conv_hidden, 1]
         self._owner = None
 
     def forward(self, X):
@@ -101,10 +107,7 @@ class DCUENet(nn.Module):
         self.model_type = dict_args["model_type"]
         if self.model_type not in REFERENCE_TYPES:
             raise ValueError("{} is not a recognized model type!".format(self.model_type))
-        if self.model_type not in SUPPORTED_TYPES:
-            raise NotImplementedError("model_type %r is valid in the reference but only %r is built "
-                                      "on MI355X so far" % (self.model_type, SUPPORTED_TYPES))
-        self.conv = _ItemTower(self.feature_dim, self.conv_hidden)
+        self.conv = _ItemTower(self.feature_dim, self.conv_hidden, self.model_type)
         self.user_embd = _UserTower(self.user_count, self.user_embdim, self.feature_dim)
         self.sim = nn.CosineSimilarity(dim=1)
         self.conv._owner = weakref.ref(self)
@@ -126,13 +129,16 @@ class DCUENet(nn.Module):
 
     def _flatten(self, device):
         """Move every dense parameter/buffer into the flat buffers the C ABI addresses."""
-        dims = nat.make_dims(self.conv_hidden, self.feature_dim, self.user_embdim, self.user_count)
+        dims = nat.make_dims(self.conv_hidden, self.feature_dim, self.user_embdim, self.user_count,
+                             self.model_type)
         poff = nat.param_layout(dims)
         boff = nat.bn_layout(dims)
         named = dict(self.named_parameters())
         P = torch.zeros(poff[-1], dtype=torch.float32, device=device)
         G = torch.zeros_like(P)
         for s, name in enumerate(nat.DENSE_NAMES):
+            if name not in named:  # BN parameters of a tower without BatchNorm: empty segment
+                continue
             p = named[name]
             n = p.numel()
             P[poff[s]:poff[s] + n].copy_(p.data.reshape(-1))
@@ -141,7 +147,9 @@ class DCUENet(nn.Module):
         stats = torch.zeros(boff[-1], dtype=torch.float32, device=device)
         nbt = torch.zeros(nat.N_BN, dtype=torch.int64, device=device)
         for l in range(nat.N_BN):
-            bn = getattr(self.conv, "bn%d" % l)
+            bn = getattr(self.conv, "bn%d" % l, None)
+            if bn is None:
+                continue
             C = bn.num_features
             stats[boff[2 * l]:boff[2 * l] + C].copy_(bn.running_mean)
             stats[boff[2 * l + 1]:boff[2 * l + 1] + C].copy_(bn.running_var)
@@ -297,8 +305,9 @@ class DCUENet(nn.Module):
         # kept compact: embedding_grad_dense() materialises it on request)
         named = dict(self.named_parameters())
         for s, name in enumerate(nat.DENSE_NAMES):
-            p = named[name]
-            p.grad = fl["G"][fl["poff"][s]:fl["poff"][s] + p.numel()].view(p.shape)
+            p = named.get(name)
+            if p is not None:
+                p.grad = fl["G"][fl["poff"][s]:fl["poff"][s] + p.numel()].view(p.shape)
         self.user_embd.embeddings.weight.grad = None
         self._grad_users = users
 

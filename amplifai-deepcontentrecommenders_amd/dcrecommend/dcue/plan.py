@@ -67,8 +67,9 @@ class TrainPlan:
         # the replayed backward writes the flat gradient: expose the reference-shaped .grad views
         named = dict(net.named_parameters())
         for s, name in enumerate(nat.DENSE_NAMES):
-            p = named[name]
-            p.grad = fl["G"][fl["poff"][s]:fl["poff"][s] + p.numel()].view(p.shape)
+            p = named.get(name)
+            if p is not None:
+                p.grad = fl["G"][fl["poff"][s]:fl["poff"][s] + p.numel()].view(p.shape)
         net.user_embd.embeddings.weight.grad = None
         net._grad_users = self.users
 

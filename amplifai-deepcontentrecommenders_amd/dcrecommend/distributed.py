@@ -60,7 +60,8 @@ def late_grad_floats(net):
     segments [0, SEG_LATE) of the reference order); everything after is final once the plan's side
     streams are in."""
     from . import _native as nat
-    dims = nat.make_dims(net.conv_hidden, net.feature_dim, net.user_embdim, net.user_count)
+    dims = net._flat["dims"] if net._flat is not None else nat.make_dims(
+        net.conv_hidden, net.feature_dim, net.user_embdim, net.user_count, net.model_type)
     return nat.param_layout(dims)[nat.SEG_LATE]
 
 

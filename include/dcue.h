@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DCUE_ABI_VERSION 5
+#define DCUE_ABI_VERSION 6
 #define DCUE_N_MELS 128
 #define DCUE_N_FRAMES 131
 #define DCUE_N_BN 6
@@ -42,11 +42,23 @@ typedef enum {
   DCUE_ERR_WORKSPACE = 4    /* workspace too small */
 } dcue_status;
 
+/* Item towers DCUENet wires by model_type (dcue/dcue.py:49-59):
+ *   BN    truedcuemel1dbn    bn0 -> 4x[conv, pool, relu, bn] -> conv, relu, bn -> fc(d -> d) (default)
+ *   PLAIN truedcuemel1d      the same without any BatchNorm
+ *   RES   truedcuemel1dres   no BN; each block's output also time-averaged (AvgPool1d over all its
+ *                            positions) and concatenated with the last block: fc(4H + d -> d)
+ *   RESBN truedcuemel1dresbn RES with the BN tower's BatchNorms (the averages taken after each BN)
+ * In the towers without BN the segments of the BN parameters are empty (dcue_param_layout). */
+#define DCUE_TOWER_BN 0
+#define DCUE_TOWER_PLAIN 1
+#define DCUE_TOWER_RES 2
+#define DCUE_TOWER_RESBN 3
+
 typedef struct dcue_dims {
   int32_t conv_hidden; /* H: nn/dcue.py:45 conv_hidden (multiple of 32, <= 256) */
   int32_t feature_dim; /* d: feature_dim (multiple of 32, <= 256) */
   int32_t user_embdim; /* E: u_embdim (<= 1024) */
-  int32_t reserved;
+  int32_t tower;       /* DCUE_TOWER_* */
   int64_t n_users;     /* rows of the (local shard of the) user table */
 } dcue_dims;
 

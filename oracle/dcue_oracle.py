@@ -35,25 +35,40 @@ BN_MOMENTUM = 0.1
 CONV_SPECS = ((4, 2, 4), (4, 2, 4), (4, 2, 4), (2, 1, 2), (1, 0, 1))
 
 
-def param_names():
-    """Reference parameter order (DCUENet.named_parameters())."""
-    names = ["conv.bn0.weight", "conv.bn0.bias"]
+TOWERS = ("truedcuemel1dbn", "truedcuemel1d", "truedcuemel1dres", "truedcuemel1dresbn")
+
+
+def has_bn(model_type):
+    return model_type in ("truedcuemel1dbn", "truedcuemel1dresbn")
+
+
+def is_res(model_type):
+    return model_type in ("truedcuemel1dres", "truedcuemel1dresbn")
+
+
+def param_names(model_type="truedcuemel1dbn"):
+    """Reference parameter order (DCUENet.named_parameters()) of each wired tower
+    (dcue/dcue.py:49-59; audiomodels/truedcuemel1d*.py __init__ order)."""
+    bn = has_bn(model_type)
+    names = ["conv.bn0.weight", "conv.bn0.bias"] if bn else []
     for l in range(1, 6):
-        names += ["conv.layer%d.weight" % l, "conv.layer%d.bias" % l,
-                  "conv.bn%d.weight" % l, "conv.bn%d.bias" % l]
+        names += ["conv.layer%d.weight" % l, "conv.layer%d.bias" % l]
+        if bn:
+            names += ["conv.bn%d.weight" % l, "conv.bn%d.bias" % l]
     names += ["conv.fc.weight", "conv.fc.bias", "user_embd.embeddings.weight",
               "user_embd.linear1.weight", "user_embd.linear1.bias",
               "user_embd.linear2.weight", "user_embd.linear2.bias"]
     return names
 
 
-def init_params(feature_dim, conv_hidden, user_embdim, user_count):
+def init_params(feature_dim, conv_hidden, user_embdim, user_count, model_type="truedcuemel1dbn"):
     """Create parameters + BN buffers consuming torch's global CPU RNG in reference order.
 
     Order of RNG use in the reference constructors: each Conv1d/Linear default reset
     (kaiming_uniform a=sqrt(5) on the weight, U(+-1/sqrt(fan_in)) on the bias) as the modules are
     built (layer1..layer5, fc), then the explicit kaiming_uniform_(relu) on layer1..5 and
-    xavier_uniform_ on fc, then Embedding N(0,1), linear1, linear2 defaults.
+    xavier_uniform_ on fc, then Embedding N(0,1), linear1, linear2 defaults. BatchNorm layers draw
+    nothing; the res towers' fc is Linear(4H + d, d) (truedcuemel1dres.py:63-64).
     """
     H, d, E = conv_hidden, feature_dim, user_embdim
     p, b = {}, {}
@@ -67,18 +82,20 @@ def init_params(feature_dim, conv_hidden, user_embdim, user_count):
     shapes = [(H, N_MELS, 4), (H, H, 4), (H, H, 4), (H, H, 2), (d, H, 1)]
     chans = [N_MELS, H, H, H, H, d]
     for l in range(6):
-        p["conv.bn%d.weight" % l] = torch.ones(chans[l])
-        p["conv.bn%d.bias" % l] = torch.zeros(chans[l])
-        b["conv.bn%d.running_mean" % l] = torch.zeros(chans[l])
-        b["conv.bn%d.running_var" % l] = torch.ones(chans[l])
-        b["conv.bn%d.num_batches_tracked" % l] = torch.tensor(0, dtype=torch.long)
+        if has_bn(model_type):
+            p["conv.bn%d.weight" % l] = torch.ones(chans[l])
+            p["conv.bn%d.bias" % l] = torch.zeros(chans[l])
+            b["conv.bn%d.running_mean" % l] = torch.zeros(chans[l])
+            b["conv.bn%d.running_var" % l] = torch.ones(chans[l])
+            b["conv.bn%d.num_batches_tracked" % l] = torch.tensor(0, dtype=torch.long)
         if l < 5:
             w = torch.empty(shapes[l])
             bias = torch.empty(shapes[l][0])
             default_reset(w, bias)
             p["conv.layer%d.weight" % (l + 1)] = w
             p["conv.layer%d.bias" % (l + 1)] = bias
-    fcw, fcb = torch.empty(d, d), torch.empty(d)
+    fi = 4 * H + d if is_res(model_type) else d
+    fcw, fcb = torch.empty(d, fi), torch.empty(d)
     default_reset(fcw, fcb)
     for l in range(1, 6):
         torch.nn.init.kaiming_uniform_(p["conv.layer%d.weight" % l], nonlinearity="relu")
@@ -92,10 +109,12 @@ def init_params(feature_dim, conv_hidden, user_embdim, user_count):
         default_reset(w, bias)
         p["user_embd.%s.weight" % name] = w
         p["user_embd.%s.bias" % name] = bias
-    return {k: p[k] for k in param_names()}, b
+    return {k: p[k] for k in param_names(model_type)}, b
 
 
 def _bn(x, p, b, l, train):
+    if "conv.bn%d.weight" % l not in p:  # towers without BatchNorm (truedcuemel1d, ...res)
+        return x
     out = F.batch_norm(x, b["conv.bn%d.running_mean" % l], b["conv.bn%d.running_var" % l],
                        p["conv.bn%d.weight" % l], p["conv.bn%d.bias" % l],
                        training=train, momentum=BN_MOMENTUM, eps=BN_EPS)
@@ -121,11 +140,20 @@ def _pool_relu(h, pool, route):
 
 
 def item_tower(p, b, X, train=True, route=None):
-    """X [M,128,131] fp32 -> [M,d] (truedcuemel1dbn.py:77-101). route: {layer: (argmax, live)}."""
+    """X [M,128,131] fp32 -> [M,d]: truedcuemel1dbn.py:77-101 (and, by the parameters present, the
+    BN-free truedcuemel1d.py and the res towers' truedcuemel1dres(bn).py forward: each block's
+    output time-averaged by AvgPool1d over its positions, concatenated with the last block before
+    the fc). route: {layer: (argmax, live)}."""
+    res = p["conv.fc.weight"].shape[1] != p["conv.fc.weight"].shape[0]  # fc(4H + d -> d)
     h = _bn(X, p, b, 0, train)
+    pools = []
     for l, (k, pad, pool) in enumerate(CONV_SPECS, start=1):
         h = F.conv1d(h, p["conv.layer%d.weight" % l], p["conv.layer%d.bias" % l], padding=pad)
         h = _bn(_pool_relu(h, pool, None if route is None else route[l]), p, b, l, train)
+        if res and l < 5:
+            pools.append(F.avg_pool1d(h, kernel_size=h.shape[2]))
+    if res:
+        h = torch.cat(pools + [h], dim=1)
     return F.linear(h.permute(0, 2, 1), p["conv.fc.weight"], p["conv.fc.bias"]).squeeze()
 
 

@@ -8,7 +8,9 @@ Every fixture is data (inputs + the reference's outputs); no reference source is
 Which reference code produced what:
 
 * model_*.npz   -- dcrecommend/dcue/dcue.py:21-108 (DCUENet fwd), nn/dcue.py:167-170 (hinge loss),
-                   torch autograd backward, torch.optim.Adam as built at nn/dcue.py:143-147.
+                   torch autograd backward, torch.optim.Adam as built at nn/dcue.py:143-147;
+                   model_{plain,res,resbn}.npz the same for the other wired towers
+                   (audiomodels/truedcuemel1d.py, truedcuemel1dres.py, truedcuemel1dresbn.py).
 * inbatch_*.npz -- the in-batch sampler spec of nn/dcue.py:698-709 (commented out in the reference;
                    the draws below follow that text literally), plus a forward/backward of the
                    reference model on the duplicated [pos; neg] batch it builds.
@@ -69,11 +71,12 @@ def _save(name, **arrays):
     print("wrote", path, sum(a.nbytes for a in out.values()) // 1024, "KiB raw")
 
 
-def model_fixture(name, H, d, n_users, B, N, lr=1e-3, store_init=True, store_steps=True, seed=0):
+def model_fixture(name, H, d, n_users, B, N, lr=1e-3, store_init=True, store_steps=True, seed=0,
+                  model_type="truedcuemel1dbn"):
     """fwd (train) -> hinge -> bwd -> Adam(lr) step -> Adam(lr, wd=1e-4) step -> eval fwd."""
     torch.manual_seed(seed)
     net = DCUENet({"feature_dim": d, "conv_hidden": H, "user_embdim": 300,
-                   "user_count": n_users, "model_type": "truedcuemel1dbn"})
+                   "user_count": n_users, "model_type": model_type})
     init = _state(net)
     gen = torch.Generator().manual_seed(seed + 1)
     u = torch.randint(0, n_users, (B,), generator=gen)
@@ -102,7 +105,7 @@ def model_fixture(name, H, d, n_users, B, N, lr=1e-3, store_init=True, store_ste
     with torch.no_grad():
         e_scores, e_uf, e_pf, e_nf = net(u, pos, neg)
 
-    payload = dict(H=H, d=d, n_users=n_users, B=B, N=N, lr=lr, seed=seed,
+    payload = dict(H=H, d=d, n_users=n_users, B=B, N=N, lr=lr, seed=seed, model_type=model_type,
                    u=u, pos=pos.half(), neg=neg.half(),
                    scores=scores, uf=uf, pf=pf, nf=nf, loss=loss,
                    eval_scores=e_scores, eval_uf=e_uf, eval_pf=e_pf, eval_nf=e_nf)
@@ -512,6 +515,10 @@ if __name__ == "__main__":
         "model": lambda: (model_fixture("model_tiny.npz", H=32, d=32, n_users=10, B=4, N=3),
                           model_fixture("model_h128.npz", H=128, d=128, n_users=10, B=2, N=2,
                                         store_init=False, store_steps=False)),
+        "towers": lambda: [model_fixture("model_%s.npz" % tag, H=32, d=32, n_users=10, B=4, N=3,
+                                         store_init=False, model_type=mt)
+                           for tag, mt in (("plain", "truedcuemel1d"), ("res", "truedcuemel1dres"),
+                                           ("resbn", "truedcuemel1dresbn"))],
         "inbatch": inbatch_fixtures, "catalogue": catalogue_fixture, "batches": batches_fixture,
         "scheduler": scheduler_fixture, "train5": train5_fixture, "metrics": metrics_fixture,
         "eval": eval_fixture, "fit": fit_fixture, "optim": optim_fixture,

@@ -23,7 +23,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
-B, N, D, H, E = 64, 20, 128, 128, 300
+E = 300
 N_USERS, N_TRACKS = 400, 700
 LRS = [1e-4, 2e-4, 1e-4, 5e-5]
 
@@ -40,7 +40,7 @@ def _close(got, ref, rtol, afrac, what):
 LP = (33, 8, 2, 1, 1)
 
 
-def _gpu_route(net, nat, B, N, M, rows):
+def _gpu_route(net, nat, B, N, M, rows, D, H):
     """The step's max-pool argmax and relu-live masks as the GPU computed them (workspace, layout
     [M][Lp][C]), as oracle routes [rows, C, Lp] over the literal [pos; neg] stack."""
     route = {}
@@ -79,8 +79,14 @@ def _check_decisions(pre, route, tie=1e-5):
     return flips
 
 
-@pytest.mark.parametrize("mode", ["inbatch", "catalogue"])
-def test_plan_at_bench_shape_against_oracle(mode):
+CASES = [("inbatch", "truedcuemel1dbn", 64, 20, 128, 128), ("catalogue", "truedcuemel1dbn", 64, 20, 128, 128)]
+# the other wired towers (dcue/dcue.py:49-59) through the same plan, at a smaller shape
+CASES += [(mode, mt, 16, 5, 64, 64) for mt in ("truedcuemel1d", "truedcuemel1dres", "truedcuemel1dresbn")
+          for mode in ("inbatch", "catalogue")]
+
+
+@pytest.mark.parametrize("mode,model_type,B,N,D,H", CASES)
+def test_plan_at_bench_shape_against_oracle(mode, model_type, B, N, D, H):
     from dcrecommend import _native as nat
     from dcrecommend.dcue.dcue import DCUENet
     from dcrecommend.dcue.plan import TrainPlan
@@ -89,9 +95,9 @@ def test_plan_at_bench_shape_against_oracle(mode):
     inbatch = mode == "inbatch"
     torch.manual_seed(0)
     net = DCUENet({"feature_dim": D, "conv_hidden": H, "user_embdim": E, "user_count": N_USERS,
-                   "model_type": "truedcuemel1dbn"}).to(DEV).train()
+                   "model_type": model_type}).to(DEV).train()
     torch.manual_seed(0)
-    p, b = O.init_params(D, H, E, N_USERS)
+    p, b = O.init_params(D, H, E, N_USERS, model_type)
     adam = O.AdamState(p)
     p0 = {k: v.clone() for k, v in p.items()}
     b0 = {k: v.clone() for k, v in b.items()}
@@ -148,7 +154,7 @@ def test_plan_at_bench_shape_against_oracle(mode):
             #     decision is not such a near-tie;
             # (2) the gradients are compared with the fp64 oracle run on the GPU's decisions.
             rows = torch.cat([torch.arange(B), r.reshape(-1)]) if inbatch else torch.arange(M)
-            route = _gpu_route(net, nat, B, N, M, rows)
+            route = _gpu_route(net, nat, B, N, M, rows, D, H)
             p64 = {k: v.double() for k, v in p0.items()}
             b64 = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in b0.items()}
             lit = torch.cat([pos, neg.reshape(B * N, 128, 131)]).double()

@@ -36,8 +36,9 @@ def _assert_close(a, b, rtol, afrac, what):
 def _net(g, seed=0):
     from dcrecommend.dcue.dcue import DCUENet
     torch.manual_seed(seed)
+    mt = str(g["model_type"]) if "model_type" in g.files else "truedcuemel1dbn"
     net = DCUENet({"feature_dim": int(g["d"]), "conv_hidden": int(g["H"]), "user_embdim": 300,
-                   "user_count": int(g["n_users"]), "model_type": "truedcuemel1dbn"})
+                   "user_count": int(g["n_users"]), "model_type": mt})
     return net.cuda()
 
 
@@ -84,8 +85,11 @@ def _check_params_after_adam(net, g, prefix, lr_budget, skip_rows=None, grad_pre
             assert float(err[firm].max()) <= tight, ("firm-gradient elements", k, float(err[firm].max()))
 
 
-@pytest.mark.parametrize("name", ["model_tiny.npz", "model_h128.npz"])
+@pytest.mark.parametrize("name", ["model_tiny.npz", "model_h128.npz", "model_plain.npz", "model_res.npz",
+                                  "model_resbn.npz"])
 def test_module_forward_backward(golden, name):
+    """The reference's own fwd / hinge / bwd / Adam steps for each wired tower (dcue/dcue.py:49-59:
+    truedcuemel1dbn at H = 32 and 128, truedcuemel1d, truedcuemel1dres, truedcuemel1dresbn)."""
     g = golden(name)
     net = _net(g, int(g["seed"]))
     u = torch.from_numpy(g["u"]).to(DEV)

@@ -104,8 +104,29 @@ def test_dcuenet_model_type_errors():
     args = {"feature_dim": 32, "conv_hidden": 32, "user_embdim": 300, "user_count": 4}
     with pytest.raises(ValueError):
         DCUENet(dict(args, model_type="nope"))
-    with pytest.raises(NotImplementedError):
-        DCUENet(dict(args, model_type="truedcuemel1dres"))
+
+
+@pytest.mark.parametrize("name", ["model_plain.npz", "model_res.npz", "model_resbn.npz"])
+def test_dcuenet_towers_init_match_reference(golden, name):
+    """truedcuemel1d / truedcuemel1dres / truedcuemel1dresbn: the reference's state_dict keys,
+    shapes and init draws (checksums), and a flat layout whose BN segments are empty without BN."""
+    from dcrecommend import _native as nat
+    from dcrecommend.dcue.dcue import DCUENet
+    g = golden(name)
+    mt = str(g["model_type"])
+    torch.manual_seed(int(g["seed"]))
+    net = DCUENet({"feature_dim": int(g["d"]), "conv_hidden": int(g["H"]), "user_embdim": 300,
+                   "user_count": int(g["n_users"]), "model_type": mt})
+    sd = net.state_dict()
+    keys = {k[len("initsum."):] for k in g.files if k.startswith("initsum.")}
+    assert set(sd) == keys
+    for k in keys:
+        assert float(sd[k].double().sum()) == pytest.approx(float(g["initsum." + k]), rel=1e-12, abs=1e-9), k
+    off = nat.param_layout(nat.make_dims(int(g["H"]), int(g["d"]), 300, int(g["n_users"]), mt))
+    named = dict(net.named_parameters())
+    for s_, n in enumerate(nat.DENSE_NAMES):
+        size = named[n].numel() if n in named else 0
+        assert size <= off[s_ + 1] - off[s_] < size + 4, n
 
 
 def test_cpu_model_refuses_compute():

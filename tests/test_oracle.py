@@ -44,11 +44,28 @@ def test_init_h128_checksums(golden):
         assert float(v.double().sum()) == pytest.approx(float(g["initsum." + k]), rel=1e-12, abs=1e-9), k
 
 
-@pytest.mark.parametrize("name", ["model_tiny.npz", "model_h128.npz"])
+def _mt(g):
+    return str(g["model_type"]) if "model_type" in g.files else "truedcuemel1dbn"
+
+
+@pytest.mark.parametrize("name", ["model_plain.npz", "model_res.npz", "model_resbn.npz"])
+def test_init_towers_checksums(golden, name):
+    """The other wired towers (dcue/dcue.py:49-59): parameter names, order and init draws."""
+    g = golden(name)
+    torch.manual_seed(int(g["seed"]))
+    p, b = O.init_params(int(g["d"]), int(g["H"]), 300, int(g["n_users"]), _mt(g))
+    keys = {k[len("initsum."):] for k in g.files if k.startswith("initsum.")}
+    assert keys == set(p) | set(b)
+    for k, v in {**p, **b}.items():
+        assert float(v.double().sum()) == pytest.approx(float(g["initsum." + k]), rel=1e-12, abs=1e-9), k
+
+
+@pytest.mark.parametrize("name", ["model_tiny.npz", "model_h128.npz", "model_plain.npz", "model_res.npz",
+                                  "model_resbn.npz"])
 def test_forward_backward_step(golden, name):
     g = golden(name)
     torch.manual_seed(int(g["seed"]))
-    p, b = O.init_params(int(g["d"]), int(g["H"]), 300, int(g["n_users"]))
+    p, b = O.init_params(int(g["d"]), int(g["H"]), 300, int(g["n_users"]), _mt(g))
     u, pos, neg = _inputs(g)
     loss, grads, (scores, uf, pf, nf) = O.loss_and_grads(p, b, u, pos, neg)
     for key, val in (("scores", scores), ("uf", uf), ("pf", pf), ("nf", nf), ("loss", loss)):
