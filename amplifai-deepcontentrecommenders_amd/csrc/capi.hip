@@ -201,6 +201,7 @@ struct Ws {
   float* g[6];
   float *dh1, *de;
   float *wpart[3], *bpart[3], *G, *S;  // wgrad partials: one set per wgrad stream
+  float *wpm[4], *bpm[4];                // k_conv_wgrad_multi's partials, layers 2..5
   float* xhat0;          // [M][kXp][128] bn0-normalised, zero-padded input: conv-1 wgrad's X operand
   float* dx1;            // [M][33][H] BN1 backward at the pooled positions: conv-1 wgrad's dz operand
   // towers without BN: the BN operands every kernel reads become the identity (mean 0, a = invstd
@@ -267,6 +268,12 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   for (int i = 0; i < 3; ++i) {
     w->wpart[i] = ar.take<float>(wp);
     w->bpart[i] = ar.take<float>(bp);
+  }
+  for (int l = 2; l <= 5; ++l) {
+    const int cin = H, cout = l == 5 ? D : H;
+    const long nch = wgrad_nchunk(l, M, cout, cin);
+    w->wpm[l - 2] = ar.take<float>(nch * cout * cin * layer_geom(l).ks);
+    w->bpm[l - 2] = ar.take<float>(nch * cout);
   }
   w->G = ar.take<float>((long)H * 4 * kMels);
   w->S = ar.take<float>(5L * H);  // the five layer-1 bias partial sums E[5][H]
@@ -779,7 +786,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   HPROF("capi:22");
 
   {  // fc weight gradient: dW[n][k] = sum_m df[m][n] bn5(y5)[m][k], db = sum_m df
-    TRY(wait_point(sw[0], ev_df));
+    TRY(wait_point(sw[1], ev_df));
     HPROF("capi:23");
     TGemmArgs g = {};
     g.M = D; g.N = c.FI; g.K = M;
@@ -788,17 +795,46 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     g.rowsum = c.Gd(SEG_FC_B);
     if (c.res) {  // dW[n][k] = sum_m df[m][n] xfc[m][k] over the concatenated fc input
       g.B = w.xfc; g.sbk = c.FI; g.sbn = 1;
-      TRY(launch_tgemm(0, 0, g, sw[0]));
+      TRY(launch_tgemm(0, 0, g, sw[1]));
     } else {
       g.B = w.y[5]; g.sbk = D; g.sbn = 1;
       g.bmean = w.mean[5]; g.ba = w.a[5]; g.bbeta = c.beta(w, 5);
-      TRY(launch_tgemm(0, 2, g, sw[0]));
+      TRY(launch_tgemm(0, 2, g, sw[1]));
     }
     HPROF("capi:24");
   }
-  // layers 5..2: alternating between the two wgrad streams (each with its own partial set)
-  hipEvent_t scratch_ev = nullptr;
-  for (int l = 5; l >= 2; --l) TRY(issue_wgrad(l, sw[l & 1], l & 1, l <= 3 ? &tail[2 + (l & 1 ? 1 : 0)] : &scratch_ev));
+  // (wgrad of layer l reads g_l, which dgrad l+1 produced: ev_layer[l]) layers 5..3 in one launch
+  // on wgrad stream 0 once dgrad 4 is done (beside dgrad 3-2); layer 2 on wgrad stream 1 (behind
+  // xhat0 and the fc weight gradient) once dgrad 3 is (beside dgrad 2 and the conv-1 tail); each
+  // + one reduce launch.
+  auto issue_multi = [&](int lo, int hi, hipStream_t so, hipEvent_t after, hipEvent_t* tl) -> int {
+    TRY(wait_point(so, after));
+    WgradMulti mw = {};
+    for (int l = hi; l >= lo; --l) {
+      const LayerGeom gm = layer_geom(l);
+      const int j = mw.n++;
+      mw.layer[j] = l;
+      WgradArgs& wa = mw.a[j];
+      wa.xsrc = w.y[l - 1];
+      wa.item_track = b->item_track;
+      wa.x_mean = w.mean[l - 1]; wa.x_a = w.a[l - 1]; wa.x_beta = c.beta(w, l - 1);
+      wa.g_l = w.g[l]; wa.y_l = w.y[l]; wa.idx_l = w.idx[l];
+      wa.mean_l = w.mean[l]; wa.invstd_l = w.invstd[l]; wa.a_l = w.a[l];
+      wa.dz_acc = bn_acc(w.bnbacc, w.cmax, l); wa.dgamma = c.dgamma(w, l); wa.dbeta = c.dbeta(w, l);
+      wa.invN = c.bn ? (float)(1.0 / (copies * gm.lp)) : 0.f;
+      wa.counts = w.counts;
+      wa.M = M; wa.cout = l == 5 ? D : H; wa.cin = H;
+      wa.wpart = w.wpm[l - 2]; wa.bpart = w.bpm[l - 2];
+      mw.nchunk[j] = wgrad_nchunk(l, M, wa.cout, wa.cin);
+      mw.dW[j] = c.Gd(seg_conv_w(l));
+      mw.db[j] = c.Gd(seg_conv_b(l));
+    }
+    ForkAfter fk(sp, so, tl);
+    TRY(launch_conv_wgrad_multi(mw, so));
+    return fk.done();
+  };
+  TRY(issue_multi(3, 5, sw[0], ev_layer[3], &tail[2]));
+  TRY(issue_multi(2, 2, sw[1], ev_layer[2], &tail[3]));
   HPROF("capi:25");
   // user tower (userembedding.py:33-44 backward), the compact embedding rows, and -- when the step
   // carries it -- the user table's Adam step (it needs nothing from the item tower)

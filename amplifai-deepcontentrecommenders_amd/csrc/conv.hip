@@ -151,9 +151,16 @@ __device__ __forceinline__ float4 slab_finish(const RowsArgs& a, const ChanOps& 
 // issues MFMAs (with four waves of 32 columns the loads' latency was exposed: ~40% of wave cycles
 // parked on s_waitcnt).
 constexpr int kRowsWaves = 8, kRowsThreads = 64 * kRowsWaves, kRowsCT = 128 / (16 * kRowsWaves);
+// B k-steps (float4 per lane per 16-column tile) requested ahead of the MFMAs by one-tile workgroups
+// (the small layers at in-batch M): a layer's whole K at H = 128 (32 steps), so they wait on the
+// weights once, not once every two steps
+#ifndef DCUE_ROWS_PD
+#define DCUE_ROWS_PD 32
+#endif
+constexpr int kRowsPD = DCUE_ROWS_PD;
 
 template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,
-          int POOLL>
+          int POOLL, bool DEEP>
 __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
   critical_path_priority();
   constexpr int RX = R + KS - 1;
@@ -173,22 +180,39 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
   const int nslab = (int)(i1 * RX + (gr1 - 1 - i1 * R) + KS - elo);
   (void)MAXI;
 
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int nout = a.nout;
+  constexpr int CT = kRowsCT;  // 16-column MFMA tiles per wave
+  const int ocol0 = blockIdx.y * 128 + wave * 16 * CT;
+  const bool colok = ocol0 < nout;
+
+  // B operand (packed weights, L2-resident): the first PD k-steps are requested before anything
+  // else -- they land while the slab is filled -- and each consumed slot is refilled PD steps ahead
+  // (DEEP: launches of at most one workgroup per CU; the larger ones keep two steps ahead -- deep
+  // prefetch there costs occupancy, and their other workgroups cover the load latency)
+  constexpr int PDW = DEEP ? kRowsPD / CT : 2;
+  constexpr int PD = NSTEP < PDW ? NSTEP : PDW;
+  const float* wp = a.wpack + ((size_t)g * nout + (colok ? ocol0 : 0) + l16) * 4;
+  const size_t wstep = (size_t)16 * nout;
+  float4 bq[PD][CT];
+#pragma unroll
+  for (int st = 0; st < PD; ++st)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) bq[st][ct] = ld4(wp + st * wstep + 64 * ct);
+
   {
     static_assert(kRowsThreads % C4 == 0, "a thread's slab slots share one channel quad");
     constexpr int FB = SRC == SRC_DZ ? 4 : 8;  // slab slots (float4) in flight per thread
     const int nfill = nslab * C4;
     const int c = 4 * (threadIdx.x % C4);
     __shared__ ChanLds chl;
-    chan_stage<SRC>(a, KC, chl);
-    if constexpr (SRC != SRC_DZ)
-      if (blockIdx.x == 0 && blockIdx.y == 0) bn_publish(a.in_bn, threadIdx.x);
-    __syncthreads();
-    const ChanOps kop = chan_ops<SRC>(chl, c);
-    for (int base = threadIdx.x; base < nfill; base += kRowsThreads * FB) {
+    int pp[FB];
+    bool ok[FB];
+    Raw raw[FB];
+    // raw global reads of one batch of slab slots, branch-free (clamped addresses, masked later)
+    auto load_batch = [&](int base) {
       long ii[FB];
-      int pp[FB];
-      bool ok[FB];
-      Raw raw[FB];
 #pragma unroll
       for (int j = 0; j < FB; ++j) {
         const int e = base + kRowsThreads * j;
@@ -208,6 +232,8 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
       }
 #pragma unroll
       for (int j = 0; j < FB; ++j) raw[j] = slab_load<SRC, KC, LIN, LPL, POOLL>(a, ii[j], pp[j], c, trk[j]);
+    };
+    auto store_batch = [&](int base, const ChanOps& kop) {
 #pragma unroll
       for (int j = 0; j < FB; ++j) {
         const int e = base + kRowsThreads * j;
@@ -216,16 +242,22 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
           st4(&slab[(e / C4) * PITCH + c], ok[j] ? v : make_float4(0.f, 0.f, 0.f, 0.f));
         }
       }
+    };
+    // the first batch's reads are in flight while the per-channel constants are finalized
+    load_batch(threadIdx.x);
+    chan_stage<SRC>(a, KC, chl);
+    if constexpr (SRC != SRC_DZ)
+      if (blockIdx.x == 0 && blockIdx.y == 0) bn_publish(a.in_bn, threadIdx.x);
+    __syncthreads();
+    const ChanOps kop = chan_ops<SRC>(chl, c);
+    store_batch(threadIdx.x, kop);
+    for (int base = threadIdx.x + kRowsThreads * FB; base < nfill; base += kRowsThreads * FB) {
+      load_batch(base);
+      store_batch(base, kop);
     }
   }
   __syncthreads();
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, l16 = lane & 15;
-  const int nout = a.nout;
-  constexpr int CT = kRowsCT;  // 16-column MFMA tiles per wave
-  const int ocol0 = blockIdx.y * 128 + wave * 16 * CT;
-  if (ocol0 >= nout) return;  // no barrier follows
+  if (!colok) return;  // no barrier follows
 
   int sbase[TW];
 #pragma unroll
@@ -242,21 +274,15 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc[r][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // B operand (packed weights, L2-resident) streamed two k-steps ahead of the MFMAs
-  const float* wp = a.wpack + ((size_t)g * nout + ocol0 + l16) * 4;
-  const size_t wstep = (size_t)16 * nout;
-  float4 b[CT], n[CT];
-#pragma unroll
-  for (int ct = 0; ct < CT; ++ct) {
-    b[ct] = ld4(wp + 64 * ct);
-    n[ct] = NSTEP > 1 ? ld4(wp + wstep + 64 * ct) : b[ct];
-  }
   // fully unrolled: straight-line code lets the wait counters track the in-flight B loads exactly
 #pragma unroll
   for (int st = 0; st < NSTEP; ++st) {
-    float4 f[CT];
+    float4 b[CT];
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) f[ct] = st + 2 < NSTEP ? ld4(wp + (st + 2) * wstep + 64 * ct) : n[ct];
+    for (int ct = 0; ct < CT; ++ct) {
+      b[ct] = bq[st % PD][ct];
+      if (st + PD < NSTEP) bq[st % PD][ct] = ld4(wp + (st + PD) * wstep + 64 * ct);
+    }
     const int k = st / (KC / 16);
     const int c0 = (st - k * (KC / 16)) * 16;
     const int aoff = k * PITCH + c0;
@@ -279,11 +305,6 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
     for (int r = 0; r < TW; ++r)
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) acc[r][ct] = mfma4(av[r].w, b[ct].w, acc[r][ct]);
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      b[ct] = n[ct];
-      n[ct] = f[ct];
-    }
   }
 
   if constexpr (MODE == 1) {
@@ -377,6 +398,21 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
 }
 
 template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,
+          int POOLL, bool DEEP>
+static int run_rows_pd(const RowsArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+  auto kern = k_conv_rows<MODE, SRC, KC, KS, PADL, LIN, R, POOL, TW, LPL, POOLL, DEEP>;
+  static bool attr = false;
+  if (!attr) {
+    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds));
+    attr = true;
+  }
+  DCUE_LAUNCH(kern, grid, dim3(kRowsThreads), lds, s, a);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,
           int POOLL>
 static int run_rows(const RowsArgs& a, hipStream_t s) {
   constexpr int ROWS = TW * 16;
@@ -384,18 +420,11 @@ static int run_rows(const RowsArgs& a, hipStream_t s) {
   constexpr int SLAB = ROWS + MAXI * (KS - 1);
   constexpr size_t LDS = (size_t)SLAB * (KC + 8) * sizeof(float);
   static_assert(LDS + sizeof(ChanLds) <= 160 * 1024, "slab exceeds LDS");
-  auto kern = k_conv_rows<MODE, SRC, KC, KS, PADL, LIN, R, POOL, TW, LPL, POOLL>;
-  static bool attr = false;
-  if (!attr) {
-    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)LDS));
-    attr = true;
-  }
   const long total = (long)a.M * R;
   dim3 grid((unsigned)((total + ROWS - 1) / ROWS), (unsigned)((a.nout + 127) / 128));
-  DCUE_LAUNCH(kern, grid, dim3(kRowsThreads), LDS, s, a);
-  DCUE_LAUNCH_CHECK();
-  return DCUE_OK;
+  if (TW == 1 && (long)grid.x * grid.y <= 256)  // one-tile workgroups, one per CU: weights run ahead
+    return run_rows_pd<MODE, SRC, KC, KS, PADL, LIN, R, POOL, TW, LPL, POOLL, true>(a, grid, LDS, s);
+  return run_rows_pd<MODE, SRC, KC, KS, PADL, LIN, R, POOL, TW, LPL, POOLL, false>(a, grid, LDS, s);
 }
 
 // Row tiles per workgroup. Each wave runs TW 16-row tiles of its 32 columns back to back, and a
@@ -532,26 +561,27 @@ static constexpr int kWgradRch = 72;  // rows per chunk step (9 per thread)
 // sums of dz at the first/last two positions: with them the reduce recovers, per tap, the sum of dz
 // over positions whose input is not zero padding -- what bn0's beta gradient and the bn0 affine
 // split of dW1 need ("bn0 without conv1 dgrad").
+// The body takes its block coordinates (kc tile bx, o tile by, chunk bz) as arguments: k_conv_wgrad
+// runs one layer per launch, k_conv_wgrad_multi the weight gradients of layers 2-5 in one launch.
 template <int SRCX, int KS, int PAD, int LIN, int R, int POOL, int LP, int RCH, bool EDGES>
-__global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
+__device__ __forceinline__ void wgrad_body(const WgradArgs& a, int bx, int by, int bz, float* lds) {
   constexpr int PW = 128 + 16;  // == 16 (mod 32): ds_read_b32 rows r and r+1 on disjoint banks
   constexpr int NB = EDGES ? 5 : 1;
   constexpr int FR = RCH / 8;   // rows per thread per chunk step (8 row slots x 32 channel quads)
   constexpr bool TRACK = SRCX == SRC_TRACK_F16 || SRCX == SRC_TRACK_F32;
-  extern __shared__ __attribute__((aligned(16))) float lds[];
   float* dzs = lds;
   float* xs = lds + RCH * PW;
-  __shared__ float bsum[8][NB][128];
+  float (*bsum)[NB][128] = reinterpret_cast<float (*)[NB][128]>(lds + 2 * RCH * PW);  // [8][NB][128]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, l16 = lane & 15;
   const int wo = wave >> 1, wk = wave & 1;
   const int cout = a.cout, cin = a.cin, kcn = KS * cin;
-  const int obase = blockIdx.y * 128, kcbase = blockIdx.x * 128;
+  const int obase = by * 128, kcbase = bx * 128;
   const long total = (long)a.M * R;
-  const long r_begin = (long)blockIdx.z * a.rows_per_chunk;
+  const long r_begin = (long)bz * a.rows_per_chunk;
   const long r_end = min(r_begin + a.rows_per_chunk, total);
-  const bool do_bias = blockIdx.x == 0;
+  const bool do_bias = bx == 0;
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -581,7 +611,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
     sD4 = make_float4(sd[0], sd[1], sd[2], sd[3]);
     sDx4 = make_float4(sdx[0], sdx[1], sdx[2], sdx[3]);
   }
-  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && tid < cout) {
+  if (bx == 0 && by == 0 && bz == 0 && tid < cout) {
     // BN_l = gamma * xhat + beta: dbeta = sum g, dgamma = sum g * xhat
     a.dbeta[tid] = (float)acc_sum(a.dz_acc, cout, 0, tid);
     a.dgamma[tid] = (float)acc_sum(a.dz_acc, cout, 1, tid);
@@ -703,7 +733,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
   }
 
   // partial block -> wpart[z][o][kc]; D lane map: o = 4g + reg, kc = l16
-  float* wp = a.wpart + (size_t)blockIdx.z * cout * kcn;
+  float* wp = a.wpart + (size_t)bz * cout * kcn;
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -725,9 +755,42 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
         float v = 0.f;
 #pragma unroll
         for (int sl = 0; sl < 8; ++sl) v += bsum[sl][e][tid];
-        a.bpart[((size_t)blockIdx.z * NB + e) * cout + obase + tid] = v;
+        a.bpart[((size_t)bz * NB + e) * cout + obase + tid] = v;
       }
     }
+  }
+}
+
+// LDS floats of the weight-gradient body: the dz and x tiles, then the bias partial sums
+constexpr size_t wgrad_lds_floats(int nb) { return (size_t)2 * kWgradRch * (128 + 16) + 8 * nb * 128; }
+
+template <int SRCX, int KS, int PAD, int LIN, int R, int POOL, int LP, int RCH, bool EDGES>
+__global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  wgrad_body<SRCX, KS, PAD, LIN, R, POOL, LP, RCH, EDGES>(a, blockIdx.x, blockIdx.y, blockIdx.z, lds);
+}
+
+// Weight gradients of several conv layers (of 2..5) in one launch: a 1-D grid of the layers'
+// (kc tile, o tile, chunk) blocks in slot order; each layer keeps its own partial buffers, summed by
+// k_wgrad_reduce_multi.
+template <int L>
+__device__ __forceinline__ void wgrad_multi_layer(const WgradMulti& w, int j, int b, float* lds) {
+  constexpr LayerGeom gm = layer_geom(L);
+  const int kt = w.kt[j], ot = w.ot[j];
+  wgrad_body<SRC_ACT, gm.ks, gm.pad, gm.lin, gm.lp * gm.pool, gm.pool, gm.lp, kWgradRch, false>(
+      w.a[j], b % kt, (b / kt) % ot, b / (kt * ot), lds);
+}
+
+__global__ __launch_bounds__(256) void k_conv_wgrad_multi(WgradMulti w) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int b = blockIdx.x;
+  int j = 0;
+  while (j + 1 < w.n && b >= w.start[j + 1]) ++j;
+  switch (w.layer[j]) {
+    case 2: wgrad_multi_layer<2>(w, j, b - w.start[j], lds); break;
+    case 3: wgrad_multi_layer<3>(w, j, b - w.start[j], lds); break;
+    case 4: wgrad_multi_layer<4>(w, j, b - w.start[j], lds); break;
+    default: wgrad_multi_layer<5>(w, j, b - w.start[j], lds); break;
   }
 }
 
@@ -1100,7 +1163,7 @@ static int wgrad_layer(const WgradArgs& a0, int nchunk, hipStream_t s) {
   constexpr LayerGeom gm = layer_geom(L);
   constexpr int R = gm.lp * gm.pool;
   constexpr bool EDGES = L == 1;
-  constexpr size_t LDS = (size_t)2 * kWgradRch * (128 + 16) * sizeof(float);
+  constexpr size_t LDS = wgrad_lds_floats(EDGES ? 5 : 1) * sizeof(float);
   auto kern = k_conv_wgrad<SRCX, gm.ks, gm.pad, gm.lin, R, gm.pool, gm.lp, kWgradRch, EDGES>;
   static bool attr = false;
   if (!attr) {
@@ -1165,18 +1228,16 @@ __device__ __forceinline__ float4 combine_groups(float4 (*red)[32], int col) {
   return r;
 }
 
-__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ wpart,
-                                                      const float* __restrict__ bpart, int nchunk,
-                                                      int cout, int cin, int ks, int nb, float* dW,
-                                                      float* db, float* G, float* S) {
-  critical_path_priority();
+__device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ wpart, const float* __restrict__ bpart,
+                                                  int nchunk, int cout, int cin, int ks, int nb, float* dW,
+                                                  float* db, float* G, float* S, long blk) {
   __shared__ float4 red[kRedGroups][32];
   const int col = threadIdx.x & 31, grp = threadIdx.x >> 5;
   const long kcn = (long)ks * cin;
   const long nw = (long)cout * kcn;  // multiple of 4 (cin % 32 == 0)
   const long nwblk = (nw + 127) / 128;
-  if ((long)blockIdx.x < nwblk) {
-    const long e4 = (long)blockIdx.x * 128 + 4 * col;
+  if (blk < nwblk) {
+    const long e4 = blk * 128 + 4 * col;
     red[grp][col] = e4 < nw ? sum_chunks(wpart + e4, (size_t)nw, nchunk, grp) : make_float4(0.f, 0.f, 0.f, 0.f);
     __syncthreads();
     if (grp == 0 && e4 < nw) {
@@ -1195,10 +1256,58 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
   }
   // bias (+ layer-1 edge) sums: bpart[z][j][o]; a workgroup owns 128 consecutive (j, o) entries
   const long nbo = (long)nb * cout;  // multiple of 4
-  const long e4 = ((long)blockIdx.x - nwblk) * 128 + 4 * col;
+  const long e4 = (blk - nwblk) * 128 + 4 * col;
   red[grp][col] = e4 < nbo ? sum_chunks(bpart + e4, (size_t)nbo, nchunk, grp) : make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
   if (grp == 0 && e4 < nbo) st4(G ? S + e4 : db + e4, combine_groups(red, col));
+}
+
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ wpart,
+                                                      const float* __restrict__ bpart, int nchunk,
+                                                      int cout, int cin, int ks, int nb, float* dW,
+                                                      float* db, float* G, float* S) {
+  critical_path_priority();
+  wgrad_reduce_body(wpart, bpart, nchunk, cout, cin, ks, nb, dW, db, G, S, blockIdx.x);
+}
+
+// the partial sums of k_conv_wgrad_multi, layers 2..5 in one launch (block ranges rstart[])
+__global__ __launch_bounds__(256) void k_wgrad_reduce_multi(WgradMulti w) {
+  const int b = blockIdx.x;
+  int j = 0;
+  while (j + 1 < w.n && b >= w.rstart[j + 1]) ++j;
+  const WgradArgs& a = w.a[j];
+  wgrad_reduce_body(a.wpart, a.bpart, w.nchunk[j], a.cout, a.cin, layer_geom(w.layer[j]).ks, 1, w.dW[j],
+                    w.db[j], nullptr, nullptr, b - w.rstart[j]);
+}
+
+int launch_conv_wgrad_multi(WgradMulti w, hipStream_t s) {
+  constexpr size_t LDS = wgrad_lds_floats(1) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_conv_wgrad_multi, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)LDS));
+    attr = true;
+  }
+  w.start[0] = 0;
+  w.rstart[0] = 0;
+  if (w.n < 1 || w.n > 4) return DCUE_ERR_INVALID;
+  for (int j = 0; j < w.n; ++j) {
+    if (w.layer[j] < 2 || w.layer[j] > 5) return DCUE_ERR_INVALID;
+    WgradArgs& a = w.a[j];
+    const LayerGeom gm = layer_geom(w.layer[j]);
+    if (a.cin % 32 || a.cout % 4) return DCUE_ERR_UNSUPPORTED;
+    const long rows = (long)a.M * gm.lp * gm.pool;
+    a.rows_per_chunk = (int)((rows + w.nchunk[j] - 1) / w.nchunk[j]);
+    w.kt[j] = (gm.ks * a.cin + 127) / 128;
+    w.ot[j] = (a.cout + 127) / 128;
+    w.start[j + 1] = w.start[j] + w.kt[j] * w.ot[j] * w.nchunk[j];
+    w.rstart[j + 1] = w.rstart[j] + (int)(((long)a.cout * gm.ks * a.cin + 127) / 128 + (a.cout + 127) / 128);
+  }
+  DCUE_LAUNCH(k_conv_wgrad_multi, dim3((unsigned)w.start[w.n]), dim3(256), LDS, s, w);
+  DCUE_LAUNCH_CHECK();
+  DCUE_LAUNCH(k_wgrad_reduce_multi, dim3((unsigned)w.rstart[w.n]), dim3(256), 0, s, w);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
 }
 
 int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int nchunk, int cout,

@@ -91,6 +91,20 @@ struct WgradArgs {
   float* bpart;               // [nchunk][NB][cout]
 };
 
+// weight gradients of n conv layers (of 2..5) in one launch, then their chunk sums in a second one
+// (the host fills n, layer[], a[], nchunk[], dW[], db[]; the launcher derives the block ranges)
+struct WgradMulti {
+  int n;
+  int layer[4];
+  WgradArgs a[4];  // one per slot, each with its own wpart / bpart
+  int nchunk[4];
+  float *dW[4], *db[4];
+  int kt[4], ot[4];  // kc / o tiles per layer
+  int start[5];      // wgrad block ranges
+  int rstart[5];     // reduce block ranges
+};
+int launch_conv_wgrad_multi(WgradMulti w, hipStream_t s);
+
 int launch_conv_fwd(int layer, int kc, int src, const RowsArgs& a, hipStream_t s);
 int launch_conv_dgrad(int layer, int kc, const RowsArgs& a, hipStream_t s);
 int launch_conv_wgrad(int layer, int src, const WgradArgs& a, int nchunk, hipStream_t s);
