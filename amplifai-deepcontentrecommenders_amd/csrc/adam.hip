@@ -4,65 +4,23 @@
 
 namespace dcue {
 
-// torch.optim.Adam, foreach=False/fused=False, per element, as torch 2.10's CPU kernels round it
-// (torch/optim/adam.py _single_tensor_adam; each form below was matched bit for bit against those
-// kernels on random inputs, tests/test_adam_cpu.py):
-//   g = fma(p, wd, g)                      grad.add(param, alpha=wd)
-//   m = fma(c, g - m, base)                exp_avg.lerp_(grad, 1-b1): c = w, base = m (w < 0.5),
-//                                          else c = w - 1, base = g (the vectorised lerp)
-//   v = fma((1-b2)*g, g, v*b2)             exp_avg_sq.mul_(b2).addcmul_(grad, grad, value=1-b2)
-//   d = sqrt(v) / bc2_sqrt + eps           (exp_avg_sq.sqrt() / bias_correction2_sqrt).add_(eps)
-//   p = p + (step * m) / d                 param.addcdiv_(exp_avg, denom, value=-step_size)
-// The one place this cannot be bit-identical is sqrt: the CPU kernel's vectorised sqrt is not
-// correctly rounded (1 ulp off on ~0.6% of inputs, tests/test_adam_cpu.py); here it is. (It must be
-// __builtin_sqrtf: hipcc lowers it to v_sqrt_f32 plus the two-fma correction, while __fsqrt_rn
-// compiles to the bare 1-ulp v_sqrt_f32.)
-struct AdamScalars {
-  float neg_step, lerp_c, b2, one_m_b2, bc2_sqrt, eps, wd;  // neg_step = -(lr / bc1)
-  float inv_bc2_sqrt;  // RN(1 / bc2_sqrt): Markstein division by the per-step constant
-};
-static_assert(sizeof(AdamScalars) == 32, "history entry is [8] floats");
-
 // Every operation rounded on its own unless written as an fma (fp contraction off for this file)
 // so that the dense sweep, the deferred replay and the touched-row step produce identical bits.
-// lerp_c < 0: the lerp weight is >= 0.5 (beta1 <= 0.5), so the blend base is g.
-__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamScalars& s) {
-#pragma clang fp contract(off)
-  if (s.wd != 0.f) g = __fmaf_rn(p, s.wd, g);
-  m = __fmaf_rn(s.lerp_c, __fsub_rn(g, m), s.lerp_c < 0.f ? g : m);
-  v = __fmaf_rn(__fmul_rn(s.one_m_b2, g), g, __fmul_rn(v, s.b2));
-  const float denom = __fadd_rn(__fdiv_rn(__builtin_sqrtf(v), s.bc2_sqrt), s.eps);
-  p = __fadd_rn(p, __fdiv_rn(__fmul_rn(s.neg_step, m), denom));
-}
+// sqrt must be __builtin_sqrtf: hipcc lowers it to v_sqrt_f32 plus the two-fma correction, while
+// __fsqrt_rn compiles to the bare 1-ulp v_sqrt_f32.
+#define DCUE_RHD __device__ __forceinline__
+DCUE_RHD float rn_fma(float a, float b, float c) { return __fmaf_rn(a, b, c); }
+DCUE_RHD float rn_mul(float a, float b) { return __fmul_rn(a, b); }
+DCUE_RHD float rn_add(float a, float b) { return __fadd_rn(a, b); }
+DCUE_RHD float rn_sub(float a, float b) { return __fsub_rn(a, b); }
+DCUE_RHD float rn_div(float a, float b) { return __fdiv_rn(a, b); }
+DCUE_RHD float rn_sqrt(float a) { return __builtin_sqrtf(a); }
 
-// The zero-gradient step (a row outside the batch, wd == 0, lerp weight < 0.5), bit-identical to
-// adam_elem(p, +0, m, v, s): fma((1-b2)*0, 0, v*b2) == v*b2 (v >= 0), and sqrt(v)/bc2_sqrt by
-// Markstein's correction with r = RN(1/bc2_sqrt): q = RN(a r), q' = RN(q + RN?(a - q bc2)*r) is the
-// correctly rounded quotient for a >= 2^-100 (below it the plain division runs). This is the
-// deferred replay's inner loop (VALU-bound).
-__device__ __forceinline__ void adam_zero_elem(float& p, float& m, float& v, const AdamScalars& s) {
-  m = __fmaf_rn(s.lerp_c, __fsub_rn(0.f, m), m);
-  v = __fmul_rn(v, s.b2);
-  const float sq = __builtin_sqrtf(v);
-  float t;
-  if (sq >= 0x1p-100f) {
-    const float q = __fmul_rn(sq, s.inv_bc2_sqrt);
-    const float r = __fmaf_rn(-q, s.bc2_sqrt, sq);
-    t = __fmaf_rn(r, s.inv_bc2_sqrt, q);
-  } else {
-    t = __fdiv_rn(sq, s.bc2_sqrt);
-  }
-  const float denom = __fadd_rn(t, s.eps);
-  p = __fadd_rn(p, __fdiv_rn(__fmul_rn(s.neg_step, m), denom));
-}
+}  // namespace dcue
 
-// replay of a zero-gradient step: the fast form when no weight decay touches g
-__device__ __forceinline__ void adam_replay(float& p, float& m, float& v, const AdamScalars& s, float gz) {
-  if (s.wd == 0.f && s.lerp_c < 0.5f)
-    adam_zero_elem(p, m, v, s);
-  else
-    adam_elem(p, gz, m, v, s);
-}
+#include "adam_replay.h"
+
+namespace dcue {
 
 // (m, v) = (+0, +0) is a fixed point of the zero-gradient step without weight decay (adam_zero_elem:
 // m - w*0 = +0, v*b2 = +0, sqrt(0)/bc2 = 0, denom = eps, p + (-lr_bc1)*(0/eps) = p + (-0) = p,
@@ -75,12 +33,37 @@ __device__ __forceinline__ bool idle_moments4(const float4& m, const float4& v) 
   return (__float_as_uint(m.x) | __float_as_uint(m.y) | __float_as_uint(m.z) | __float_as_uint(m.w) |
           __float_as_uint(v.x) | __float_as_uint(v.y) | __float_as_uint(v.z) | __float_as_uint(v.w)) == 0u;
 }
-// whether every replayed step of [j0, j1] (history slots j % cap) is free of weight decay
-__device__ __forceinline__ bool no_decay(const AdamScalars* hs, int j0, int j1, int cap, float gz) {
-  if (gz != 0.f) return false;
-  for (int j = j0; j <= j1; ++j)
-    if (hs[j % cap].wd != 0.f) return false;
-  return true;
+// The replay bound (adam_replay.h) of the staged window [j0, j1] (history slots j % cap in LDS),
+// folded by wave 0 and published to *out; the caller syncs the block before reading it.
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+  return x;
+}
+__device__ __forceinline__ float wave_min(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fminf(x, __shfl_xor(x, o));
+  return x;
+}
+__device__ __forceinline__ int wave_and(int x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x &= __shfl_xor(x, o);
+  return x;
+}
+__device__ __forceinline__ void window_bound(const AdamScalars* hs, int j0, int j1, int cap, float gz,
+                                             ReplayBound* out) {
+  if (threadIdx.x >= 64) return;
+  ReplayBound b = bound_init(gz);
+  for (int j = j0 + (int)threadIdx.x; j <= j1; j += 64) bound_fold(b, hs[j % cap]);
+  b.S = wave_max(b.S);
+  b.b2min = wave_min(b.b2min);
+  b.eps = wave_min(b.eps);
+  b.ok = wave_and(b.ok);
+  b.nd = wave_and(b.nd);
+  if (threadIdx.x == 0) {
+    bound_finalize(b, j1 - j0 + 1);
+    *out = b;
+  }
 }
 
 struct PackSeg {
@@ -196,6 +179,7 @@ __global__ __launch_bounds__(1024) void k_emb_sync(float* __restrict__ p, float*
                                                   int32_t* emb_step, const int64_t* users, int E,
                                                   float gz) {
   __shared__ AdamScalars hs[DCUE_MAX_LOG_CAP];
+  __shared__ ReplayBound sb;
   __shared__ int s_from;
   const int T = hdr->step_done, F = hdr->flush_step, cap = hdr->cap;
   const int64_t u = users[blockIdx.x];
@@ -211,18 +195,20 @@ __global__ __launch_bounds__(1024) void k_emb_sync(float* __restrict__ p, float*
   const AdamScalars* hist = log_hist(hdr);
   for (int j = from + 1 + (int)threadIdx.x; j <= T; j += blockDim.x) hs[j % cap] = hist[j % cap];
   __syncthreads();
-  const bool nd = no_decay(hs, from + 1, T, cap, gz);
+  window_bound(hs, from + 1, T, cap, gz, &sb);
+  __syncthreads();
+  const ReplayBound b = sb;
   float* pr = p + u * E;
   float* mr = m + u * E;
   float* vr = v + u * E;
   // one element per thread: each element's replay is a dependent chain of VALU-bound steps, so the
   // row is spread over as many lanes as it has elements (launch: blockDim >= E)
   for (int k = threadIdx.x; k < E; k += blockDim.x) {
-    float mm = mr[k], vv = vr[k];
-    if (nd && idle_moments(mm, vv)) continue;  // fixed point (idle_moments)
-    float pp = pr[k];
-    for (int j = from + 1; j <= T; ++j) adam_replay(pp, mm, vv, hs[j % cap], gz);
-    pr[k] = pp; mr[k] = mm; vr[k] = vv;
+    float mm[1] = {mr[k]}, vv[1] = {vr[k]};
+    if (b.nd && idle_moments(mm[0], vv[0])) continue;  // fixed point (idle_moments)
+    float pp[1] = {pr[k]};
+    replay_run<1>(pp, mm, vv, hs, from + 1, T, cap, b, gz);
+    pr[k] = pp[0]; mr[k] = mm[0]; vr[k] = vv[0];
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -238,6 +224,7 @@ __global__ __launch_bounds__(256) void k_emb_flush(float* __restrict__ p, float*
                                                    const int32_t* __restrict__ emb_step, long n_rows,
                                                    int E, float gz) {
   __shared__ AdamScalars hs[DCUE_MAX_LOG_CAP];
+  __shared__ ReplayBound sb;
   const int T = hdr->step_done, F = hdr->flush_step, cap = hdr->cap;
   if (T <= F) return;
   const AdamScalars* hist = log_hist(const_cast<dcue_emb_log*>(hdr));
@@ -247,34 +234,33 @@ __global__ __launch_bounds__(256) void k_emb_flush(float* __restrict__ p, float*
   const int lo = max(F + 1, T - cap + 1);
   for (int j = lo + (int)threadIdx.x; j <= T; j += blockDim.x) hs[j % cap] = hist[j % cap];
   __syncthreads();
-  const bool nd = no_decay(hs, lo, T, cap, gz);
+  window_bound(hs, lo, T, cap, gz, &sb);
+  __syncthreads();
+  const ReplayBound b = sb;
   const long stride = (long)gridDim.x * blockDim.x;
   if ((E & 3) == 0) {
     const int E4 = E >> 2;
     const long n4 = n_rows * E4;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
       const int from = max(emb_step[i / E4], F);
-      float4 mm = ld4(m + 4 * i), vv = ld4(v + 4 * i);
-      if (nd && idle_moments4(mm, vv)) continue;  // fixed point (idle_moments)
-      float4 pp = ld4(p + 4 * i);
-      for (int j = max(from + 1, lo); j <= T; ++j) {
-        const AdamScalars s = hs[j % cap];
-        adam_replay(pp.x, mm.x, vv.x, s, gz);
-        adam_replay(pp.y, mm.y, vv.y, s, gz);
-        adam_replay(pp.z, mm.z, vv.z, s, gz);
-        adam_replay(pp.w, mm.w, vv.w, s, gz);
-      }
-      st4(p + 4 * i, pp); st4(m + 4 * i, mm); st4(v + 4 * i, vv);
+      const float4 m4 = ld4(m + 4 * i), v4 = ld4(v + 4 * i);
+      if (b.nd && idle_moments4(m4, v4)) continue;  // fixed point (idle_moments)
+      const float4 p4 = ld4(p + 4 * i);
+      float pp[4] = {p4.x, p4.y, p4.z, p4.w}, mm[4] = {m4.x, m4.y, m4.z, m4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
+      replay_run<4>(pp, mm, vv, hs, max(from + 1, lo), T, cap, b, gz);
+      st4(p + 4 * i, make_float4(pp[0], pp[1], pp[2], pp[3]));
+      st4(m + 4 * i, make_float4(mm[0], mm[1], mm[2], mm[3]));
+      st4(v + 4 * i, make_float4(vv[0], vv[1], vv[2], vv[3]));
     }
   } else {
     const long n = n_rows * E;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
       const int from = max(emb_step[i / E], F);
-      float mm = m[i], vv = v[i];
-      if (nd && idle_moments(mm, vv)) continue;
-      float pp = p[i];
-      for (int j = max(from + 1, lo); j <= T; ++j) adam_replay(pp, mm, vv, hs[j % cap], gz);
-      p[i] = pp; m[i] = mm; v[i] = vv;
+      float mm[1] = {m[i]}, vv[1] = {v[i]};
+      if (b.nd && idle_moments(mm[0], vv[0])) continue;
+      float pp[1] = {p[i]};
+      replay_run<1>(pp, mm, vv, hs, max(from + 1, lo), T, cap, b, gz);
+      p[i] = pp[0]; m[i] = mm[0]; v[i] = vv[0];
     }
   }
 }
@@ -290,6 +276,7 @@ __global__ __launch_bounds__(256) void k_emb_flush_rows(float* __restrict__ p, f
                                                         int32_t* emb_step, long r0, long r1, int E,
                                                         int rows_per_block, float gz) {
   __shared__ AdamScalars hs[DCUE_MAX_LOG_CAP];
+  __shared__ ReplayBound sb;
   __shared__ int from_s[256];
   const int T = hdr->step_done, F = hdr->flush_step, cap = hdr->cap;
   const long rb = r0 + (long)blockIdx.x * rows_per_block;
@@ -300,33 +287,32 @@ __global__ __launch_bounds__(256) void k_emb_flush_rows(float* __restrict__ p, f
   for (int j = lo + (int)threadIdx.x; j <= T; j += blockDim.x) hs[j % cap] = hist[j % cap];
   for (int i = threadIdx.x; i < nr; i += blockDim.x) from_s[i] = max(emb_step[rb + i], F);
   __syncthreads();
-  const bool nd = no_decay(hs, lo, T, cap, gz);
+  window_bound(hs, lo, T, cap, gz, &sb);
+  __syncthreads();
+  const ReplayBound b = sb;
   if ((E & 3) == 0) {
     const int E4 = E >> 2;
     for (int e = threadIdx.x; e < nr * E4; e += blockDim.x) {
       const int i = e / E4;
       const long off = (rb + i) * E + 4 * (e - i * E4);
-      float4 mm = ld4(m + off), vv = ld4(v + off);
-      if (nd && idle_moments4(mm, vv)) continue;  // fixed point (idle_moments)
-      float4 pp = ld4(p + off);
-      for (int j = from_s[i] + 1; j <= T; ++j) {
-        const AdamScalars s = hs[j % cap];
-        adam_replay(pp.x, mm.x, vv.x, s, gz);
-        adam_replay(pp.y, mm.y, vv.y, s, gz);
-        adam_replay(pp.z, mm.z, vv.z, s, gz);
-        adam_replay(pp.w, mm.w, vv.w, s, gz);
-      }
-      st4(p + off, pp); st4(m + off, mm); st4(v + off, vv);
+      const float4 m4 = ld4(m + off), v4 = ld4(v + off);
+      if (b.nd && idle_moments4(m4, v4)) continue;  // fixed point (idle_moments)
+      const float4 p4 = ld4(p + off);
+      float pp[4] = {p4.x, p4.y, p4.z, p4.w}, mm[4] = {m4.x, m4.y, m4.z, m4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
+      replay_run<4>(pp, mm, vv, hs, from_s[i] + 1, T, cap, b, gz);
+      st4(p + off, make_float4(pp[0], pp[1], pp[2], pp[3]));
+      st4(m + off, make_float4(mm[0], mm[1], mm[2], mm[3]));
+      st4(v + off, make_float4(vv[0], vv[1], vv[2], vv[3]));
     }
   } else {
     for (int e = threadIdx.x; e < nr * E; e += blockDim.x) {
       const int i = e / E;
       const long off = (rb + i) * E + (e - i * E);
-      float mm = m[off], vv = v[off];
-      if (nd && idle_moments(mm, vv)) continue;
-      float pp = p[off];
-      for (int j = from_s[i] + 1; j <= T; ++j) adam_replay(pp, mm, vv, hs[j % cap], gz);
-      p[off] = pp; m[off] = mm; v[off] = vv;
+      float mm[1] = {m[off]}, vv[1] = {v[off]};
+      if (b.nd && idle_moments(mm[0], vv[0])) continue;
+      float pp[1] = {p[off]};
+      replay_run<1>(pp, mm, vv, hs, from_s[i] + 1, T, cap, b, gz);
+      p[off] = pp[0]; m[off] = mm[0]; v[off] = vv[0];
     }
   }
   __syncthreads();

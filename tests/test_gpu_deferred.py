@@ -37,15 +37,18 @@ def _assert_equal_state(a, b):
         assert torch.equal(a[k], b[k]), "%s differs: max |diff| %.3e" % (k, float((a[k].double() - b[k].double()).abs().max()))
 
 
-@pytest.mark.parametrize("E,wd,flush_every,steps", [(40, 0.0, 4, 13), (30, 1e-3, 5, 13), (300, 0.0, 64, 13),
-                                                    # > DCUE_MAX_LOG_CAP (256) steps between full
-                                                    # flushes: only the rolling slices keep rows current
-                                                    (40, 0.0, 8, 300), (30, 1e-3, 16, 270)])
-def test_deferred_matches_dense_bit_exact(E, wd, flush_every, steps):
+@pytest.mark.parametrize("E,wd,flush_every,steps,n_users,B", [
+    (40, 0.0, 4, 13, 40, 8), (30, 1e-3, 5, 13, 40, 8), (300, 0.0, 64, 13, 40, 8),
+    # > DCUE_MAX_LOG_CAP (256) steps between full flushes: only the rolling slices keep rows current
+    (40, 0.0, 8, 300, 40, 8), (30, 1e-3, 16, 270, 40, 8),
+    # users idle for hundreds of steps: the replay's long-idle shortcut (csrc/adam_replay.h) runs in
+    # the rolling slices and in the forward's sync of returning users
+    (300, 0.0, 64, 420, 600, 4), (64, 0.0, 16, 420, 600, 4)])
+def test_deferred_matches_dense_bit_exact(E, wd, flush_every, steps, n_users, B):
     from dcrecommend import _native as nat
     from dcrecommend.optim import NativeAdam
     from dcrecommend.optim.cyclic_scheduler import CyclicLRWithRestarts
-    n_users, B, N, n_tracks = 40, 8, 3, 48
+    N, n_tracks = 3, 48
     dense, lazy = _pair(E, n_users)
     gen = torch.Generator(device=DEV).manual_seed(7)
     tracks = torch.randn((n_tracks, 131, 128), generator=gen, device=DEV).half()
