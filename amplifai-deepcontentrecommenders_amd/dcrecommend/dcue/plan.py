@@ -38,6 +38,9 @@ class TrainPlan:
         self.neg_item = torch.zeros((B, N), dtype=torch.int32, device=dev) if self.inbatch else None
         self.mt_state = mt_state
         self.ws = net._workspace(B, N, M)
+        off = nat.workspace_outputs(fl["dims"], B, N, M)
+        # the last launched step's mean hinge loss (nn/dcue.py:167-170), a device view into the workspace
+        self.loss = self.ws[off[3]:off[3] + 4].view(torch.float32)[0]
         self.optimizer = optimizer
         # with an optimizer the plan also owns the Adam step (step()); the struct then carries its state
         self._fused_adam = optimizer is not None and hasattr(optimizer, "_adam_state")

@@ -230,10 +230,6 @@ class DCUE(Trainer):
             self._plan = TrainPlan(self.model, self._tracks, self.batch_size, N,
                                    margin=self.margin, optimizer=self.optimizer)
             self._plan_n = N
-            fl = self.model._flat
-            M = self.batch_size * (1 + N)
-            off = nat.workspace_outputs(fl["dims"], self.batch_size, N, M)
-            self._plan_loss = self._plan.ws[off[3]:off[3] + 4].view(torch.float32)
         return self._plan
 
     # ------------------------------------------------------------------ epochs
@@ -261,7 +257,7 @@ class DCUE(Trainer):
                       "dcue_build_catalogue_batch")
             plan.step()
             self.scheduler.batch_step()
-            loss_sum += self._plan_loss[0].double() * B
+            loss_sum += plan.loss.double() * B
             samples += B
         _mt_to_numpy(mt)
         return samples, float(loss_sum) / max(samples, 1)
