@@ -211,6 +211,22 @@ def test_train_dcue_driver_synthetic(tmp_path):
     assert os.listdir(tmp_path)
 
 
+def test_train_dcue_driver_config1(tmp_path):
+    """BASELINE.json configs[0]'s shape -- d=64, H=128, 1k users x 5k tracks of 131-frame
+    spectrograms -- through the reference trainer API end to end (train_dcue.py: datasets from
+    triplets/metadata frames, spectrogram files loaded once into the HBM table, DCUE.fit's sub-epoch
+    loop with validation AUC, checkpoints)."""
+    import train_dcue
+    dcue = train_dcue.main(["--synthetic", "--synthetic-users", "1000", "--synthetic-tracks", "5000",
+                            "--synthetic-pairs", "20000", "--feature-dim", "64", "--conv-hidden", "128",
+                            "--batch-size", "64", "--neg-batch-size", "20", "--num-epochs", "1",
+                            "--lr", "1e-4", "--save-dir", str(tmp_path)])
+    assert dcue._plan_n == 20 and dcue.nn_epoch >= 9
+    assert dcue.feature_dim == 64 and dcue.conv_hidden == 128
+    assert 0.0 <= dcue.best_val_auc <= 1.0
+    assert os.listdir(tmp_path)
+
+
 def test_saturated_user_raises_like_numpy(tmp_path):
     """40 tracks: the val split holds 3 songs and one user has all of them, so the reference's
     np.random.choice over that user's (empty) non-items raises ValueError

@@ -127,7 +127,7 @@ def test_module_forward_backward(golden, name):
     _check_params_after_adam(net, g, "step2.", 2 * lr, skip_rows=np.unique(g["u"]))
 
 
-@pytest.mark.parametrize("H,d", [(64, 64), (256, 128), (128, 256)])
+@pytest.mark.parametrize("H,d", [(64, 64), (128, 64), (256, 128), (128, 256)])  # (128, 64): config 1
 def test_widths_against_oracle(H, d):
     """conv_hidden / feature_dim the golden fixtures do not cover (they hold 32 and 128): one train
     step's scores, loss and every dense gradient against the CPU oracle (oracle/dcue_oracle.py, the
