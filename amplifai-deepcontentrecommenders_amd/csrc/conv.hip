@@ -433,6 +433,13 @@ static int run_rows(const RowsArgs& a, hipStream_t s) {
 // workgroups, eight CUs doubled up) but 3 at TW = 3 (176). Ties go to the larger TW (fewer
 // re-reads of the weights, which every workgroup streams whole).
 static int choose_tw(long rows, int twmax) {
+  // tuning diagnostic: DCUE_ROWS_TW=n forces n tiles per workgroup where the slab fits (A/B runs)
+  static const int forced = [] {
+    const char* e = getenv("DCUE_ROWS_TW");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 1 || forced == 2 || forced == 3 || forced == 4 || forced == 8)
+    if (forced <= twmax) return forced;
   constexpr long kCUs = 256;
   const long tiles = (rows + 15) / 16;
   int best = 1;
