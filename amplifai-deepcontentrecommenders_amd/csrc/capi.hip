@@ -349,7 +349,7 @@ int init_ctx(Ctx* c, const dcue_model* m) {
 // producing kernels) + running-stat update by each BN's first consumer; eval: running statistics.
 int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t* item_track, int M,
                  double copies, bool train, const float* counts, float* f_out, hipStream_t s,
-                 bool acc_cleared = false) {
+                 bool acc_cleared = false, bool stats_done = false, bool clear_bn0 = false) {
   const dcue_model* m = c.m;
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
   // one BN's finalize/publish record for its first consumer (train) -- bnacc.h
@@ -373,7 +373,10 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
   } else if (train) {
     if (!acc_cleared)
       DCUE_HIP_CHECK(hipMemsetAsync(w.bnacc, 0, sizeof(unsigned long long) * 6 * 2 * w.cmax * 2, s));
-    TRY(launch_input_stats(src, t->data, item_track, counts, M, bn_acc(w.bnacc, w.cmax, 0), s));
+    if (clear_bn0 && !stats_done)  // sums of a batch announced ahead but not the one launched
+      DCUE_HIP_CHECK(hipMemsetAsync(bn_acc(w.bnacc, w.cmax, 0), 0, sizeof(unsigned long long) * 2 * w.cmax * 2, s));
+    if (!stats_done)  // else computed one step ahead into this accumulator block (plans)
+      TRY(launch_input_stats(src, t->data, item_track, counts, M, bn_acc(w.bnacc, w.cmax, 0), s));
   } else {
     for (int l = 0; l < 6; ++l)
       TRY(launch_bn_eval(bn_channels(&m->dims, l), c.P(seg_bn_w(l)), c.rmean(l), c.rvar(l), w.mean[l],
@@ -577,7 +580,7 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   if (!o.prologue_done) TRY(launch_item_counts(b, w.counts, s));
   HPROF("capi:4");
   TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s,
-                   o.prologue_done));
+                   o.prologue_done, o.input_stats_done && o.prologue_done, o.clear_bn0));
   TRY(wait_point(su, ev_in));
   HPROF("capi:5");
   if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
@@ -605,6 +608,21 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   }
   return launch_score_fwd(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.hinge, w.loss,
                           w.dhinge, s);
+}
+
+int ahead_item_inputs(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, const int32_t* items,
+                      const float* counts, unsigned long long* acc, float* xhat0, hipStream_t s) {
+  Ctx c;
+  TRY(init_ctx(&c, m));
+  if (!c.bn) return DCUE_ERR_UNSUPPORTED;  // bn0-free towers have no input statistics to prepare
+  Ws w;
+  carve(&m->dims, b->n_rows, b->n_neg, b->n_items, nullptr, &w);
+  rebase_acc(&w, acc);
+  const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
+  const int M = b->n_items;
+  const double copies = (double)b->n_rows * (1 + b->n_neg);
+  TRY(launch_input_stats(src, t->data, items, counts, M, bn_acc(w.bnacc, w.cmax, 0), s));
+  return launch_xhat0(src, t->data, items, M, bn_acc(w.bnacc, w.cmax, 0), copies * kFrames, xhat0, s);
 }
 
 long step_acc_words(const dcue_dims* d, int B, int N, int M) {
@@ -673,7 +691,8 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   // the conv-1 weight gradient's X operand, bn0(x) without gamma/beta, materialised once beside the
   // backward chain (it needs only the forward's input statistics); waited for just before that kernel
   hipEvent_t ev_x0 = nullptr;
-  {
+  const float* xhat0 = o.xhat0 ? o.xhat0 : w.xhat0;  // prepared one step ahead (plans), or built here
+  if (!o.xhat0) {
     TRY(wait_point(sw[1], ev_score));
     ForkAfter fk(sp, sw[1], &ev_x0);
     TRY(launch_xhat0(src, t->data, b->item_track, M, c.bn ? bn_acc(w.bnacc, w.cmax, 0) : nullptr,
@@ -726,11 +745,16 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     ra.oy = w.y[l - 1]; ra.omean = w.mean[l - 1]; ra.oinvstd = w.invstd[l - 1];
     ra.M = M;
     ra.nout = H;
-    ForkAfter fk(sp, s, &ev_layer[l - 1]);
-    TRY(launch_conv_dgrad(l, l == 5 ? D : H, ra, s));
+    // a fork point only where a side stream waits (wgrads of layers 3-5 after g_3, of layer 2
+    // after g_2): every event bound to a launch costs the chain a gap before its next kernel
+    if (l - 1 == 3 || l - 1 == 2) {
+      ForkAfter fk(sp, s, &ev_layer[l - 1]);
+      TRY(launch_conv_dgrad(l, l == 5 ? D : H, ra, s));
+      TRY(fk.done());
+    } else {
+      TRY(launch_conv_dgrad(l, l == 5 ? D : H, ra, s));
+    }
     HPROF("capi:16");
-    TRY(fk.done());
-    HPROF("capi:17");
   }
   // conv weight gradient of layer l on stream `so` (its own split-K partial set `ps`); `tail`:
   // a fork point after its last kernel
@@ -741,7 +765,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     if (so != s) TRY(wait_point(so, ev_layer[l]));
     HPROF("capi:18");
     WgradArgs wa = {};
-    wa.xsrc = l == 1 ? (const void*)w.xhat0 : (const void*)w.y[l - 1];
+    wa.xsrc = l == 1 ? (const void*)xhat0 : (const void*)w.y[l - 1];
     wa.item_track = b->item_track;
     wa.x_mean = w.mean[l - 1];
     wa.x_a = l == 1 ? w.invstd[0] : w.a[l - 1];
@@ -781,7 +805,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   };
   hipEvent_t tail[4] = {};  // caller's stream, user stream, wgrad streams 0 and 1
   // layer 1 (the step's tail) follows the chain on the caller's stream, issued right away
-  TRY(wait_point(s, ev_x0));
+  if (ev_x0) TRY(wait_point(s, ev_x0));
   TRY(issue_wgrad(1, s, 2, &tail[0]));
   HPROF("capi:22");
 

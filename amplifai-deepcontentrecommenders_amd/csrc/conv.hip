@@ -442,6 +442,11 @@ static int choose_tw(long rows, int twmax) {
     if (forced <= twmax) return forced;
   constexpr long kCUs = 256;
   const long tiles = (rows + 15) / 16;
+  // Many tiles (catalogue M): four tiles per workgroup once that still leaves two workgroups per
+  // CU. Every workgroup streams the layer's whole packed weights from L2, so one-tile workgroups
+  // re-read them 4x as often; measured at M = 1,344 (tw_sweep.sh): layer-2 dgrad 179 -> 105 us,
+  // layer-2 forward 86 -> 65 us against the pass-count model's TW = 1.
+  if (twmax >= 4 && tiles >= 4 * 2 * kCUs) return 4;
   int best = 1;
   long best_cost = -1;
   for (int tw : {1, 2, 3, 4, 8}) {

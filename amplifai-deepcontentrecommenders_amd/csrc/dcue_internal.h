@@ -322,7 +322,17 @@ struct StepOpts {
   // tower -- same stream order relative to every Adam step, but off the next step's user-tower path
   bool defer_flush_slice = false;
   int flush_slice_step = -1;
+  // prepared one step ahead from the announced next batch (plans, dcue_plan_set_next): bn0's batch
+  // sums already in `acc`, and the conv-1 weight gradient's X operand (k_xhat0) already built
+  bool input_stats_done = false;
+  const float* xhat0 = nullptr;
+  bool clear_bn0 = false;  // the block holds bn0 sums of an announced batch this step did not use
 };
+// A batch's model-independent item inputs, issued ahead of its step (plans): bn0's count-weighted
+// batch sums into the accumulator block `acc` (cleared, counts written, on the same stream before)
+// and bn0(x) zero-padded into xhat0 ([M+1][kXp][128] floats).
+int ahead_item_inputs(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, const int32_t* items,
+                      const float* counts, unsigned long long* acc, float* xhat0, hipStream_t s);
 // words of the per-step accumulator block (BN sums) cleared before each step
 long step_acc_words(const dcue_dims* d, int B, int N, int M);
 int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,

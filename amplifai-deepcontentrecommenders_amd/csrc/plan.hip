@@ -38,6 +38,11 @@ struct dcue_plan {
   unsigned long long* acc[2] = {};
   long nacc = 0;
   dcue_mt_state* mt_ahead = nullptr;
+  // lookahead (dcue_plan_set_next): each slot's conv-1 wgrad X operand, the items its bn0 sums and
+  // xhat0 were prepared from (nullptr: not prepared), and the announced next batch
+  float* xh[2] = {};
+  const int32_t* ahead_items[2] = {};
+  const int32_t* next_items = nullptr;
   long launches = 0;
   hipEvent_t tails[2] = {};       // the last launched step's end (StepOpts::tails)
   int pending_flush = -1;         // step whose rolling-flush slice the next launch issues
@@ -128,12 +133,19 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   if (users_src) b.users = users_src;
   if (items_src) b.item_track = items_src;
   if (inbatch) b.neg_item = p->neg[cur];
+  // this step's inputs were prepared ahead from exactly these items
+  const bool prepared = p->ahead_items[cur] != nullptr;
+  const bool ahead = prepared && items_src == p->ahead_items[cur];
+  p->ahead_items[cur] = nullptr;
   StepOpts o;
   o.prologue_done = true;
   o.fuse_score = true;
   o.emb_adam = emb_adam;
   o.counts = p->counts[cur];
   o.acc = p->acc[cur];
+  o.input_stats_done = ahead;
+  o.xhat0 = ahead ? p->xh[cur] : nullptr;
+  o.clear_bn0 = prepared && !ahead;
   hipEvent_t score_done = nullptr;
   o.score_done = &score_done;
   o.tails = p->tails;
@@ -143,6 +155,17 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   o.defer_flush_slice = deferred && emb_adam != nullptr;
   TRY(forward_impl(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, 1, p->cfg.margin, o, s));
   HPROF("plan:4");
+  // lookahead: the announced next batch's bn0 sums (into slot nxt's accumulator block, cleared and
+  // weighted by the counts drawn above on the same stream) and its xhat0. The items are the
+  // caller's, written in the caller's stream order: wait for this step's score kernel (a fork point
+  // the step records anyway), which comes after everything the caller enqueued before this launch.
+  p->ahead_items[nxt] = nullptr;
+  if (p->next_items && p->xh[nxt] && score_done) {
+    TRY(wait_point(sa, score_done));
+    TRY(ahead_item_inputs(&p->model, &b0, &p->tracks, p->next_items, p->counts[nxt], p->acc[nxt], p->xh[nxt], sa));
+    p->ahead_items[nxt] = p->next_items;
+  }
+  p->next_items = nullptr;
   TRY(backward_impl(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, nullptr, p->cfg.emb_grad_scale, o, s));
   HPROF("plan:5");
   p->pending_flush = o.defer_flush_slice ? emb_adam->step : -1;
@@ -183,8 +206,11 @@ extern "C" int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const 
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t bneg = al(sizeof(int32_t) * (nneg > 0 ? nneg : 1)), bcnt = al(sizeof(float) * M),
                  bacc = al(sizeof(unsigned long long) * nacc), bmt = al(sizeof(dcue_mt_state));
+    // lookahead slots (in-batch plans of BatchNorm towers): xhat0 per slot
+    const bool look = (cfg->flags & DCUE_PLAN_SAMPLE_INBATCH) && dcue::tower_has_bn(&m->dims);
+    const size_t bxh = look ? al(sizeof(float) * (size_t)(M + 1) * dcue::kXp * dcue::kMels) : 0;
     void* mem = nullptr;
-    DCUE_HIP_CHECK(hipMalloc(&mem, 2 * (bneg + bcnt + bacc) + bmt));
+    DCUE_HIP_CHECK(hipMalloc(&mem, 2 * (bneg + bcnt + bacc + bxh) + bmt));
     dcue_plan* p = new dcue_plan;
     p->model = *m;
     p->batch = *b;
@@ -198,6 +224,7 @@ extern "C" int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const 
       p->neg[i] = (int32_t*)q; q += bneg;
       p->counts[i] = (float*)q; q += bcnt;
       p->acc[i] = (unsigned long long*)q; q += bacc;
+      if (bxh) { p->xh[i] = (float*)q; q += bxh; }
     }
     p->mt_ahead = (dcue_mt_state*)q;
     p->nacc = nacc;
@@ -327,6 +354,13 @@ extern "C" int dcue_plan_set_comm(dcue_plan* p, dcue_comm* comm) {
   p->late = off[DCUE_SEG_LATE];
   p->n_dense = off[DCUE_N_DENSE_SEGMENTS];
   p->comm_world = dcue::comm_world(comm);
+  return DCUE_OK;
+}
+
+extern "C" int dcue_plan_set_next(dcue_plan* p, const int32_t* next_item_track) {
+  if (!p) return DCUE_ERR_INVALID;
+  if (p->exec || !p->xh[0]) return DCUE_ERR_UNSUPPORTED;
+  p->next_items = next_item_track;
   return DCUE_OK;
 }
 

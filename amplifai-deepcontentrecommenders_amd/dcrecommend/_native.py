@@ -17,6 +17,7 @@ N_FRAMES = 131
 N_BN = 6
 N_DENSE_SEGMENTS = 28
 SEG_LATE = 6  # DCUE_SEG_LATE: bn0, conv layer 1, bn1 come first in the flat layout
+ERR_UNSUPPORTED = 2
 LAYOUT_CATALOGUE = 0
 LAYOUT_GATHER = 1
 
@@ -97,7 +98,7 @@ class PlanConfig(ctypes.Structure):
 
 MT_STATE_BYTES = 624 * 4 + 16
 MAX_LOG_CAP = 256
-ABI_VERSION = 6
+ABI_VERSION = 7
 RANK_SPLIT, RANK_SINGLE = 0, 1
 
 _P = ctypes.c_void_p
@@ -142,6 +143,7 @@ _SIGS = {
     "dcue_plan_destroy": ([_P], ctypes.c_int),
     "dcue_plan_step": ([_P, _P, _P, ctypes.POINTER(AdamArgs), _P], ctypes.c_int),
     "dcue_plan_wait_side": ([_P, _P], ctypes.c_int),
+    "dcue_plan_set_next": ([_P, _P], ctypes.c_int),
     "dcue_comm_unique_id": ([_P], ctypes.c_int),
     "dcue_comm_create": ([_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
     "dcue_comm_destroy": ([_P], ctypes.c_int),

@@ -123,6 +123,20 @@ class TrainPlan:
         if st != 0:
             nat.check(st, "dcue_plan_step")
 
+    def set_next(self, item_track):
+        """Announce the NEXT launch's item_track source (device [M] int32, unchanged until that
+        launch): this step then also prepares that batch's bn0 statistics and conv-1 wgrad input
+        beside itself, off the next step's critical path (include/dcue.h dcue_plan_set_next).
+        Returns False where the plan cannot look ahead (graph, catalogue or BatchNorm-free plans)."""
+        if self._handle is None:
+            raise RuntimeError("TrainPlan was closed")
+        st = self._lib.dcue_plan_set_next(self._handle, None if item_track is None else item_track.data_ptr())
+        if st == nat.ERR_UNSUPPORTED:
+            return False
+        nat.check(st, "dcue_plan_set_next")
+        self._hold.append((None, item_track))
+        return True
+
     def set_comm(self, comm):
         """Data parallelism inside step(): with a distributed.NativeComm bound, each step() also
         all-reduces the dense gradient over RCCL between the backward and Adam (two buckets, the

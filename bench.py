@@ -363,6 +363,8 @@ def main():
                 D.allreduce_mean_overlapped_(plan, G, G_late)
                 opt.step()
             else:
+                if s + 1 < users_b.shape[0]:  # the next batch is known: its bn0 inputs ride beside this step
+                    plan.set_next(items_b[s + 1])
                 plan.step(users_b[s], items_b[s])  # sample + fwd + bwd (+ RCCL) + Adam: one host call
             sched_step()
         return fn

@@ -38,10 +38,13 @@ def _state(net, opt):
     return out
 
 
-@pytest.mark.parametrize("inbatch,graph,fused_adam", [(True, False, False), (False, False, False),
-                                                      (True, True, False), (False, True, False),
-                                                      (True, False, True)])
-def test_plan_replay_matches_eager(inbatch, graph, fused_adam):
+@pytest.mark.parametrize("inbatch,graph,fused_adam,lookahead", [
+    (True, False, False, False), (False, False, False, False), (True, True, False, False),
+    (False, True, False, False), (True, False, True, False),
+    # dcue_plan_set_next: bn0 statistics and the conv-1 wgrad input prepared one step ahead (a
+    # withdrawn announcement and a mismatched one fall back to computing them in the step)
+    (True, False, True, True), (True, False, False, True)])
+def test_plan_replay_matches_eager(inbatch, graph, fused_adam, lookahead):
     from dcrecommend import _native as nat
     from dcrecommend.dcue.plan import TrainPlan
     from dcrecommend.optim import NativeAdam
@@ -56,9 +59,19 @@ def test_plan_replay_matches_eager(inbatch, graph, fused_adam):
     plan = TrainPlan(replayed, tracks, B, N, mt_state=mts[1] if inbatch else None, graph=graph,
                      optimizer=opts[1] if fused_adam else None)
     neg = torch.zeros((B, N), dtype=torch.int32, device=DEV)
+    all_users = [torch.randint(0, n_users, (B,), generator=gen, device=DEV) for _ in range(steps)]
+    all_items = [torch.randint(0, n_tracks, (M,), generator=gen, device=DEV, dtype=torch.int64).to(torch.int32)
+                 for _ in range(steps)]
+    decoy = all_items[0].clone()
     for s in range(steps):
-        users = torch.randint(0, n_users, (B,), generator=gen, device=DEV)
-        items = torch.randint(0, n_tracks, (M,), generator=gen, device=DEV, dtype=torch.int64).to(torch.int32)
+        users, items = all_users[s], all_items[s]
+        if lookahead and s + 1 < steps:
+            if s == 2:
+                assert plan.set_next(None)  # withdrawn: step 3 computes its own
+            elif s == 3:
+                assert plan.set_next(decoy)  # step 4 passes another buffer: computed in the step
+            else:
+                assert plan.set_next(all_items[s + 1])
         if inbatch:
             nat.check(nat.lib().dcue_sample_inbatch(nat.ptr(mts[0]), B, N, nat.ptr(neg), nat.stream_handle()),
                       "sample")
