@@ -719,13 +719,11 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(launch_tgemm(0, 0, g, s));
     TRY(fk.done());
   } else {  // per-item feature gradients df, then (same kernel) the fc input gradient g5 = df W and BN5's sums
-    ForkAfter fk(sp, s, &ev_layer[5]);
+    // (no fork point here: the fc weight gradient waits with the layer 3-5 weight gradients, below)
     TRY(launch_item_grad(w.dfcopy, b, D, w.df, c.P(SEG_FC_W), w.g[5], bn_acc(w.bnbacc, w.cmax, 5),
                          w.y[5], w.mean[5], w.invstd[5], o.fuse_score ? w.rowsum : nullptr, w.loss, s));
-    TRY(fk.done());
     HPROF("capi:15");
   }
-  const hipEvent_t ev_df = ev_layer[5];
   for (int l = 5; l >= 2; --l) {  // dgrad chain: g_l (+ BN_l sums) -> g_{l-1} (+ BN_{l-1} sums)
     const LayerGeom gm = layer_geom(l);
     RowsArgs ra = {};
@@ -810,7 +808,9 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   HPROF("capi:22");
 
   {  // fc weight gradient: dW[n][k] = sum_m df[m][n] bn5(y5)[m][k], db = sum_m df
-    TRY(wait_point(sw[1], ev_df));
+    // df is final after the item gradient; the res towers fork right there, the others at the
+    // layer 3-5 weight gradients' fork point (one fork point fewer on the chain)
+    TRY(wait_point(sw[1], c.res ? ev_layer[5] : ev_layer[3]));
     HPROF("capi:23");
     TGemmArgs g = {};
     g.M = D; g.N = c.FI; g.K = M;

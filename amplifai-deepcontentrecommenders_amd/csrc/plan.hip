@@ -206,8 +206,8 @@ extern "C" int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const 
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t bneg = al(sizeof(int32_t) * (nneg > 0 ? nneg : 1)), bcnt = al(sizeof(float) * M),
                  bacc = al(sizeof(unsigned long long) * nacc), bmt = al(sizeof(dcue_mt_state));
-    // lookahead slots (in-batch plans of BatchNorm towers): xhat0 per slot
-    const bool look = (cfg->flags & DCUE_PLAN_SAMPLE_INBATCH) && dcue::tower_has_bn(&m->dims);
+    // lookahead slots (plans of BatchNorm towers): xhat0 per slot
+    const bool look = dcue::tower_has_bn(&m->dims);
     const size_t bxh = look ? al(sizeof(float) * (size_t)(M + 1) * dcue::kXp * dcue::kMels) : 0;
     void* mem = nullptr;
     DCUE_HIP_CHECK(hipMalloc(&mem, 2 * (bneg + bcnt + bacc + bxh) + bmt));

@@ -127,7 +127,8 @@ class TrainPlan:
         """Announce the NEXT launch's item_track source (device [M] int32, unchanged until that
         launch): this step then also prepares that batch's bn0 statistics and conv-1 wgrad input
         beside itself, off the next step's critical path (include/dcue.h dcue_plan_set_next).
-        Returns False where the plan cannot look ahead (graph, catalogue or BatchNorm-free plans)."""
+        The items must already be written in this stream's order. Returns False where the plan
+        cannot look ahead (graph or BatchNorm-free plans)."""
         if self._handle is None:
             raise RuntimeError("TrainPlan was closed")
         st = self._lib.dcue_plan_set_next(self._handle, None if item_track is None else item_track.data_ptr())

@@ -93,11 +93,11 @@ class _Negatives:
         if len(self.saturated):
             check_catalogue_users(users.cpu().numpy() if torch.is_tensor(users) else users, self.saturated)
 
-    def draw(self, mt, users, N, out):
+    def draw(self, mt, users, N, out, stream=None):
         nat.check(nat.lib().dcue_sample_catalogue(
             None if self.reseed else nat.ptr(mt), int(self.reseed), self.seed, nat.ptr(self.split),
             self.split.numel(), nat.ptr(self.indptr), nat.ptr(self.ranks), nat.ptr(users), users.numel(), N,
-            nat.ptr(out), nat.stream_handle(self.device)), "dcue_sample_catalogue")
+            nat.ptr(out), nat.stream_handle(self.device) if stream is None else stream), "dcue_sample_catalogue")
 
 
 def _mt_from_numpy(device):
@@ -234,33 +234,64 @@ class DCUE(Trainer):
 
     # ------------------------------------------------------------------ epochs
     def _train_epoch(self, loader):
-        """nn/dcue.py:172-218: per batch sample negatives, forward, hinge, backward, Adam, LR step."""
+        """nn/dcue.py:172-218: per batch sample negatives, forward, hinge, backward, Adam, LR step.
+
+        The reference draws each row's catalogue negatives in its DataLoader workers, ahead of the
+        step that consumes them (datasets/dcuedataset.py:207-256). Here the batches' negatives are
+        drawn two steps ahead on a sampling stream -- in batch order on the one numpy-compatible
+        MT19937 stream, so the very same negatives -- and each batch's item list is built there too,
+        so the plan also prepares the next batch's bn0 statistics beside the current step."""
         self.model.train()
         ds = loader.dataset if hasattr(loader, "dataset") else self.train_data
         neg = self._negatives(ds)
         B, N = self.batch_size, self._n_neg(ds)
         plan = self._train_plan(N)
         users_all, items_all = self._rows(ds)
-        mt = _mt_from_numpy(self.device)
-        negs = torch.empty((B, N), dtype=torch.int64, device=self.device)
-        loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
-        samples = 0
-        for rows in loader:
-            r = torch.from_numpy(rows).to(self.device, non_blocking=True)
-            users = users_all.index_select(0, r)
-            pos = items_all.index_select(0, r)
-            neg.check(users)
-            neg.draw(mt, users, N, negs)
-            plan.users.copy_(users)
-            nat.check(nat.lib().dcue_build_catalogue_batch(nat.ptr(pos), nat.ptr(negs), B, N,
-                                                           nat.ptr(plan.item_track), nat.stream_handle()),
-                      "dcue_build_catalogue_batch")
-            plan.step()
+        batches = list(loader)  # the loader's RNG draws happen when its iteration starts, as before
+        dev = self.device
+        main = torch.cuda.current_stream(dev)
+        samp = torch.cuda.Stream(device=dev)
+        mt = _mt_from_numpy(dev)
+        users = [torch.empty(B, dtype=torch.int64, device=dev) for _ in range(3)]
+        pos = [torch.empty(B, dtype=torch.int64, device=dev) for _ in range(3)]
+        negs = [torch.empty((B, N), dtype=torch.int64, device=dev) for _ in range(3)]
+        items = [torch.empty(B * (1 + N), dtype=torch.int32, device=dev) for _ in range(3)]
+        ready = [torch.cuda.Event() for _ in range(3)]
+        done = [torch.cuda.Event() for _ in range(3)]
+        loss_sum = torch.zeros((), dtype=torch.float64, device=dev)
+        samp.wait_stream(main)  # the sampler state and the row tables are written on the main stream
+
+        def prepare(s):
+            k = s % 3
+            with torch.cuda.stream(samp):
+                r = torch.from_numpy(batches[s]).to(dev)
+                torch.index_select(users_all, 0, r, out=users[k])
+                torch.index_select(items_all, 0, r, out=pos[k])
+                neg.check(users[k])
+                neg.draw(mt, users[k], N, negs[k], stream=samp.cuda_stream)
+                nat.check(nat.lib().dcue_build_catalogue_batch(nat.ptr(pos[k]), nat.ptr(negs[k]), B, N,
+                                                               nat.ptr(items[k]), samp.cuda_stream),
+                          "dcue_build_catalogue_batch")
+                ready[k].record(samp)
+
+        n = len(batches)
+        for s in range(min(2, n)):
+            prepare(s)
+        for s in range(n):
+            main.wait_event(ready[min(s + 1, n - 1) % 3])  # this batch and the next one are built
+            if s + 1 < n:
+                plan.set_next(items[(s + 1) % 3])
+            plan.step(users[s % 3], items[s % 3])
             self.scheduler.batch_step()
             loss_sum += plan.loss.double() * B
-            samples += B
+            done[s % 3].record(main)
+            if s + 2 < n:  # buffers (s+2) % 3 were batch s-1's
+                if s >= 1:
+                    samp.wait_event(done[(s - 1) % 3])
+                prepare(s + 2)
+        main.wait_stream(samp)
         _mt_to_numpy(mt)
-        return samples, float(loss_sum) / max(samples, 1)
+        return n * B, float(loss_sum) / max(n * B, 1)
 
     def _eval_epoch(self, loader):
         """nn/dcue.py:220-262: eval-mode loss over the val set in order (last batch partial)."""

@@ -504,25 +504,55 @@ def main():
         split_d64 = torch.from_numpy(split_items).to(dev)
         indptr_d = torch.from_numpy(indptr).to(dev)
         ranks_d = torch.from_numpy(ranks_).to(dev)
-        negs = torch.empty((B, N), dtype=torch.int64, device=dev)
         cplan = make_plan(True)
         ub, ib = batches(args.warmup + args.steps)
         check_catalogue_users(ub.cpu().numpy(), sat)
         ib64 = ib.long()
+        # catalogue negatives are drawn two steps ahead on a sampling stream, as the reference's
+        # DataLoader workers draw them (datasets/dcuedataset.py:207-256, in __getitem__) ahead of the
+        # training step: same draw order on the one numpy-compatible stream, so the same negatives.
+        # Three batch buffers; step s+1's items are built before step s is launched, so the plan
+        # also prepares step s+1's bn0 statistics beside step s (dcue_plan_set_next).
+        main = torch.cuda.current_stream(dev)
+        samp = torch.cuda.Stream(device=dev)
+        negs = [torch.empty((B, N), dtype=torch.int64, device=dev) for _ in range(3)]
+        items = [torch.empty(B * (1 + N), dtype=torch.int32, device=dev) for _ in range(3)]
+        ready = [torch.cuda.Event() for _ in range(3)]
+        done = [torch.cuda.Event() for _ in range(3)]
+        n_all = ub.shape[0]
+
+        def draw(s):
+            k = s % 3
+            with torch.cuda.stream(samp):
+                nat.check(nat.lib().dcue_sample_catalogue(
+                    nat.ptr(mt), 0, 0, nat.ptr(split_d64), split_d64.numel(), nat.ptr(indptr_d), nat.ptr(ranks_d),
+                    nat.ptr(ub[s]), B, N, nat.ptr(negs[k]), samp.cuda_stream), "dcue_sample_catalogue")
+                nat.check(nat.lib().dcue_build_catalogue_batch(nat.ptr(ib64[s]), nat.ptr(negs[k]), B, N,
+                                                               nat.ptr(items[k]), samp.cuda_stream),
+                          "dcue_build_catalogue_batch")
+                ready[k].record(samp)
+
+        samp.wait_stream(main)  # the batch tensors and the sampler state are written on the main stream
+        draw(0)
+        if n_all > 1:
+            draw(1)
 
         def cat_step(plan, s):
-            nat.check(nat.lib().dcue_sample_catalogue(nat.ptr(mt), 0, 0, nat.ptr(split_d64), split_d64.numel(),
-                                                      nat.ptr(indptr_d), nat.ptr(ranks_d), nat.ptr(ub[s]), B, N,
-                                                      nat.ptr(negs), nat.stream_handle()), "dcue_sample_catalogue")
-            nat.check(nat.lib().dcue_build_catalogue_batch(nat.ptr(ib64[s]), nat.ptr(negs), B, N,
-                                                           nat.ptr(cplan.item_track), nat.stream_handle()),
-                      "dcue_build_catalogue_batch")
+            last = min(s + 1, n_all - 1)
+            main.wait_event(ready[last % 3])  # step s's batch and (lookahead) step s+1's
+            if s + 1 < n_all:
+                plan.set_next(items[(s + 1) % 3])
             if world > 1 and comm is None:
-                plan.launch(ub[s], None)
+                plan.launch(ub[s], items[s % 3])
                 D.allreduce_mean_overlapped_(plan, G, G_late)
                 opt.step()
             else:
-                plan.step(ub[s], None)
+                plan.step(ub[s], items[s % 3])
+            done[s % 3].record(main)
+            if s + 2 < n_all:  # buffer (s+2) % 3 was step s-1's: free once that step is done
+                if s >= 1:
+                    samp.wait_event(done[(s - 1) % 3])
+                draw(s + 2)
             sched_step()
         dt, t_enq, _, kern = timed_phase("catalogue", cplan, cat_step)
         out["catalogue"] = summary(dt, t_enq, kern, B * (1 + N), 1 + N, "catalogue")

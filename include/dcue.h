@@ -309,14 +309,16 @@ int dcue_plan_step(dcue_plan* plan, const int64_t* users_src, const int32_t* ite
  * post-backward all-reduce of the DDP-style loop (nn/dcue.py:208-209 under data parallelism). */
 #define DCUE_SEG_LATE 6
 int dcue_plan_wait_side(dcue_plan* plan, void* stream);
-/* Lookahead (eager in-batch plans of a BatchNorm tower): announces the item_track_src buffer of the
+/* Lookahead (eager plans of a BatchNorm tower): announces the item_track_src buffer of the
  * NEXT launch ([M] int32 device ids, contents fixed until that launch). The following launch then
  * also prepares that batch's model-independent item inputs beside its own step -- bn0's batch
  * statistics (k_input_stats) and bn0(x) zero-padded for the conv-1 weight gradient (k_xhat0) -- so
  * the next step's chain starts at conv 1. A next launch whose item_track_src is not the announced
  * buffer computes them itself, as without lookahead; NULL withdraws the announcement. The batch
  * composition of the reference is likewise prepared ahead, by its DataLoader workers
- * (nn/dcue.py:711-721). DCUE_ERR_UNSUPPORTED for graph, catalogue or BatchNorm-free plans. */
+ * (nn/dcue.py:711-721). The announced items must be written, in `stream` order, before the
+ * announcing launch (the lookahead reads them after that launch's score kernel, on a side stream).
+ * DCUE_ERR_UNSUPPORTED for graph or BatchNorm-free plans. */
 int dcue_plan_set_next(dcue_plan* plan, const int32_t* next_item_track);
 int dcue_plan_destroy(dcue_plan* plan);
 

@@ -16,6 +16,7 @@ for TW in "$@"; do
   timeout -k 10 200 rocprofv3 --kernel-trace -f csv -d "$OUT/trace_$TW" -o run -- python3 $ROOT/bench.py \
     --no-cpu-baseline --no-eval --steps 30 --warmup 5 --modes $MODES --profile-phase $PH > "$OUT/prof_$TW.log" 2>&1 || exit 1
   python3 $ROOT/profiles/phase_kernels.py "$OUT/trace_$TW" 14 > "$OUT/kernels_$TW.txt"
+  python3 $ROOT/profiles/timeline.py "$OUT/trace_$TW" "k_conv_rows<0, 0," > "$OUT/timeline_$TW.txt" 2>&1
   python3 - "$OUT/plain_$TW.log" "$PH" <<'PY' >> "$OUT/kernels_$TW.txt"
 import json, sys
 line = [l for l in open(sys.argv[1]) if l.startswith("{")][-1]
