@@ -98,7 +98,7 @@ class PlanConfig(ctypes.Structure):
 
 MT_STATE_BYTES = 624 * 4 + 16
 MAX_LOG_CAP = 256
-ABI_VERSION = 7
+ABI_VERSION = 8
 RANK_SPLIT, RANK_SINGLE = 0, 1
 
 _P = ctypes.c_void_p
@@ -144,6 +144,8 @@ _SIGS = {
     "dcue_plan_step": ([_P, _P, _P, ctypes.POINTER(AdamArgs), _P], ctypes.c_int),
     "dcue_plan_wait_side": ([_P, _P], ctypes.c_int),
     "dcue_plan_set_next": ([_P, _P], ctypes.c_int),
+    "dcue_check_finite": ([_P, ctypes.c_int64, _P, ctypes.c_int32, _P], ctypes.c_int),
+    "dcue_check_ids": ([_P, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_int32, _P], ctypes.c_int),
     "dcue_comm_unique_id": ([_P], ctypes.c_int),
     "dcue_comm_create": ([_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
     "dcue_comm_destroy": ([_P], ctypes.c_int),

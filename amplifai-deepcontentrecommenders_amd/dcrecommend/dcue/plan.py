@@ -16,12 +16,13 @@ import ctypes
 import torch
 
 from dcrecommend import _native as nat
+from dcrecommend.check import StepCheck, enabled_by_env
 
 
 class TrainPlan:
 
     def __init__(self, net, tracks, n_rows, n_neg, mt_state=None, item_track=None, margin=0.2,
-                 emb_grad_scale=1.0, graph=False, optimizer=None):
+                 emb_grad_scale=1.0, graph=False, optimizer=None, check=None):
         """tracks: HBM track table [n_tracks][131][128] (fp16/fp32). In-batch mode (mt_state given):
         positives are items 0..B-1 of item_track, negatives drawn in-graph. Otherwise item_track holds
         B*(1+N) items in catalogue order (datasets/dcuedataset.py:242-250)."""
@@ -75,6 +76,25 @@ class TrainPlan:
                 p.grad = fl["G"][fl["poff"][s]:fl["poff"][s] + p.numel()].view(p.shape)
         net.user_embd.embeddings.weight.grad = None
         net._grad_users = self.users
+        # check mode (dcrecommend.check): ids validated before each step, loss/params/grads after
+        if check is None:
+            check = enabled_by_env()
+        self._check = StepCheck(dev) if check else None
+        self._n_users = int(fl["dims"].n_users)
+
+    def _check_before(self, users, item_track):
+        ck = self._check
+        ck.ids(self.users if users is None else users, self._n_users, "user ids outside the table")
+        ck.ids(self.item_track if item_track is None else item_track, self.tracks.shape[0],
+               "item ids outside the track table")
+        ck.raise_if_any()
+
+    def _check_after(self):
+        ck, fl = self._check, self.net._flat
+        ck.finite(self.loss.view(1), "non-finite loss")
+        ck.finite(fl["P"], "non-finite dense parameters")
+        ck.finite(fl["G"], "non-finite dense gradients")
+        ck.raise_if_any()
 
     def _check_bound(self):
         net = self.net
@@ -91,12 +111,16 @@ class TrainPlan:
         if self._handle is None:
             raise RuntimeError("TrainPlan was closed")
         self._check_bound()
+        if self._check is not None:
+            self._check_before(users, item_track)
         self._hold.append((users, item_track))
         st = self._lib.dcue_plan_launch(self._handle, None if users is None else users.data_ptr(),
                                         None if item_track is None else item_track.data_ptr(),
                                         self._stream if stream is None else stream)
         if st != 0:
             nat.check(st, "dcue_plan_launch")
+        if self._check is not None:
+            self._check_after()
 
     def step(self, users=None, item_track=None, stream=None):
         """One whole single-GPU training step in one host call: launch() + the optimizer step
@@ -111,6 +135,8 @@ class TrainPlan:
         if self._handle is None:
             raise RuntimeError("TrainPlan was closed")
         self._check_bound()
+        if self._check is not None:
+            self._check_before(users, item_track)
         self._hold.append((users, item_track))
         g = opt.param_groups[0]
         opt.step_count += 1
@@ -122,6 +148,8 @@ class TrainPlan:
                                       ctypes.byref(args), self._stream if stream is None else stream)
         if st != 0:
             nat.check(st, "dcue_plan_step")
+        if self._check is not None:
+            self._check_after()
 
     def set_next(self, item_track):
         """Announce the NEXT launch's item_track source (device [M] int32, unchanged until that

@@ -493,6 +493,27 @@ def main():
         out["inbatch"] = summary(dt, t_enq, kern, B, 1, "inbatch")
         if gpu_ms is not None:
             out["inbatch"]["gpu_only_ms_per_step"] = gpu_ms
+    checks = {"after": [], "failed": []}
+
+    def check_state(p, phase):
+        """Correctness signal of the full-size run, outside the timed region (check mode's probes,
+        dcrecommend.check): the last step's loss, the dense parameters and gradients, and the
+        flushed user table with both Adam moments, all finite."""
+        from dcrecommend.check import StepCheck
+        opt.flush()
+        ck = StepCheck(dev)
+        ck.finite(p.loss.view(1), "loss")
+        ck.finite(net._flat["P"], "dense parameters")
+        ck.finite(G, "dense gradients")
+        st = opt._adam_state()
+        ck.finite(net.user_embd.embeddings.weight, "user table")
+        for k in ("em", "ev"):
+            ck.finite(st[k], "user table Adam " + k)
+        checks["after"].append(phase)
+        checks["failed"] += [phase + ": " + f for f in ck.failed()]
+        checks["last_loss_" + phase] = float(p.loss)
+
+    check_state(plan, "inbatch")
     plan.close()
     # ---- phase 3: catalogue negatives (the reference's live sampler)
     if "catalogue" in modes:
@@ -556,6 +577,7 @@ def main():
             sched_step()
         dt, t_enq, _, kern = timed_phase("catalogue", cplan, cat_step)
         out["catalogue"] = summary(dt, t_enq, kern, B * (1 + N), 1 + N, "catalogue")
+        check_state(cplan, "catalogue")
         cplan.close()
     head = out.get("inbatch", out["inbatch_cold"])
     E = args.user_embdim
@@ -598,6 +620,8 @@ def main():
         result["gpu_only_ms_per_step"] = head["gpu_only_ms_per_step"]
     if "catalogue" in out:
         result["catalogue"] = out["catalogue"]
+    checks["finite"] = not checks["failed"]
+    result["checks"] = checks
     if world > 1:
         D.broadcast_buffers_(net)  # DDP semantics: evaluate with rank 0's BN statistics
     if rank == 0 and not args.no_eval:

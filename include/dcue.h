@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DCUE_ABI_VERSION 7
+#define DCUE_ABI_VERSION 8
 #define DCUE_N_MELS 128
 #define DCUE_N_FRAMES 131
 #define DCUE_N_BN 6
@@ -320,6 +320,15 @@ int dcue_plan_wait_side(dcue_plan* plan, void* stream);
  * announcing launch (the lookahead reads them after that launch's score kernel, on a side stream).
  * DCUE_ERR_UNSUPPORTED for graph or BatchNorm-free plans. */
 int dcue_plan_set_next(dcue_plan* plan, const int32_t* next_item_track);
+
+/* ---- check mode (a HIP bounds/NaN check mode; the reference has none) ----
+ * Probes run between steps. Each ORs `bit` into the device word *flags when it finds a problem and
+ * never faults on the data it inspects: ids can be validated before a step indexes with them, and
+ * the loss, parameters, gradients and user table after it. */
+int dcue_check_finite(const float* buf, int64_t n, int32_t* flags, int32_t bit, void* stream);
+/* ids: int32 (id_bytes 4) or int64 (8); flags any id outside [0, limit). */
+int dcue_check_ids(const void* ids, int32_t id_bytes, int64_t n, int64_t limit, int32_t* flags, int32_t bit,
+                   void* stream);
 int dcue_plan_destroy(dcue_plan* plan);
 
 /* ------------------------------------------------- data-parallel gradient exchange (RCCL) */

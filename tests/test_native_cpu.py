@@ -135,3 +135,12 @@ def test_cpu_model_refuses_compute():
                    "model_type": "truedcuemel1dbn"})
     with pytest.raises(RuntimeError, match="GPU"):
         net(torch.zeros(2, dtype=torch.long), torch.zeros(2, 128, 131), torch.zeros(2, 1, 128, 131))
+
+
+def test_check_mode_disabled_by_default(monkeypatch):
+    """Check mode (dcrecommend.check) is opt-in: DCUE_CHECK unset or 0 leaves it off."""
+    from dcrecommend import check
+    monkeypatch.delenv("DCUE_CHECK", raising=False)
+    assert not check.enabled_by_env()
+    monkeypatch.setenv("DCUE_CHECK", "1")
+    assert check.enabled_by_env()
