@@ -450,7 +450,8 @@ def main():
         return out
 
     def traffic_for(kernel_name, mode):
-        tag = {"k_conv1_wgrad": "conv1_wgrad", "k_emb_flush_rows": "emb_flush_rows"}.get(kernel_name.split(" ")[0])
+        tag = {"k_conv1_wgrad": "conv1_wgrad", "k_emb_flush_rows": "emb_flush_rows",
+               "k_conv_rows<0,0>": "conv1_fwd"}.get(kernel_name.split(" ")[0])
         path = os.path.join(ROOT, "profiles", "pmc_%s_%s.json" % (tag, mode)) if tag else None
         if path and os.path.exists(path):
             try:

@@ -21,7 +21,8 @@ import json
 import os
 import sys
 
-KERNELS = {"conv1_wgrad": "k_conv1_wgrad", "emb_flush_rows": "k_emb_flush_rows"}
+KERNELS = {"conv1_wgrad": "k_conv1_wgrad", "emb_flush_rows": "k_emb_flush_rows",
+           "conv1_fwd": "k_conv_rows<0, 0,"}
 MARK = "spin_kernel"
 
 
