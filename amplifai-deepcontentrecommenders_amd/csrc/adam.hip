@@ -67,7 +67,7 @@ __device__ __forceinline__ void window_bound(const AdamScalars* hs, int j0, int 
 }
 
 struct PackSeg {
-  long src, fwd, bwd;  // floats: W in params; forward pack; dgrad pack (-1: none)
+  long src, fwd, bwd, f16;  // floats: W in params; forward pack; dgrad pack (-1: none); split-f16 pack
   int cout, cin, ks;
 };
 struct PackArgs;
@@ -88,6 +88,14 @@ __device__ __forceinline__ void pack_store(const PackSeg& sg, long e, float w, f
     const long kr = sg.ks - 1 - k;
     wpack[sg.bwd + (((kr * (sg.cout / 4) + o / 4) * sg.cin + cc) * 4 + (o & 3))] = w;
   }
+  // split-f16 forward operand: hi = fp16(w), lo = fp16(w - hi) (w - hi is exact in f32)
+  const _Float16 hi = (_Float16)w;
+  const _Float16 lo = (_Float16)(w - (float)hi);
+  _Float16* h16 = reinterpret_cast<_Float16*>(wpack + sg.f16);
+  const long q = k * (sg.cin / 32) + cc / 32;
+  const long base = ((q * sg.cout + o) * 4 + (cc & 31) / 8) * 16 + (cc & 7);
+  h16[base] = hi;
+  h16[base + 8] = lo;
 }
 
 // Adam over the flat dense buffer with the conv-weight repack fused in: a float4 that lies in a
@@ -469,19 +477,9 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
 // k' = ks-1-k.
 __global__ void k_pack(const float* __restrict__ params, float* wpack, PackArgs pa) {
   const PackSeg sg = pa.seg[blockIdx.y];
-  const long ks = sg.ks;
-  const long n = (long)sg.cout * sg.cin * ks;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
-    const long o = e / ((long)sg.cin * ks);
-    const long rem = e - o * sg.cin * ks;
-    const long c = rem / ks, k = rem - c * ks;
-    const float w = params[sg.src + e];  // W[o][c][k]
-    wpack[sg.fwd + (((k * (sg.cin / 4) + c / 4) * sg.cout + o) * 4 + (c & 3))] = w;
-    if (sg.bwd >= 0) {
-      const long kr = sg.ks - 1 - k;
-      wpack[sg.bwd + (((kr * (sg.cout / 4) + o / 4) * sg.cin + c) * 4 + (o & 3))] = w;
-    }
-  }
+  const long n = (long)sg.cout * sg.cin * sg.ks;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x)
+    pack_store(sg, e, params[sg.src + e], wpack);  // W[o][c][k]
 }
 
 PackArgs pack_args(const dcue_model* md, const int64_t* poff) {
@@ -496,6 +494,7 @@ PackArgs pack_args(const dcue_model* md, const int64_t* poff) {
     sg.src = poff[2 + 4 * (l - 1)];  // conv.layer{l}.weight
     sg.fwd = wl.conv_fwd[l];
     sg.bwd = l >= 2 ? wl.conv_bwd[l] : -1;
+    sg.f16 = wl.conv_f16[l];
   }
   return pa;
 }

@@ -392,6 +392,7 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     a.in_bn = bn_of(l - 1);
     a.counts = counts;
     a.wpack = m->wpack + wpack_offset(&m->dims, l, false);
+    a.wpack16 = reinterpret_cast<const uint4*>(m->wpack + wpack_layout(&m->dims).conv_f16[l]);
     a.bias = c.P(seg_conv_b(l));
     a.out = w.y[l];
     a.out_idx = w.idx[l];

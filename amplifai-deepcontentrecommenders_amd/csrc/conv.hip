@@ -151,6 +151,24 @@ __device__ __forceinline__ float4 slab_finish(const RowsArgs& a, const ChanOps& 
 // issues MFMAs (with four waves of 32 columns the loads' latency was exposed: ~40% of wave cycles
 // parked on s_waitcnt).
 constexpr int kRowsWaves = 8, kRowsThreads = 64 * kRowsWaves, kRowsCT = 128 / (16 * kRowsWaves);
+
+// Split-f16 forward (F16): the slab holds every input value v as v = hi + lo, hi = fp16(v), lo =
+// fp16(v - hi), per 8-channel octet q of a row as [hi x 8][lo x 8] at dwords 8q .. 8q+7 (the row
+// pitch is unchanged: 16 bytes of halves per 4 channels, as the f32 slab). |v| must stay below the
+// fp16 range (65504), which the fp16 track table bounds for layer 1; BatchNorm keeps the others O(1).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ void st_split(float* row, int c, float4 v) {
+  const f16x4 h = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+  const f16x4 l = {(_Float16)(v.x - (float)h[0]), (_Float16)(v.y - (float)h[1]),
+                   (_Float16)(v.z - (float)h[2]), (_Float16)(v.w - (float)h[3])};
+  const int o = 8 * (c >> 3) + 2 * ((c >> 2) & 1);
+  *reinterpret_cast<f16x4*>(row + o) = h;
+  *reinterpret_cast<f16x4*>(row + o + 4) = l;
+}
 // B k-steps (float4 per lane per 16-column tile) requested ahead of the MFMAs by one-tile workgroups
 // (the small layers at in-batch M): a layer's whole K at H = 128 (32 steps), so they wait on the
 // weights once, not once every two steps
@@ -160,7 +178,7 @@ constexpr int kRowsWaves = 8, kRowsThreads = 64 * kRowsWaves, kRowsCT = 128 / (1
 constexpr int kRowsPD = DCUE_ROWS_PD;
 
 template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,
-          int POOLL, bool DEEP>
+          int POOLL, bool DEEP, bool F16>
 __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
   critical_path_priority();
   constexpr int RX = R + KS - 1;
@@ -195,11 +213,29 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
   constexpr int PD = NSTEP < PDW ? NSTEP : PDW;
   const float* wp = a.wpack + ((size_t)g * nout + (colok ? ocol0 : 0) + l16) * 4;
   const size_t wstep = (size_t)16 * nout;
-  float4 bq[PD][CT];
+  float4 bq[F16 ? 1 : PD][CT];
+  // split-f16 path: 32-channel K chunks, a lane's (hi, lo) octets of its column per chunk
+  constexpr int NCH = KS * (KC / 32);
+  constexpr int PDW16 = DEEP ? kRowsPD / (2 * CT) : 4;  // 4 chunks = 2 KB in flight per wave
+  constexpr int PD16 = NCH < PDW16 ? NCH : PDW16;
+  const f16x8* wp16 = reinterpret_cast<const f16x8*>(a.wpack16) +
+                      (((size_t)(colok ? ocol0 : 0) + l16) * 4 + g) * 2;
+  const size_t wstep16 = (size_t)8 * nout;
+  f16x8 bh[F16 ? PD16 : 1][CT][2];
+  if constexpr (F16) {
 #pragma unroll
-  for (int st = 0; st < PD; ++st)
+    for (int st = 0; st < PD16; ++st)
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) bq[st][ct] = ld4(wp + st * wstep + 64 * ct);
+      for (int ct = 0; ct < CT; ++ct) {
+        bh[st][ct][0] = wp16[st * wstep16 + 128 * ct];
+        bh[st][ct][1] = wp16[st * wstep16 + 128 * ct + 1];
+      }
+  } else {
+#pragma unroll
+    for (int st = 0; st < PD; ++st)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) bq[st][ct] = ld4(wp + st * wstep + 64 * ct);
+  }
 
   {
     static_assert(kRowsThreads % C4 == 0, "a thread's slab slots share one channel quad");
@@ -239,7 +275,10 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
         const int e = base + kRowsThreads * j;
         if (e < nfill) {
           const float4 v = slab_finish<SRC, POOLL>(a, kop, pp[j], raw[j]);
-          st4(&slab[(e / C4) * PITCH + c], ok[j] ? v : make_float4(0.f, 0.f, 0.f, 0.f));
+          if constexpr (F16)
+            st_split(&slab[(e / C4) * PITCH], c, ok[j] ? v : make_float4(0.f, 0.f, 0.f, 0.f));
+          else
+            st4(&slab[(e / C4) * PITCH + c], ok[j] ? v : make_float4(0.f, 0.f, 0.f, 0.f));
         }
       }
     };
@@ -274,9 +313,43 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc[r][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (F16) {
+    // x*w = (xh + xl)(wh + wl) ~ xl*wh + xh*wl + xh*wh: three v_mfma_f32_16x16x32_f16 per 32-channel
+    // chunk (fp16 products are exact in f32; the dropped xl*wl and the lo roundings are ~2^-22 of
+    // |x*w|), the small terms first
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      f16x8 b[CT][2];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        b[ct][0] = bh[ch % PD16][ct][0];
+        b[ct][1] = bh[ch % PD16][ct][1];
+        if (ch + PD16 < NCH) {
+          bh[ch % PD16][ct][0] = wp16[(ch + PD16) * wstep16 + 128 * ct];
+          bh[ch % PD16][ct][1] = wp16[(ch + PD16) * wstep16 + 128 * ct + 1];
+        }
+      }
+      const int k = ch / (KC / 32);
+      const int aoff = k * PITCH + 32 * (ch - k * (KC / 32)) + 4 * g;  // sbase holds 4g: octet g is 8g
+      f16x8 ah[TW], al[TW];
+#pragma unroll
+      for (int r = 0; r < TW; ++r) {
+        ah[r] = *reinterpret_cast<const f16x8*>(&slab[sbase[r] + aoff]);
+        al[r] = *reinterpret_cast<const f16x8*>(&slab[sbase[r] + aoff + 4]);
+      }
+#pragma unroll
+      for (int r = 0; r < TW; ++r)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          acc[r][ct] = mfma16(al[r], b[ct][0], acc[r][ct]);
+          acc[r][ct] = mfma16(ah[r], b[ct][1], acc[r][ct]);
+          acc[r][ct] = mfma16(ah[r], b[ct][0], acc[r][ct]);
+        }
+    }
+  }
   // fully unrolled: straight-line code lets the wait counters track the in-flight B loads exactly
 #pragma unroll
-  for (int st = 0; st < NSTEP; ++st) {
+  for (int st = 0; st < (F16 ? 0 : NSTEP); ++st) {
     float4 b[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
@@ -398,9 +471,9 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
 }
 
 template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,
-          int POOLL, bool DEEP>
+          int POOLL, bool DEEP, bool F16>
 static int run_rows_pd(const RowsArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-  auto kern = k_conv_rows<MODE, SRC, KC, KS, PADL, LIN, R, POOL, TW, LPL, POOLL, DEEP>;
+  auto kern = k_conv_rows<MODE, SRC, KC, KS, PADL, LIN, R, POOL, TW, LPL, POOLL, DEEP, F16>;
   static bool attr = false;
   if (!attr) {
     DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -413,7 +486,7 @@ static int run_rows_pd(const RowsArgs& a, dim3 grid, size_t lds, hipStream_t s) 
 }
 
 template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,
-          int POOLL>
+          int POOLL, bool F16 = false>
 static int run_rows(const RowsArgs& a, hipStream_t s) {
   constexpr int ROWS = TW * 16;
   constexpr int MAXI = (ROWS + R - 1) / R + 1;
@@ -423,8 +496,8 @@ static int run_rows(const RowsArgs& a, hipStream_t s) {
   const long total = (long)a.M * R;
   dim3 grid((unsigned)((total + ROWS - 1) / ROWS), (unsigned)((a.nout + 127) / 128));
   if (TW == 1 && (long)grid.x * grid.y <= 256)  // one-tile workgroups, one per CU: weights run ahead
-    return run_rows_pd<MODE, SRC, KC, KS, PADL, LIN, R, POOL, TW, LPL, POOLL, true>(a, grid, LDS, s);
-  return run_rows_pd<MODE, SRC, KC, KS, PADL, LIN, R, POOL, TW, LPL, POOLL, false>(a, grid, LDS, s);
+    return run_rows_pd<MODE, SRC, KC, KS, PADL, LIN, R, POOL, TW, LPL, POOLL, true, F16>(a, grid, LDS, s);
+  return run_rows_pd<MODE, SRC, KC, KS, PADL, LIN, R, POOL, TW, LPL, POOLL, false, F16>(a, grid, LDS, s);
 }
 
 // Row tiles per workgroup. Each wave runs TW 16-row tiles of its 32 columns back to back, and a
@@ -462,9 +535,22 @@ static int choose_tw(long rows, int twmax) {
 }
 
 
+// Split-f16 forward (three f16 MFMAs per 32-channel chunk, ~2^-22 relative per product, at 3/16 of
+// the f32 MFMA time) unless DCUE_CONV_F16=0 selects the exact-f32 path
+static bool conv_f16_on() {
+  static const bool on = [] {
+    const char* e = getenv("DCUE_CONV_F16");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <int L, int KC, int SRC, int TW>
 static int fwd_layer_tw(const RowsArgs& a, hipStream_t s) {
   constexpr LayerGeom gm = layer_geom(L);
+  static_assert(KC % 32 == 0, "split-f16 chunks are 32 channels");
+  if (a.wpack16 && conv_f16_on())
+    return run_rows<0, SRC, KC, gm.ks, gm.pad, gm.lin, gm.lp * gm.pool, gm.pool, TW, 1, 1, true>(a, s);
   return run_rows<0, SRC, KC, gm.ks, gm.pad, gm.lin, gm.lp * gm.pool, gm.pool, TW, 1, 1>(a, s);
 }
 

@@ -51,6 +51,7 @@ struct RowsArgs {
   float invN;                 // 1 / (copies * positions)
   const float* counts;        // [M] copies per item (nullable -> 1)
   const float* wpack;         // [KS][KC/4][nout][4]
+  const uint4* wpack16;       // forward, split-f16 path: [KS*KC/32][nout][4][hi, lo] x 8 halves
   const float* bias;          // forward [nout]
   float* out;                 // forward y_l [M][Lp][nout]; dgrad g_{l-1} [M][R][nout]
   uint8_t* out_idx;           // forward argmax [M][Lp][nout]
@@ -132,8 +133,11 @@ int launch_bn_eval(int C, const float* gamma, const float* rmean, const float* r
 
 // ------------------------------------------------------------------ packed weight layout
 // wpack = conv B operands (forward per layer, dgrad per layer >= 2). Dense weights are read in place.
+// conv_f16[l]: the forward B operand split into fp16 pairs w = hi + lo (hi = fp16(w), lo =
+// fp16(w - hi)) for the split-f16 MFMA forward (conv.hip), as halves
+// [k * cin/32 + c/32][cout][(c % 32) / 8][hi, lo][c % 8] -- one float slot per weight
 struct WpackLayout {
-  long conv_fwd[6], conv_bwd[6];
+  long conv_fwd[6], conv_bwd[6], conv_f16[6];
   long total;
 };
 inline WpackLayout wpack_layout(const dcue_dims* dm) {
@@ -147,6 +151,8 @@ inline WpackLayout wpack_layout(const dcue_dims* dm) {
     n += e;
     w.conv_bwd[l] = l >= 2 ? n : -1;
     if (l >= 2) n += e;
+    w.conv_f16[l] = n;  // cin is a multiple of 32 (128, or H in 32..256)
+    n += e;
   }
   w.total = n;
   return w;

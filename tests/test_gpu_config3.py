@@ -91,7 +91,9 @@ def test_inbatch_training_at_config3(world):
     plan = TrainPlan(net, tracks, B, N, mt_state=mt, optimizer=opt)
     steps = 300
     gen = torch.Generator(device=DEV).manual_seed(9)
-    rows = torch.randint(0, N_PAIRS, (steps, B), generator=gen, device=DEV)
+    # a pool of 10 batches cycled: the loss must fall as the towers fit them (fresh random
+    # interactions every step leave nothing to learn, and their loss only wanders)
+    rows = torch.randint(0, N_PAIRS, (10, B), generator=gen, device=DEV).repeat(steps // 10, 1)
     ub = pair_user[rows].contiguous()
     ib = pair_track[rows].to(torch.int32).contiguous()
     losses = torch.empty(steps, device=DEV)

@@ -76,7 +76,8 @@ def test_layouts_match_reference_shapes(golden):
         assert off[s + 1] - off[s] < n + 4, name
     boff = nat.bn_layout(dims)
     assert boff[1] - boff[0] >= 128 and boff[-1] > 0
-    assert nat.wpack_floats(dims) == 128 * H * 4 + 2 * (2 * H * H * 4 + H * H * 2 + d * H)  # conv packs only
+    # conv packs only: forward, dgrad (layers 2-5) and the split-f16 forward copy
+    assert nat.wpack_floats(dims) == 2 * 128 * H * 4 + 3 * (2 * H * H * 4 + H * H * 2 + d * H)
     assert nat.workspace_bytes(dims, 4, 3, 16) > 0
 
 
