@@ -216,7 +216,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
   float4 bq[F16 ? 1 : PD][CT];
   // split-f16 path: 32-channel K chunks, a lane's (hi, lo) octets of its column per chunk
   constexpr int NCH = KS * (KC / 32);
-  constexpr int PDW16 = DEEP ? kRowsPD / (2 * CT) : 4;  // 4 chunks = 2 KB in flight per wave
+  constexpr int PDW16 = DEEP ? kRowsPD / (2 * CT) : 3;  // 3 chunks: keeps <= 128 VGPRs (2 WGs per CU)
   constexpr int PD16 = NCH < PDW16 ? NCH : PDW16;
   const f16x8* wp16 = reinterpret_cast<const f16x8*>(a.wpack16) +
                       (((size_t)(colok ? ocol0 : 0) + l16) * 4 + g) * 2;
@@ -329,6 +329,9 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
           bh[ch % PD16][ct][1] = wp16[(ch + PD16) * wstep16 + 128 * ct + 1];
         }
       }
+      // one chunk's operands live at a time: without the barrier hipcc hoists every chunk's LDS reads
+      // (223 VGPRs, one workgroup per CU, no fill/MFMA overlap between workgroups)
+      __builtin_amdgcn_sched_barrier(0);
       const int k = ch / (KC / 32);
       const int aoff = k * PITCH + 32 * (ch - k * (KC / 32)) + 4 * g;  // sbase holds 4g: octet g is 8g
       f16x8 ah[TW], al[TW];

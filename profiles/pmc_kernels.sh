@@ -9,8 +9,8 @@ OUT=$ROOT/gpurun_out/pmc_${TAG}_$PH
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 MODES=$([ "$PH" = catalogue ] && echo catalogue || echo inbatch)
-timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
-  SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE \
+COUNTERS=${PMC_COUNTERS:-SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE}
+timeout -s KILL 240 rocprofv3 --pmc $COUNTERS \
   -f csv -d "$OUT/raw" -o run -- python3 $ROOT/bench.py --no-cpu-baseline --no-eval --steps 20 --warmup 5 \
   --modes $MODES --profile-phase $PH > "$OUT/run.log" 2>&1 || exit 1
 python3 - "$OUT" > "$OUT/summary.txt" <<'PY'
@@ -37,6 +37,9 @@ for k in order:
     print("%-90s n=%d gui=%.0f waveQ=%.0f wait=%.2f waitinst=%.2f active=%.2f mfma_busy=%.0f valu=%.0f lds=%.0f" % (
         k, n, a.get("GRBM_GUI_ACTIVE", 0), wc, a.get("SQ_WAIT_ANY", 0) / wc, a.get("SQ_WAIT_INST_ANY", 0) / wc,
         a.get("SQ_ACTIVE_INST_ANY", 0) / wc, a.get("SQ_VALU_MFMA_BUSY_CYCLES", 0), a.get("SQ_INSTS_VALU", 0),
-        a.get("SQ_INSTS_LDS", 0)))
+        a.get("SQ_INSTS_LDS", 0)),
+          " ".join("%s=%.0f" % (c, v) for c, v in sorted(a.items()) if c not in (
+              "GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+              "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU", "SQ_INSTS_LDS")))
 PY
 rm -rf "$OUT/raw"
