@@ -153,21 +153,24 @@ __device__ __forceinline__ float4 slab_finish(const RowsArgs& a, const ChanOps& 
 constexpr int kRowsWaves = 8, kRowsThreads = 64 * kRowsWaves, kRowsCT = 128 / (16 * kRowsWaves);
 
 // Split-f16 forward (F16): the slab holds every input value v as v = hi + lo, hi = fp16(v), lo =
-// fp16(v - hi), per 8-channel octet q of a row as [hi x 8][lo x 8] at dwords 8q .. 8q+7 (the row
-// pitch is unchanged: 16 bytes of halves per 4 channels, as the f32 slab). |v| must stay below the
-// fp16 range (65504), which the fp16 track table bounds for layer 1; BatchNorm keeps the others O(1).
+// fp16(v - hi); a row is [hi x KC][lo x KC] halves (channel c's hi at dword c/2, its lo KC/2 dwords
+// further; the pitch is unchanged, KC + 8 dwords). A lane's 8 channels of a 32-channel chunk are
+// then 4 dwords at 4g, as in the f32 slab, so the ds_read_b128 lane groups stay conflict-free (an
+// interleaved [hi x 8][lo x 8] octet layout put them 8g apart: 2-way on every read, measured 53 % of
+// the LDS cycles). |v| must stay below the fp16 range (65504), which the fp16 track table bounds
+// for layer 1; BatchNorm keeps the others O(1).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
+template <int KC>
 __device__ __forceinline__ void st_split(float* row, int c, float4 v) {
   const f16x4 h = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
   const f16x4 l = {(_Float16)(v.x - (float)h[0]), (_Float16)(v.y - (float)h[1]),
                    (_Float16)(v.z - (float)h[2]), (_Float16)(v.w - (float)h[3])};
-  const int o = 8 * (c >> 3) + 2 * ((c >> 2) & 1);
-  *reinterpret_cast<f16x4*>(row + o) = h;
-  *reinterpret_cast<f16x4*>(row + o + 4) = l;
+  *reinterpret_cast<f16x4*>(row + c / 2) = h;
+  *reinterpret_cast<f16x4*>(row + KC / 2 + c / 2) = l;
 }
 // B k-steps (float4 per lane per 16-column tile) requested ahead of the MFMAs by one-tile workgroups
 // (the small layers at in-batch M): a layer's whole K at H = 128 (32 steps), so they wait on the
@@ -276,7 +279,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
         if (e < nfill) {
           const float4 v = slab_finish<SRC, POOLL>(a, kop, pp[j], raw[j]);
           if constexpr (F16)
-            st_split(&slab[(e / C4) * PITCH], c, ok[j] ? v : make_float4(0.f, 0.f, 0.f, 0.f));
+            st_split<KC>(&slab[(e / C4) * PITCH], c, ok[j] ? v : make_float4(0.f, 0.f, 0.f, 0.f));
           else
             st4(&slab[(e / C4) * PITCH + c], ok[j] ? v : make_float4(0.f, 0.f, 0.f, 0.f));
         }
@@ -333,12 +336,12 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
       // (223 VGPRs, one workgroup per CU, no fill/MFMA overlap between workgroups)
       __builtin_amdgcn_sched_barrier(0);
       const int k = ch / (KC / 32);
-      const int aoff = k * PITCH + 32 * (ch - k * (KC / 32)) + 4 * g;  // sbase holds 4g: octet g is 8g
+      const int aoff = k * PITCH + 16 * (ch - k * (KC / 32));  // + sbase's 4g: the lane's 8 channels
       f16x8 ah[TW], al[TW];
 #pragma unroll
       for (int r = 0; r < TW; ++r) {
         ah[r] = *reinterpret_cast<const f16x8*>(&slab[sbase[r] + aoff]);
-        al[r] = *reinterpret_cast<const f16x8*>(&slab[sbase[r] + aoff + 4]);
+        al[r] = *reinterpret_cast<const f16x8*>(&slab[sbase[r] + aoff + KC / 2]);
       }
 #pragma unroll
       for (int r = 0; r < TW; ++r)
