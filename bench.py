@@ -37,6 +37,10 @@ import torch.distributed as dist  # noqa: E402
 
 F32_PEAK_TFLOPS = 157.3   # MI355X dense FP32 (matrix and vector), MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
+F16_PEAK_TFLOPS = 2500.0  # MI355X dense FP16/BF16 MFMA (no sparsity), MI355X_MICROARCH.md
+# conv forwards run on split-f16 MFMA (three f16 products per f32 product) unless DCUE_CONV_F16=0
+CONV_F16 = os.environ.get("DCUE_CONV_F16", "1")[:1] != "0"
+
 
 
 def parse():
@@ -420,7 +424,10 @@ def main():
         rows_slice = n_users_local / args.flush_every
         spec = {
             nat.TIMED_CONV1_WGRAD: ("k_conv1_wgrad (conv-1 weight gradient, f32 MFMA 32x32x2)", "mfma", conv1),
-            nat.TIMED_CONV1_FWD: ("k_conv_rows<0,0> layer 1 (conv-1 forward + pool + BN partials, f32 MFMA)",
+            nat.TIMED_CONV1_FWD: (("k_conv_rows<0,0> layer 1 (conv-1 forward + pool + BN partials, split-f16 "
+                                   "MFMA 16x16x32: three f16 products per f32 product; peak = f16 dense peak / 3)")
+                                  if CONV_F16 else
+                                  "k_conv_rows<0,0> layer 1 (conv-1 forward + pool + BN partials, f32 MFMA)",
                                   "mfma", conv1),
             nat.TIMED_EMB_SLICE: ("k_emb_flush_rows (deferred user-table Adam, one rolling slice; user "
                                   "stream, beside the item tower: its duration includes waiting behind the "
@@ -438,9 +445,11 @@ def main():
             ent = {"kernel": name, "bound": bound, "avg_ms": avg, "launches_timed": n,
                    "ms_per_step": avg * per_step, "critical_path": k != nat.TIMED_EMB_SLICE}
             if bound == "mfma":
-                ent.update(achieved=work / (avg * 1e-3) / 1e12, peak=F32_PEAK_TFLOPS, unit="TFLOP/s",
-                           algorithmic_flops=work)
-                ent["frac"] = ent["achieved"] / F32_PEAK_TFLOPS
+                split = k == nat.TIMED_CONV1_FWD and CONV_F16
+                peak = F16_PEAK_TFLOPS / 3.0 if split else F32_PEAK_TFLOPS
+                ent.update(achieved=work / (avg * 1e-3) / 1e12, peak=peak,
+                           unit="TFLOP/s (f32-equivalent)" if split else "TFLOP/s", algorithmic_flops=work)
+                ent["frac"] = ent["achieved"] / peak
             elif bound == "hbm":
                 ent.update(achieved=work / (avg * 1e-3) / 1e9, peak=HBM_PEAK_GBS, unit="GB/s",
                            algorithmic_bytes=work)
@@ -594,7 +603,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32 (conv forwards: f32 values as split fp16 hi+lo pairs on f16 MFMA, f32 accumulate)"
+                 if CONV_F16 else "f32",
         "data": "synthetic",
         "rows_per_s": head["rows_per_s"],
         "auc_val": None,
