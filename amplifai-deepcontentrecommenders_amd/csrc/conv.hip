@@ -1248,8 +1248,15 @@ int wgrad_nchunk(int layer, int M, int cout, int cin) {
   const LayerGeom gm = layer_geom(layer);
   const long rows = (long)M * gm.lp * gm.pool;
   if (layer == 1) {  // k_conv1_wgrad: 64x64 tiles, >= 4 steps per chunk, <= ~512 workgroups (2 per CU)
+    // tuning diagnostic: DCUE_W1_CHUNKS=n caps the split-K chunk count (A/B runs; the workspace is
+    // sized through this same function, so it follows)
+    static const long forced = [] {
+      const char* e = getenv("DCUE_W1_CHUNKS");
+      const long v = e ? atol(e) : 0;
+      return v >= 1 && v <= 64 ? v : 0L;
+    }();
     const long tiles1 = (4L * kMels / kW1Tile) * ((cout + kW1Tile - 1) / kW1Tile);
-    long n = 512 / tiles1;
+    long n = forced ? forced : 512 / tiles1;
     const long wins = (long)M * gm.lp;
     if (n > (wins + 4 * kW1Win - 1) / (4 * kW1Win)) n = (wins + 4 * kW1Win - 1) / (4 * kW1Win);
     return (int)(n < 1 ? 1 : n);
