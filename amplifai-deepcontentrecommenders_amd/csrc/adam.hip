@@ -483,7 +483,7 @@ __global__ void k_pack(const float* __restrict__ params, float* wpack, PackArgs 
 }
 
 PackArgs pack_args(const dcue_model* md, const int64_t* poff) {
-  const int H = md->dims.conv_hidden, d = md->dims.feature_dim;
+  const int H = st_hidden(&md->dims), d = st_feature(&md->dims);
   const WpackLayout wl = wpack_layout(&md->dims);
   PackArgs pa;
   for (int l = 1; l <= 5; ++l) {

@@ -118,14 +118,12 @@ namespace {
 
 constexpr int kSeg = DCUE_N_DENSE_SEGMENTS;
 
-bool pow2_32_256(int v) { return v == 32 || v == 64 || v == 128 || v == 256; }
-
 int check_dims(const dcue_dims* d) {
   if (!d) return DCUE_ERR_INVALID;
   if (d->conv_hidden <= 0 || d->feature_dim <= 0 || d->user_embdim <= 0 || d->n_users < 0)
     return DCUE_ERR_INVALID;
-  if (!pow2_32_256(d->conv_hidden) || !pow2_32_256(d->feature_dim) || d->user_embdim > 1024)
-    return DCUE_ERR_UNSUPPORTED;
+  // any width up to 256 (run at its storage width, dcue_common.h); the user tower's E up to 1024
+  if (d->conv_hidden > 256 || d->feature_dim > 256 || d->user_embdim > 1024) return DCUE_ERR_UNSUPPORTED;
   if (d->tower < DCUE_TOWER_BN || d->tower > DCUE_TOWER_RESBN) return DCUE_ERR_INVALID;
   return DCUE_OK;
 }
@@ -133,7 +131,7 @@ int check_dims(const dcue_dims* d) {
 long al4(long v) { return (v + 3) & ~3L; }
 
 void param_sizes(const dcue_dims* d, long* sz) {
-  const long H = d->conv_hidden, D = d->feature_dim, E = d->user_embdim;
+  const long H = st_hidden(d), D = st_feature(d), E = d->user_embdim;
   const long cin[5] = {kMels, H, H, H, H}, cout[5] = {H, H, H, H, D};
   const long bn = tower_has_bn(d) ? 1 : 0;  // the BN parameters' segments are empty without BN
   int s = 0;
@@ -165,7 +163,7 @@ void param_offsets(const dcue_dims* d, int64_t* off) {
 }
 
 int bn_channels(const dcue_dims* d, int l) {
-  return l == 0 ? kMels : l == 5 ? d->feature_dim : d->conv_hidden;
+  return l == 0 ? kMels : l == 5 ? st_feature(d) : st_hidden(d);
 }
 
 void bn_offsets(const dcue_dims* d, int64_t* off) {
@@ -220,7 +218,7 @@ void rebase_acc(Ws* w, unsigned long long* acc) {
 
 size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   Arena ar{(char*)base, 0, 0};
-  const int H = d->conv_hidden, D = d->feature_dim, E = d->user_embdim;
+  const int H = st_hidden(d), D = st_feature(d), E = d->user_embdim;
   const int Cmax = H > kMels ? H : kMels;
   w->counts = ar.take<float>(M);
   for (int l = 0; l < 6; ++l) {
@@ -287,7 +285,7 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   }
   if (tower_res(d)) {
     w->xfc = ar.take<float>((long)M * fc_in(d));
-    w->dtp = ar.take<float>((long)M * 4 * H);
+    w->dtp = ar.take<float>((long)M * 4 * d->conv_hidden);  // the fc input's block columns: reference H
   }
   return ar.used + 256;
 }
@@ -300,7 +298,8 @@ struct Ctx {
   const dcue_model* m;
   int64_t poff[kSeg + 1];
   int64_t boff[2 * DCUE_N_BN + 1];
-  int H, D, E;
+  int H, D, E;   // storage widths (H, d padded to 32/64/128/256) and E
+  int HL;        // the reference's conv_hidden: column width of the res towers' time-pooled blocks
   bool bn, res;  // tower variant (dcue_dims.tower)
   int FI;        // fc input width: D, or 4H + D in the res towers
   const float* P(int seg) const { return m->params + poff[seg]; }
@@ -336,8 +335,9 @@ int init_ctx(Ctx* c, const dcue_model* m) {
   c->m = m;
   param_offsets(&m->dims, c->poff);
   bn_offsets(&m->dims, c->boff);
-  c->H = m->dims.conv_hidden;
-  c->D = m->dims.feature_dim;
+  c->H = st_hidden(&m->dims);
+  c->D = st_feature(&m->dims);
+  c->HL = m->dims.conv_hidden;
   c->E = m->dims.user_embdim;
   c->bn = tower_has_bn(&m->dims);
   c->res = tower_res(&m->dims);
@@ -407,7 +407,7 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
   if (c.res) {  // fc on [tp1, tp2, tp3, tp4, bn5(y5)] (truedcuemel1dres.py:93-97)
     TRY(launch_timepool(w.y, w.mean, w.a, c.bn ? c.P(seg_bn_b(1)) : nullptr, c.bn ? c.P(seg_bn_b(2)) : nullptr,
                         c.bn ? c.P(seg_bn_b(3)) : nullptr, c.bn ? c.P(seg_bn_b(4)) : nullptr,
-                        c.bn ? c.P(seg_bn_b(5)) : nullptr, bn_of(5), M, c.H, c.D, w.xfc, s));
+                        c.bn ? c.P(seg_bn_b(5)) : nullptr, bn_of(5), M, c.H, c.HL, c.D, w.xfc, s));
     TGemmArgs g = {};
     g.M = M; g.N = c.D; g.K = c.FI;
     g.A = w.xfc; g.sam = c.FI; g.sak = 1;
@@ -466,6 +466,15 @@ int check_batch(const dcue_batch* b) {
 extern "C" {
 
 int dcue_abi_version(void) { return DCUE_ABI_VERSION; }
+
+int dcue_storage_dims(const dcue_dims* dims, dcue_dims* storage_host) {
+  TRY(check_dims(dims));
+  if (!storage_host) return DCUE_ERR_INVALID;
+  *storage_host = *dims;
+  storage_host->conv_hidden = st_hidden(dims);
+  storage_host->feature_dim = st_feature(dims);
+  return DCUE_OK;
+}
 
 int dcue_param_layout(const dcue_dims* dims, int64_t* offsets_host) {
   TRY(check_dims(dims));
@@ -538,7 +547,7 @@ int dcue_forward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   Ws w;
   carve(&m->dims, b->n_rows, b->n_neg, b->n_items, ws, &w);
   hipStream_t s = (hipStream_t)stream;
-  const int B = b->n_rows, N = b->n_neg, M = b->n_items, D = m->dims.feature_dim;
+  const int B = b->n_rows, N = b->n_neg, M = b->n_items, D = st_feature(&m->dims);
   if (scores && N > 0) DCUE_HIP_CHECK(hipMemcpyAsync(scores, w.scores, sizeof(float) * B * N, hipMemcpyDeviceToDevice, s));
   if (user_feat) DCUE_HIP_CHECK(hipMemcpyAsync(user_feat, w.uf, sizeof(float) * B * D, hipMemcpyDeviceToDevice, s));
   if (item_feat) DCUE_HIP_CHECK(hipMemcpyAsync(item_feat, w.f, sizeof(float) * (size_t)M * D, hipMemcpyDeviceToDevice, s));
@@ -707,15 +716,15 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TGemmArgs g = {};
     g.M = M; g.N = D; g.K = D;
     g.A = w.df; g.sam = D; g.sak = 1;
-    g.B = c.P(SEG_FC_W) + 4 * H; g.sbk = c.FI; g.sbn = 1;
+    g.B = c.P(SEG_FC_W) + 4 * c.HL; g.sbk = c.FI; g.sbn = 1;
     g.C = w.g[5]; g.scm = D; g.scn = 1;
     g.colacc = bn_acc(w.bnbacc, w.cmax, 5); g.xy = w.y[5]; g.xmean = w.mean[5]; g.xinvstd = w.invstd[5];
     TRY(launch_tgemm(0, 0, g, s));
     g = TGemmArgs{};
-    g.M = M; g.N = 4 * H; g.K = D;
+    g.M = M; g.N = 4 * c.HL; g.K = D;
     g.A = w.df; g.sam = D; g.sak = 1;
     g.B = c.P(SEG_FC_W); g.sbk = c.FI; g.sbn = 1;
-    g.C = w.dtp; g.scm = 4 * H; g.scn = 1;
+    g.C = w.dtp; g.scm = 4 * c.HL; g.scn = 1;
     ForkAfter fk(sp, s, &ev_layer[5]);
     TRY(launch_tgemm(0, 0, g, s));
     TRY(fk.done());
@@ -734,8 +743,9 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     ra.invN = c.bn ? (float)(1.0 / (copies * gm.lp)) : 0.f;  // 0: BN backward is the identity
     ra.counts = w.counts;
     if (c.res) {  // + d tp_{l-1} / Lp_{l-1} at every position of block l-1 (AvgPool1d backward)
-      ra.skip = w.dtp + (l - 2) * H;
-      ra.skip_ld = 4 * H;
+      ra.skip = w.dtp + (l - 2) * c.HL;
+      ra.skip_ld = 4 * c.HL;
+      ra.skip_n = c.HL;  // storage channels past the reference's H get no skip gradient
       ra.skip_scale = 1.0f / (float)layer_geom(l - 1).lp;
     }
     ra.wpack = m->wpack + wpack_offset(&m->dims, l, true);

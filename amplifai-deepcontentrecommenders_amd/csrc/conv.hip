@@ -406,7 +406,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
         for (int j = 0; j < 4; ++j)
           if (grb + j < total) {
             float gv = acc[r][ct][j];
-            if (a.skip) gv += a.skip[((grb + j) / R) * a.skip_ld + o] * a.skip_scale;
+            if (a.skip && o < a.skip_n) gv += a.skip[((grb + j) / R) * a.skip_ld + o] * a.skip_scale;
             a.out[(grb + j) * nout + o] = gv;
             sg[ct] += gv;
             sgx[ct] += gv * ((yv[j] - mu) * is);

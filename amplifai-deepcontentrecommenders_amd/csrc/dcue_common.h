@@ -68,9 +68,21 @@ __host__ __device__ inline bool tower_has_bn(const dcue_dims* d) {
 __host__ __device__ inline bool tower_res(const dcue_dims* d) {
   return d->tower == DCUE_TOWER_RES || d->tower == DCUE_TOWER_RESBN;
 }
-// fc input width: d, or 4H + d with the four time-pooled block outputs (truedcuemel1dres.py:63-64)
+// Storage widths. The reference accepts any conv_hidden / feature_dim (dcue/dcue.py:39-47; its
+// trainer's default is feature_dim = 100, nn/dcue.py:44). The kernels run at the width rounded up to
+// 32, 64, 128 or 256 channels (their MFMA tiles and slab layouts), and the extra channels are
+// zero-padded in every parameter that has them: zero weights, bias, BN gamma and beta give those
+// channels exactly zero activations, features and gradients, so Adam keeps them zero for good and
+// the real channels compute what the unpadded model does. The reference-shaped parameters are
+// strided views of the padded segments (dcue_storage_dims).
+__host__ __device__ inline int storage_width(int v) { return v <= 32 ? 32 : v <= 64 ? 64 : v <= 128 ? 128 : 256; }
+__host__ __device__ inline int st_hidden(const dcue_dims* d) { return storage_width(d->conv_hidden); }
+__host__ __device__ inline int st_feature(const dcue_dims* d) { return storage_width(d->feature_dim); }
+// fc input width: d, or 4H + d with the four time-pooled block outputs (truedcuemel1dres.py:63-64).
+// The time-pooled blocks keep the reference's H columns each (the fc weight is then a view of its
+// padded [d_s][4H + d_s] segment); only the block-5 part is padded.
 __host__ __device__ inline int fc_in(const dcue_dims* d) {
-  return tower_res(d) ? 4 * d->conv_hidden + d->feature_dim : d->feature_dim;
+  return tower_res(d) ? 4 * d->conv_hidden + st_feature(d) : st_feature(d);
 }
 
 // Per-layer geometry of the default item tower (truedcuemel1dbn.py:25-61).

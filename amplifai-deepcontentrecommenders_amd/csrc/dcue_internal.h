@@ -67,6 +67,7 @@ struct RowsArgs {
   const float* skip;
   int skip_ld;
   float skip_scale;
+  int skip_n;  // channels o < skip_n carry a skip gradient (the reference's H; storage pads none)
 };
 
 struct WgradArgs {
@@ -142,7 +143,7 @@ struct WpackLayout {
 };
 inline WpackLayout wpack_layout(const dcue_dims* dm) {
   WpackLayout w = {};
-  const long H = dm->conv_hidden, D = dm->feature_dim;
+  const long H = st_hidden(dm), D = st_feature(dm);
   long n = 0;
   for (int l = 1; l <= 5; ++l) {
     const long cin = l == 1 ? kMels : H, cout = l == 5 ? D : H;
@@ -231,9 +232,10 @@ int launch_bn_identity(float* const* mean, float* const* invstd, float* const* a
                        int cmax, int H, int D, hipStream_t s);
 // res towers: xfc[i] = [mean_t bn_1(y_1), ..., mean_t bn_4(y_4), bn_5(y_5)] (truedcuemel1dres.py:93-97);
 // p5 (train, BN): BN_5 finalized from its accumulators here (block 0 publishes it)
+// H: storage width of y_1..y_4; HL: the reference's H, the column width of each block in xfc
 int launch_timepool(float* const* y, float* const* mean, float* const* a, const float* beta1, const float* beta2,
                     const float* beta3, const float* beta4, const float* beta5, const BnPublish& p5, int M, int H,
-                    int D, float* xfc, hipStream_t s);
+                    int HL, int D, float* xfc, hipStream_t s);
 // SGD / Ranger over the dense buffer and the user table (optim.hip)
 int launch_opt(const dcue_model* m, const dcue_opt_args* a, const dcue_opt_state* st, long n_dense,
                hipStream_t s);

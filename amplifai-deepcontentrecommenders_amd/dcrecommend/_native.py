@@ -98,13 +98,14 @@ class PlanConfig(ctypes.Structure):
 
 MT_STATE_BYTES = 624 * 4 + 16
 MAX_LOG_CAP = 256
-ABI_VERSION = 8
+ABI_VERSION = 9
 RANK_SPLIT, RANK_SINGLE = 0, 1
 
 _P = ctypes.c_void_p
 _SIGS = {
     "dcue_abi_version": ([], ctypes.c_int),
     "dcue_last_error": ([], ctypes.c_char_p),
+    "dcue_storage_dims": ([ctypes.POINTER(Dims), ctypes.POINTER(Dims)], ctypes.c_int),
     "dcue_param_layout": ([ctypes.POINTER(Dims), _P], ctypes.c_int),
     "dcue_bn_layout": ([ctypes.POINTER(Dims), _P], ctypes.c_int),
     "dcue_wpack_floats": ([ctypes.POINTER(Dims), _P], ctypes.c_int),
@@ -208,6 +209,38 @@ TOWERS = {"truedcuemel1dbn": 0, "truedcuemel1d": 1, "truedcuemel1dres": 2, "true
 
 def make_dims(conv_hidden, feature_dim, user_embdim, n_users, model_type="truedcuemel1dbn"):
     return Dims(conv_hidden, feature_dim, user_embdim, TOWERS[model_type], n_users)
+
+
+def storage_dims(dims):
+    """The widths the library stores and computes at (H, d rounded up to 32/64/128/256)."""
+    out = Dims()
+    check(lib().dcue_storage_dims(ctypes.byref(dims), ctypes.byref(out)), "dcue_storage_dims")
+    return out
+
+
+def segment_shapes(dims):
+    """Storage shape of each dense segment (DENSE_NAMES order) for the storage widths of `dims`;
+    the reference-shaped parameter is the leading corner of it (include/dcue.h, dcue_storage_dims)."""
+    sd = storage_dims(dims)
+    Hs, Ds, E, H = sd.conv_hidden, sd.feature_dim, sd.user_embdim, dims.conv_hidden
+    res = dims.tower in (TOWERS["truedcuemel1dres"], TOWERS["truedcuemel1dresbn"])
+    cin = [N_MELS, Hs, Hs, Hs, Hs]
+    cout = [Hs, Hs, Hs, Hs, Ds]
+    ks = [4, 4, 4, 2, 1]
+    shapes = [(N_MELS,), (N_MELS,)]
+    for l in range(5):
+        shapes += [(cout[l], cin[l], ks[l]), (cout[l],), (cout[l],), (cout[l],)]
+    shapes += [(Ds, 4 * H + Ds if res else Ds), (Ds,), (E, E), (E,), (Ds, E), (Ds,)]
+    return shapes
+
+
+def corner(buf, off, storage_shape, shape):
+    """View of the reference-shaped corner `shape` of the segment at `off` with `storage_shape`."""
+    n = 1
+    for v in storage_shape:
+        n *= v
+    seg = buf[off:off + n].view(storage_shape)
+    return seg[tuple(slice(0, v) for v in shape)]
 
 
 def param_layout(dims):

@@ -133,16 +133,18 @@ class DCUENet(nn.Module):
                              self.model_type)
         poff = nat.param_layout(dims)
         boff = nat.bn_layout(dims)
+        shapes = nat.segment_shapes(dims)
         named = dict(self.named_parameters())
+        # zero-filled: the storage channels past the reference's H / d stay exactly zero (dcue.h)
         P = torch.zeros(poff[-1], dtype=torch.float32, device=device)
         G = torch.zeros_like(P)
         for s, name in enumerate(nat.DENSE_NAMES):
             if name not in named:  # BN parameters of a tower without BatchNorm: empty segment
                 continue
             p = named[name]
-            n = p.numel()
-            P[poff[s]:poff[s] + n].copy_(p.data.reshape(-1))
-            p.data = P[poff[s]:poff[s] + n].view(p.shape)
+            view = nat.corner(P, poff[s], shapes[s], p.shape)
+            view.copy_(p.data)
+            p.data = view
             p._dcue_owner = weakref.ref(self)
         stats = torch.zeros(boff[-1], dtype=torch.float32, device=device)
         nbt = torch.zeros(nat.N_BN, dtype=torch.int64, device=device)
@@ -161,11 +163,12 @@ class DCUENet(nn.Module):
         emb._dcue_owner = weakref.ref(self)
         slot = torch.full((max(self.user_count, 1),), -1, dtype=torch.int32, device=device)
         wpack = torch.empty(nat.wpack_floats(dims), dtype=torch.float32, device=device)
-        self._flat = dict(dims=dims, poff=poff, boff=boff, P=P, G=G, stats=stats, nbt=nbt, slot=slot,
+        self._flat = dict(dims=dims, poff=poff, boff=boff, shapes=shapes, P=P, G=G, stats=stats, nbt=nbt, slot=slot,
                           wpack=wpack, emb_grad=torch.zeros(0, device=device),
                           emb_rows=torch.zeros(0, dtype=torch.int64, device=device), m=None, v=None,
                           em=None, ev=None)
         self._ws = None
+        self._ds = nat.storage_dims(dims).feature_dim
         self._repack()
 
     def _repack(self):
@@ -278,12 +281,12 @@ class DCUENet(nn.Module):
         if fl.get("out_key") != key:
             fl["out_off"], fl["out_key"] = nat.workspace_outputs(fl["dims"], B, n_neg, M), key
         off = fl["out_off"]
-        d = self.feature_dim
+        d, ds = self.feature_dim, self._ds  # feature rows are stored d_s wide, zero past d
 
         def view(o, n, shape):
             return ws[o:o + 4 * n].view(torch.float32).view(shape)
-        outs = (view(off[0], B * n_neg, (B, n_neg)), view(off[1], B * d, (B, d)),
-                view(off[2], M * d, (M, d)), view(off[3], 1, ()))
+        outs = (view(off[0], B * n_neg, (B, n_neg)), view(off[1], B * ds, (B, ds))[:, :d],
+                view(off[2], M * ds, (M, ds))[:, :d], view(off[3], 1, ()))
         return tuple(o.clone() for o in outs) if copy_outputs else outs
 
     def native_backward(self, dscores=None, emb_grad_scale=1.0):
@@ -303,13 +306,17 @@ class DCUENet(nn.Module):
                   "dcue_train_backward")
         # expose reference-shaped .grad views of the flat gradient (the user table's gradient is
         # kept compact: embedding_grad_dense() materialises it on request)
+        self._expose_grads()
+        self.user_embd.embeddings.weight.grad = None
+        self._grad_users = users
+
+    def _expose_grads(self):
+        fl = self._flat
         named = dict(self.named_parameters())
         for s, name in enumerate(nat.DENSE_NAMES):
             p = named.get(name)
             if p is not None:
-                p.grad = fl["G"][fl["poff"][s]:fl["poff"][s] + p.numel()].view(p.shape)
-        self.user_embd.embeddings.weight.grad = None
-        self._grad_users = users
+                p.grad = nat.corner(fl["G"], fl["poff"][s], fl["shapes"][s], p.shape)
 
     def embedding_grad_dense(self):
         """Dense [n_users, E] view of the last backward's embedding gradient (for inspection)."""
@@ -338,7 +345,7 @@ class DCUENet(nn.Module):
         fl = self._require_device()
         table = self._spectro_table(X)
         M = table.shape[0]
-        out = torch.empty((M, self.feature_dim), dtype=torch.float32, device=table.device)
+        out = torch.empty((M, self._ds), dtype=torch.float32, device=table.device)
         if self.training:
             raise NotImplementedError("DCUENet.conv(X) in train mode is only reachable through forward()")
         ws = self._workspace(1, 0, M)
@@ -347,19 +354,19 @@ class DCUENet(nn.Module):
         nat.check(nat.lib().dcue_item_tower_eval(ctypes.byref(self._model_struct()), ctypes.byref(tr),
                                                  nat.ptr(item_track), M, nat.ptr(ws), ws.numel(),
                                                  nat.ptr(out), nat.stream_handle()), "dcue_item_tower_eval")
-        return out.squeeze()
+        return out[:, :self.feature_dim].squeeze()
 
     def user_features(self, user_idx):
         self._require_device()
         nat.require_gpu(user_idx, "user_idx")
         shape = tuple(user_idx.shape)
         u = user_idx.reshape(-1).to(torch.int64).contiguous()
-        out = torch.empty((u.shape[0], self.feature_dim), dtype=torch.float32, device=u.device)
+        out = torch.empty((u.shape[0], self._ds), dtype=torch.float32, device=u.device)
         ws = self._workspace(u.shape[0], 0, 1)
         nat.check(nat.lib().dcue_user_tower(ctypes.byref(self._model_struct()), nat.ptr(u), u.shape[0],
                                             nat.ptr(ws), ws.numel(), nat.ptr(out), nat.stream_handle()),
                   "dcue_user_tower")
-        return out.view(*shape, self.feature_dim)
+        return out[:, :self.feature_dim].reshape(*shape, self.feature_dim)
 
     def forward(self, u, pos, neg=None):
         """dcue/dcue.py:70-108 -> (scores [B,N], user feats [B,d], pos feats [B,d], neg feats [B,N,d])."""
@@ -375,4 +382,4 @@ class DCUENet(nn.Module):
             scores, uf, f = _StepFunction.apply(self._anchor, self, u, X, N)
         else:
             scores, uf, f, _ = self._native_forward(u, X, N, train=self.training, margin=0.0)
-        return scores, uf, f[:B], f[B:].view(B, N, self.feature_dim)
+        return scores, uf, f[:B], f[B:].reshape(B, N, self.feature_dim)

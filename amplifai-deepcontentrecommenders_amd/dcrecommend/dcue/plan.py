@@ -69,11 +69,7 @@ class TrainPlan:
         # asynchronously (the caching allocator must not hand their memory out meanwhile)
         self._hold = collections.deque(maxlen=4)
         # the replayed backward writes the flat gradient: expose the reference-shaped .grad views
-        named = dict(net.named_parameters())
-        for s, name in enumerate(nat.DENSE_NAMES):
-            p = named.get(name)
-            if p is not None:
-                p.grad = fl["G"][fl["poff"][s]:fl["poff"][s] + p.numel()].view(p.shape)
+        net._expose_grads()
         net.user_embd.embeddings.weight.grad = None
         net._grad_users = self.users
         # check mode (dcrecommend.check): ids validated before each step, loss/params/grads after

@@ -398,7 +398,9 @@ class DCUE(Trainer):
         self.user_factors = torch.zeros([self.n_users, self.feature_dim], device=self.device)
         idx = torch.as_tensor(np.fromiter(item_data.user_index.values(), dtype=np.int64)).to(self.device)
         step = 65536
-        feat = torch.empty((min(step, max(idx.numel(), 1)), self.feature_dim), device=self.device)
+        # the towers write rows at the storage width d_s (zero past d; include/dcue.h)
+        ds = nat.storage_dims(self.model._flat["dims"]).feature_dim
+        feat = torch.empty((min(step, max(idx.numel(), 1)), ds), device=self.device)
         model = self.model._model_struct()
         for s in range(0, idx.numel(), step):
             part = idx[s:s + step].contiguous()
@@ -406,7 +408,7 @@ class DCUE(Trainer):
             ws = self._factor_ws(n, 1)
             nat.check(nat.lib().dcue_user_tower(ctypes.byref(model), nat.ptr(part), n, nat.ptr(ws), ws.numel(),
                                                 nat.ptr(feat), nat.stream_handle()), "dcue_user_tower")
-            self.user_factors.index_copy_(0, part, feat[:n])
+            self.user_factors.index_copy_(0, part, feat[:n, :self.feature_dim])
 
     def _factor_ws(self, rows, items):
         """Workspace of the factor passes, apart from the model's (a TrainPlan binds that one)."""
@@ -434,7 +436,8 @@ class DCUE(Trainer):
         items = np.nonzero(self._item_meta >= 0)[0].astype(np.int32)
         if len(items):
             step = 8192
-            feat = torch.empty((min(step, len(items)), self.feature_dim), device=self.device)
+            ds = nat.storage_dims(self.model._flat["dims"]).feature_dim
+            feat = torch.empty((min(step, len(items)), ds), device=self.device)
             tr = nat.Tracks(self._tracks.data_ptr(), self._tracks.shape[0],
                             0 if self._tracks.dtype == torch.float16 else 1, 0)
             model = self.model._model_struct()
@@ -446,7 +449,7 @@ class DCUE(Trainer):
                                                          nat.ptr(ws), ws.numel(), nat.ptr(feat), nat.stream_handle()),
                           "dcue_item_tower_eval")
                 rows = torch.from_numpy(self._item_meta[items[s:s + step]]).to(self.device)
-                out.index_copy_(0, rows, feat[:n])
+                out.index_copy_(0, rows, feat[:n, :self.feature_dim])
             nat.check(nat.lib().dcue_factor_repeat_mean(nat.ptr(out), out.numel(), int(n_iter), nat.stream_handle()),
                       "dcue_factor_repeat_mean")
         return out

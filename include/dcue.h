@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DCUE_ABI_VERSION 8
+#define DCUE_ABI_VERSION 9
 #define DCUE_N_MELS 128
 #define DCUE_N_FRAMES 131
 #define DCUE_N_BN 6
@@ -37,7 +37,7 @@ extern "C" {
 typedef enum {
   DCUE_OK = 0,
   DCUE_ERR_INVALID = 1,     /* bad argument (null pointer, size out of range) */
-  DCUE_ERR_UNSUPPORTED = 2, /* valid for the reference, not (yet) for this build (e.g. d % 32 != 0) */
+  DCUE_ERR_UNSUPPORTED = 2, /* valid for the reference, not for this build (e.g. d > 256) */
   DCUE_ERR_HIP = 3,         /* a HIP launch failed */
   DCUE_ERR_WORKSPACE = 4    /* workspace too small */
 } dcue_status;
@@ -55,8 +55,8 @@ typedef enum {
 #define DCUE_TOWER_RESBN 3
 
 typedef struct dcue_dims {
-  int32_t conv_hidden; /* H: nn/dcue.py:45 conv_hidden (multiple of 32, <= 256) */
-  int32_t feature_dim; /* d: feature_dim (multiple of 32, <= 256) */
+  int32_t conv_hidden; /* H: nn/dcue.py:45 conv_hidden (1..256; stored padded, dcue_storage_dims) */
+  int32_t feature_dim; /* d: feature_dim (1..256; the trainer's default is 100, nn/dcue.py:44) */
   int32_t user_embdim; /* E: u_embdim (<= 1024) */
   int32_t tower;       /* DCUE_TOWER_* */
   int64_t n_users;     /* rows of the (local shard of the) user table */
@@ -148,7 +148,17 @@ typedef struct dcue_adam_args {
 int dcue_abi_version(void);
 /* The HIP call behind the most recent DCUE_ERR_HIP (file:line, call, HIP error), "" if none. */
 const char* dcue_last_error(void);
-/* offsets[DCUE_N_DENSE_SEGMENTS+1] (floats) of each dense parameter in `params` */
+/* Storage widths. Any conv_hidden / feature_dim in 1..256 is accepted (DCUENet takes any,
+ * dcue/dcue.py:39-47). The library stores and computes them at the width rounded up to 32, 64, 128
+ * or 256: every dense segment below is laid out for the storage dims (e.g. conv.layer5.weight is
+ * [d_s][H_s][1], conv.fc.weight [d_s][d_s], or [d_s][4H + d_s] in the res towers, whose four
+ * time-pooled blocks keep H columns each), and the reference-shaped parameter is the leading
+ * [:d, :H, ...] corner of its segment. The caller zero-fills everything outside those corners
+ * (weights, biases, BN gamma/beta and running statistics); the padded channels then carry exact
+ * zeros through forward, backward and every optimizer, so they never leave zero and the corners
+ * compute the reference model. Item / user feature outputs are [.][d_s] rows, zero past d. */
+int dcue_storage_dims(const dcue_dims* dims, dcue_dims* storage_host);
+/* offsets[DCUE_N_DENSE_SEGMENTS+1] (floats) of each dense parameter in `params` (storage dims) */
 int dcue_param_layout(const dcue_dims* dims, int64_t* offsets_host);
 /* offsets[2*DCUE_N_BN+1]: running_mean(l), running_var(l) for l = 0..5 */
 int dcue_bn_layout(const dcue_dims* dims, int64_t* offsets_host);
@@ -156,14 +166,14 @@ int dcue_wpack_floats(const dcue_dims* dims, int64_t* n_floats_host);
 int dcue_workspace_bytes(const dcue_dims* dims, int32_t max_rows, int32_t max_neg,
                          int32_t max_items, size_t* bytes_host);
 /* Byte offsets inside a workspace carved for (B, N, M) of the forward outputs a train/eval
- * dcue_forward leaves there: [0] scores [B][N], [1] user feats [B][d], [2] item feats [M][d],
+ * dcue_forward leaves there: [0] scores [B][N], [1] user feats [B][d_s], [2] item feats [M][d_s],
  * [3] loss (one float). Valid until the next call on the same workspace. */
 int dcue_workspace_outputs(const dcue_dims* dims, int32_t B, int32_t N, int32_t M,
                            size_t* offsets_host);
 /* Inspection (tests): byte offsets of the train forward's per-layer activations in the same
  * workspace. offsets[2(l-1)] = y_l, float [M][Lp_l][C_l] = relu(max-pooled conv + bias), before
  * BN; offsets[2(l-1)+1] = its uint8 [M][Lp_l][C_l] window argmax (0..pool-1, first maximum), for
- * conv layers l = 1..5 (Lp = 33, 8, 2, 1, 1; C = H, H, H, H, d). */
+ * conv layers l = 1..5 (Lp = 33, 8, 2, 1, 1; C = H_s, H_s, H_s, H_s, d_s: storage widths). */
 int dcue_workspace_activations(const dcue_dims* dims, int32_t B, int32_t N, int32_t M,
                                size_t* offsets_host);
 
@@ -175,7 +185,7 @@ int dcue_pack_weights(const dcue_model* m, void* stream);
  * train != 0: model.train() semantics -- BatchNorm batch statistics over all copies, running stats
  * and num_batches_tracked updated, activations kept in `ws` for dcue_train_backward.
  * train == 0: model.eval() semantics (running statistics, nothing updated).
- * Outputs (each nullable): scores[B][N], user feats [B][d], item feats [M][d], loss[1] (mean over
+ * Outputs (each nullable): scores[B][N], user feats [B][d_s], item feats [M][d_s], loss[1] (mean over
  * rows of the summed hinge). */
 int dcue_forward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws,
                  size_t ws_bytes, int32_t train, float margin, float* scores, float* user_feat,
@@ -229,10 +239,11 @@ int dcue_emb_log_init(const dcue_model* m, int32_t cap, int32_t step, void* stre
 int dcue_embedding_sync(const dcue_model* m, const int64_t* users, int32_t n, void* stream);
 int dcue_embedding_flush(const dcue_model* m, void* stream);
 
-/* Eval-mode item tower (running BN stats): DCUENet.conv(X) under model.eval() (nn/dcue.py:663). */
+/* Eval-mode item tower (running BN stats): DCUENet.conv(X) under model.eval() (nn/dcue.py:663).
+ * item_feat: [n_items][d_s]. */
 int dcue_item_tower_eval(const dcue_model* m, const dcue_tracks* t, const int32_t* item_track,
                          int32_t n_items, void* ws, size_t ws_bytes, float* item_feat, void* stream);
-/* Eval user tower: DCUENet.user_embd(idx) (nn/dcue.py:638). */
+/* Eval user tower: DCUENet.user_embd(idx) (nn/dcue.py:638). user_feat: [n][d_s]. */
 int dcue_user_tower(const dcue_model* m, const int64_t* users, int32_t n, void* ws, size_t ws_bytes,
                     float* user_feat, void* stream);
 

@@ -10,7 +10,9 @@ Which reference code produced what:
 * model_*.npz   -- dcrecommend/dcue/dcue.py:21-108 (DCUENet fwd), nn/dcue.py:167-170 (hinge loss),
                    torch autograd backward, torch.optim.Adam as built at nn/dcue.py:143-147;
                    model_{plain,res,resbn}.npz the same for the other wired towers
-                   (audiomodels/truedcuemel1d.py, truedcuemel1dres.py, truedcuemel1dresbn.py).
+                   (audiomodels/truedcuemel1d.py, truedcuemel1dres.py, truedcuemel1dresbn.py);
+                   model_d100.npz at the trainer's default widths (feature_dim=100, conv_hidden=128,
+                   nn/dcue.py:44-45), model_w_*.npz at odd H / d in the other towers.
 * inbatch_*.npz -- the in-batch sampler spec of nn/dcue.py:698-709 (commented out in the reference;
                    the draws below follow that text literally), plus a forward/backward of the
                    reference model on the duplicated [pos; neg] batch it builds.
@@ -519,6 +521,15 @@ if __name__ == "__main__":
                                          store_init=False, model_type=mt)
                            for tag, mt in (("plain", "truedcuemel1d"), ("res", "truedcuemel1dres"),
                                            ("resbn", "truedcuemel1dresbn"))],
+        # widths outside 32/64/128/256: the trainer's default feature_dim = 100 (nn/dcue.py:44) and
+        # odd H / d in the other towers (the library pads them to its storage widths)
+        "widths": lambda: (model_fixture("model_d100.npz", H=128, d=100, n_users=10, B=2, N=2,
+                                         store_init=False, store_steps=False),
+                           [model_fixture("model_w_%s.npz" % tag, H=H, d=d, n_users=10, B=4, N=3,
+                                          store_init=False, model_type=mt)
+                            for tag, H, d, mt in (("plain", 36, 20, "truedcuemel1d"),
+                                                  ("res", 48, 52, "truedcuemel1dres"),
+                                                  ("resbn", 40, 24, "truedcuemel1dresbn"))]),
         "inbatch": inbatch_fixtures, "catalogue": catalogue_fixture, "batches": batches_fixture,
         "scheduler": scheduler_fixture, "train5": train5_fixture, "metrics": metrics_fixture,
         "eval": eval_fixture, "fit": fit_fixture, "optim": optim_fixture,

@@ -42,13 +42,15 @@ LP = (33, 8, 2, 1, 1)
 
 def _gpu_route(net, nat, B, N, M, rows, D, H):
     """The step's max-pool argmax and relu-live masks as the GPU computed them (workspace, layout
-    [M][Lp][C]), as oracle routes [rows, C, Lp] over the literal [pos; neg] stack."""
+    [M][Lp][C_s] at the storage widths), as oracle routes [rows, C, Lp] over the literal [pos; neg]
+    stack (the reference's C channels)."""
     route = {}
+    sd = nat.storage_dims(net._flat["dims"])
     for l, (yo, io) in enumerate(nat.workspace_activations(net._flat["dims"], B, N, M), start=1):
-        C = D if l == 5 else H
-        n = M * LP[l - 1] * C
-        y = net._ws[yo:yo + 4 * n].view(torch.float32).view(M, LP[l - 1], C).permute(0, 2, 1).cpu()
-        ix = net._ws[io:io + n].view(M, LP[l - 1], C).permute(0, 2, 1).long().cpu()
+        C, Cs = (D, sd.feature_dim) if l == 5 else (H, sd.conv_hidden)
+        n = M * LP[l - 1] * Cs
+        y = net._ws[yo:yo + 4 * n].view(torch.float32).view(M, LP[l - 1], Cs)[:, :, :C].permute(0, 2, 1).cpu()
+        ix = net._ws[io:io + n].view(M, LP[l - 1], Cs)[:, :, :C].permute(0, 2, 1).long().cpu()
         route[l] = (ix[rows].contiguous(), (y > 0)[rows].contiguous())
     return route
 
@@ -80,6 +82,8 @@ def _check_decisions(pre, route, tie=1e-5):
 
 
 CASES = [("inbatch", "truedcuemel1dbn", 64, 20, 128, 128), ("catalogue", "truedcuemel1dbn", 64, 20, 128, 128)]
+# the reference trainer's default widths (feature_dim = 100, conv_hidden = 128; nn/dcue.py:44-45)
+CASES += [("inbatch", "truedcuemel1dbn", 64, 20, 100, 128), ("catalogue", "truedcuemel1dbn", 64, 20, 100, 128)]
 # the other wired towers (dcue/dcue.py:49-59) through the same plan, at a smaller shape
 CASES += [(mode, mt, 16, 5, 64, 64) for mt in ("truedcuemel1d", "truedcuemel1dres", "truedcuemel1dresbn")
           for mode in ("inbatch", "catalogue")]
@@ -114,6 +118,8 @@ def test_plan_at_bench_shape_against_oracle(mode, model_type, B, N, D, H):
     M = B if inbatch else B * (1 + N)
     off = nat.workspace_outputs(net._flat["dims"], B, N, M)
 
+    Ds = nat.storage_dims(net._flat["dims"]).feature_dim  # feature rows are stored Ds wide
+
     def ws_view(o, n, shape):
         return net._ws[o:o + 4 * n].view(torch.float32).view(shape)
 
@@ -138,8 +144,11 @@ def test_plan_at_bench_shape_against_oracle(mode, model_type, B, N, D, H):
             if inbatch:
                 assert torch.equal(plan.neg_item.cpu().long(), r), "in-batch draws differ from numpy"
             _close(ws_view(off[0], B * N, (B, N)), rs_, 1e-4, 1e-4, "scores")
-            _close(ws_view(off[1], B * D, (B, D)), ruf, 1e-4, 1e-4, "user feats")
-            feats = ws_view(off[2], M * D, (M, D)).cpu()
+            uf_s = ws_view(off[1], B * Ds, (B, Ds)).cpu()
+            _close(uf_s[:, :D], ruf, 1e-4, 1e-4, "user feats")
+            feats_s = ws_view(off[2], M * Ds, (M, Ds)).cpu()
+            assert not bool(uf_s[:, D:].any()) and not bool(feats_s[:, D:].any()), "storage pads not zero"
+            feats = feats_s[:, :D]
             _close(feats[:B], rpf, 1e-4, 1e-4, "positive feats")
             if not inbatch:
                 _close(feats[B:].reshape(B, N, D), rnf, 1e-4, 1e-4, "negative feats")
@@ -186,4 +195,6 @@ def test_plan_at_bench_shape_against_oracle(mode, model_type, B, N, D, H):
         tol = budget + 1e-4 * float(ref.abs().max()) if k in p else 1e-4 * float(ref.abs().max()) + 1e-6
         assert float((got - ref).abs().max()) <= tol, "%s after %d steps: %.3e" % (
             k, len(LRS), float((got - ref).abs().max()))
+    from test_gpu_parity import assert_storage_pads_zero
+    assert_storage_pads_zero(net)
     plan.close()

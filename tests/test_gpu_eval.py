@@ -227,6 +227,22 @@ def test_train_dcue_driver_config1(tmp_path):
     assert os.listdir(tmp_path)
 
 
+def test_train_dcue_reference_defaults(tmp_path):
+    """train_dcue.py with the reference trainer's defaults (DCUE(feature_dim=100, conv_hidden=128,
+    u_embdim=300, batch_size=64, ...), nn/dcue.py:44-50): only the synthetic data is chosen here.
+    feature_dim = 100 runs at the library's 128-wide storage; the factors are d = 100 wide."""
+    import train_dcue
+    dcue = train_dcue.main(["--synthetic", "--synthetic-users", "300", "--synthetic-tracks", "600",
+                            "--synthetic-pairs", "6000", "--num-epochs", "1", "--lr", "1e-4",
+                            "--save-dir", str(tmp_path)])
+    assert dcue.feature_dim == 100 and dcue.conv_hidden == 128 and dcue.u_embdim == 300
+    assert dcue.model.conv.fc.weight.shape == (100, 100)
+    assert dcue.user_factors.shape[1] == 100 and dcue.item_factors.shape[1] == 100
+    assert 0.0 <= dcue.best_val_auc <= 1.0 and os.listdir(tmp_path)
+    from test_gpu_parity import assert_storage_pads_zero
+    assert_storage_pads_zero(dcue.model)
+
+
 def test_saturated_user_raises_like_numpy(tmp_path):
     """40 tracks: the val split holds 3 songs and one user has all of them, so the reference's
     np.random.choice over that user's (empty) non-items raises ValueError

@@ -42,6 +42,27 @@ def _net(g, seed=0):
     return net.cuda()
 
 
+def assert_storage_pads_zero(net):
+    """Outside the reference-shaped corners of the flat parameter, gradient and BN-statistics buffers
+    (the storage channels past H / d, include/dcue.h dcue_storage_dims) everything is exactly zero."""
+    from dcrecommend import _native as nat
+    fl = net._flat
+    named = dict(net.named_parameters())
+    for buf, what in ((fl["P"], "params"), (fl["G"], "grads")):
+        mask = torch.ones_like(buf, dtype=torch.bool)
+        for s, name in enumerate(nat.DENSE_NAMES):
+            if name in named:
+                nat.corner(mask, fl["poff"][s], fl["shapes"][s], named[name].shape).fill_(False)
+        assert not bool(buf[mask].any()), "%s: storage pads not zero" % what
+    mask = torch.ones_like(fl["stats"], dtype=torch.bool)
+    for l in range(nat.N_BN):
+        bn = getattr(net.conv, "bn%d" % l, None)
+        if bn is not None:
+            for j in (2 * l, 2 * l + 1):
+                mask[fl["boff"][j]:fl["boff"][j] + bn.num_features] = False
+    assert not bool(fl["stats"][mask].any()), "BN statistics: storage pads not zero"
+
+
 def _hinge(scores, margin=0.2):  # the reference's _loss_func, nn/dcue.py:167-170
     return torch.max(torch.zeros_like(scores), margin - scores).sum(dim=1).mean()
 
@@ -86,10 +107,13 @@ def _check_params_after_adam(net, g, prefix, lr_budget, skip_rows=None, grad_pre
 
 
 @pytest.mark.parametrize("name", ["model_tiny.npz", "model_h128.npz", "model_plain.npz", "model_res.npz",
-                                  "model_resbn.npz"])
+                                  "model_resbn.npz", "model_d100.npz", "model_w_plain.npz", "model_w_res.npz",
+                                  "model_w_resbn.npz"])
 def test_module_forward_backward(golden, name):
     """The reference's own fwd / hinge / bwd / Adam steps for each wired tower (dcue/dcue.py:49-59:
-    truedcuemel1dbn at H = 32 and 128, truedcuemel1d, truedcuemel1dres, truedcuemel1dresbn)."""
+    truedcuemel1dbn at H = 32 and 128, truedcuemel1d, truedcuemel1dres, truedcuemel1dresbn), at the
+    trainer's default widths (d = 100, H = 128: model_d100) and at odd H / d in the other towers
+    (model_w_*: the library's zero-padded storage channels must stay invisible)."""
     g = golden(name)
     net = _net(g, int(g["seed"]))
     u = torch.from_numpy(g["u"]).to(DEV)
@@ -111,6 +135,7 @@ def test_module_forward_backward(golden, name):
                 assert int(v) == int(g["fwd." + k]), k
             else:
                 _assert_close(v, g["fwd." + k], 1e-4, 1e-4, k)
+    assert_storage_pads_zero(net)
     if "step1.conv.fc.weight" not in g.files:
         return
     from dcrecommend.optim import NativeAdam
@@ -125,6 +150,7 @@ def test_module_forward_backward(golden, name):
     opt.step()
     torch.cuda.synchronize()
     _check_params_after_adam(net, g, "step2.", 2 * lr, skip_rows=np.unique(g["u"]))
+    assert_storage_pads_zero(net)
 
 
 @pytest.mark.parametrize("H,d", [(64, 64), (128, 64), (256, 128), (128, 256)])  # (128, 64): config 1

@@ -81,10 +81,48 @@ def test_layouts_match_reference_shapes(golden):
     assert nat.workspace_bytes(dims, 4, 3, 16) > 0
 
 
+@pytest.mark.parametrize("H,d,mt", [(128, 100, "truedcuemel1dbn"), (40, 24, "truedcuemel1dresbn"),
+                                     (36, 20, "truedcuemel1d"), (200, 7, "truedcuemel1dres"),
+                                     (1, 256, "truedcuemel1dbn")])
+def test_any_width_accepted(H, d, mt):
+    """Any conv_hidden / feature_dim in 1..256 (the reference's DCUENet takes any; its trainer's
+    default is feature_dim = 100, nn/dcue.py:44). The library stores them at the width rounded up to
+    32/64/128/256, and every reference-shaped parameter is the leading corner of its segment."""
+    from dcrecommend import _native as nat
+    from dcrecommend.dcue.dcue import DCUENet
+    dims = nat.make_dims(H, d, 300, 10, mt)
+    sd = nat.storage_dims(dims)
+    for w, ws in ((H, sd.conv_hidden), (d, sd.feature_dim)):
+        assert ws in (32, 64, 128, 256) and ws >= w and (ws == 32 or ws // 2 < w)
+    off = nat.param_layout(dims)
+    shapes = nat.segment_shapes(dims)
+    torch.manual_seed(0)
+    net = DCUENet({"feature_dim": d, "conv_hidden": H, "user_embdim": 300, "user_count": 10, "model_type": mt})
+    named = dict(net.named_parameters())
+    P = torch.zeros(off[-1])
+    for s, name in enumerate(nat.DENSE_NAMES):
+        seg = off[s + 1] - off[s]
+        n = int(np.prod(shapes[s]))
+        if name not in named:  # BN parameters of a tower without BN: empty segment
+            assert seg == 0
+            continue
+        p = named[name]
+        assert len(shapes[s]) == p.dim() and all(a >= b for a, b in zip(shapes[s], p.shape)), name
+        assert n <= seg < n + 4, name
+        nat.corner(P, off[s], shapes[s], p.shape).copy_(p.data)
+    # the corners tile the buffer without overlap: every parameter's values appear exactly once
+    total = sum(p.numel() for n, p in named.items() if n in nat.DENSE_NAMES)
+    assert int((P != 0).sum()) <= total
+    for s, name in enumerate(nat.DENSE_NAMES):
+        if name in named:
+            assert torch.equal(nat.corner(P, off[s], shapes[s], named[name].shape), named[name].data), name
+
+
 def test_unsupported_dims_rejected():
     from dcrecommend import _native as nat
-    with pytest.raises(RuntimeError, match="UNSUPPORTED"):
-        nat.param_layout(nat.make_dims(128, 100, 300, 10))
+    for H, d in ((128, 257), (300, 128), (0, 128)):
+        with pytest.raises(RuntimeError, match="UNSUPPORTED|INVALID"):
+            nat.param_layout(nat.make_dims(H, d, 300, 10))
 
 
 def test_dcuenet_init_matches_reference(golden):

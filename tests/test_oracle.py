@@ -48,7 +48,8 @@ def _mt(g):
     return str(g["model_type"]) if "model_type" in g.files else "truedcuemel1dbn"
 
 
-@pytest.mark.parametrize("name", ["model_plain.npz", "model_res.npz", "model_resbn.npz"])
+@pytest.mark.parametrize("name", ["model_plain.npz", "model_res.npz", "model_resbn.npz", "model_d100.npz",
+                                  "model_w_plain.npz", "model_w_res.npz", "model_w_resbn.npz"])
 def test_init_towers_checksums(golden, name):
     """The other wired towers (dcue/dcue.py:49-59): parameter names, order and init draws."""
     g = golden(name)
@@ -61,7 +62,8 @@ def test_init_towers_checksums(golden, name):
 
 
 @pytest.mark.parametrize("name", ["model_tiny.npz", "model_h128.npz", "model_plain.npz", "model_res.npz",
-                                  "model_resbn.npz"])
+                                  "model_resbn.npz", "model_d100.npz", "model_w_plain.npz", "model_w_res.npz",
+                                  "model_w_resbn.npz"])
 def test_forward_backward_step(golden, name):
     g = golden(name)
     torch.manual_seed(int(g["seed"]))

@@ -34,7 +34,7 @@ def parse(argv=None):
     ap.add_argument("--synthetic-users", type=int, default=60)
     ap.add_argument("--synthetic-tracks", type=int, default=120)
     ap.add_argument("--synthetic-pairs", type=int, default=1500)
-    ap.add_argument("--feature-dim", type=int, default=128)
+    ap.add_argument("--feature-dim", type=int, default=100)  # DCUE's default, nn/dcue.py:44
     ap.add_argument("--conv-hidden", type=int, default=128)
     ap.add_argument("--batch-size", type=int, default=64)
     ap.add_argument("--neg-batch-size", type=int, default=20)
