@@ -435,7 +435,8 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
   const double w = 1.0 - a->beta1;
   AdamScalars sc;
   sc.neg_step = (float)(-(a->lr / bc1));
-  sc.lerp_c = w < 0.5 ? (float)w : (float)w - 1.0f;
+  // sign bit = the lerp's base (adam_replay.h lerp_base_g): -(1 - w) is -0 at beta1 = 0
+  sc.lerp_c = w < 0.5 ? (float)w : -(1.0f - (float)w);
   sc.b2 = (float)a->beta2;
   sc.one_m_b2 = (float)(1.0 - a->beta2);
   sc.bc2_sqrt = (float)pow(bc2, 0.5);  // bias_correction2 ** 0.5

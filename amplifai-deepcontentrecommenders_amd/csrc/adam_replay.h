@@ -24,16 +24,21 @@ struct AdamScalars {
 };
 static_assert(sizeof(AdamScalars) == 32, "history entry is [8] floats");
 
-// lerp_c < 0: the lerp weight is >= 0.5 (beta1 <= 0.5), so the blend base is g.
+// The lerp's blend base is carried by lerp_c's SIGN BIT: lerp_c = w (base m) for a weight w < 0.5
+// (beta1 > 0.5), else lerp_c = -(1 - w) (base g) -- a negative zero when w = 1 (beta1 = 0), where the
+// lerp returns g itself. launch_adam forms it as -(1 - (float)w), never (float)w - 1, which would
+// give +0 at w = 1 and lose the branch.
+DCUE_RHD bool lerp_base_g(const AdamScalars& s) { return __builtin_signbit(s.lerp_c); }
+
 DCUE_RHD void adam_elem(float& p, float g, float& m, float& v, const AdamScalars& s) {
   if (s.wd != 0.f) g = rn_fma(p, s.wd, g);
-  m = rn_fma(s.lerp_c, rn_sub(g, m), s.lerp_c < 0.f ? g : m);
+  m = rn_fma(s.lerp_c, rn_sub(g, m), lerp_base_g(s) ? g : m);
   v = rn_fma(rn_mul(s.one_m_b2, g), g, rn_mul(v, s.b2));
   const float denom = rn_add(rn_div(rn_sqrt(v), s.bc2_sqrt), s.eps);
   p = rn_add(p, rn_div(rn_mul(s.neg_step, m), denom));
 }
 
-// The zero-gradient step (a row outside the batch, wd == 0, lerp weight < 0.5), bit-identical to
+// The zero-gradient step (a row outside the batch, wd == 0, lerp base m: weight < 0.5), bit-identical to
 // adam_elem(p, +0, m, v, s): fma((1-b2)*0, 0, v*b2) == v*b2 (v >= 0), and sqrt(v)/bc2_sqrt by
 // Markstein's correction with r = RN(1/bc2_sqrt): q = RN(a r), q' = RN(q + RN?(a - q bc2)*r) is the
 // correctly rounded quotient for a >= 2^-100 (below it the plain division runs).
@@ -55,7 +60,7 @@ DCUE_RHD void adam_zero_elem(float& p, float& m, float& v, const AdamScalars& s)
 
 // replay of a zero-gradient step: the fast form when no weight decay touches g
 DCUE_RHD void adam_replay(float& p, float& m, float& v, const AdamScalars& s, float gz) {
-  if (s.wd == 0.f && s.lerp_c < 0.5f)
+  if (s.wd == 0.f && !lerp_base_g(s) && s.lerp_c < 0.5f)
     adam_zero_elem(p, m, v, s);
   else
     adam_elem(p, gz, m, v, s);
@@ -82,7 +87,8 @@ struct ReplayBound {
   float b2min;  // min b2
   float eps;    // min eps
   float vdec;   // lower bound of v_end / v_start over the window (finalize)
-  int ok;       // every step: wd == 0, 0 <= lerp_c < 0.5, eps > 0, 0 <= b2 < 1, 0 < bc2_sqrt <= 1
+  int ok;       // every step: wd == 0, lerp base m (+0 <= lerp_c < 0.5), eps > 0, 0 <= b2 < 1,
+                // 0 < bc2_sqrt <= 1
   int nd;       // every step free of weight decay (and the replayed gradient is +0)
 };
 
@@ -104,7 +110,7 @@ DCUE_RHD void bound_fold(ReplayBound& b, const AdamScalars& s) {
   b.eps = s.eps < b.eps ? s.eps : b.eps;
   const int nd = s.wd == 0.f;
   b.nd &= nd;
-  b.ok &= nd & (s.lerp_c >= 0.f) & (s.lerp_c < 0.5f) & (s.eps > 0.f) & (s.b2 >= 0.f) & (s.b2 < 1.f) &
+  b.ok &= nd & !lerp_base_g(s) & (s.lerp_c < 0.5f) & (s.eps > 0.f) & (s.b2 >= 0.f) & (s.b2 < 1.f) &
           (s.bc2_sqrt > 0.f) & (s.bc2_sqrt <= 1.f) & (a <= 0x1p60f);
 }
 

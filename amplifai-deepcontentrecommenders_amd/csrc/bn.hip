@@ -7,18 +7,22 @@
 namespace dcue {
 
 // --------------------------------------------------------------------------- BN statistics
-// bn0 input statistics over the gathered spectrograms, weighted by item copy counts.
+// bn0 input statistics over the gathered spectrograms, weighted by item copy counts (acc; nullable)
+// and the per-mel range of the raw input (range; nullable: [0][c] max ord(x), [1][c] max ord(-x),
+// ordered keys, kRngC apart) -- what layer 1's split-f16 forward scales its operand by (conv.hip).
 template <int SRC>
 __global__ __launch_bounds__(256) void k_input_stats(const void* tracks, const int32_t* item_track,
                                                      const float* counts, int M, int rows_per_blk,
-                                                     unsigned long long* acc) {
+                                                     unsigned long long* acc, unsigned* range) {
   critical_path_priority();
   __shared__ float red[8][2][kMels];
+  __shared__ float rmx[8][2][kMels];
   const int q = threadIdx.x & 31, slot = threadIdx.x >> 5;
   const long rows = (long)M * kFrames;
   const long r0 = (long)blockIdx.x * rows_per_blk;
   const long r1 = min(r0 + rows_per_blk, rows);
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f), ss = s;
+  float4 hi = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY), nlo = hi;  // max x, max -x
   constexpr int FB = 4;  // rows in flight per thread
   for (long rb = r0 + slot; rb < r1; rb += 8 * FB) {
     long trk[FB];
@@ -57,22 +61,30 @@ __global__ __launch_bounds__(256) void k_input_stats(const void* tracks, const i
       const float ww = w[j];
       s.x += ww * x[0]; s.y += ww * x[1]; s.z += ww * x[2]; s.w += ww * x[3];
       ss.x += ww * x[0] * x[0]; ss.y += ww * x[1] * x[1]; ss.z += ww * x[2] * x[2]; ss.w += ww * x[3] * x[3];
+      hi.x = fmaxf(hi.x, x[0]); hi.y = fmaxf(hi.y, x[1]); hi.z = fmaxf(hi.z, x[2]); hi.w = fmaxf(hi.w, x[3]);
+      nlo.x = fmaxf(nlo.x, -x[0]); nlo.y = fmaxf(nlo.y, -x[1]); nlo.z = fmaxf(nlo.z, -x[2]); nlo.w = fmaxf(nlo.w, -x[3]);
     }
   }
   st4(&red[slot][0][4 * q], s);
   st4(&red[slot][1][4 * q], ss);
+  st4(&rmx[slot][0][4 * q], hi);
+  st4(&rmx[slot][1][4 * q], nlo);
   __syncthreads();
   {
     const int c = threadIdx.x & 127, which = threadIdx.x >> 7;
-    float v = 0.f;
+    float v = 0.f, m = -INFINITY;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v += red[k][which][c];
-    acc128_add(acc_at(acc, kMels, which, c), v);
+    for (int k = 0; k < 8; ++k) {
+      v += red[k][which][c];
+      m = fmaxf(m, rmx[k][which][c]);
+    }
+    if (acc) acc128_add(acc_at(acc, kMels, which, c), v);
+    if (range && m > -INFINITY) atomicMax(range + which * kRngC + c, ord_key(m));
   }
 }
 
 int launch_input_stats(int src, const void* tracks, const int32_t* item_track, const float* counts,
-                       int M, unsigned long long* acc, hipStream_t s) {
+                       int M, unsigned long long* acc, unsigned* range, hipStream_t s) {
   const long rows = (long)M * kFrames;
   int nb = (int)((rows + 31) / 32);  // short per-block row loops: the gather is latency-bound
   if (nb > 256) nb = 256;
@@ -80,10 +92,10 @@ int launch_input_stats(int src, const void* tracks, const int32_t* item_track, c
   nb = (int)((rows + rpb - 1) / rpb);
   if (src == SRC_TRACK_F16)
     DCUE_LAUNCH(k_input_stats<SRC_TRACK_F16>, dim3(nb), dim3(256), 0, s, tracks, item_track,
-                       counts, M, rpb, acc);
+                       counts, M, rpb, acc, range);
   else
     DCUE_LAUNCH(k_input_stats<SRC_TRACK_F32>, dim3(nb), dim3(256), 0, s, tracks, item_track,
-                       counts, M, rpb, acc);
+                       counts, M, rpb, acc, range);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }

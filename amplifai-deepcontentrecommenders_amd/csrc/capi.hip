@@ -188,7 +188,11 @@ struct Ws {
   float *mean[6], *invstd[6], *a[6];
   // exact BN sums (bnacc.h), [6 layers][2 sums][Cmax][2 words]: forward stats, backward sums
   unsigned long long *bnacc, *bnbacc;
+  // the forward's value ranges (split-f16 operand scales, conv.hip): [5 layers][2][kRngC] ordered
+  // keys, between the forward and backward sums of the block (cleared with the forward sums)
+  unsigned* rng;
   long nzero;            // words of the accumulator block (one clear per step)
+  long nfwd;             // its forward part: the sums and the ranges
   float* rowsum;         // [B] per-row hinge sums (score_fused)
   int cmax;
   float* y[6];
@@ -211,10 +215,16 @@ struct Ws {
 };
 
 // the accumulator block's parts: [6][2][Cmax][2] forward sums, then the same for the backward
+constexpr long kRngWords = 5L * 2 * kRngC / 2;  // the ranges' 64-bit words
+
 void rebase_acc(Ws* w, unsigned long long* acc) {
   w->bnacc = acc;
-  w->bnbacc = acc + 6L * 2 * w->cmax * 2;
+  w->rng = reinterpret_cast<unsigned*>(acc + 6L * 2 * w->cmax * 2);
+  w->bnbacc = acc + 6L * 2 * w->cmax * 2 + kRngWords;
 }
+
+// layer l's range (l = 0: the raw input of conv 1; l = 1..4: the ReLU output of conv l)
+unsigned* rng_at(const Ws& w, int l) { return w.rng + (size_t)l * 2 * kRngC; }
 
 size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   Arena ar{(char*)base, 0, 0};
@@ -228,7 +238,8 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
     w->a[l] = ar.take<float>(C);
   }
   w->cmax = Cmax > D ? Cmax : D;
-  w->nzero = 2L * 6 * 2 * w->cmax * 2;
+  w->nfwd = 6L * 2 * w->cmax * 2 + kRngWords;
+  w->nzero = w->nfwd + 6L * 2 * w->cmax * 2;
   w->bnacc = ar.take<unsigned long long>(w->nzero);
   rebase_acc(w, w->bnacc);
   w->rowsum = ar.take<float>(B);
@@ -366,21 +377,25 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     p.C = bn_channels(&m->dims, l);
     return p;
   };
+  // the forward sums and value ranges start cleared (train: by the step prologue, or here)
+  if (!train || !acc_cleared)
+    DCUE_HIP_CHECK(hipMemsetAsync(w.bnacc, 0, sizeof(unsigned long long) * w.nfwd, s));
   if (!c.bn) {  // mean 0, invstd = a = 1, beta 0 for every layer: the BN-free towers
     TRY(launch_bn_identity(w.mean, w.invstd, w.a, w.ones, w.zeros, w.cmax, c.H, c.D, s));
-    if (train && !acc_cleared)  // the epilogues still add their (unused) BN sums
-      DCUE_HIP_CHECK(hipMemsetAsync(w.bnacc, 0, sizeof(unsigned long long) * 6 * 2 * w.cmax * 2, s));
+    // (the epilogues still add their unused BN sums) the raw input's range, for conv 1's split
+    TRY(launch_input_stats(src, t->data, item_track, nullptr, M, nullptr, rng_at(w, 0), s));
   } else if (train) {
-    if (!acc_cleared)
-      DCUE_HIP_CHECK(hipMemsetAsync(w.bnacc, 0, sizeof(unsigned long long) * 6 * 2 * w.cmax * 2, s));
-    if (clear_bn0 && !stats_done)  // sums of a batch announced ahead but not the one launched
+    if (clear_bn0 && !stats_done) {  // sums of a batch announced ahead but not the one launched
       DCUE_HIP_CHECK(hipMemsetAsync(bn_acc(w.bnacc, w.cmax, 0), 0, sizeof(unsigned long long) * 2 * w.cmax * 2, s));
+      DCUE_HIP_CHECK(hipMemsetAsync(rng_at(w, 0), 0, sizeof(unsigned) * 2 * kRngC, s));
+    }
     if (!stats_done)  // else computed one step ahead into this accumulator block (plans)
-      TRY(launch_input_stats(src, t->data, item_track, counts, M, bn_acc(w.bnacc, w.cmax, 0), s));
+      TRY(launch_input_stats(src, t->data, item_track, counts, M, bn_acc(w.bnacc, w.cmax, 0), rng_at(w, 0), s));
   } else {
     for (int l = 0; l < 6; ++l)
       TRY(launch_bn_eval(bn_channels(&m->dims, l), c.P(seg_bn_w(l)), c.rmean(l), c.rvar(l), w.mean[l],
                          w.invstd[l], w.a[l], s));
+    TRY(launch_input_stats(src, t->data, item_track, nullptr, M, nullptr, rng_at(w, 0), s));
   }
   for (int l = 1; l <= 5; ++l) {
     RowsArgs a = {};
@@ -397,6 +412,8 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     a.out = w.y[l];
     a.out_idx = w.idx[l];
     a.out_acc = train ? bn_acc(w.bnacc, w.cmax, l) : nullptr;
+    a.in_range = rng_at(w, l - 1);
+    a.out_range = l < 5 ? rng_at(w, l) : nullptr;
     a.M = M;
     a.nout = l == 5 ? c.D : c.H;
     TimerScope tsc;
@@ -631,7 +648,7 @@ int ahead_item_inputs(const dcue_model* m, const dcue_batch* b, const dcue_track
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
   const int M = b->n_items;
   const double copies = (double)b->n_rows * (1 + b->n_neg);
-  TRY(launch_input_stats(src, t->data, items, counts, M, bn_acc(w.bnacc, w.cmax, 0), s));
+  TRY(launch_input_stats(src, t->data, items, counts, M, bn_acc(w.bnacc, w.cmax, 0), rng_at(w, 0), s));
   return launch_xhat0(src, t->data, items, M, bn_acc(w.bnacc, w.cmax, 0), copies * kFrames, xhat0, s);
 }
 

@@ -81,6 +81,16 @@ int comm_exchange_step(dcue_comm* c, float* grad, long late, long n, hipEvent_t 
   return DCUE_OK;
 }
 
+// grad[0:n) /= world on `s` (DDP's grad.div_(world)), for steps whose optimizer does not fold the
+// divide into its sweep (plan launches followed by a separate optimizer call)
+int comm_divide(const dcue_comm* c, float* grad, long n, hipStream_t s) {
+  if (c->world <= 1 || n <= 0) return DCUE_OK;
+  const long blocks = std::min<long>((n + 255) / 256, 2048);
+  DCUE_LAUNCH(k_div_world, dim3((unsigned)blocks), dim3(256), 0, s, grad, n, (float)c->world);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
 }  // namespace dcue
 
 using namespace dcue;
@@ -134,10 +144,5 @@ extern "C" int dcue_comm_allreduce_mean(dcue_comm* c, float* buf, int64_t n, voi
   TRY(comm_allreduce_sum(c, buf, n));
   DCUE_HIP_CHECK(hipEventRecord(c->ev_done, c->stream));
   DCUE_HIP_CHECK(hipStreamWaitEvent(s, c->ev_done, 0));
-  if (c->world > 1) {
-    const long blocks = std::min<long>((n + 255) / 256, 2048);
-    DCUE_LAUNCH(k_div_world, dim3((unsigned)blocks), dim3(256), 0, s, buf, (long)n, (float)c->world);
-    DCUE_LAUNCH_CHECK();
-  }
-  return DCUE_OK;
+  return comm_divide(c, buf, (long)n, s);
 }

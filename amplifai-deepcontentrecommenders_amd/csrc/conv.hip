@@ -37,7 +37,53 @@ __device__ __forceinline__ float2 bwd_sums(const unsigned long long* acc, int C,
 // channel t) into LDS, then read by quad: the fp64 finalize is one short chain per thread.
 struct ChanLds {
   float v[5][256];
+  float wmax[4];  // split-f16 forward: the per-wave maxima of the channels' value bounds
 };
+
+// Split-f16 forward operand scale. Every slab value v is stored as v*S = hi + lo in
+// fp16, S a power of two, and the epilogue multiplies the accumulators by 1/S: exact, so the result
+// is what the unscaled split computes wherever that one is in range. S puts the largest |v| the layer
+// can produce in [2^14, 2^15): no fp16 overflow (65504) whatever the input magnitudes, and small
+// activations (unnormalised towers, tiny inputs) keep hi/lo out of fp16's subnormals, so the split
+// stays ~2^-22 relative to the layer's scale. The bound of channel c comes from the input layer's
+// range (RowsArgs::in_range): v = (x - mu) sc + be is monotone in x, so its extremes over the batch
+// are at x = min and x = max (the ReLU outputs of layers >= 2 have min 0). Every workgroup of the
+// launch reads the same ranges, so all use the same S. Threads t < KC own channel t (chan_stage);
+// waves 0-3 reduce the bounds, and after the block barrier every thread forms S from the four.
+template <int SRC>
+__device__ __forceinline__ void range_stage(const RowsArgs& a, int KC, ChanLds& L) {
+  const int t = threadIdx.x;
+  if (t >= 256) return;  // waves 0-3 (uniform per wave)
+  float bnd = 0.f;
+  if (t < KC && a.in_range) {
+    const unsigned khi = a.in_range[t], knlo = a.in_range[kRngC + t];
+    float hi = khi ? ord_value(khi) : 0.f;
+    float lo = (SRC == SRC_ACT) ? 0.f : (knlo ? -ord_value(knlo) : 0.f);
+    if (SRC == SRC_ACT) hi = fmaxf(hi, 0.f);
+    const float mu = L.v[0][t], sc = L.v[1][t], be = L.v[2][t];
+    bnd = fmaxf(fabsf((lo - mu) * sc + be), fabsf((hi - mu) * sc + be));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) bnd = fmaxf(bnd, __shfl_xor(bnd, off, 64));
+  if ((t & 63) == 0) L.wmax[t >> 6] = bnd;
+}
+
+struct SplitScale {
+  float s, inv;
+};
+__device__ __forceinline__ SplitScale split_scale(const ChanLds& L, int KC) {
+  float m = L.wmax[0];
+  for (int w = 1; w < (KC + 63) / 64; ++w) m = fmaxf(m, L.wmax[w]);
+  SplitScale r = {1.f, 1.f};
+  if (m > 0.f && m < INFINITY) {  // else (all zero, or a non-finite input that propagates anyway) 1
+    int e;
+    (void)frexpf(m, &e);  // m in [2^(e-1), 2^e)
+    const int k = min(max(15 - e, -120), 120);
+    r.s = ldexpf(1.f, k);
+    r.inv = ldexpf(1.f, -k);
+  }
+  return r;
+}
 
 template <int SRC>
 __device__ __forceinline__ void chan_stage(const RowsArgs& a, int KC, ChanLds& L) {
@@ -240,6 +286,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
       for (int ct = 0; ct < CT; ++ct) bq[st][ct] = ld4(wp + st * wstep + 64 * ct);
   }
 
+  SplitScale sscale = {1.f, 1.f};  // split-f16 operand scale (range_stage)
   {
     static_assert(kRowsThreads % C4 == 0, "a thread's slab slots share one channel quad");
     constexpr int FB = SRC == SRC_DZ ? 4 : 8;  // slab slots (float4) in flight per thread
@@ -279,7 +326,9 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
         if (e < nfill) {
           const float4 v = slab_finish<SRC, POOLL>(a, kop, pp[j], raw[j]);
           if constexpr (F16)
-            st_split<KC>(&slab[(e / C4) * PITCH], c, ok[j] ? v : make_float4(0.f, 0.f, 0.f, 0.f));
+            st_split<KC>(&slab[(e / C4) * PITCH], c,
+                         ok[j] ? make_float4(v.x * sscale.s, v.y * sscale.s, v.z * sscale.s, v.w * sscale.s)
+                               : make_float4(0.f, 0.f, 0.f, 0.f));
           else
             st4(&slab[(e / C4) * PITCH + c], ok[j] ? v : make_float4(0.f, 0.f, 0.f, 0.f));
         }
@@ -288,9 +337,11 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
     // the first batch's reads are in flight while the per-channel constants are finalized
     load_batch(threadIdx.x);
     chan_stage<SRC>(a, KC, chl);
+    if constexpr (F16) range_stage<SRC>(a, KC, chl);
     if constexpr (SRC != SRC_DZ)
       if (blockIdx.x == 0 && blockIdx.y == 0) bn_publish(a.in_bn, threadIdx.x);
     __syncthreads();
+    if constexpr (F16) sscale = split_scale(chl, KC);
     const ChanOps kop = chan_ops<SRC>(chl, c);
     store_batch(threadIdx.x, kop);
     for (int base = threadIdx.x + kRowsThreads * FB; base < nfill; base += kRowsThreads * FB) {
@@ -428,7 +479,8 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
     }
   } else {
     constexpr int LP = R / POOL;
-    float ssum[CT] = {}, ssq[CT] = {};
+    float ssum[CT] = {}, ssq[CT] = {}, ymax[CT] = {};
+    const float inv_s = sscale.inv;  // 1 on the f32 path; exact power of two on the split path
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int o = ocol0 + 16 * ct + l16;
@@ -442,14 +494,15 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
           if (row < total) {
             const long i = row / R;
             const int w = (int)(row - i * R) / POOL;
-            float best = acc[r][ct][win * POOL] + bias;
+            float best = acc[r][ct][win * POOL] * inv_s + bias;
             int arg = 0;
 #pragma unroll
             for (int j = 1; j < POOL; ++j) {
-              const float v = acc[r][ct][win * POOL + j] + bias;
+              const float v = acc[r][ct][win * POOL + j] * inv_s + bias;
               if (v > best) { best = v; arg = j; }  // first maximum wins (max_pool1d)
             }
             const float y = best > 0.f ? best : 0.f;
+            ymax[ct] = fmaxf(ymax[ct], y);
             const long oidx = (i * LP + w) * nout + o;
             a.out[oidx] = y;
             a.out_idx[oidx] = (uint8_t)arg;
@@ -471,6 +524,15 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
           acc128_add(acc_at(a.out_acc, nout, 0, o), s);
           acc128_add(acc_at(a.out_acc, nout, 1, o), q);
         }
+      }
+    }
+    if (a.out_range) {  // the output's per-channel maximum: the next layer's split scale
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        float m = ymax[ct];
+        m = fmaxf(m, __shfl_xor(m, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        if (g == 0) atomicMax(a.out_range + ocol0 + 16 * ct + l16, ord_key(m));
       }
     }
   }

@@ -119,6 +119,19 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Value ranges for the split-f16 forwards (conv.hip): per channel, the maximum of x and of -x as
+// ORDERED keys (a float's bits with the sign folded so unsigned order is float order), so producers
+// can merge them with integer atomicMax; a cleared word (0) is below every key and means "no value".
+// One layer's range is [2][kRngC] words.
+constexpr int kRngC = 256;
+__device__ __forceinline__ unsigned ord_key(float f) {
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord_value(unsigned k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
 // bump allocator over a caller-owned workspace (host side)
 struct Arena {
   char* base;

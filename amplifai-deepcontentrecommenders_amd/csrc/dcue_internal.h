@@ -68,6 +68,12 @@ struct RowsArgs {
   int skip_ld;
   float skip_scale;
   int skip_n;  // channels o < skip_n carry a skip gradient (the reference's H; storage pads none)
+  // forward, split-f16: the input layer's value range ([2][kRngC] ordered keys, dcue_common.h) --
+  // the raw track values (layer 1) or the previous layer's ReLU output (min 0) -- from which every
+  // workgroup derives the same power-of-two operand scale; out_range: this layer's output maximum,
+  // merged by the epilogue (nullable)
+  const unsigned* in_range;
+  unsigned* out_range;
 };
 
 struct WgradArgs {
@@ -126,8 +132,9 @@ int launch_bn0_grads(const float* G, const float* E, const float* W1, const floa
 
 // ------------------------------------------------------------------------------- BatchNorm
 // bn0 statistics of the gathered spectrograms (count-weighted) into accumulators [2][128]
+// (acc nullable: the range only) and the raw input's per-mel range into `range` (nullable)
 int launch_input_stats(int src, const void* tracks, const int32_t* item_track, const float* counts,
-                       int M, unsigned long long* acc, hipStream_t s);
+                       int M, unsigned long long* acc, unsigned* range, hipStream_t s);
 // eval mode: running statistics -> mean / invstd / gamma*invstd
 int launch_bn_eval(int C, const float* gamma, const float* rmean, const float* rvar, float* mean,
                    float* invstd, float* a, hipStream_t s);
@@ -268,6 +275,7 @@ void timer_add_recorded(int cls, hipEvent_t a, hipEvent_t b);
 // after the caller's stream `s`; `s` then waits for both
 int comm_exchange_step(dcue_comm* c, float* grad, long late, long n, hipEvent_t side_done, hipStream_t s);
 int comm_world(const dcue_comm* c);
+int comm_divide(const dcue_comm* c, float* grad, long n, hipStream_t s);
 // whether this occurrence of a timed class is one to time (every stride-th; for intervals timed by
 // event records rather than a bound launch, e.g. the RCCL exchange)
 bool timer_take_turn(int cls);

@@ -292,7 +292,14 @@ extern "C" int dcue_plan_launch(dcue_plan* p, const int64_t* users_src, const in
   const dcue_batch& b = p->batch;
   if (users_src == b.users) users_src = nullptr;
   if (item_track_src == b.item_track) item_track_src = nullptr;
-  if (!p->exec) return issue_eager(p, users_src, item_track_src, s, nullptr);
+  if (!p->exec) {
+    TRY(issue_eager(p, users_src, item_track_src, s, nullptr));
+    if (!p->comm) return DCUE_OK;
+    // a bound communicator: the step's dense gradient leaves as the mean over the ranks, whatever
+    // optimizer the caller runs next (SGD, Ranger, or Adam as a separate call)
+    TRY(dcue::comm_exchange_step(p->comm, p->model.grads, p->late, p->n_dense, p->tails[1], s));
+    return dcue::comm_divide(p->comm, p->model.grads, p->n_dense, s);
+  }
   if (users_src)
     DCUE_HIP_CHECK(hipMemcpyAsync(const_cast<int64_t*>(b.users), users_src, sizeof(int64_t) * b.n_rows,
                                   hipMemcpyDeviceToDevice, s));
@@ -375,9 +382,15 @@ extern "C" int dcue_plan_destroy(dcue_plan* p) {
   if (!p) return DCUE_OK;
   // a rolling-flush slice deferred to the next launch must still run: every row has to be replayed
   // within `cap` steps of the current one, or the history ring it needs is overwritten
+  // It goes on the user stream, where the last step's user-table Adam (k_adam_touched) ran: a
+  // normal launch issues it there too (after that step's user tower), and the caller's stream is
+  // not ordered after k_adam_touched (nothing joins it back before the dense Adam).
   if (p->pending_flush >= 0 && p->model.emb_step) {
-    (void)dcue::launch_emb_flush_rows(&p->model, p->pending_flush, p->last_stream);
-    (void)hipStreamSynchronize(p->last_stream);
+    dcue::SidePool* sp = dcue::side_pool();
+    if (sp) {
+      (void)dcue::launch_emb_flush_rows(&p->model, p->pending_flush, sp->st[0]);
+      (void)hipStreamSynchronize(sp->st[0]);
+    }
   }
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->graph) (void)hipGraphDestroy(p->graph);

@@ -166,7 +166,9 @@ class TrainPlan:
         """Data parallelism inside step(): with a distributed.NativeComm bound, each step() also
         all-reduces the dense gradient over RCCL between the backward and Adam (two buckets, the
         larger overlapping the conv-1 weight gradient) and Adam averages it -- one host call per
-        step, as on one GPU. Build the plan with emb_grad_scale = 1/world. None unbinds."""
+        step, as on one GPU. launch() -- and so step() with NativeSGD / NativeRanger, which run
+        their own sweep after it -- makes the same exchange and leaves the mean over the ranks in
+        the gradient. Build the plan with emb_grad_scale = 1/world. None unbinds."""
         if self._handle is None:
             raise RuntimeError("TrainPlan was closed")
         nat.check(self._lib.dcue_plan_set_comm(self._handle, None if comm is None else comm.handle),

@@ -359,8 +359,11 @@ int dcue_comm_allreduce_mean(dcue_comm* comm, float* buf, int64_t n, void* strea
  * dense gradient between the backward and Adam, in two buckets on the communicator's stream: the
  * gradients the side streams finish (everything after DCUE_SEG_LATE) as soon as they are in,
  * overlapping the conv-1 weight gradient on the caller's stream, then bn0/conv-1/bn1 once the step
- * ends; Adam then divides by the world size (dcue_adam_args.grad_div) in its sweep. Collective
- * order is the same on every rank. The plan must have been created with emb_grad_scale = 1/world. */
+ * ends; Adam then divides by the world size (dcue_adam_args.grad_div) in its sweep. dcue_plan_launch
+ * makes the same exchange and divides by the world size itself, so the gradient it leaves is the
+ * mean over the ranks for any optimizer called after it (dcue_optimizer_step, dcue_adam_step with
+ * grad_div 0). Collective order is the same on every rank. The plan must have been created with
+ * emb_grad_scale = 1/world. */
 int dcue_plan_set_comm(dcue_plan* plan, dcue_comm* comm);
 
 /* ------------------------------------------------------------------- live kernel timing */

@@ -39,7 +39,7 @@ static AdamScalars scalars(double lr, double b1, double b2, double eps, int t) {
   const double w = 1.0 - b1;
   AdamScalars s;
   s.neg_step = (float)(-(lr / bc1));
-  s.lerp_c = w < 0.5 ? (float)w : (float)w - 1.0f;
+  s.lerp_c = w < 0.5 ? (float)w : -(1.0f - (float)w);  // as launch_adam (sign bit = base g)
   s.b2 = (float)b2;
   s.one_m_b2 = (float)(1.0 - b2);
   s.bc2_sqrt = (float)std::pow(bc2, 0.5);
@@ -63,7 +63,9 @@ int main(int argc, char** argv) {
   double worst = 0.0;
   for (long c = 0; c < cases; ++c) {
     const int cap = 1 + pick(DCUE_MAX_LOG_CAP);
-    const double b1 = pick(4) ? 0.9 : 0.5 + 0.49 * U(rng);
+    // beta1 <= 0.5 (lerp weight >= 0.5, base g; 0 -> weight 1) as well as the usual > 0.5
+    const double b1s[4] = {0.0, 0.3, 0.5, 0.5 + 0.49 * U(rng)};
+    const double b1 = pick(3) ? 0.9 : b1s[pick(4)];
     const double b2 = pick(3) ? (pick(2) ? 0.99 : 0.999) : 0.9 + 0.0999 * U(rng);
     const double eps = pick(4) ? 1e-8 : logu(-12, -4);
     const double lr_hi = logu(-5, -1);
@@ -119,7 +121,8 @@ int main(int argc, char** argv) {
     float rp[4], rm[4], rv[4];
     for (int w = 0; w < 4; ++w) {
       rp[w] = p[w]; rm[w] = m[w]; rv[w] = v[w];
-      for (int j = j0; j <= T; ++j) adam_zero_elem(rp[w], rm[w], rv[w], hs[j % cap]);
+      // the full Adam step with g = +0 -- what the dense sweep computes for a row outside the batch
+      for (int j = j0; j <= T; ++j) adam_elem(rp[w], 0.f, rm[w], rv[w], hs[j % cap]);
     }
     // margin: where replay_run switches, the largest skipped update relative to 2^(e-25)
     if (b.ok) {

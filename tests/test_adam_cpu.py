@@ -24,7 +24,8 @@ def _inputs(n, steps, seed):
 
 
 @pytest.mark.parametrize("lr,betas,wd", [(1e-5, (0.9, 0.99), 0.0), (1e-3, (0.9, 0.999), 1e-4),
-                                         (3e-4, (0.3, 0.99), 1e-2)])
+                                         (3e-4, (0.3, 0.99), 1e-2), (3e-4, (0.3, 0.99), 0.0),
+                                         (1e-3, (0.0, 0.99), 0.0), (1e-3, (0.5, 0.99), 0.0)])
 def test_restatement_matches_torch_adam_bit_exact(lr, betas, wd):
     n, steps = 40_003, 4
     p0, gs = _inputs(n, steps, 1)

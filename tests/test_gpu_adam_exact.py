@@ -31,7 +31,11 @@ def _snapshot(net, opt):
 
 
 @pytest.mark.parametrize("defer,wd,betas", [(False, 0.0, (0.9, 0.99)), (True, 0.0, (0.9, 0.99)),
-                                            (False, 1e-3, (0.9, 0.999)), (True, 1e-3, (0.3, 0.99))])
+                                            (False, 1e-3, (0.9, 0.999)), (True, 1e-3, (0.3, 0.99)),
+                                            # beta1 <= 0.5: the lerp's base is g (0: weight 1, m = g);
+                                            # the deferred replay's zero-gradient steps must follow it
+                                            (True, 0.0, (0.3, 0.99)), (True, 0.0, (0.0, 0.99)),
+                                            (False, 0.0, (0.0, 0.99)), (True, 0.0, (0.5, 0.99))])
 def test_native_adam_bit_exact_with_restatement(defer, wd, betas):
     from dcrecommend import _native as nat
     from dcrecommend.dcue.dcue import DCUENet

@@ -169,3 +169,41 @@ def test_bench_launches_its_own_ranks():
     assert r["n_gpus"] == 2 and r["config"]["process_group_world"] == 2
     assert r["config"]["global_batch"] == 2 * r["config"]["batch_per_gpu"]
     assert r["value"] > 0 and r["catalogue"]["rows_per_s"] > 0
+
+
+@pytest.mark.parametrize("kind", ["sgd", "ranger"])
+def test_plan_launch_with_comm_feeds_other_optimizers_world1(kind):
+    """TrainPlan.step with NativeSGD / NativeRanger runs launch() then the optimizer's own
+    sweep. With a communicator bound, launch() now exchanges the dense gradient and leaves the mean
+    (dcue_plan_launch + comm_divide), so no optimizer sees an un-averaged gradient. At world 1 the
+    step is bit-exact with the unbound one (the exchange path runs; the mean is the identity)."""
+    import torch.distributed as dist
+    from dcrecommend import distributed as D
+    from dcrecommend.dcue.plan import TrainPlan
+    from dcrecommend.optim import NativeRanger, NativeSGD
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1)
+    try:
+        comm = D.NativeComm()
+        a, b = _pair_nets()
+        gen = torch.Generator(device="cuda:0").manual_seed(12)
+        tracks = torch.randn((48, 131, 128), generator=gen, device="cuda:0").half()
+        mk = ((lambda ps: NativeSGD(ps, 1e-3, momentum=0.9, nesterov=True)) if kind == "sgd"
+              else (lambda ps: NativeRanger(ps, 1e-3)))
+        opts = [mk(n.parameters()) for n in (a, b)]
+        B, N = 8, 3
+        plans = [TrainPlan(n, tracks, B, N, mt_state=None, optimizer=o) for n, o in zip((a, b), opts)]
+        plans[0].set_comm(comm)
+        for _ in range(4):
+            users = torch.randint(0, 40, (B,), generator=gen, device="cuda:0")
+            items = torch.randint(0, 48, (B * (1 + N),), generator=gen, device="cuda:0").to(torch.int32)
+            for p in plans:
+                p.step(users, items)
+        torch.cuda.synchronize()
+        for k, v in a.state_dict().items():
+            assert torch.equal(v, b.state_dict()[k]), k
+        assert torch.equal(a._flat["G"], b._flat["G"])
+        for p in plans:
+            p.close()
+        comm.close()
+    finally:
+        dist.destroy_process_group()

@@ -119,3 +119,31 @@ def test_timer_counts_eager_and_plan_launches():
             plan.close()
     finally:
         nat.timer_enable(nat.TIMED_CONV1_WGRAD, False)
+
+
+def test_destroy_right_after_step_keeps_deferred_table_exact():
+    """A deferred-embedding plan closed straight after plan.step(): the rolling-flush slice the next
+    launch would have issued runs at destruction, ordered after the last step's user-table Adam on
+    the user stream. The table and its moments then equal a dense-sweep run bit for bit."""
+    from dcrecommend.dcue.plan import TrainPlan
+    from dcrecommend.optim import NativeAdam
+    n_users, B, N, n_tracks = 40, 8, 3, 48
+    deferred, dense = _nets()
+    gen = torch.Generator(device=DEV).manual_seed(13)
+    tracks = torch.randn((n_tracks, 131, 128), generator=gen, device=DEV).half()
+    batches = [(torch.randint(0, n_users, (B,), generator=gen, device=DEV),
+                torch.randint(0, n_tracks, (B,), generator=gen, device=DEV).to(torch.int32)) for _ in range(7)]
+    outs = []
+    for net, defer in ((deferred, True), (dense, False)):
+        opt = NativeAdam(net.parameters(), 1e-3, (0.9, 0.99), 1e-8, 0, defer_embedding=defer, flush_every=4)
+        plan = TrainPlan(net, tracks, B, N, mt_state=_mt(21), optimizer=opt)
+        for u, it in batches:
+            plan.step(u, it)
+        plan.close()  # no synchronisation in between
+        opt.flush() if defer else None
+        torch.cuda.synchronize()
+        outs.append(_state(net, opt))
+    for k in outs[1]:
+        if k == "grad":
+            continue
+        assert torch.equal(outs[0][k], outs[1][k]), k
