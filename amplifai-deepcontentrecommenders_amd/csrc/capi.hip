@@ -185,6 +185,7 @@ long wpack_offset(const dcue_dims* d, int l, bool bwd) {
 // pointers into the caller's workspace
 struct Ws {
   float* counts;
+  int32_t *copy_ptr, *copy_idx;  // gather layout: per-item copy lists (StepPrologue), M <= kCopyListMaxItems
   float *mean[6], *invstd[6], *a[6];
   // exact BN sums (bnacc.h), [6 layers][2 sums][Cmax][2 words]: forward stats, backward sums
   unsigned long long *bnacc, *bnbacc;
@@ -203,7 +204,7 @@ struct Ws {
   float* g[6];
   float *dh1, *de;
   float *wpart[3], *bpart[3], *G, *S;  // wgrad partials: one set per wgrad stream
-  float *wpm[4], *bpm[4];                // k_conv_wgrad_multi's partials, layers 2..5
+  float *wpm[5], *bpm[5];                // k_conv_wgrad_multi's partials, layers 2..5 and the fc
   float* xhat0;          // [M][kXp][128] bn0-normalised, zero-padded input: conv-1 wgrad's X operand
   float* dx1;            // [M][33][H] BN1 backward at the pooled positions: conv-1 wgrad's dz operand
   // towers without BN: the BN operands every kernel reads become the identity (mean 0, a = invstd
@@ -231,6 +232,8 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   const int H = st_hidden(d), D = st_feature(d), E = d->user_embdim;
   const int Cmax = H > kMels ? H : kMels;
   w->counts = ar.take<float>(M);
+  w->copy_ptr = ar.take<int32_t>(M + 1);
+  w->copy_idx = ar.take<int32_t>((long)B * (N + 1));
   for (int l = 0; l < 6; ++l) {
     const int C = bn_channels(d, l);
     w->mean[l] = ar.take<float>(C);
@@ -278,10 +281,10 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
     w->wpart[i] = ar.take<float>(wp);
     w->bpart[i] = ar.take<float>(bp);
   }
-  for (int l = 2; l <= 5; ++l) {
-    const int cin = H, cout = l == 5 ? D : H;
+  for (int l = 2; l <= 6; ++l) {  // 6: the fc layer (a 1x1 conv over bn5(y5), D -> D)
+    const int cin = l == 6 ? D : H, cout = l >= 5 ? D : H;
     const long nch = wgrad_nchunk(l, M, cout, cin);
-    w->wpm[l - 2] = ar.take<float>(nch * cout * cin * layer_geom(l).ks);
+    w->wpm[l - 2] = ar.take<float>(nch * cout * cin * layer_geom(l == 6 ? 5 : l).ks);
     w->bpm[l - 2] = ar.take<float>(nch * cout);
   }
   w->G = ar.take<float>((long)H * 4 * kMels);
@@ -464,6 +467,25 @@ int user_forward(const Ctx& c, const Ws& w, const int64_t* users, int B, float* 
   return launch_tgemm(1, 0, g, s);
 }
 
+// whether a gather batch gets per-item copy lists (the prologue's histogram path)
+bool copy_lists(const dcue_batch* b) {
+  return b->layout == DCUE_LAYOUT_GATHER && b->n_items <= kCopyListMaxItems;
+}
+
+// counts (+ copy lists) of a batch issued outside a plan: the prologue kernel without draws, so
+// eager steps and plan replays sum the item gradients in the same order
+int batch_counts(const dcue_batch* b, const Ws& w, hipStream_t s) {
+  if (!copy_lists(b)) return launch_item_counts(b, w.counts, s);
+  StepPrologue p = {};
+  p.B = b->n_rows; p.N = b->n_neg; p.M = b->n_items;
+  p.gather = 1;
+  p.neg = const_cast<int32_t*>(b->neg_item);
+  p.counts = w.counts;
+  p.copy_ptr = w.copy_ptr;
+  p.copy_idx = w.copy_idx;
+  return launch_step_prologue(p, s);
+}
+
 int check_batch(const dcue_batch* b) {
   if (!b || !b->users || !b->item_track || b->n_rows <= 0 || b->n_neg < 0 || b->n_items <= 0)
     return DCUE_ERR_INVALID;
@@ -604,7 +626,7 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   hipEvent_t ev_in = nullptr;
   TRY(fork_point(sp, s, &ev_in));
   HPROF("capi:3");
-  if (!o.prologue_done) TRY(launch_item_counts(b, w.counts, s));
+  if (!o.prologue_done) TRY(batch_counts(b, w, s));
   HPROF("capi:4");
   TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s,
                    o.prologue_done, o.input_stats_done && o.prologue_done, o.clear_bn0));
@@ -672,6 +694,10 @@ int step_prologue(const dcue_model* m, const dcue_batch* b, void* ws, size_t ws_
   p.items_dst = const_cast<int32_t*>(b->item_track); p.items_src = items_src;
   p.zero = w.bnacc; p.nzero = w.nzero;
   p.counts = w.counts;
+  if (copy_lists(b)) {
+    p.copy_ptr = w.copy_ptr;
+    p.copy_idx = w.copy_idx;
+  }
   return launch_step_prologue(p, s);
 }
 
@@ -693,6 +719,10 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   const double copies = (double)B * (1 + N);
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
   if (o.fuse_score && dscores) return DCUE_ERR_INVALID;
+  // the item gradients' copy lists: the plan's (current slot), else the workspace's (eager steps and
+  // graph plans built them in the forward / prologue)
+  const int32_t* cptr = o.copy_ptr ? o.copy_ptr : (copy_lists(b) ? w.copy_ptr : nullptr);
+  const int32_t* cidx = o.copy_ptr ? o.copy_idx : (copy_lists(b) ? w.copy_idx : nullptr);
   if (o.emb_adam && (o.emb_adam->parts & ~DCUE_ADAM_EMBEDDING)) return DCUE_ERR_INVALID;
   SidePool* sp = side_pool();
   if (!sp) return DCUE_ERR_HIP;
@@ -729,7 +759,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   if (c.res) {  // df; then the fc input gradient split: g5 = df W[:, 4H:] (+ BN5's sums) and the
                 // time-pooled blocks' dtp = df W[:, :4H]
     TRY(launch_item_grad(w.dfcopy, b, D, w.df, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                         o.fuse_score ? w.rowsum : nullptr, w.loss, s));
+                         o.fuse_score ? w.rowsum : nullptr, w.loss, cptr, cidx, s));
     TGemmArgs g = {};
     g.M = M; g.N = D; g.K = D;
     g.A = w.df; g.sam = D; g.sak = 1;
@@ -748,7 +778,8 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   } else {  // per-item feature gradients df, then (same kernel) the fc input gradient g5 = df W and BN5's sums
     // (no fork point here: the fc weight gradient waits with the layer 3-5 weight gradients, below)
     TRY(launch_item_grad(w.dfcopy, b, D, w.df, c.P(SEG_FC_W), w.g[5], bn_acc(w.bnbacc, w.cmax, 5),
-                         w.y[5], w.mean[5], w.invstd[5], o.fuse_score ? w.rowsum : nullptr, w.loss, s));
+                         w.y[5], w.mean[5], w.invstd[5], o.fuse_score ? w.rowsum : nullptr, w.loss,
+                         cptr, cidx, s));
     HPROF("capi:15");
   }
   for (int l = 5; l >= 2; --l) {  // dgrad chain: g_l (+ BN_l sums) -> g_{l-1} (+ BN_{l-1} sums)
@@ -835,33 +866,39 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   TRY(issue_wgrad(1, s, 2, &tail[0]));
   HPROF("capi:22");
 
-  {  // fc weight gradient: dW[n][k] = sum_m df[m][n] bn5(y5)[m][k], db = sum_m df
-    // df is final after the item gradient; the res towers fork right there, the others at the
-    // layer 3-5 weight gradients' fork point (one fork point fewer on the chain)
-    TRY(wait_point(sw[1], c.res ? ev_layer[5] : ev_layer[3]));
+  if (c.res) {  // fc weight gradient of the res towers: dW[n][k] = sum_m df[m][n] xfc[m][k], db = sum df
+    // over the concatenated fc input (the other towers' fc rides in the layer 3-5 launch, below)
+    TRY(wait_point(sw[1], ev_layer[5]));
     HPROF("capi:23");
     TGemmArgs g = {};
     g.M = D; g.N = c.FI; g.K = M;
     g.A = w.df; g.sam = 1; g.sak = D;
     g.C = c.Gd(SEG_FC_W); g.scm = c.FI; g.scn = 1;
     g.rowsum = c.Gd(SEG_FC_B);
-    if (c.res) {  // dW[n][k] = sum_m df[m][n] xfc[m][k] over the concatenated fc input
-      g.B = w.xfc; g.sbk = c.FI; g.sbn = 1;
-      TRY(launch_tgemm(0, 0, g, sw[1]));
-    } else {
-      g.B = w.y[5]; g.sbk = D; g.sbn = 1;
-      g.bmean = w.mean[5]; g.ba = w.a[5]; g.bbeta = c.beta(w, 5);
-      TRY(launch_tgemm(0, 2, g, sw[1]));
-    }
+    g.B = w.xfc; g.sbk = c.FI; g.sbn = 1;
+    TRY(launch_tgemm(0, 0, g, sw[1]));
     HPROF("capi:24");
   }
   // (wgrad of layer l reads g_l, which dgrad l+1 produced: ev_layer[l]) layers 5..3 in one launch
   // on wgrad stream 0 once dgrad 4 is done (beside dgrad 3-2); layer 2 on wgrad stream 1 (behind
   // xhat0 and the fc weight gradient) once dgrad 3 is (beside dgrad 2 and the conv-1 tail); each
   // + one reduce launch.
-  auto issue_multi = [&](int lo, int hi, hipStream_t so, hipEvent_t after, hipEvent_t* tl) -> int {
+  auto issue_multi = [&](int lo, int hi, bool with_fc, hipStream_t so, hipEvent_t after, hipEvent_t* tl) -> int {
     TRY(wait_point(so, after));
     WgradMulti mw = {};
+    if (with_fc) {  // fc: dW[n][k] = sum_m df[m][n] bn5(y5)[m][k], db = sum_m df (df final since item_grad)
+      const int j = mw.n++;
+      mw.layer[j] = 6;
+      WgradArgs& wa = mw.a[j];
+      wa.xsrc = w.y[5];
+      wa.x_mean = w.mean[5]; wa.x_a = w.a[5]; wa.x_beta = c.beta(w, 5);
+      wa.g_l = w.df;
+      wa.M = M; wa.cout = D; wa.cin = D;
+      wa.wpart = w.wpm[4]; wa.bpart = w.bpm[4];
+      mw.nchunk[j] = wgrad_nchunk(6, M, D, D);
+      mw.dW[j] = c.Gd(SEG_FC_W);
+      mw.db[j] = c.Gd(SEG_FC_B);
+    }
     for (int l = hi; l >= lo; --l) {
       const LayerGeom gm = layer_geom(l);
       const int j = mw.n++;
@@ -885,8 +922,8 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(launch_conv_wgrad_multi(mw, so));
     return fk.done();
   };
-  TRY(issue_multi(3, 5, sw[0], ev_layer[3], &tail[2]));
-  TRY(issue_multi(2, 2, sw[1], ev_layer[2], &tail[3]));
+  TRY(issue_multi(3, 5, !c.res, sw[0], ev_layer[3], &tail[2]));
+  TRY(issue_multi(2, 2, false, sw[1], ev_layer[2], &tail[3]));
   HPROF("capi:25");
   // user tower (userembedding.py:33-44 backward), the compact embedding rows, and -- when the step
   // carries it -- the user table's Adam step (it needs nothing from the item tower)

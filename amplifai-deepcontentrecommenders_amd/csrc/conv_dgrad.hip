@@ -1,0 +1,49 @@
+// Input gradients of conv layers 2..5 (k_conv_rows MODE 1): the launch dispatch. Kernel body:
+// conv_rows.h.
+#include "conv_rows.h"
+
+namespace dcue {
+
+// dgrad of layer L: rows = (item, input position t' < Lin_L), slab = layer-L conv positions
+// [0, Lp*pool) carrying dz, taps reversed (PADL = ks-1-pad).
+template <int L, int KC, int TW>
+static int dgrad_layer_tw(const RowsArgs& a, hipStream_t s) {
+  constexpr LayerGeom gm = layer_geom(L);
+  return run_rows<1, SRC_DZ, KC, gm.ks, gm.ks - 1 - gm.pad, gm.lp * gm.pool, gm.lin, 1, TW, gm.lp,
+                  gm.pool>(a, s);
+}
+
+template <int L, int KC>
+static int dgrad_layer(const RowsArgs& a, hipStream_t s) {
+  constexpr LayerGeom gm = layer_geom(L);
+  constexpr int TWMAX = max_tw(gm.lin, gm.ks, KC);
+  const int tw = choose_tw((long)a.M * gm.lin, TWMAX);
+  if constexpr (TWMAX >= 8) if (tw == 8) return dgrad_layer_tw<L, KC, 8>(a, s);
+  if constexpr (TWMAX >= 4) if (tw == 4) return dgrad_layer_tw<L, KC, 4>(a, s);
+  if constexpr (TWMAX >= 3) if (tw == 3) return dgrad_layer_tw<L, KC, 3>(a, s);
+  if constexpr (TWMAX >= 2) if (tw == 2) return dgrad_layer_tw<L, KC, 2>(a, s);
+  return dgrad_layer_tw<L, KC, 1>(a, s);
+}
+
+template <int L>
+static int dgrad_kc(int kc, const RowsArgs& a, hipStream_t s) {
+  switch (kc) {
+    case 32: return dgrad_layer<L, 32>(a, s);
+    case 64: return dgrad_layer<L, 64>(a, s);
+    case 128: return dgrad_layer<L, 128>(a, s);
+    case 256: return dgrad_layer<L, 256>(a, s);
+    default: return DCUE_ERR_UNSUPPORTED;
+  }
+}
+
+int launch_conv_dgrad(int layer, int kc, const RowsArgs& a, hipStream_t s) {
+  switch (layer) {
+    case 2: return dgrad_kc<2>(kc, a, s);
+    case 3: return dgrad_kc<3>(kc, a, s);
+    case 4: return dgrad_kc<4>(kc, a, s);
+    case 5: return dgrad_kc<5>(kc, a, s);
+    default: return DCUE_ERR_INVALID;
+  }
+}
+
+}  // namespace dcue

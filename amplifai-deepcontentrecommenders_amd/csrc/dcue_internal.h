@@ -101,15 +101,17 @@ struct WgradArgs {
 
 // weight gradients of n conv layers (of 2..5) in one launch, then their chunk sums in a second one
 // (the host fills n, layer[], a[], nchunk[], dW[], db[]; the launcher derives the block ranges)
+// slot layer 6 = the fc layer (dW = df^T bn5(y5), db = sum df; a 1x1 conv with dz = df, no BN)
+constexpr int kWgradMultiMax = 5;
 struct WgradMulti {
   int n;
-  int layer[4];
-  WgradArgs a[4];  // one per slot, each with its own wpart / bpart
-  int nchunk[4];
-  float *dW[4], *db[4];
-  int kt[4], ot[4];  // kc / o tiles per layer
-  int start[5];      // wgrad block ranges
-  int rstart[5];     // reduce block ranges
+  int layer[kWgradMultiMax];
+  WgradArgs a[kWgradMultiMax];  // one per slot, each with its own wpart / bpart
+  int nchunk[kWgradMultiMax];
+  float *dW[kWgradMultiMax], *db[kWgradMultiMax];
+  int kt[kWgradMultiMax], ot[kWgradMultiMax];  // kc / o tiles per layer
+  int start[kWgradMultiMax + 1];      // wgrad block ranges
+  int rstart[kWgradMultiMax + 1];     // reduce block ranges
 };
 int launch_conv_wgrad_multi(WgradMulti w, hipStream_t s);
 
@@ -170,6 +172,8 @@ inline WpackLayout wpack_layout(const dcue_dims* dm) {
 // copies per item (BatchNorm weights); in-batch negatives are found by wave ballots over neg_item
 int launch_item_counts(const dcue_batch* b, float* counts, hipStream_t s);
 
+// gather-layout batches of at most this many items get per-item copy lists (StepPrologue)
+constexpr int kCopyListMaxItems = 2048;
 // step prologue of a plan (sampler.hip): batch copies, accumulator clear, in-batch draw, counts
 struct StepPrologue {
   dcue_mt_state* mt;  // null: no draw (neg already given, or catalogue)
@@ -188,6 +192,11 @@ struct StepPrologue {
   const int32_t* copy_src;   // nullable: copy_dst[0..ncopy) = copy_src[..] (published negatives)
   int32_t* copy_dst;
   long ncopy;
+  // nullable (gather layout): each item's copies as a CSR for the item-gradient sums -- copy_ptr[M+1],
+  // copy_idx[B(N+1)] holding copy indices row*(N+1)+c, the positive first, then the negatives that
+  // drew the item in (row, j) order
+  int32_t* copy_ptr;
+  int32_t* copy_idx;
 };
 int launch_step_prologue(const StepPrologue& p, hipStream_t s);
 
@@ -222,10 +231,12 @@ int launch_score_fused(const float* uf, const float* f, const dcue_batch* b, int
 int launch_score_bwd(const float* uf, const float* f, const dcue_batch* b, int d,
                      const float* dscores, const float* cosv, const float* norms, float* du,
                      float* dfcopy, hipStream_t s);
-// per-item feature gradients; with fcW also the fc input gradient g5 = df W and BN5's backward sums
+// per-item feature gradients; with fcW also the fc input gradient g5 = df W and BN5's backward sums.
+// copy_ptr / copy_idx (nullable): the gather layout's per-item copy lists from the step prologue
 int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df, const float* fcW, float* g5,
                      unsigned long long* acc5, const float* y5, const float* mean5, const float* invstd5,
-                     const float* rowsum, float* loss, hipStream_t s);
+                     const float* rowsum, float* loss, const int32_t* copy_ptr, const int32_t* copy_idx,
+                     hipStream_t s);
 int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float scale,
                     float* emb_grad, int32_t* slot, int64_t* emb_rows, dcue_emb_log* log,
                     hipStream_t s);
@@ -343,6 +354,9 @@ struct StepOpts {
   bool input_stats_done = false;
   const float* xhat0 = nullptr;
   bool clear_bn0 = false;  // the block holds bn0 sums of an announced batch this step did not use
+  // the step's per-item copy lists (gather layout, built by the plan's prologue; StepPrologue)
+  const int32_t* copy_ptr = nullptr;
+  const int32_t* copy_idx = nullptr;
 };
 // A batch's model-independent item inputs, issued ahead of its step (plans): bn0's count-weighted
 // batch sums into the accumulator block `acc` (cleared, counts written, on the same stream before)

@@ -35,6 +35,8 @@ struct dcue_plan {
   void* ahead = nullptr;
   int32_t* neg[2] = {};
   float* counts[2] = {};
+  int32_t* copy_ptr[2] = {};  // per-item copy lists (gather layout, StepPrologue)
+  int32_t* copy_idx[2] = {};
   unsigned long long* acc[2] = {};
   long nacc = 0;
   dcue_mt_state* mt_ahead = nullptr;
@@ -99,6 +101,8 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
     q.neg = inbatch ? p->neg[slot] : const_cast<int32_t*>(b0.neg_item);
     q.zero = p->acc[slot]; q.nzero = p->nacc;
     q.counts = p->counts[slot];
+    q.copy_ptr = p->copy_ptr[slot];
+    q.copy_idx = p->copy_idx[slot];
     return q;
   };
   if (p->launches == 0) {  // the first step's inputs, on the caller's stream
@@ -142,6 +146,8 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   o.fuse_score = true;
   o.emb_adam = emb_adam;
   o.counts = p->counts[cur];
+  o.copy_ptr = p->copy_ptr[cur];
+  o.copy_idx = p->copy_idx[cur];
   o.acc = p->acc[cur];
   o.input_stats_done = ahead;
   o.xhat0 = ahead ? p->xh[cur] : nullptr;
@@ -206,11 +212,15 @@ extern "C" int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const 
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t bneg = al(sizeof(int32_t) * (nneg > 0 ? nneg : 1)), bcnt = al(sizeof(float) * M),
                  bacc = al(sizeof(unsigned long long) * nacc), bmt = al(sizeof(dcue_mt_state));
+    // copy lists: in-batch plans (the prologue's histogram path holds M <= 2048 items)
+    const bool lists = (cfg->flags & DCUE_PLAN_SAMPLE_INBATCH) && M <= dcue::kCopyListMaxItems;
+    const size_t bptr = lists ? al(sizeof(int32_t) * (M + 1)) : 0,
+                 bidx = lists ? al(sizeof(int32_t) * ((size_t)B * (N + 1))) : 0;
     // lookahead slots (plans of BatchNorm towers): xhat0 per slot
     const bool look = dcue::tower_has_bn(&m->dims);
     const size_t bxh = look ? al(sizeof(float) * (size_t)(M + 1) * dcue::kXp * dcue::kMels) : 0;
     void* mem = nullptr;
-    DCUE_HIP_CHECK(hipMalloc(&mem, 2 * (bneg + bcnt + bacc + bxh) + bmt));
+    DCUE_HIP_CHECK(hipMalloc(&mem, 2 * (bneg + bcnt + bacc + bxh + bptr + bidx) + bmt));
     dcue_plan* p = new dcue_plan;
     p->model = *m;
     p->batch = *b;
@@ -225,6 +235,10 @@ extern "C" int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const 
       p->counts[i] = (float*)q; q += bcnt;
       p->acc[i] = (unsigned long long*)q; q += bacc;
       if (bxh) { p->xh[i] = (float*)q; q += bxh; }
+      if (lists) {
+        p->copy_ptr[i] = (int32_t*)q; q += bptr;
+        p->copy_idx[i] = (int32_t*)q; q += bidx;
+      }
     }
     p->mt_ahead = (dcue_mt_state*)q;
     p->nacc = nacc;

@@ -758,10 +758,159 @@ __global__ __launch_bounds__(256) void k_item_grad(const float* __restrict__ dfc
   }
 }
 
+// IT items per workgroup: the fc weight is staged once per IT items (k_item_grad stages it once per
+// item: 64 KB of L2 reads per item, 86 MB a catalogue step, which made that kernel 80 us), and
+// BN5's sums leave the block once per column. Item i's copies: catalogue, its one copy; gather, the
+// prologue's list (positive first, then (row, j) order). Wave w sums items w, w+4, ... copy by copy
+// in list order (eight row loads in flight); the fc input gradient g5 = df W splits k in halves over
+// the two thread halves, items inner (fixed order); BN5's per-column sums add the block's items in
+// order, then enter the exact accumulators.
+template <int IT, bool WLDS>
+__global__ __launch_bounds__(256) void k_item_grad_multi(const float* __restrict__ dfcopy, dcue_batch b, int d,
+                                                         float* df, const int32_t* __restrict__ copy_ptr,
+                                                         const int32_t* __restrict__ copy_idx, ItemGradFc fc) {
+  critical_path_priority();
+  __shared__ float dfs[IT][256];
+  __shared__ float part[2][IT][128];
+  __shared__ float rs[1024];
+  extern __shared__ __attribute__((aligned(16))) float wl[];  // [d][d] when WLDS
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i0 = blockIdx.x * IT;
+  const int N = b.n_neg, B = b.n_rows, M = b.n_items;
+  const bool gather = b.layout != DCUE_LAYOUT_CATALOGUE;
+  const int per = (d + 63) / 64;
+  if constexpr (WLDS) {
+    if (fc.W) {
+      const int n4 = d * d / 4;
+      for (int q = threadIdx.x; q < n4; q += blockDim.x)
+        reinterpret_cast<float4*>(wl)[q] = reinterpret_cast<const float4*>(fc.W)[q];
+    }
+  }
+  if (fc.rowsum && blockIdx.x == 0)
+    for (int r = threadIdx.x; r < B; r += blockDim.x) rs[r] = fc.rowsum[r];
+  for (int it = wave; it < IT; it += 4) {
+    const int i = i0 + it;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (i < M) {
+      int c0, c1;
+      long cat_idx = 0;
+      if (gather) {
+        c0 = copy_ptr[i];
+        c1 = copy_ptr[i + 1];
+      } else {
+        c0 = 0;
+        c1 = 1;
+        cat_idx = i < B ? (long)i * (N + 1) : (long)((i - B) / N) * (N + 1) + 1 + (i - B) % N;
+      }
+      constexpr int kRows = 8;
+      for (int qb = c0; qb < c1; qb += kRows) {
+        long ci[kRows];
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) ci[r] = qb + r < c1 ? (gather ? (long)copy_idx[qb + r] : cat_idx) : -1;
+        float v[kRows][4];
+#pragma unroll
+        for (int r = 0; r < kRows; ++r)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int k = lane + 64 * e;
+            v[r][e] = (ci[r] >= 0 && e < per && k < d) ? dfcopy[ci[r] * d + k] : 0.f;
+          }
+#pragma unroll
+        for (int r = 0; r < kRows; ++r)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[e] += v[r][e];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = lane + 64 * e;
+        if (e < per && k < d) df[(long)i * d + k] = acc[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = lane + 64 * e;
+      if (e < per && k < d) dfs[it][k] = acc[e];
+    }
+  }
+  if (fc.W) {
+    __syncthreads();
+    // g5[i][n] = sum_k df[i][k] W[k][n], k in two halves (first + second); d <= 128 here
+    const int hk = (d + 1) / 2;
+    for (int t = threadIdx.x; t < 2 * d; t += blockDim.x) {
+      const int n = t % d, h = t / d;
+      const int k0 = h * hk, k1 = h ? d : hk;
+      float g[IT];
+#pragma unroll
+      for (int it = 0; it < IT; ++it) g[it] = 0.f;
+      for (int k = k0; k < k1; ++k) {
+        const float w = WLDS ? wl[k * d + n] : fc.W[(long)k * d + n];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) g[it] += dfs[it][k] * w;
+      }
+#pragma unroll
+      for (int it = 0; it < IT; ++it) part[h][it][n] = g[it];
+    }
+    __syncthreads();
+    if (threadIdx.x < d) {
+      const int n = threadIdx.x;
+      const float mu5 = fc.mean5[n], is5 = fc.invstd5[n];
+      float sg = 0.f, sgx = 0.f;
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int i = i0 + it;
+        if (i < M) {
+          const float g = part[0][it][n] + part[1][it][n];
+          fc.g5[(long)i * d + n] = g;
+          sg += g;
+          sgx += g * ((fc.y5[(long)i * d + n] - mu5) * is5);
+        }
+      }
+      acc128_add(acc_at(fc.acc, d, 0, n), sg);
+      acc128_add(acc_at(fc.acc, d, 1, n), sgx);
+    }
+  }
+  if (fc.rowsum && blockIdx.x == 0) {  // loss = mean of the row sums in row order (k_loss_mean's sums)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float s = 0.f;
+      for (int r = 0; r < B; ++r) s += rs[r];
+      *fc.loss = s / (float)B;
+    }
+  }
+}
+
+template <int IT, bool WLDS>
+static int item_grad_multi(const float* dfcopy, const dcue_batch* b, int d, float* df, const int32_t* copy_ptr,
+                           const int32_t* copy_idx, const ItemGradFc& fc, size_t lds, hipStream_t s) {
+  static bool attr = false;
+  if (WLDS && !attr) {
+    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_item_grad_multi<IT, WLDS>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(float) * 128 * 128)));
+    attr = true;
+  }
+  DCUE_LAUNCH((k_item_grad_multi<IT, WLDS>), dim3((unsigned)((b->n_items + IT - 1) / IT)), dim3(256), lds, s,
+              dfcopy, *b, d, df, copy_ptr, copy_idx, fc);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
 int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df, const float* fcW, float* g5,
                      unsigned long long* acc5, const float* y5, const float* mean5, const float* invstd5,
-                     const float* rowsum, float* loss, hipStream_t s) {
+                     const float* rowsum, float* loss, const int32_t* copy_ptr, const int32_t* copy_idx,
+                     hipStream_t s) {
   if (d > 256 || (rowsum && b->n_rows > 1024)) return DCUE_ERR_UNSUPPORTED;
+  const bool gather = b->layout == DCUE_LAYOUT_GATHER;
+  if ((!gather || copy_ptr) && (!fcW || d <= 128)) {  // multi-item workgroups
+    const ItemGradFc fc = {rowsum, loss, fcW, g5, acc5, y5, mean5, invstd5};
+    const bool wlds = fcW && d % 4 == 0;
+    const size_t lds = wlds ? sizeof(float) * d * d : 0;
+    // many items (catalogue M = B(1+N)): 16 per workgroup; a few (in-batch M = B): 4
+    if (b->n_items >= 512)
+      return wlds ? item_grad_multi<16, true>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s)
+                  : item_grad_multi<16, false>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s);
+    return wlds ? item_grad_multi<4, true>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s)
+                : item_grad_multi<4, false>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s);
+  }
   if (b->layout == DCUE_LAYOUT_GATHER && (long)b->n_rows * b->n_neg + 1 > kItemGradCap) return DCUE_ERR_UNSUPPORTED;
   const ItemGradFc fc = {rowsum, loss, fcW, g5, acc5, y5, mean5, invstd5};
   if (fcW && d <= kItemGradWLds && d % 4 == 0) {

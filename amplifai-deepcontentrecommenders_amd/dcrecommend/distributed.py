@@ -106,6 +106,23 @@ def max_over_ranks(value, device, group=None):
     return float(t.item())
 
 
+def replica_checksums(buf, group=None):
+    """Whether every rank holds the same dense replica: a per-rank fingerprint of `buf` (fp64 sum,
+    sum of squares and a position-weighted sum, so a permutation or a sign flip shows), reduced
+    with MIN and MAX over the ranks. Returns (identical, fingerprint min, fingerprint max)."""
+    x = buf.detach().double().reshape(-1)
+    w = torch.arange(1, x.numel() + 1, dtype=torch.float64, device=x.device) / max(x.numel(), 1)
+    fp = torch.stack([x.sum(), (x * x).sum(), (x * w).sum()])
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        v = fp.cpu().tolist()
+        return True, v, v
+    lo, hi = fp.clone(), fp.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    lo, hi = lo.cpu().tolist(), hi.cpu().tolist()
+    return lo == hi, lo, hi
+
+
 def broadcast_buffers_(net, group=None, src=0):
     """Every rank takes rank `src`'s BN running statistics and batch counters (DDP's
     broadcast_buffers semantics), e.g. before evaluation or saving on rank 0."""

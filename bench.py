@@ -76,13 +76,19 @@ def parse():
                          "marker kernel (profiles/summarize_pmc.py keeps what lies between)")
     ap.add_argument("--py-exchange", action="store_true",
                     help="N>1: all-reduce from Python over torch.distributed instead of the plan's RCCL")
+    ap.add_argument("--stall-s", type=float, default=180.0,
+                    help="N>1: a rank that makes no progress for this long reports where and exits 3")
+    ap.add_argument("--deadline-s", type=float, default=1500.0,
+                    help="bench.py --gpus N started directly: end every rank after this long")
     return ap.parse_args()
 
 
 # ----------------------------------------------------------------------------------- launching
-def spawn_ranks(n):
+def spawn_ranks(n, deadline_s):
     """`bench.py --gpus N` started directly: one child process per GPU with the torch.distributed
-    env (rendezvous on 127.0.0.1), before this process touches a GPU; rank 0 prints the line."""
+    env (rendezvous on 127.0.0.1), before this process touches a GPU; rank 0 prints the line. The
+    children are polled, never waited on blindly: one failing rank ends the others (they would wait
+    in a collective forever), and past `deadline_s` every rank is ended with a message."""
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -92,19 +98,59 @@ def spawn_ranks(n):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     rc = 0
+    t0 = time.monotonic()
     try:
-        for p in procs:
-            r = p.wait()
-            rc = rc or r
-            if r:  # one rank failed: the others would wait in a collective forever
+        while any(p.poll() is None for p in procs):
+            failed = [(i, p.returncode) for i, p in enumerate(procs) if p.returncode]
+            if failed or time.monotonic() - t0 > deadline_s:
+                why = ("rank %d exited with %d" % failed[0]) if failed else "deadline of %.0f s passed" % deadline_s
+                print("bench.py: %s; ending the other ranks" % why, file=sys.stderr, flush=True)
+                rc = failed[0][1] if failed else 124
                 for q in procs:
                     if q.poll() is None:
                         q.terminate()
+                t1 = time.monotonic()
+                while any(q.poll() is None for q in procs) and time.monotonic() - t1 < 20:
+                    time.sleep(0.2)
+                break
+            time.sleep(0.2)
+        rc = rc or next((p.returncode for p in procs if p.returncode), 0)
     finally:
         for q in procs:
             if q.poll() is None:
                 q.kill()
     return rc
+
+
+class Watchdog:
+    """Per-rank deadline on progress. The ranks meet in RCCL collectives (the plan's gradient
+    exchange, two buckets per step, and the barriers around each timed phase); a rank stuck there
+    never returns to Python. Every step reports its position here; if none arrives for `limit_s`,
+    the watchdog thread prints where the rank stopped -- phase, step, and which collective was
+    pending -- and ends the process with status 3 (no re-exec; the parent or torchrun sees it)."""
+
+    def __init__(self, rank, limit_s):
+        import threading
+        self.rank, self.limit = rank, limit_s
+        self.where = "start-up"
+        self.t = time.monotonic()
+        self.lock = threading.Lock()
+        th = threading.Thread(target=self._run, daemon=True)
+        th.start()
+
+    def mark(self, where):
+        with self.lock:
+            self.where, self.t = where, time.monotonic()
+
+    def _run(self):
+        while True:
+            time.sleep(1.0)
+            with self.lock:
+                idle, where = time.monotonic() - self.t, self.where
+            if idle > self.limit:
+                print("bench.py rank %d: no progress for %.0f s; last position: %s" % (self.rank, idle, where),
+                      file=sys.stderr, flush=True)
+                os._exit(3)
 
 
 # ------------------------------------------------------------------------------ synthetic data
@@ -155,7 +201,7 @@ def evaluate_val(args, net, tracks, pair_user, pair_track, split, n_users, dev):
     t0 = time.perf_counter()
     net.sync_user_table()
     net.eval()
-    d = args.feature_dim
+    d = nat.storage_dims(net._flat["dims"]).feature_dim  # factor rows at the storage width (zero past d)
     n_tracks = tracks.shape[0]
     model = net._model_struct()
     tr = nat.Tracks(tracks.data_ptr(), n_tracks, 0 if tracks.dtype == torch.float16 else 1, 0)
@@ -258,7 +304,7 @@ def cpu_baseline(args, n_users_local):
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(spawn_ranks(args.gpus))
+        sys.exit(spawn_ranks(args.gpus, args.deadline_s))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -268,6 +314,12 @@ def main():
     local = local % torch.cuda.device_count() if backend != "nccl" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    wd = Watchdog(rank, args.stall_s) if world > 1 else None
+
+    def mark(where):
+        if wd is not None:
+            wd.mark(where)
+
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -356,8 +408,12 @@ def main():
             plan.set_comm(comm)
         return plan
 
-    def run(plan, step_fn, n):
+    def run(plan, step_fn, n, phase="warm-up"):
         for s in range(n):
+            # a step's exchange is issued inside plan.step; a rank stuck in it stops here or in the
+            # synchronize after the loop, with that step's two buckets (bn0/conv1/bn1 and the rest)
+            # pending on the communicator's stream
+            mark("%s step %d/%d issued (its RCCL buckets: late segments then bn0/conv-1/bn1)" % (phase, s + 1, n))
             step_fn(plan, s)
 
     def inbatch_step(users_b, items_b):
@@ -384,8 +440,9 @@ def main():
     def timed_phase(name, plan, step_fn, gpu_only=False):
         """W warm-up steps, then EXACTLY K timed steps between barrier + synchronize on both
         sides; max over ranks. Returns (seconds, host enqueue seconds, gpu-only ms or None)."""
-        run(plan, step_fn, args.warmup)
+        run(plan, step_fn, args.warmup, name + " warm-up")
         opt.flush()
+        mark(name + ": barrier before the timed steps")
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -400,14 +457,16 @@ def main():
             torch.cuda._sleep(int(2.4e6 * args.steps))  # ~1 ms of GPU per step (2.4 GHz cycles)
             ev0.record()
         t0 = time.perf_counter()
-        run(plan, lambda p, s: step_fn(p, args.warmup + s), args.steps)
+        run(plan, lambda p, s: step_fn(p, args.warmup + s), args.steps, name + " timed")
         opt.flush()  # deferred user-table steps still pending are part of the timed work
         t_enq = time.perf_counter() - t0
         if gpu_only:
             ev1.record()
+        mark(name + ": synchronize after the timed steps (every issued step's exchange pending)")
         torch.cuda.synchronize()
         if profiled:
             profile_mark()
+        mark(name + ": barrier after the timed steps")
         if world > 1:
             dist.barrier()
         dt = D.max_over_ranks(time.perf_counter() - t0, dev)
@@ -489,6 +548,12 @@ def main():
         return res
 
     out = {}
+    if world > 1 and os.environ.get("DCUE_BENCH_STALL_RANK") == str(rank):
+        # fault injection for the self-diagnosis test (tests/test_gpu_dp.py): this rank stops, as if
+        # stuck in a collective; the watchdogs and the launcher must end the job with a report
+        mark("DCUE_BENCH_STALL_RANK: held before the first step")
+        while True:
+            time.sleep(1.0)
     # ---- phase 1: in-batch, cold user table
     plan = make_plan(False)
     ub, ib = batches(args.warmup + args.steps)
@@ -633,6 +698,13 @@ def main():
         result["catalogue"] = out["catalogue"]
     checks["finite"] = not checks["failed"]
     result["checks"] = checks
+    # data parallelism's invariant: every rank steps the same dense replica (the exchange averaged
+    # the same gradient into every rank's Adam); a broken exchange shows up here as differing replicas
+    mark("replica checksum all-reduce")
+    same, lo, hi = D.replica_checksums(net._flat["P"])
+    result["replicas_identical"] = same
+    if not same:
+        result["replica_fingerprint_min_max"] = [lo, hi]
     if world > 1:
         D.broadcast_buffers_(net)  # DDP semantics: evaluate with rank 0's BN statistics
     if rank == 0 and not args.no_eval:

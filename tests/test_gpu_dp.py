@@ -169,6 +169,20 @@ def test_bench_launches_its_own_ranks():
     assert r["n_gpus"] == 2 and r["config"]["process_group_world"] == 2
     assert r["config"]["global_batch"] == 2 * r["config"]["batch_per_gpu"]
     assert r["value"] > 0 and r["catalogue"]["rows_per_s"] > 0
+    assert r["replicas_identical"] is True  # every rank stepped the same dense replica
+
+
+def test_bench_stalled_rank_reports_and_exits():
+    """a rank that stops making progress (here rank 1 is held before its first
+    step by DCUE_BENCH_STALL_RANK, as a hung collective would hold it) is reported -- which rank,
+    how long, its last position -- and every rank ends with a non-zero status instead of waiting
+    for the driver's kill."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--stall-s", "15"] + SMALL,
+                         capture_output=True, text=True, timeout=200,
+                         env=dict(os.environ, DCUE_DIST_BACKEND="gloo", DCUE_BENCH_STALL_RANK="1"))
+    assert out.returncode != 0
+    assert "no progress for" in out.stderr and "last position" in out.stderr, out.stderr[-3000:]
+    assert not [l for l in out.stdout.splitlines() if l.startswith("{")]
 
 
 @pytest.mark.parametrize("kind", ["sgd", "ranger"])
