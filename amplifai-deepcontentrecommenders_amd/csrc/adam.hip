@@ -102,12 +102,14 @@ __device__ __forceinline__ void pack_store(const PackSeg& sg, long e, float w, f
 // conv weight segment (segments are 4-float aligned) also writes its four packed copies.
 // gdiv > 0: the gradient is an all-reduced sum over gdiv ranks; it becomes the mean first (stored
 // back, as grad.div_(world) leaves it) -- DDP's averaging fused into the sweep.
+// [lo, n) of the buffer (lo a multiple of 4): the plan's split step runs the head and the tail of
+// the flat buffer as two launches on two streams.
 __global__ __launch_bounds__(256) void k_adam_dense_pack(float* __restrict__ p, float* __restrict__ g,
                                                          float* __restrict__ m, float* __restrict__ v,
-                                                         long n, AdamScalars s, PackArgs pa,
+                                                         long lo, long n, AdamScalars s, PackArgs pa,
                                                          float* __restrict__ wpack, float gdiv) {
   const long n4 = n / 4;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+  for (long i = lo / 4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     float4 pp = ld4(p + 4 * i), gg = ld4(g + 4 * i), mm = ld4(m + 4 * i), vv = ld4(v + 4 * i);
     if (gdiv > 0.f) {
       gg.x = __fdiv_rn(gg.x, gdiv); gg.y = __fdiv_rn(gg.y, gdiv);
@@ -133,7 +135,8 @@ __global__ __launch_bounds__(256) void k_adam_dense_pack(float* __restrict__ p, 
       }
     }
   }
-  for (long i = 4 * n4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+  for (long i = max(4 * n4, lo) + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
     float gi = g[i];  // tail past the last float4: never a conv weight
     if (gdiv > 0.f) g[i] = gi = __fdiv_rn(gi, gdiv);
     adam_elem(p[i], gi, m[i], v[i], s);
@@ -427,7 +430,7 @@ int launch_emb_flush(const dcue_model* md, hipStream_t s) {
 }
 
 int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* poff, hipStream_t s,
-                bool flush_slice) {
+                bool flush_slice, long dense_lo, long dense_hi) {
   // host scalars as torch.optim.Adam forms them from Python floats (double), each rounded once to
   // float where the CPU kernel takes it as a float scalar
   const double bc1 = 1.0 - pow(a->beta1, (double)a->step);
@@ -445,10 +448,12 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
   sc.inv_bc2_sqrt = 1.0f / sc.bc2_sqrt;  // IEEE single division on the host: RN(1/bc2_sqrt)
   const float gdiv = a->grad_div > 1.0 ? (float)a->grad_div : 0.f;
   const int parts = a->parts ? a->parts : (DCUE_ADAM_DENSE | DCUE_ADAM_EMBEDDING);
-  const long n = poff[DCUE_N_DENSE_SEGMENTS];
+  const long n = dense_hi >= 0 ? dense_hi : poff[DCUE_N_DENSE_SEGMENTS];
   if (parts & DCUE_ADAM_DENSE) {  // Adam + the conv-weight repack in one sweep
-    DCUE_LAUNCH(k_adam_dense_pack, dim3(512), dim3(256), 0, s, md->params, md->grads, md->exp_avg,
-                       md->exp_avg_sq, n, sc, pack_args(md, poff), md->wpack, gdiv);
+    const long len = n - dense_lo;
+    const long blocks = len >= 512L * 1024 ? 512 : (len / 4 + 255) / 256 + 1;
+    DCUE_LAUNCH(k_adam_dense_pack, dim3((unsigned)blocks), dim3(256), 0, s, md->params, md->grads, md->exp_avg,
+                       md->exp_avg_sq, dense_lo, n, sc, pack_args(md, poff), md->wpack, gdiv);
     DCUE_LAUNCH_CHECK();
   }
   if ((parts & DCUE_ADAM_EMBEDDING) && md->emb_step) {

@@ -20,16 +20,35 @@ namespace dcue {
 // (alternating between two streams, each with its own partial-sum buffers). Forks and joins are
 // event-ordered against the caller's stream, so the calls stay stream-ordered (and capturable).
 
+unsigned sync_event_flags() {
+  static const unsigned f = [] {
+    const char* e = getenv("DCUE_EVENT_SCOPE");
+    return (e && e[0] == 's') ? (unsigned)hipEventDisableTiming
+                              : (unsigned)(hipEventDisableTiming | hipEventReleaseToDevice);
+  }();
+  return f;
+}
+
 SidePool* side_pool() {
   static SidePool pools[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   SidePool& p = pools[dev];
   if (!p.st[0]) {
+    // DCUE_SIDE_PRIO=low: the side streams at the device's least stream priority, so the command
+    // processor favours the caller's (critical-path) queue when both have workgroups to dispatch
+    static const bool low = [] {
+      const char* e = getenv("DCUE_SIDE_PRIO");
+      return e && e[0] == 'l';
+    }();
+    int least = 0, greatest = 0;
+    if (low && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
     for (auto& s : p.st)
-      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+      if ((low ? hipStreamCreateWithPriority(&s, hipStreamNonBlocking, least)
+               : hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess)
+        return nullptr;
     for (auto& e : p.ev)
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+      if (hipEventCreateWithFlags(&e, sync_event_flags()) != hipSuccess) return nullptr;
   }
   return &p;
 }
@@ -363,7 +382,8 @@ int init_ctx(Ctx* c, const dcue_model* m) {
 // producing kernels) + running-stat update by each BN's first consumer; eval: running statistics.
 int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t* item_track, int M,
                  double copies, bool train, const float* counts, float* f_out, hipStream_t s,
-                 bool acc_cleared = false, bool stats_done = false, bool clear_bn0 = false) {
+                 bool acc_cleared = false, bool stats_done = false, bool clear_bn0 = false,
+                 hipEvent_t before_l2 = nullptr) {
   const dcue_model* m = c.m;
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
   // one BN's finalize/publish record for its first consumer (train) -- bnacc.h
@@ -401,6 +421,9 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     TRY(launch_input_stats(src, t->data, item_track, nullptr, M, nullptr, rng_at(w, 0), s));
   }
   for (int l = 1; l <= 5; ++l) {
+    // the previous step's late-segment Adam (split plans, StepOpts::dense_split) ran on the user
+    // stream: conv 2 is the first kernel on this stream to read those parameters
+    if (l == 2 && before_l2) TRY(wait_point(s, before_l2));
     RowsArgs a = {};
     a.src = l == 1 ? t->data : (const void*)w.y[l - 1];
     a.item_track = item_track;
@@ -574,12 +597,15 @@ int dcue_workspace_activations(const dcue_dims* dims, int32_t B, int32_t N, int3
 int dcue_pack_weights(const dcue_model* m, void* stream) {
   Ctx c;
   TRY(init_ctx(&c, m));
+  TRY(join_user_stream((hipStream_t)stream));
   return launch_pack(m, c.poff, (hipStream_t)stream);
 }
 
 int dcue_forward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws,
                  size_t ws_bytes, int32_t train, float margin, float* scores, float* user_feat,
                  float* item_feat, float* loss, void* stream) {
+  // a plan step may leave Adam work on the user stream (its late dense segments, the user table)
+  TRY(join_user_stream((hipStream_t)stream));
   TRY(dcue::forward_impl(m, b, t, ws, ws_bytes, train, margin, StepOpts{}, (hipStream_t)stream));
   // the outputs live in the workspace (dcue_workspace_outputs gives their offsets); copies are
   // made only for callers that ask for their own buffers
@@ -596,6 +622,7 @@ int dcue_forward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
 
 int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws,
                         size_t ws_bytes, const float* dscores, float emb_grad_scale, void* stream) {
+  TRY(join_user_stream((hipStream_t)stream));
   return dcue::backward_impl(m, b, t, ws, ws_bytes, dscores, emb_grad_scale, StepOpts{},
                              (hipStream_t)stream);
 }
@@ -629,7 +656,7 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   if (!o.prologue_done) TRY(batch_counts(b, w, s));
   HPROF("capi:4");
   TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s,
-                   o.prologue_done, o.input_stats_done && o.prologue_done, o.clear_bn0));
+                   o.prologue_done, o.input_stats_done && o.prologue_done, o.clear_bn0, o.wait_late));
   TRY(wait_point(su, ev_in));
   HPROF("capi:5");
   if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
@@ -989,7 +1016,23 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   hipEvent_t joined = nullptr;
   TRY(fork_point(sp, sw[0], &joined));
   HPROF("capi:35");
-  TRY(wait_point(s, joined));
+  if (o.dense_split) {
+    // split dense Adam: the late segments (every gradient the side streams made) on the user stream
+    // once they are in, bn0 / conv 1 / bn1 on this stream behind its conv-1 tail; this stream does
+    // not wait for the join (the next forward waits for *late_done before conv 2)
+    dcue_adam_args dense = *o.dense_split;
+    dense.parts = DCUE_ADAM_DENSE;
+    const long late = c.poff[DCUE_SEG_LATE];
+    TRY(wait_point(su, joined));
+    {
+      ForkAfter fk(sp, su, o.late_done);
+      TRY(launch_adam(m, &dense, c.poff, su, true, late, -1));
+      TRY(fk.done());
+    }
+    TRY(launch_adam(m, &dense, c.poff, s, true, 0, late));
+  } else {
+    TRY(wait_point(s, joined));
+  }
   HPROF("capi:36");
   if (o.tails) {
     o.tails[0] = tail[0];
@@ -1012,7 +1055,7 @@ int dcue_adam_step(const dcue_model* m, const dcue_adam_args* a, void* stream) {
       (!m->emb || !m->emb_exp_avg || !m->emb_exp_avg_sq || !m->emb_slot || !m->emb_grad))
     return DCUE_ERR_INVALID;
   if ((parts & DCUE_ADAM_EMBEDDING) && m->emb_step && !m->emb_rows) return DCUE_ERR_INVALID;
-  if (parts & DCUE_ADAM_EMBEDDING) TRY(join_user_stream((hipStream_t)stream));
+  TRY(join_user_stream((hipStream_t)stream));
   TRY(launch_adam(m, a, c.poff, (hipStream_t)stream));
   // the dense sweep repacked the conv weights as it went (k_adam_dense_pack)
   return DCUE_OK;
@@ -1046,6 +1089,7 @@ int dcue_item_tower_eval(const dcue_model* m, const dcue_tracks* t, const int32_
   Ws w;
   if (carve(&m->dims, 1, 0, n_items, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
   carve(&m->dims, 1, 0, n_items, ws, &w);
+  TRY(join_user_stream((hipStream_t)stream));
   return item_forward(c, w, t, item_track, n_items, (double)n_items, false, nullptr, item_feat,
                       (hipStream_t)stream);
 }

@@ -114,8 +114,8 @@ extern "C" int dcue_comm_create(const void* id_host, int32_t world, int32_t rank
   c->rank = rank;
   int st = nccl_status(ncclCommInitRank(&c->nc, world, id, rank), "ncclCommInitRank", __LINE__);
   if (!st && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) st = DCUE_ERR_HIP;
-  if (!st && hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming) != hipSuccess) st = DCUE_ERR_HIP;
-  if (!st && hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess) st = DCUE_ERR_HIP;
+  if (!st && hipEventCreateWithFlags(&c->ev_tail, sync_event_flags()) != hipSuccess) st = DCUE_ERR_HIP;
+  if (!st && hipEventCreateWithFlags(&c->ev_done, sync_event_flags()) != hipSuccess) st = DCUE_ERR_HIP;
   if (st) {
     dcue_comm_destroy(c);
     return st;

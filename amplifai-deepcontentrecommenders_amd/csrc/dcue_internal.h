@@ -242,8 +242,9 @@ int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float s
                     hipStream_t s);
 // flush_slice = false: the user-table part leaves this step's rolling-flush slice to the caller
 // (plans issue it during the next step, after that step's user tower: launch_emb_flush_rows)
+// dense_lo / dense_hi: the dense part over [dense_lo, dense_hi) of the flat buffer only (-1: to the end)
 int launch_adam(const dcue_model* m, const dcue_adam_args* a, const int64_t* poff, hipStream_t s,
-                bool flush_slice = true);
+                bool flush_slice = true, long dense_lo = 0, long dense_hi = -1);
 int launch_emb_flush_rows(const dcue_model* m, int step, hipStream_t s);
 // BN-free towers: mean 0, invstd = a = 1 for the six BN layers, plus the ones / zeros arrays
 int launch_bn_identity(float* const* mean, float* const* invstd, float* const* a, float* ones, float* zeros,
@@ -292,6 +293,12 @@ int comm_divide(const dcue_comm* c, float* grad, long n, hipStream_t s);
 bool timer_take_turn(int cls);
 std::vector<CapturedTimer> timer_take_captured();
 
+// Flags of the library's stream-ordering events. They only order work between streams of one
+// device, so they take a device-scope release: the default system-scope one writes back and
+// invalidates the caches when the event completes, which measured 4-9 us of idle on the waiting and
+// the recording stream after every event-bound kernel of a step (profiles/r03: the critical
+// chain's gaps). DCUE_EVENT_SCOPE=system restores the default (A/B).
+unsigned sync_event_flags();
 // side streams (capi.hip): three per device, plus a ring of fork/join events
 struct SidePool {
   // st[0]: user tower + user-table Adam; st[1], st[2]: weight gradients of layers 5..2
@@ -354,6 +361,14 @@ struct StepOpts {
   bool input_stats_done = false;
   const float* xhat0 = nullptr;
   bool clear_bn0 = false;  // the block holds bn0 sums of an announced batch this step did not use
+  // split dense Adam (plans without a communicator): the caller's stream runs Adam over bn0 / conv 1 /
+  // bn1 (segments [0, DCUE_SEG_LATE)) right after its conv-1 tail, and the user stream the rest once
+  // the side streams' gradients are in -- the caller's stream never waits for the join. *late_done
+  // receives the user stream's point after that part; the next forward waits for it before conv 2
+  // (the first reader of a late segment on the caller's stream).
+  const dcue_adam_args* dense_split = nullptr;
+  hipEvent_t* late_done = nullptr;
+  hipEvent_t wait_late = nullptr;  // forward: the previous split step's late_done
   // the step's per-item copy lists (gather layout, built by the plan's prologue; StepPrologue)
   const int32_t* copy_ptr = nullptr;
   const int32_t* copy_idx = nullptr;

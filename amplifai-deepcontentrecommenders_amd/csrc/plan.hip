@@ -47,6 +47,7 @@ struct dcue_plan {
   const int32_t* next_items = nullptr;
   long launches = 0;
   hipEvent_t tails[2] = {};       // the last launched step's end (StepOpts::tails)
+  hipEvent_t late_done = nullptr; // the last split step's late-segment Adam (StepOpts::dense_split)
   int pending_flush = -1;         // step whose rolling-flush slice the next launch issues
   hipStream_t last_stream = nullptr;  // the caller's stream of the last launch
   dcue_comm* comm = nullptr;      // data-parallel exchange between backward and Adam (plan_step)
@@ -86,7 +87,7 @@ int issue_step(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, v
 // the bound batch buffers and, into cfg.mt, the draw stream's state after step t's draw (the
 // plan's own copy runs one step ahead).
 int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src, hipStream_t s,
-                const dcue_adam_args* emb_adam) {
+                const dcue_adam_args* emb_adam, const dcue_adam_args* dense_split = nullptr) {
   using namespace dcue;
   SidePool* sp = side_pool();
   if (!sp) return DCUE_ERR_HIP;
@@ -155,6 +156,10 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   hipEvent_t score_done = nullptr;
   o.score_done = &score_done;
   o.tails = p->tails;
+  o.wait_late = p->late_done;  // the previous split step's late Adam, before conv 2
+  o.dense_split = dense_split;
+  hipEvent_t late_done = nullptr;
+  o.late_done = &late_done;
   // the previous step's rolling-flush slice runs after this step's user tower (StepOpts)
   const bool deferred = p->model.emb_step != nullptr;
   o.flush_slice_step = deferred ? p->pending_flush : -1;
@@ -175,9 +180,19 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   TRY(backward_impl(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, nullptr, p->cfg.emb_grad_scale, o, s));
   HPROF("plan:5");
   p->pending_flush = o.defer_flush_slice ? emb_adam->step : -1;
+  p->late_done = dense_split ? late_done : nullptr;
   p->last_stream = s;
   ++p->launches;
   return DCUE_OK;
+}
+
+// DCUE_SPLIT_ADAM=0 keeps the whole dense Adam on the caller's stream after the join (A/B)
+bool split_adam_on() {
+  static const bool on = [] {
+    const char* e = getenv("DCUE_SPLIT_ADAM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 int capture(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
@@ -351,6 +366,11 @@ extern "C" int dcue_plan_step(dcue_plan* p, const int64_t* users_src, const int3
   dcue_adam_args emb = *adam, dense = *adam;
   emb.parts = DCUE_ADAM_EMBEDDING;
   dense.parts = DCUE_ADAM_DENSE;
+  if (!p->comm && split_adam_on()) {  // one GPU: the dense Adam split over two streams (StepOpts)
+    TRY(issue_eager(p, users_src, item_track_src, (hipStream_t)stream, &emb, &dense));
+    HPROF("plan_step:issue");
+    return DCUE_OK;
+  }
   const int st = issue_eager(p, users_src, item_track_src, (hipStream_t)stream, &emb);
   if (st) return st;
   HPROF("plan_step:issue");
@@ -383,6 +403,14 @@ extern "C" int dcue_plan_set_next(dcue_plan* p, const int32_t* next_item_track) 
   if (p->exec || !p->xh[0]) return DCUE_ERR_UNSUPPORTED;
   p->next_items = next_item_track;
   return DCUE_OK;
+}
+
+extern "C" int dcue_plan_sync(dcue_plan* p, void* stream) {
+  if (!p) return DCUE_ERR_INVALID;
+  if (p->exec) return DCUE_OK;  // graph replays run whole on the stream they were launched on
+  // the user stream holds the step's last Adam work (split dense segments, user table); the weight
+  // gradient streams are joined into it by then
+  return dcue::join_user_stream((hipStream_t)stream);
 }
 
 extern "C" int dcue_plan_wait_side(dcue_plan* p, void* stream) {

@@ -905,11 +905,29 @@ int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df,
     const bool wlds = fcW && d % 4 == 0;
     const size_t lds = wlds ? sizeof(float) * d * d : 0;
     // many items (catalogue M = B(1+N)): 16 per workgroup; a few (in-batch M = B): 4
-    if (b->n_items >= 512)
+    // (DCUE_ITEMGRAD_IT = 1, 2, 4 or 16 forces one: A/B diagnostic)
+    static const int forced = [] {
+      const char* e = getenv("DCUE_ITEMGRAD_IT");
+      return e ? atoi(e) : 0;
+    }();
+    if (forced == 1)
+      return wlds ? item_grad_multi<1, true>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s)
+                  : item_grad_multi<1, false>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s);
+    if (forced == 2)
+      return wlds ? item_grad_multi<2, true>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s)
+                  : item_grad_multi<2, false>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s);
+    if (forced == 4)
+      return wlds ? item_grad_multi<4, true>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s)
+                  : item_grad_multi<4, false>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s);
+    if (b->n_items >= 512 || forced == 16)
       return wlds ? item_grad_multi<16, true>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s)
                   : item_grad_multi<16, false>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s);
-    return wlds ? item_grad_multi<4, true>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s)
-                : item_grad_multi<4, false>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s);
+    if (b->n_items >= 256)
+      return wlds ? item_grad_multi<4, true>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s)
+                  : item_grad_multi<4, false>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s);
+    // in-batch M = B = 64: one item per workgroup (measured GPU-only, A/B: 3 us under four per workgroup)
+    return wlds ? item_grad_multi<1, true>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s)
+                : item_grad_multi<1, false>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s);
   }
   if (b->layout == DCUE_LAYOUT_GATHER && (long)b->n_rows * b->n_neg + 1 > kItemGradCap) return DCUE_ERR_UNSUPPORTED;
   const ItemGradFc fc = {rowsum, loss, fcW, g5, acc5, y5, mean5, invstd5};

@@ -41,7 +41,9 @@ hipEvent_t timer_event() {
     return e;
   }
   hipEvent_t e = nullptr;
-  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  // timing only (hipEventElapsedTime after a host wait): no system-scope fence at completion, which
+  // would cost the timed stream a cache writeback (hip_runtime_api.h, hipEventDisableSystemFence)
+  if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
   return e;
 }
 

@@ -144,6 +144,7 @@ _SIGS = {
     "dcue_plan_destroy": ([_P], ctypes.c_int),
     "dcue_plan_step": ([_P, _P, _P, ctypes.POINTER(AdamArgs), _P], ctypes.c_int),
     "dcue_plan_wait_side": ([_P, _P], ctypes.c_int),
+    "dcue_plan_sync": ([_P, _P], ctypes.c_int),
     "dcue_plan_set_next": ([_P, _P], ctypes.c_int),
     "dcue_check_finite": ([_P, ctypes.c_int64, _P, ctypes.c_int32, _P], ctypes.c_int),
     "dcue_check_ids": ([_P, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_int32, _P], ctypes.c_int),

@@ -114,6 +114,7 @@ class DCUENet(nn.Module):
         self.user_embd._owner = weakref.ref(self)
         self._anchor = torch.zeros((), requires_grad=True)
         self._flat = None  # device-side state, built by _apply when moved to the GPU
+        self._pending_plan = None  # a TrainPlan whose last step left Adam work on a side stream
         self._ws = None
         self._ws_key = None
 
@@ -182,10 +183,19 @@ class DCUENet(nn.Module):
         # conv weights' counters are what records a host-side write to them
         return tuple(getattr(self.conv, "layer%d" % l).weight._version for l in range(1, 6))
 
+    def _sync_plan(self):
+        """Order torch's current stream after the last plan step's side-stream Adam work
+        (TrainPlan.sync): parameters read from torch are then current."""
+        plan = getattr(self, "_pending_plan", None)
+        if plan is not None:
+            self._pending_plan = None
+            plan.sync(nat.stream_handle())
+
     def _require_device(self):
         if self._flat is None:
             raise RuntimeError("DCUENet must be moved to the GPU (.cuda()) before use: its forward "
                                "and backward run only through libdcue_hip on the MI355X")
+        self._sync_plan()
         if self.conv.layer1.weight.data_ptr() != self._flat["P"].data_ptr() + 4 * self._flat["poff"][2]:
             # parameters were re-assigned behind our back (load_state_dict copies in place, so this
             # only happens if a caller replaced .data): rebuild the flat view
@@ -226,11 +236,13 @@ class DCUENet(nn.Module):
 
     def state_dict(self, *args, **kwargs):
         if self._flat is not None:
+            self._sync_plan()
             self.sync_user_table()
         return super().state_dict(*args, **kwargs)
 
     def load_state_dict(self, state_dict, strict=True, assign=False):
         if self._flat is not None:
+            self._sync_plan()
             self.sync_user_table()  # pending deferred steps belong to the table being replaced
         return super().load_state_dict(state_dict, strict=strict, assign=assign)
 

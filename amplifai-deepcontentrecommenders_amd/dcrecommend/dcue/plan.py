@@ -86,6 +86,7 @@ class TrainPlan:
         ck.raise_if_any()
 
     def _check_after(self):
+        self.sync()
         ck, fl = self._check, self.net._flat
         ck.finite(self.loss.view(1), "non-finite loss")
         ck.finite(fl["P"], "non-finite dense parameters")
@@ -144,8 +145,19 @@ class TrainPlan:
                                       ctypes.byref(args), self._stream if stream is None else stream)
         if st != 0:
             nat.check(st, "dcue_plan_step")
+        # the step's last Adam work may still run on the library's user stream (include/dcue.h
+        # dcue_plan_step); the model joins it before anything reads the parameters from torch
+        self.net._pending_plan = self
         if self._check is not None:
             self._check_after()
+
+    def sync(self, stream=None):
+        """`stream` (default: the plan's) waits for the work the last step left on the library's side
+        streams (include/dcue.h dcue_plan_sync): the parameters are then current on it."""
+        if self._handle is None:
+            return
+        nat.check(self._lib.dcue_plan_sync(self._handle, self._stream if stream is None else stream),
+                  "dcue_plan_sync")
 
     def set_next(self, item_track):
         """Announce the NEXT launch's item_track source (device [M] int32, unchanged until that
@@ -186,7 +198,10 @@ class TrainPlan:
 
     def close(self):
         if getattr(self, "_handle", None) is not None:
+            self.sync()
             torch.cuda.synchronize()
+            if getattr(self.net, "_pending_plan", None) is self:
+                self.net._pending_plan = None
             self._lib.dcue_plan_destroy(self._handle)
             self._handle = None
 

@@ -575,6 +575,7 @@ def main():
         dcrecommend.check): the last step's loss, the dense parameters and gradients, and the
         flushed user table with both Adam moments, all finite."""
         from dcrecommend.check import StepCheck
+        net._sync_plan()
         opt.flush()
         ck = StepCheck(dev)
         ck.finite(p.loss.view(1), "loss")
@@ -701,6 +702,7 @@ def main():
     # data parallelism's invariant: every rank steps the same dense replica (the exchange averaged
     # the same gradient into every rank's Adam); a broken exchange shows up here as differing replicas
     mark("replica checksum all-reduce")
+    net._sync_plan()
     same, lo, hi = D.replica_checksums(net._flat["P"])
     result["replicas_identical"] = same
     if not same:

@@ -308,10 +308,16 @@ int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const dcue_tracks
 int dcue_plan_launch(dcue_plan* plan, const int64_t* users_src, const int32_t* item_track_src,
                      void* stream);
 /* dcue_plan_launch, then (adam != NULL) dcue_adam_step on the plan's model: one host call per
- * single-GPU training step (under data parallelism the gradient all-reduce sits between the two,
- * so launch and dcue_adam_step are issued separately). */
+ * training step (a bound communicator's exchange included, dcue_plan_set_comm). Without a
+ * communicator the dense Adam is split: bn0 / conv 1 / bn1 on `stream` right behind the conv-1
+ * weight gradient, the other segments on the library's user stream once the side streams'
+ * gradients are in, so `stream` never waits for that join; the plan's next launch waits for it
+ * before conv 2. Until then the parameters are current only for work ordered after dcue_plan_sync
+ * (every library entry point that reads them joins by itself). */
 int dcue_plan_step(dcue_plan* plan, const int64_t* users_src, const int32_t* item_track_src,
                    const dcue_adam_args* adam, void* stream);
+/* `stream` waits for everything the plan's last step left on the library's side streams. */
+int dcue_plan_sync(dcue_plan* plan, void* stream);
 /* Data-parallel overlap (row e): `stream` waits until every side-stream part of the plan's last
  * launched step is in. From then on the flat gradient buffer is final except its first
  * DCUE_SEG_LATE segments (bn0, conv layer 1, bn1: written by the caller's stream at the step's end),

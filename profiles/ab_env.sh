@@ -13,14 +13,14 @@ for r in $(seq 1 $ROUNDS); do
     i=$((i + 1))
     EV=$([ "$E" = "-" ] && echo "DCUE_AB_VARIANT=$i" || echo "$E")
     env $EV timeout -k 10 200 python3 $ROOT/bench.py --no-cpu-baseline --no-eval --steps 200 --warmup 20 \
-      --modes $MODES > "$OUT/v${i}_$r.log" 2>&1 || exit 1
+      --modes $MODES ${BENCH_EXTRA:-} > "$OUT/v${i}_$r.log" 2>&1 || exit 1
     python3 - "$OUT/v${i}_$r.log" "$EV" <<'PY' >> "$OUT/summary.txt"
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 cat = d.get("catalogue", {})
 cold = d.get("inbatch_cold", {})
-print(sys.argv[2], "warm %.4f (host %.4f) cold %s cat %s (host %s)" % (
-    d["ms_per_step"], d.get("host_enqueue_ms_per_step", 0), cold.get("ms_per_step"),
+print(sys.argv[2], "warm %.4f (host %.4f, gpu-only %s) cold %s cat %s (host %s)" % (
+    d["ms_per_step"], d.get("host_enqueue_ms_per_step", 0), d.get("gpu_only_ms_per_step"), cold.get("ms_per_step"),
     cat.get("ms_per_step"), cat.get("host_enqueue_ms_per_step")))
 PY
   done

@@ -60,6 +60,22 @@ def main():
                 ce = max(ce, e)
         tot += ce - cs
         print("queue %s busy %.1f us of %.1f (%.0f%%)" % (q, tot / 1e3, per / 1e3, 100.0 * tot / per))
+    # the anchor queue over every step: median gap before each of its kernels (by position in the
+    # step) -- what cross-stream waits, event records and dispatch cost the critical chain
+    gaps = {}
+    for j in range(len(starts) - 1):
+        a, b = starts[j], starts[j + 1]
+        chain = [k for k in ks if a <= k[0] < b and k[3] == q_anchor]
+        for n, (k0, k1) in enumerate(zip(chain, chain[1:])):
+            name = k1[2].split("(")[0].replace("void ", "").replace("dcue::", "")[:60]
+            gaps.setdefault((n, name), []).append((k1[0] - k0[1]) / 1e3)
+    print("anchor-queue gaps (median over %d steps, us):" % (len(starts) - 1))
+    tot = 0.0
+    for (n, name), v in sorted(gaps.items()):
+        g = statistics.median(v)
+        tot += g
+        print("  %6.1f  before %s" % (g, name))
+    print("  %6.1f  total" % tot)
 
 
 if __name__ == "__main__":
