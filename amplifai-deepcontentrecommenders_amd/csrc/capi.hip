@@ -208,9 +208,12 @@ struct Ws {
   float *mean[6], *invstd[6], *a[6];
   // exact BN sums (bnacc.h), [6 layers][2 sums][Cmax][2 words]: forward stats, backward sums
   unsigned long long *bnacc, *bnbacc;
-  // the forward's value ranges (split-f16 operand scales, conv.hip): [5 layers][2][kRngC] ordered
-  // keys, between the forward and backward sums of the block (cleared with the forward sums)
+  // the forward's value ranges (split-f16 operand scales, conv_rows.h / conv_wgrad.hip): [6 layers]
+  // [2][kRngC] ordered keys, between the forward and backward sums of the block (cleared with the
+  // forward sums); the backward's gradient maxima [7][kRngC] (max |g_l| for l = 1..5, max |df| at 6)
+  // after the backward sums (cleared with them)
   unsigned* rng;
+  unsigned* grng;
   long nzero;            // words of the accumulator block (one clear per step)
   long nfwd;             // its forward part: the sums and the ranges
   float* rowsum;         // [B] per-row hinge sums (score_fused)
@@ -235,16 +238,20 @@ struct Ws {
 };
 
 // the accumulator block's parts: [6][2][Cmax][2] forward sums, then the same for the backward
-constexpr long kRngWords = 5L * 2 * kRngC / 2;  // the ranges' 64-bit words
+constexpr long kRngWords = 6L * 2 * kRngC / 2;   // the ranges' 64-bit words
+constexpr long kGrngWords = 7L * kRngC / 2 + 64;  // the gradient maxima's (+ padding to keep 16-B alignment)
 
 void rebase_acc(Ws* w, unsigned long long* acc) {
   w->bnacc = acc;
   w->rng = reinterpret_cast<unsigned*>(acc + 6L * 2 * w->cmax * 2);
   w->bnbacc = acc + 6L * 2 * w->cmax * 2 + kRngWords;
+  w->grng = reinterpret_cast<unsigned*>(w->bnbacc + 6L * 2 * w->cmax * 2);
 }
 
-// layer l's range (l = 0: the raw input of conv 1; l = 1..4: the ReLU output of conv l)
+// layer l's range (l = 0: the raw input of conv 1; l = 1..5: the ReLU output of conv l)
 unsigned* rng_at(const Ws& w, int l) { return w.rng + (size_t)l * 2 * kRngC; }
+// max |g_l| per channel (l = 1..5), max |df| (l = 6)
+unsigned* grng_at(const Ws& w, int l) { return w.grng + (size_t)l * kRngC; }
 
 size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   Arena ar{(char*)base, 0, 0};
@@ -261,7 +268,7 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   }
   w->cmax = Cmax > D ? Cmax : D;
   w->nfwd = 6L * 2 * w->cmax * 2 + kRngWords;
-  w->nzero = w->nfwd + 6L * 2 * w->cmax * 2;
+  w->nzero = w->nfwd + 6L * 2 * w->cmax * 2 + kGrngWords;
   w->bnacc = ar.take<unsigned long long>(w->nzero);
   rebase_acc(w, w->bnacc);
   w->rowsum = ar.take<float>(B);
@@ -439,7 +446,7 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     a.out_idx = w.idx[l];
     a.out_acc = train ? bn_acc(w.bnacc, w.cmax, l) : nullptr;
     a.in_range = rng_at(w, l - 1);
-    a.out_range = l < 5 ? rng_at(w, l) : nullptr;
+    a.out_range = rng_at(w, l);
     a.M = M;
     a.nout = l == 5 ? c.D : c.H;
     TimerScope tsc;
@@ -698,6 +705,7 @@ int ahead_item_inputs(const dcue_model* m, const dcue_batch* b, const dcue_track
   const int M = b->n_items;
   const double copies = (double)b->n_rows * (1 + b->n_neg);
   TRY(launch_input_stats(src, t->data, items, counts, M, bn_acc(w.bnacc, w.cmax, 0), rng_at(w, 0), s));
+  if (wgrad_f16_on()) return DCUE_OK;  // the split-f16 conv-1 weight gradient reads the table itself
   return launch_xhat0(src, t->data, items, M, bn_acc(w.bnacc, w.cmax, 0), copies * kFrames, xhat0, s);
 }
 
@@ -759,8 +767,8 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   // dgrad chain) is enqueued first, recording a fork point before each layer; the side streams'
   // work (user tower, fc weight gradient, per-layer weight gradients) is enqueued afterwards
   // against those recorded points, so issuing it never delays the chain.
-  if (!o.prologue_done)
-    DCUE_HIP_CHECK(hipMemsetAsync(w.bnbacc, 0, sizeof(unsigned long long) * 6 * 2 * w.cmax * 2, s));
+  if (!o.prologue_done)  // the backward sums and the gradient maxima
+    DCUE_HIP_CHECK(hipMemsetAsync(w.bnbacc, 0, sizeof(unsigned long long) * (6 * 2 * w.cmax * 2 + kGrngWords), s));
     HPROF("capi:13");
   if (!o.fuse_score)  // else the fused score kernel already produced du / dfcopy
     TRY(launch_score_bwd(w.uf, w.f, b, D, dscores ? dscores : w.dhinge, w.cosv, w.norms, w.du,
@@ -775,8 +783,12 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   // the conv-1 weight gradient's X operand, bn0(x) without gamma/beta, materialised once beside the
   // backward chain (it needs only the forward's input statistics); waited for just before that kernel
   hipEvent_t ev_x0 = nullptr;
+  const bool f16w = wgrad_f16_on();  // split-f16 weight gradients (conv_wgrad.hip)
+  // the largest copy count of an item (in-batch: a positive drawn by every other row), the
+  // split-f16 dz bounds' kD factor
+  const double kd_max = b->layout == DCUE_LAYOUT_GATHER ? 1.0 + (double)B * N : 1.0;
   const float* xhat0 = o.xhat0 ? o.xhat0 : w.xhat0;  // prepared one step ahead (plans), or built here
-  if (!o.xhat0) {
+  if (!o.xhat0 && !f16w) {
     TRY(wait_point(sw[1], ev_score));
     ForkAfter fk(sp, sw[1], &ev_x0);
     TRY(launch_xhat0(src, t->data, b->item_track, M, c.bn ? bn_acc(w.bnacc, w.cmax, 0) : nullptr,
@@ -786,13 +798,14 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   if (c.res) {  // df; then the fc input gradient split: g5 = df W[:, 4H:] (+ BN5's sums) and the
                 // time-pooled blocks' dtp = df W[:, :4H]
     TRY(launch_item_grad(w.dfcopy, b, D, w.df, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                         o.fuse_score ? w.rowsum : nullptr, w.loss, cptr, cidx, s));
+                         o.fuse_score ? w.rowsum : nullptr, w.loss, cptr, cidx, nullptr, grng_at(w, 6), s));
     TGemmArgs g = {};
     g.M = M; g.N = D; g.K = D;
     g.A = w.df; g.sam = D; g.sak = 1;
     g.B = c.P(SEG_FC_W) + 4 * c.HL; g.sbk = c.FI; g.sbn = 1;
     g.C = w.g[5]; g.scm = D; g.scn = 1;
     g.colacc = bn_acc(w.bnbacc, w.cmax, 5); g.xy = w.y[5]; g.xmean = w.mean[5]; g.xinvstd = w.invstd[5];
+    g.colmax = grng_at(w, 5);
     TRY(launch_tgemm(0, 0, g, s));
     g = TGemmArgs{};
     g.M = M; g.N = 4 * c.HL; g.K = D;
@@ -806,7 +819,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     // (no fork point here: the fc weight gradient waits with the layer 3-5 weight gradients, below)
     TRY(launch_item_grad(w.dfcopy, b, D, w.df, c.P(SEG_FC_W), w.g[5], bn_acc(w.bnbacc, w.cmax, 5),
                          w.y[5], w.mean[5], w.invstd[5], o.fuse_score ? w.rowsum : nullptr, w.loss,
-                         cptr, cidx, s));
+                         cptr, cidx, grng_at(w, 5), grng_at(w, 6), s));
     HPROF("capi:15");
   }
   for (int l = 5; l >= 2; --l) {  // dgrad chain: g_l (+ BN_l sums) -> g_{l-1} (+ BN_{l-1} sums)
@@ -827,6 +840,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     ra.out = w.g[l - 1];
     ra.out_acc = bn_acc(w.bnbacc, w.cmax, l - 1);
     ra.oy = w.y[l - 1]; ra.omean = w.mean[l - 1]; ra.oinvstd = w.invstd[l - 1];
+    ra.out_grange = grng_at(w, l - 1);  // max |g_{l-1}|: the split-f16 weight gradient's dz bound
     ra.M = M;
     ra.nout = H;
     // a fork point only where a side stream waits (wgrads of layers 3-5 after g_3, of layer 2
@@ -849,7 +863,8 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     if (so != s) TRY(wait_point(so, ev_layer[l]));
     HPROF("capi:18");
     WgradArgs wa = {};
-    wa.xsrc = l == 1 ? (const void*)xhat0 : (const void*)w.y[l - 1];
+    // split-f16 kernels: layer 1 reads the track table itself (bn0 applied at the fill), not xhat0
+    wa.xsrc = l == 1 ? (f16w ? t->data : (const void*)xhat0) : (const void*)w.y[l - 1];
     wa.item_track = b->item_track;
     wa.x_mean = w.mean[l - 1];
     wa.x_a = l == 1 ? w.invstd[0] : w.a[l - 1];
@@ -861,8 +876,12 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     wa.counts = w.counts;
     wa.M = M; wa.cout = C; wa.cin = cin;
     wa.wpart = w.wpart[ps]; wa.bpart = w.bpart[ps];
+    if (f16w) {
+      wa.x_range = rng_at(w, l - 1); wa.y_range = rng_at(w, l); wa.g_range = grng_at(w, l);
+      wa.kd_max = kd_max * wa.invN;
+    }
     const int nch = wgrad_nchunk(l, M, C, cin);
-    if (l == 1) {  // the GEMM reads the pooled BN1 backward, expanded to rows at MFMA time
+    if (l == 1 && !f16w) {  // the GEMM reads the pooled BN1 backward, expanded to rows at MFMA time
       TRY(launch_conv1_dx(wa, w.dx1, so));
       wa.g_l = w.dx1;
     }
@@ -882,7 +901,9 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(launch_wgrad_reduce(l, wa.wpart, wa.bpart, nch, C, cin, c.Gd(seg_conv_w(l)),
                             c.Gd(seg_conv_b(l)), w.G, w.S, so));
     ForkAfter fk(sp, so, tail);
-    TRY(launch_bn0_grads(w.G, w.S, c.P(seg_conv_w(1)), c.gamma(w, 0), c.beta(w, 0), H,
+    const bool graw = f16w && src == SRC_TRACK_F16;  // G over the raw fp16 input (conv_wgrad.hip)
+    TRY(launch_bn0_grads(w.G, w.S, c.P(seg_conv_w(1)), c.gamma(w, 0), c.beta(w, 0),
+                         graw ? w.mean[0] : nullptr, graw ? w.invstd[0] : nullptr, H,
                          c.Gd(seg_conv_w(1)), c.dgamma(w, 0), c.dbeta(w, 0),
                          c.Gd(seg_conv_b(1)), so));
     return fk.done();
@@ -922,6 +943,9 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       wa.g_l = w.df;
       wa.M = M; wa.cout = D; wa.cin = D;
       wa.wpart = w.wpm[4]; wa.bpart = w.bpm[4];
+      if (f16w) {
+        wa.x_range = rng_at(w, 5); wa.g_range = grng_at(w, 6);
+      }
       mw.nchunk[j] = wgrad_nchunk(6, M, D, D);
       mw.dW[j] = c.Gd(SEG_FC_W);
       mw.db[j] = c.Gd(SEG_FC_B);
@@ -941,6 +965,10 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       wa.counts = w.counts;
       wa.M = M; wa.cout = l == 5 ? D : H; wa.cin = H;
       wa.wpart = w.wpm[l - 2]; wa.bpart = w.bpm[l - 2];
+      if (f16w) {
+        wa.x_range = rng_at(w, l - 1); wa.y_range = rng_at(w, l); wa.g_range = grng_at(w, l);
+        wa.kd_max = (float)kd_max * wa.invN;
+      }
       mw.nchunk[j] = wgrad_nchunk(l, M, wa.cout, wa.cin);
       mw.dW[j] = c.Gd(seg_conv_w(l));
       mw.db[j] = c.Gd(seg_conv_b(l));

@@ -442,7 +442,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
 
   if constexpr (MODE == 1) {
     // g_{l-1} rows, plus this tile's share of BN_{l-1}'s backward sums (sum g, sum g*xhat)
-    float sg[CT] = {}, sgx[CT] = {};
+    float sg[CT] = {}, sgx[CT] = {}, gmx[CT] = {};
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int o = ocol0 + 16 * ct + l16;
@@ -462,6 +462,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
             float gv = acc[r][ct][j];
             if (a.skip && o < a.skip_n) gv += a.skip[((grb + j) / R) * a.skip_ld + o] * a.skip_scale;
             a.out[(grb + j) * nout + o] = gv;
+            gmx[ct] = fmaxf(gmx[ct], fabsf(gv));
             sg[ct] += gv;
             sgx[ct] += gv * ((yv[j] - mu) * is);
           }
@@ -478,6 +479,15 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
           acc128_add(acc_at(a.out_acc, nout, 0, o), s);
           acc128_add(acc_at(a.out_acc, nout, 1, o), q);
         }
+      }
+    }
+    if (a.out_grange) {  // max |g_{l-1}| per channel: the split-f16 weight gradient's dz bound
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        float m = gmx[ct];
+        m = fmaxf(m, __shfl_xor(m, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        if (g == 0) atomicMax(a.out_grange + ocol0 + 16 * ct + l16, ord_key(m));
       }
     }
   } else {

@@ -264,6 +264,424 @@ __global__ __launch_bounds__(256) void k_conv_wgrad_multi(WgradMulti w) {
 }
 
 
+// ------------------------------------------------------------ split-f16 weight gradient
+// The same GEMM as wgrad_body, dW[o][kc] = sum over rows of dz[row][o] x[row][kc], on f16 MFMA
+// (v_mfma_f32_16x16x32_f16, 16x the f32 MFMA rate): both operands are split into fp16 pairs,
+// v = hi + lo (hi = fp16(v), lo = fp16(v - hi)), and each product is hi*hi + lo*hi + hi*lo (the
+// dropped lo*lo and the lo roundings are ~2^-22 of the product; f32 accumulation), i.e. three f16
+// MFMAs per product at 3/16 of the f32 MFMA time. Every dz column (output channel o) and every x
+// column (input channel c) is scaled by its own power of two, 2^e_o and 2^e_c, from a bound of
+// the column's largest magnitude -- so the largest value lands in [2^14, 2^15): no fp16 overflow,
+// and small gradients (~1e-6) stay clear of fp16's subnormals -- and the epilogue multiplies each
+// output by 2^-(e_o + e_c): exact, so the scaling changes no rounding. The bounds (WgradArgs
+// x_range, y_range, g_range, kd_max):
+//   x = (src - mu) sc + be is monotone in src: its extremes are at the source's min and max (the
+//       forward's per-channel value ranges; a ReLU output's min is 0);
+//   dz = a (g - kD sD - kD xhat sDx) (masked): |dz| <= |a| (max|g| + kDmax (|sD| + max|xhat| |sDx|)),
+//       max|g| from the producing dgrad / item-gradient epilogue, max|xhat| from y_l's range;
+//   RAW (fc): |dz| = |df| <= max|df|.
+// A loose bound only lowers the scaled maximum: values down to 2^-17 of the bound keep all 22 bits.
+// LDS: the four operand images (dz hi/lo, x hi/lo) are [64 rows][128 channels] fp16, 256-byte rows
+// with the 16-byte chunks XOR-swizzled (guide T10, layout (b)); the fill writes a thread's four
+// channels as one 8-byte store per image, and the MFMA fragments (8 consecutive rows of one
+// column: K = rows) come out of ds_read_b64_tr_b16 transposed reads, two per fragment.
+typedef short w16_s16x4 __attribute__((vector_size(8)));
+typedef __attribute__((address_space(3))) w16_s16x4 w16_lds_s16x4;
+typedef _Float16 w16_h4 __attribute__((ext_vector_type(4)));
+typedef _Float16 w16_h8 __attribute__((ext_vector_type(8)));
+
+constexpr int kW16Rows = 64;                    // rows per LDS stage: two 32-row MFMA k-steps
+constexpr int kW16ImgB = kW16Rows * 256;        // bytes per operand image
+constexpr size_t kW16LdsB = 4 * kW16ImgB + 2 * 128 * sizeof(int);  // + the column exponents
+
+__device__ __forceinline__ int w16_off(int r, int ch) {  // byte offset of 16-byte chunk ch of row r
+  return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3)));
+}
+__device__ __forceinline__ w16_h4 w16_tr(const char* lds, int off) {
+  const w16_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (w16_lds_s16x4*)((__attribute__((address_space(3))) char*)lds + off));
+  return __builtin_bit_cast(w16_h4, v);
+}
+__device__ __forceinline__ void w16_split_store(char* hi_img, char* lo_img, int off, float4 v) {
+  const w16_h4 h = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+  const w16_h4 l = {(_Float16)(v.x - (float)h[0]), (_Float16)(v.y - (float)h[1]),
+                    (_Float16)(v.z - (float)h[2]), (_Float16)(v.w - (float)h[3])};
+  *reinterpret_cast<w16_h4*>(hi_img + off) = h;
+  *reinterpret_cast<w16_h4*>(lo_img + off) = l;
+}
+// e with bound * 2^e in [2^14, 2^15); 0 for a zero or non-finite bound
+__device__ __forceinline__ int w16_exp(float bound) {
+  if (!(bound > 0.f) || !(bound < INFINITY)) return 0;
+  int ex;
+  (void)frexpf(bound, &ex);
+  return min(max(15 - ex, -120), 120);
+}
+__device__ __forceinline__ float w16_key(const unsigned* keys, int i) {
+  const unsigned k = keys ? keys[i] : 0u;
+  return k ? ord_value(k) : 0.f;
+}
+
+template <int SRCX, int KS, int PAD, int LIN, int R, int POOL, int LP, bool EDGES, bool RAW = false>
+__device__ __forceinline__ void wgrad16_body(const WgradArgs& a, int bx, int by, int bz, char* lds) {
+  constexpr int RCH = kW16Rows;
+  constexpr int NB = EDGES ? 5 : 1;
+  constexpr int FR = RCH / 8;          // x rows per thread per stage (8 row slots x 32 channel quads)
+  constexpr int FW = RCH / POOL / 8;   // dz pool windows per thread per stage
+  static_assert(RCH % (8 * POOL) == 0 && R % POOL == 0, "a stage holds whole pool windows");
+  constexpr bool TRACK = SRCX == SRC_TRACK_F16 || SRCX == SRC_TRACK_F32;
+  // an fp16 track table is its own exact fp16 operand: one image, no split, one MFMA fewer per
+  // product, and bn0's affine (x - mu0) * invstd0 is applied to the reduced sums (k_bn0_grads)
+  constexpr bool XRAW = SRCX == SRC_TRACK_F16;
+  char* dzh = lds;
+  char* dzl = lds + kW16ImgB;
+  char* xh = lds + 2 * kW16ImgB;
+  char* xl = lds + 3 * kW16ImgB;
+  int* exp_o = reinterpret_cast<int*>(lds + 4 * kW16ImgB);
+  int* exp_c = exp_o + 128;
+  float (*bsum)[NB][128] = reinterpret_cast<float (*)[NB][128]>(lds);  // after the last stage
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int wo = wave >> 1, wk = wave & 1;
+  const int cout = a.cout, cin = a.cin, kcn = KS * cin;
+  const int obase = by * 128, kcbase = bx * 128;
+  const int total = a.M * R;  // rows (the host keeps M * R below 2^31)
+  const int r_begin = bz * a.rows_per_chunk;  // a multiple of RCH: stages hold whole windows
+  const int r_end = min(r_begin + a.rows_per_chunk, total);
+  const bool do_bias = bx == 0;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 bacc[NB];
+#pragma unroll
+  for (int e = 0; e < NB; ++e) bacc[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  // this thread fills channel quad q (dz outputs o..o+3, x columns kc..kc+3): dz of pool windows
+  // slot, slot+8, ... and x of row slots slot, slot+8, ...; everything per channel is set up once
+  const int q = tid & 31, slot = tid >> 5;
+  const int o = obase + 4 * q, kc = kcbase + 4 * q;
+  const bool o_ok = o < cout, kc_ok = kc < kcn;
+  const int oc = o_ok ? o : 0, kcc = kc_ok ? kc : 0;
+  const int kx = kcc / cin, cx = kcc - kx * cin;
+  float mu[4] = {}, iv[4] = {}, av[4] = {}, sd[4] = {}, sdx[4] = {};
+  if constexpr (!RAW) {
+    const float4 m4 = ld4(a.mean_l + oc), i4 = ld4(a.invstd_l + oc), a4 = ld4(a.a_l + oc);
+    mu[0] = m4.x; mu[1] = m4.y; mu[2] = m4.z; mu[3] = m4.w;
+    iv[0] = i4.x; iv[1] = i4.y; iv[2] = i4.z; iv[3] = i4.w;
+    av[0] = a4.x; av[1] = a4.y; av[2] = a4.z; av[3] = a4.w;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sd[s] = (float)acc_sum(a.dz_acc, cout, 0, oc + s);
+      sdx[s] = (float)acc_sum(a.dz_acc, cout, 1, oc + s);
+    }
+  }
+  if (!RAW && bx == 0 && by == 0 && bz == 0 && tid < cout) {
+    // BN_l = gamma * xhat + beta: dbeta = sum g, dgamma = sum g * xhat
+    a.dbeta[tid] = (float)acc_sum(a.dz_acc, cout, 0, tid);
+    a.dgamma[tid] = (float)acc_sum(a.dz_acc, cout, 1, tid);
+  }
+  const float4 xmu = ld4(a.x_mean + cx), xsc = ld4(a.x_a + cx);
+  const float4 xbe = a.x_beta ? ld4(a.x_beta + cx) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float xm[4] = {xmu.x, xmu.y, xmu.z, xmu.w}, xs_[4] = {xsc.x, xsc.y, xsc.z, xsc.w};
+  const float xb[4] = {xbe.x, xbe.y, xbe.z, xbe.w};
+
+  // the column scales (exponents also to LDS for the epilogue), folded into the per-channel
+  // coefficients: scaled dz = cas g - count (cA + xhat cB), scaled x = (src - xm) xas + xbs
+  float cas[4], cA[4], cB[4], xas[4], xbs[4];
+  {
+    int eo[4], ec[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float gmax = w16_key(a.g_range, oc + s);
+      float bo;
+      if constexpr (RAW) {
+        bo = gmax;
+      } else {
+        const float ym = fmaxf(w16_key(a.y_range, oc + s), 0.f);
+        const float xhm = fmaxf(fabsf(mu[s]), fabsf(ym - mu[s])) * iv[s];
+        bo = fabsf(av[s]) * (gmax + a.kd_max * (fabsf(sd[s]) + xhm * fabsf(sdx[s])));
+      }
+      eo[s] = o_ok ? w16_exp(bo) : 0;
+      float lo, hi;
+      if constexpr (TRACK) {
+        lo = -w16_key(a.x_range + kRngC, cx + s);
+        hi = w16_key(a.x_range, cx + s);
+      } else {
+        lo = 0.f;
+        hi = fmaxf(w16_key(a.x_range, cx + s), 0.f);
+      }
+      const float bx_ = fmaxf(fabsf((lo - xm[s]) * xs_[s] + xb[s]), fabsf((hi - xm[s]) * xs_[s] + xb[s]));
+      ec[s] = (kc_ok && !XRAW) ? w16_exp(bx_) : 0;
+      const float so = ldexpf(1.f, eo[s]), sx = ldexpf(1.f, ec[s]);
+      if constexpr (RAW) {
+        cas[s] = so; cA[s] = 0.f; cB[s] = 0.f;
+      } else {
+        cas[s] = av[s] * so;
+        cA[s] = av[s] * a.invN * sd[s] * so;
+        cB[s] = av[s] * a.invN * sdx[s] * so;
+      }
+      xas[s] = xs_[s] * sx;
+      xbs[s] = xb[s] * sx;
+    }
+    if (slot == 0) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        exp_o[4 * q + s] = eo[s];
+        exp_c[4 * q + s] = ec[s];
+      }
+    }
+  }
+  __syncthreads();  // the exponents are read by other waves' epilogues (even with no stage to run)
+
+  // raw operands of one stage, loaded branch-free (clamped addresses, masks applied at the fill):
+  // per pool window g, y, the argmax bytes and the item's count; per x row its four channels
+  float4 wg[FW], wy[FW];
+  uint32_t wid[FW];
+  float wcnt[FW];
+  float4 xr[XRAW ? 1 : FR];
+  uint2 xr16[XRAW ? FR : 1];
+  uint32_t xvalid = 0;
+  auto issue = [&](int rb) {
+#pragma unroll
+    for (int j = 0; j < FW; ++j) {
+      int rw = rb + (slot + 8 * j) * POOL;
+      rw = rw < r_end ? rw : r_begin;
+      const int ii = rw / R, t0 = rw - ii * R;
+      const long base = ((long)ii * LP + t0 / POOL) * cout + oc;
+      wg[j] = ld4(a.g_l + base);
+      if constexpr (!RAW) {
+        wy[j] = ld4(a.y_l + base);
+        wid[j] = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
+        wcnt[j] = a.counts ? a.counts[ii] : 1.f;
+      }
+    }
+    int ii[FR], pc[FR];
+    uint32_t vm = 0;
+#pragma unroll
+    for (int j = 0; j < FR; ++j) {
+      const int row = rb + slot + 8 * j;
+      const int rowc = row < r_end ? row : r_begin;
+      ii[j] = rowc / R;
+      const int p = rowc - ii[j] * R + kx - PAD;
+      vm |= (row < r_end && kc_ok && p >= 0 && p < LIN) ? (1u << j) : 0u;
+      pc[j] = p < 0 ? 0 : (p >= LIN ? LIN - 1 : p);
+    }
+    xvalid = vm;
+    if constexpr (TRACK) {
+      int trk[FR];
+#pragma unroll
+      for (int j = 0; j < FR; ++j) trk[j] = a.item_track[ii[j]];
+#pragma unroll
+      for (int j = 0; j < FR; ++j) {
+        const long e = ((long)trk[j] * kFrames + pc[j]) * kMels + cx;
+        if constexpr (XRAW)
+          xr16[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.xsrc) + e);
+        else
+          xr[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + e);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < FR; ++j)
+        xr[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + (((long)ii[j] * LIN + pc[j]) * cin + cx));
+    }
+  };
+
+  // fragment read offsets: lane 4q'+p of its 16-lane group g supplies row (8g + 4h + q') of the
+  // k-step, columns 4p..4p+3 of the 16-column tile (chunk = tile/8 + p/2, +8 B for odd p)
+  const int fq = l16 >> 2, fp = l16 & 3;
+  const int qoff = 8 * (q & 1);
+  if (r_begin < r_end) issue(r_begin);
+  for (int rb = r_begin; rb < r_end; rb += RCH) {
+    // dz: BN_l's backward once per pool window, scaled and split, then written to the window's
+    // rows -- the argmax row of each channel carries it, the others are zero (relu + max-pool)
+#pragma unroll
+    for (int j = 0; j < FW; ++j) {
+      const int wl = slot + 8 * j;
+      const int rw = rb + wl * POOL;
+      const bool wv = rw < r_end && o_ok;
+      const float gv[4] = {wg[j].x, wg[j].y, wg[j].z, wg[j].w};
+      float d[4];
+      if constexpr (RAW) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) d[s] = wv ? gv[s] * cas[s] : 0.f;
+      } else {
+        const float yv[4] = {wy[j].x, wy[j].y, wy[j].z, wy[j].w};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const float xh_ = (yv[s] - mu[s]) * iv[s];
+          const float v = cas[s] * gv[s] - wcnt[j] * (cA[s] + xh_ * cB[s]);
+          d[s] = (wv && yv[s] > 0.f) ? v : 0.f;
+        }
+      }
+      if (do_bias) {
+        bacc[0].x += d[0]; bacc[0].y += d[1]; bacc[0].z += d[2]; bacc[0].w += d[3];
+        if constexpr (EDGES) {  // t = 0, 1 (first window), R-2, R-1 (last): static indices only
+          const int t0 = rw - (rw / R) * R;
+          const bool first = t0 == 0, last = t0 == R - POOL;
+          float e1[4], e2[4], e3[4], e4[4];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const uint32_t r = (wid[j] >> (8 * s)) & 0xffu;
+            e1[s] = (first && r == 0u) ? d[s] : 0.f;
+            e2[s] = (first && r == 1u) ? d[s] : 0.f;
+            e3[s] = (last && r == (uint32_t)(POOL - 2)) ? d[s] : 0.f;
+            e4[s] = (last && r == (uint32_t)(POOL - 1)) ? d[s] : 0.f;
+          }
+          bacc[1].x += e1[0]; bacc[1].y += e1[1]; bacc[1].z += e1[2]; bacc[1].w += e1[3];
+          bacc[2 % NB].x += e2[0]; bacc[2 % NB].y += e2[1]; bacc[2 % NB].z += e2[2]; bacc[2 % NB].w += e2[3];
+          bacc[3 % NB].x += e3[0]; bacc[3 % NB].y += e3[1]; bacc[3 % NB].z += e3[2]; bacc[3 % NB].w += e3[3];
+          bacc[4 % NB].x += e4[0]; bacc[4 % NB].y += e4[1]; bacc[4 % NB].z += e4[2]; bacc[4 % NB].w += e4[3];
+        }
+      }
+      const w16_h4 h = {(_Float16)d[0], (_Float16)d[1], (_Float16)d[2], (_Float16)d[3]};
+      const w16_h4 l = {(_Float16)(d[0] - (float)h[0]), (_Float16)(d[1] - (float)h[1]),
+                        (_Float16)(d[2] - (float)h[2]), (_Float16)(d[3] - (float)h[3])};
+      const uint2 hb = __builtin_bit_cast(uint2, h), lb = __builtin_bit_cast(uint2, l);
+#pragma unroll
+      for (int jp = 0; jp < POOL; ++jp) {
+        uint32_t m0 = 0xffffffffu, m1 = 0xffffffffu;
+        if constexpr (POOL > 1) {
+          const uint32_t id = wid[j];
+          m0 = ((id & 0xffu) == (uint32_t)jp ? 0x0000ffffu : 0u) |
+               (((id >> 8) & 0xffu) == (uint32_t)jp ? 0xffff0000u : 0u);
+          m1 = (((id >> 16) & 0xffu) == (uint32_t)jp ? 0x0000ffffu : 0u) |
+               ((id >> 24) == (uint32_t)jp ? 0xffff0000u : 0u);
+        }
+        const int off = w16_off(wl * POOL + jp, q >> 1) + qoff;
+        *reinterpret_cast<uint2*>(dzh + off) = make_uint2(hb.x & m0, hb.y & m1);
+        *reinterpret_cast<uint2*>(dzl + off) = make_uint2(lb.x & m0, lb.y & m1);
+      }
+    }
+    // x: the layer input at tap kx (zero padding outside [0, LIN)), scaled and split
+#pragma unroll
+    for (int j = 0; j < FR; ++j) {
+      const bool ok = (xvalid >> j) & 1u;
+      const int off = w16_off(slot + 8 * j, q >> 1) + qoff;
+      if constexpr (XRAW) {
+        *reinterpret_cast<uint2*>(xh + off) = ok ? xr16[j] : make_uint2(0u, 0u);
+      } else {
+        const float x[4] = {xr[j].x, xr[j].y, xr[j].z, xr[j].w};
+        float v[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) v[s] = ok ? (x[s] - xm[s]) * xas[s] + xbs[s] : 0.f;
+        w16_split_store(xh, xl, off, make_float4(v[0], v[1], v[2], v[3]));
+      }
+    }
+    __syncthreads();
+    if (rb + RCH < r_end) issue(rb + RCH);  // next stage's loads fly while the MFMAs run
+#pragma unroll
+    for (int ks = 0; ks < RCH / 32; ++ks) {
+      w16_h8 ah[4], al[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int ch = (64 * wo + 16 * m) / 8 + (fp >> 1);
+        const int r0 = 32 * ks + 8 * g + fq;
+        const int o0 = w16_off(r0, ch) + 8 * (fp & 1), o1 = w16_off(r0 + 4, ch) + 8 * (fp & 1);
+        const w16_h4 h0 = w16_tr(dzh, o0), h1 = w16_tr(dzh, o1), l0 = w16_tr(dzl, o0), l1 = w16_tr(dzl, o1);
+        ah[m] = w16_h8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        al[m] = w16_h8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+      }
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int ch = (64 * wk + 16 * n) / 8 + (fp >> 1);
+        const int r0 = 32 * ks + 8 * g + fq;
+        const int o0 = w16_off(r0, ch) + 8 * (fp & 1), o1 = w16_off(r0 + 4, ch) + 8 * (fp & 1);
+        const w16_h4 h0 = w16_tr(xh, o0), h1 = w16_tr(xh, o1);
+        const w16_h8 bh = w16_h8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        if constexpr (XRAW) {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[m], bh, acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[m], bh, acc[m][n], 0, 0, 0);
+          }
+        } else {
+          const w16_h4 l0 = w16_tr(xl, o0), l1 = w16_tr(xl, o1);
+          const w16_h8 bl = w16_h8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[m], bh, acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[m], bl, acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[m], bh, acc[m][n], 0, 0, 0);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // partial block -> wpart[z][o][kc], unscaled; D lane map: o = 4g + reg, kc = l16
+  float* wp = a.wpart + (size_t)bz * cout * kcn;
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int kcl = 64 * wk + 16 * n + l16;
+    const int kcg = kcbase + kcl;
+    const int ecn = exp_c[kcl];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ol = 64 * wo + 16 * m + 4 * g + j;
+        if (obase + ol < cout && kcg < kcn)
+          wp[(size_t)(obase + ol) * kcn + kcg] = ldexpf(acc[m][n][j], -(exp_o[ol] + ecn));
+      }
+  }
+  if (do_bias) {  // (the operand images are free: the last stage ended with a barrier)
+#pragma unroll
+    for (int e = 0; e < NB; ++e) st4(&bsum[slot][e][4 * q], bacc[e]);
+    __syncthreads();
+    if (tid < 128 && obase + tid < cout) {
+      const int eo = exp_o[tid];
+#pragma unroll
+      for (int e = 0; e < NB; ++e) {
+        float v = 0.f;
+#pragma unroll
+        for (int sl = 0; sl < 8; ++sl) v += bsum[sl][e][tid];
+        a.bpart[((size_t)bz * NB + e) * cout + obase + tid] = ldexpf(v, -eo);
+      }
+    }
+  }
+}
+
+template <int SRCX, int KS, int PAD, int LIN, int R, int POOL, int LP, bool EDGES>
+__global__ __launch_bounds__(256) void k_conv_wgrad16(WgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds16[];
+  wgrad16_body<SRCX, KS, PAD, LIN, R, POOL, LP, EDGES>(a, blockIdx.x, blockIdx.y, blockIdx.z, lds16);
+}
+
+template <int L>
+__device__ __forceinline__ void wgrad16_multi_layer(const WgradMulti& w, int j, int b, char* lds) {
+  constexpr LayerGeom gm = layer_geom(L == 6 ? 5 : L);
+  const int kt = w.kt[j], ot = w.ot[j];
+  wgrad16_body<SRC_ACT, gm.ks, gm.pad, gm.lin, gm.lp * gm.pool, gm.pool, gm.lp, false, L == 6>(
+      w.a[j], b % kt, (b / kt) % ot, b / (kt * ot), lds);
+}
+
+__global__ __launch_bounds__(256) void k_conv_wgrad16_multi(WgradMulti w) {
+  extern __shared__ __attribute__((aligned(16))) char lds16[];
+  const int b = blockIdx.x;
+  int j = 0;
+  while (j + 1 < w.n && b >= w.start[j + 1]) ++j;
+  switch (w.layer[j]) {
+    case 2: wgrad16_multi_layer<2>(w, j, b - w.start[j], lds16); break;
+    case 3: wgrad16_multi_layer<3>(w, j, b - w.start[j], lds16); break;
+    case 4: wgrad16_multi_layer<4>(w, j, b - w.start[j], lds16); break;
+    case 5: wgrad16_multi_layer<5>(w, j, b - w.start[j], lds16); break;
+    default: wgrad16_multi_layer<6>(w, j, b - w.start[j], lds16); break;
+  }
+}
+
+// whether the weight gradients run on split-f16 MFMA (DCUE_WGRAD_F16=0: the f32-MFMA kernels)
+bool wgrad_f16_on() {
+  static const bool on = [] {
+    const char* e = getenv("DCUE_WGRAD_F16");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // Layer-1 weight gradient (the step's largest MFMA kernel). The GEMM is
 // dW1[o][kc] = sum over conv-1 rows (item, t) of dz1[row][o] * xhat0[item][t + kx - 2][c], K = M*132
 // rows, kc = kx*128 + c. dz1 is BN1's backward through relu + max-pool: of each pool window's four
@@ -612,7 +1030,7 @@ int wgrad_nchunk(int layer, int M, int cout, int cin) {
   // blocks cost a write + a read of cout*ks*cin floats per chunk (layer 6: the fc, geometry of 5)
   const LayerGeom gm = layer_geom(layer == 6 ? 5 : layer);
   const long rows = (long)M * gm.lp * gm.pool;
-  if (layer == 1) {  // k_conv1_wgrad: 64x64 tiles, >= 4 steps per chunk, <= ~512 workgroups (2 per CU)
+  if (layer == 1 && !wgrad_f16_on()) {  // k_conv1_wgrad: 64x64 tiles, >= 4 steps per chunk, <= ~512 workgroups (2 per CU)
     // tuning diagnostic: DCUE_W1_CHUNKS=n caps the split-K chunk count (A/B runs; the workspace is
     // sized through this same function, so it follows)
     static const long forced = [] {
@@ -657,7 +1075,46 @@ static int wgrad_layer(const WgradArgs& a0, int nchunk, hipStream_t s) {
   return DCUE_OK;
 }
 
+// split-K chunk length of the split-f16 kernels: whole stages (so whole pool windows), and chunks
+// past the rows simply contribute zero partial blocks
+static long w16_rows_per_chunk(long rows, int nchunk) {
+  const long rpc = (rows + nchunk - 1) / nchunk;
+  return (rpc + kW16Rows - 1) / kW16Rows * kW16Rows;
+}
+
+template <int L, int SRCX>
+static int wgrad16_layer(const WgradArgs& a0, int nchunk, hipStream_t s) {
+  constexpr LayerGeom gm = layer_geom(L);
+  constexpr int R = gm.lp * gm.pool;
+  auto kern = k_conv_wgrad16<SRCX, gm.ks, gm.pad, gm.lin, R, gm.pool, gm.lp, L == 1>;
+  static bool attr = false;
+  if (!attr) {
+    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)kW16LdsB));
+    attr = true;
+  }
+  WgradArgs a = a0;
+  const long rows = (long)a.M * R;
+  if (rows >= (1L << 30)) return DCUE_ERR_UNSUPPORTED;  // 32-bit row indices
+  a.rows_per_chunk = (int)w16_rows_per_chunk(rows, nchunk);
+  dim3 grid((unsigned)((gm.ks * a.cin + 127) / 128), (unsigned)((a.cout + 127) / 128), (unsigned)nchunk);
+  DCUE_LAUNCH(kern, grid, dim3(256), kW16LdsB, s, a);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
 int launch_conv_wgrad(int layer, int src, const WgradArgs& a, int nchunk, hipStream_t s) {
+  if (wgrad_f16_on()) {  // layer 1 reads the track table (bn0 applied at the fill), not xhat0
+    switch (layer) {
+      case 1: return src == SRC_TRACK_F16 ? wgrad16_layer<1, SRC_TRACK_F16>(a, nchunk, s)
+                                          : wgrad16_layer<1, SRC_TRACK_F32>(a, nchunk, s);
+      case 2: return wgrad16_layer<2, SRC_ACT>(a, nchunk, s);
+      case 3: return wgrad16_layer<3, SRC_ACT>(a, nchunk, s);
+      case 4: return wgrad16_layer<4, SRC_ACT>(a, nchunk, s);
+      case 5: return wgrad16_layer<5, SRC_ACT>(a, nchunk, s);
+      default: return DCUE_ERR_INVALID;
+    }
+  }
   switch (layer) {
     case 1: (void)src; return conv1_wgrad(a, nchunk, s);  // X = xhat0 (k_xhat0), whatever the table dtype
     case 2: return wgrad_layer<2, SRC_ACT>(a, nchunk, s);
@@ -757,11 +1214,14 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce_multi(WgradMulti w) {
 }
 
 int launch_conv_wgrad_multi(WgradMulti w, hipStream_t s) {
-  constexpr size_t LDS = wgrad_lds_floats(1) * sizeof(float);
+  const bool f16 = wgrad_f16_on();
+  const size_t LDS = f16 ? kW16LdsB : wgrad_lds_floats(1) * sizeof(float);
   static bool attr = false;
   if (!attr) {
     DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_conv_wgrad_multi, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)LDS));
+                                       (int)(wgrad_lds_floats(1) * sizeof(float))));
+    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_conv_wgrad16_multi,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kW16LdsB));
     attr = true;
   }
   w.start[0] = 0;
@@ -773,13 +1233,17 @@ int launch_conv_wgrad_multi(WgradMulti w, hipStream_t s) {
     const LayerGeom gm = layer_geom(w.layer[j] == 6 ? 5 : w.layer[j]);
     if (a.cin % 32 || a.cout % 4) return DCUE_ERR_UNSUPPORTED;
     const long rows = (long)a.M * gm.lp * gm.pool;
-    a.rows_per_chunk = (int)((rows + w.nchunk[j] - 1) / w.nchunk[j]);
+    if (f16 && rows >= (1L << 30)) return DCUE_ERR_UNSUPPORTED;
+    a.rows_per_chunk = (int)(f16 ? w16_rows_per_chunk(rows, w.nchunk[j]) : (rows + w.nchunk[j] - 1) / w.nchunk[j]);
     w.kt[j] = (gm.ks * a.cin + 127) / 128;
     w.ot[j] = (a.cout + 127) / 128;
     w.start[j + 1] = w.start[j] + w.kt[j] * w.ot[j] * w.nchunk[j];
     w.rstart[j + 1] = w.rstart[j] + (int)(((long)a.cout * gm.ks * a.cin + 127) / 128 + (a.cout + 127) / 128);
   }
-  DCUE_LAUNCH(k_conv_wgrad_multi, dim3((unsigned)w.start[w.n]), dim3(256), LDS, s, w);
+  if (f16)
+    DCUE_LAUNCH(k_conv_wgrad16_multi, dim3((unsigned)w.start[w.n]), dim3(256), LDS, s, w);
+  else
+    DCUE_LAUNCH(k_conv_wgrad_multi, dim3((unsigned)w.start[w.n]), dim3(256), LDS, s, w);
   DCUE_LAUNCH_CHECK();
   DCUE_LAUNCH(k_wgrad_reduce_multi, dim3((unsigned)w.rstart[w.n]), dim3(256), 0, s, w);
   DCUE_LAUNCH_CHECK();
@@ -801,9 +1265,12 @@ int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int n
 // bn0 gradients without conv1's input gradient: with xhat0 the normalised input and
 // G[o][k*128+c] = sum dz1 * xhat0_pad, S[k][o] = sum of dz1 over rows whose tap-k input is real,
 //   dW1[o][c][k] = gamma0[c] G + beta0[c] S,   dgamma0[c] = sum_{o,k} W1 G,   dbeta0[c] = sum_{o,k} W1 S.
+// With mean0 set, G holds the contraction with the raw fp16 input instead (the split-f16 weight
+// gradient's exact operand): sum dz1 * xhat0 = invstd0 (G - mean0 S) over the same rows.
 __global__ __launch_bounds__(256) void k_bn0_grads(const float* __restrict__ G, const float* __restrict__ E,
                                                    const float* __restrict__ W1, const float* gamma0,
-                                                   const float* beta0, int H, float* dW1,
+                                                   const float* beta0, const float* mean0,
+                                                   const float* invstd0, int H, float* dW1,
                                                    float* dgamma0, float* dbeta0, float* db1) {
   critical_path_priority();
   // E = the five layer-1 bias-partial sums [5][H]: sum dz1 and its parts at t = 0, 1, R-2, R-1.
@@ -812,12 +1279,14 @@ __global__ __launch_bounds__(256) void k_bn0_grads(const float* __restrict__ G, 
   __shared__ float rg[256], rb[256];
   const int c = blockIdx.x, t = threadIdx.x;
   const float ga = gamma0[c], be = beta0[c];
+  const float m0 = mean0 ? mean0[c] : 0.f, i0 = mean0 ? invstd0[c] : 1.f;
   float dg = 0.f, db = 0.f;
   for (int e = t; e < 4 * H; e += blockDim.x) {  // e = o*4 + k: dW1[o][c][k] layout
     const int o = e >> 2, k = e & 3;
-    const float gv = G[(size_t)o * 4 * kMels + k * kMels + c];
     const float e0 = E[o], e1 = E[H + o], e2 = E[2 * H + o], e3 = E[3 * H + o], e4 = E[4 * H + o];
     const float sv = k == 0 ? e0 - e1 - e2 : k == 1 ? e0 - e1 : k == 2 ? e0 - e4 : e0 - e3 - e4;
+    const float gr = G[(size_t)o * 4 * kMels + k * kMels + c];
+    const float gv = mean0 ? i0 * (gr - m0 * sv) : gr;
     const float w = W1[((size_t)o * kMels + c) * 4 + k];
     dg += w * gv;
     db += w * sv;
@@ -842,10 +1311,10 @@ __global__ __launch_bounds__(256) void k_bn0_grads(const float* __restrict__ G, 
 }
 
 int launch_bn0_grads(const float* G, const float* E, const float* W1, const float* gamma0,
-                     const float* beta0, int H, float* dW1, float* dgamma0, float* dbeta0, float* db1,
-                     hipStream_t s) {
-  DCUE_LAUNCH(k_bn0_grads, dim3(kMels), dim3(256), 0, s, G, E, W1, gamma0, beta0, H, dW1, dgamma0,
-                     dbeta0, db1);
+                     const float* beta0, const float* mean0, const float* invstd0, int H, float* dW1,
+                     float* dgamma0, float* dbeta0, float* db1, hipStream_t s) {
+  DCUE_LAUNCH(k_bn0_grads, dim3(kMels), dim3(256), 0, s, G, E, W1, gamma0, beta0, mean0, invstd0, H, dW1,
+              dgamma0, dbeta0, db1);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }

@@ -74,6 +74,7 @@ struct RowsArgs {
   // merged by the epilogue (nullable)
   const unsigned* in_range;
   unsigned* out_range;
+  unsigned* out_grange;  // dgrad: max |g_{l-1}| per channel (ordered keys), for the split-f16 wgrad
 };
 
 struct WgradArgs {
@@ -97,6 +98,11 @@ struct WgradArgs {
   int rows_per_chunk;
   float* wpart;               // [nchunk][cout][KS*cin]  (kc = k*cin + c)
   float* bpart;               // [nchunk][NB][cout]
+  // split-f16 kernels (conv_wgrad.hip wgrad16_body): the operand columns' magnitude bounds
+  const unsigned* x_range;    // the x source's value range, [2][kRngC] ordered keys (+x, -x)
+  const unsigned* y_range;    // y_l's range ([0][c]: its maximum; a ReLU output)
+  const unsigned* g_range;    // max |g_l| per channel (ordered keys of |g|), from its producer
+  float kd_max;               // the largest copies(item) * invN of the batch
 };
 
 // weight gradients of n conv layers (of 2..5) in one launch, then their chunk sums in a second one
@@ -114,6 +120,8 @@ struct WgradMulti {
   int rstart[kWgradMultiMax + 1];     // reduce block ranges
 };
 int launch_conv_wgrad_multi(WgradMulti w, hipStream_t s);
+// weight gradients on split-f16 MFMA (DCUE_WGRAD_F16=0: the f32-MFMA kernels)
+bool wgrad_f16_on();
 
 int launch_conv_fwd(int layer, int kc, int src, const RowsArgs& a, hipStream_t s);
 int launch_conv_dgrad(int layer, int kc, const RowsArgs& a, hipStream_t s);
@@ -128,9 +136,10 @@ int wgrad_nchunk(int layer, int M, int cout, int cin);
 int launch_conv1_dx(const WgradArgs& a, float* dx1, hipStream_t s);
 int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int nchunk, int cout,
                         int cin, float* dW, float* db, float* G_tmp, float* E_tmp, hipStream_t s);
+// mean0 / invstd0 (nullable): G is the contraction with the raw input (split-f16 path, fp16 table)
 int launch_bn0_grads(const float* G, const float* E, const float* W1, const float* gamma0,
-                     const float* beta0, int H, float* dW1, float* dgamma0, float* dbeta0, float* db1,
-                     hipStream_t s);
+                     const float* beta0, const float* mean0, const float* invstd0, int H, float* dW1,
+                     float* dgamma0, float* dbeta0, float* db1, hipStream_t s);
 
 // ------------------------------------------------------------------------------- BatchNorm
 // bn0 statistics of the gathered spectrograms (count-weighted) into accumulators [2][128]
@@ -217,6 +226,7 @@ struct TGemmArgs {
   // xhat = (xy[m][n] - xmean[n]) * xinvstd[n]
   unsigned long long* colacc;
   const float *xy, *xmean, *xinvstd;
+  unsigned* colmax;  // nullable: max |C| per column (ordered keys), the split-f16 wgrad's dz bound
 };
 int launch_tgemm(int ta, int tb, const TGemmArgs& g, hipStream_t s);
 
@@ -233,10 +243,11 @@ int launch_score_bwd(const float* uf, const float* f, const dcue_batch* b, int d
                      float* dfcopy, hipStream_t s);
 // per-item feature gradients; with fcW also the fc input gradient g5 = df W and BN5's backward sums.
 // copy_ptr / copy_idx (nullable): the gather layout's per-item copy lists from the step prologue
+// g5max / dfmax (nullable): max |g5| / max |df| per column, ordered keys (split-f16 wgrad bounds)
 int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df, const float* fcW, float* g5,
                      unsigned long long* acc5, const float* y5, const float* mean5, const float* invstd5,
                      const float* rowsum, float* loss, const int32_t* copy_ptr, const int32_t* copy_idx,
-                     hipStream_t s);
+                     unsigned* g5max, unsigned* dfmax, hipStream_t s);
 int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float scale,
                     float* emb_grad, int32_t* slot, int64_t* emb_rows, dcue_emb_log* log,
                     hipStream_t s);

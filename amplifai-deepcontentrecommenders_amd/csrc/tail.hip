@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   }
   // epilogue operands: every load issued (at clamped, in-bounds indices) before any is used -- a
   // per-element conditional load makes hipcc wait for each one in turn
-  float cs = 0.f, csx = 0.f;
+  float cs = 0.f, csx = 0.f, cmx = 0.f;
   const int nc = min(n, g.N - 1);
   float bn = 0.f, xmu = 0.f, xis = 0.f;
   float cmv[4] = {1.f, 1.f, 1.f, 1.f}, xyv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -217,6 +217,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       float v = acc[j] + bn;
       if (g.cmask && !(cmv[j] > 0.f)) v = 0.f;
       g.C[(long)mm * g.scm + (long)n * g.scn] = v;
+      cmx = fmaxf(cmx, fabsf(v));
       if (g.colacc) {
         cs += v;
         csx += v * ((xyv[j] - xmu) * xis);
@@ -230,6 +231,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       acc128_add(acc_at(g.colacc, g.N, 0, n), cs);
       acc128_add(acc_at(g.colacc, g.N, 1, n), csx);
     }
+  }
+  if (g.colmax) {  // max |C| per column over the tile
+    cmx = fmaxf(cmx, __shfl_xor(cmx, 16, 64));
+    cmx = fmaxf(cmx, __shfl_xor(cmx, 32, 64));
+    if (kq == 0 && nok) atomicMax(g.colmax + n, ord_key(cmx));
   }
 }
 
@@ -584,6 +590,8 @@ struct ItemGradFc {
   float* g5;               // [M][d]
   unsigned long long* acc; // BN5 backward accumulators [2][d]
   const float *y5, *mean5, *invstd5;
+  unsigned* g5max;         // nullable: max |g5| per column (ordered keys; split-f16 wgrad bound)
+  unsigned* dfmax;         // nullable: max |df| per column
 };
 
 constexpr int kItemGradWLds = 128;  // W staged in LDS up to d = 128 (64 KB)
@@ -743,10 +751,15 @@ __global__ __launch_bounds__(256) void k_item_grad(const float* __restrict__ dfc
       const int n = threadIdx.x;
       const float g = part[0][n] + part[1][n];
       fc.g5[(long)i * d + n] = g;
+      if (fc.g5max) atomicMax(fc.g5max + n, ord_key(fabsf(g)));
       const float xh = (y5v - mu5) * is5;
       acc128_add(acc_at(fc.acc, d, 0, n), g);
       acc128_add(acc_at(fc.acc, d, 1, n), g * xh);
     }
+  }
+  if (fc.dfmax) {
+    __syncthreads();
+    for (int k = threadIdx.x; k < d; k += blockDim.x) atomicMax(fc.dfmax + k, ord_key(fabsf(dfs[k])));
   }
   if (fc.rowsum && i == 0) {  // loss = mean of the row sums in row order (k_loss_mean's sums)
     __syncthreads();
@@ -832,6 +845,16 @@ __global__ __launch_bounds__(256) void k_item_grad_multi(const float* __restrict
       if (e < per && k < d) dfs[it][k] = acc[e];
     }
   }
+  if (fc.dfmax) {  // max |df| per column over the block's items
+    __syncthreads();
+    if (threadIdx.x < d) {
+      float m = 0.f;
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+        if (i0 + it < M) m = fmaxf(m, fabsf(dfs[it][threadIdx.x]));
+      atomicMax(fc.dfmax + threadIdx.x, ord_key(m));
+    }
+  }
   if (fc.W) {
     __syncthreads();
     // g5[i][n] = sum_k df[i][k] W[k][n], k in two halves (first + second); d <= 128 here
@@ -854,19 +877,21 @@ __global__ __launch_bounds__(256) void k_item_grad_multi(const float* __restrict
     if (threadIdx.x < d) {
       const int n = threadIdx.x;
       const float mu5 = fc.mean5[n], is5 = fc.invstd5[n];
-      float sg = 0.f, sgx = 0.f;
+      float sg = 0.f, sgx = 0.f, gm = 0.f;
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
         const int i = i0 + it;
         if (i < M) {
           const float g = part[0][it][n] + part[1][it][n];
           fc.g5[(long)i * d + n] = g;
+          gm = fmaxf(gm, fabsf(g));
           sg += g;
           sgx += g * ((fc.y5[(long)i * d + n] - mu5) * is5);
         }
       }
       acc128_add(acc_at(fc.acc, d, 0, n), sg);
       acc128_add(acc_at(fc.acc, d, 1, n), sgx);
+      if (fc.g5max) atomicMax(fc.g5max + n, ord_key(gm));
     }
   }
   if (fc.rowsum && blockIdx.x == 0) {  // loss = mean of the row sums in row order (k_loss_mean's sums)
@@ -897,11 +922,11 @@ static int item_grad_multi(const float* dfcopy, const dcue_batch* b, int d, floa
 int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df, const float* fcW, float* g5,
                      unsigned long long* acc5, const float* y5, const float* mean5, const float* invstd5,
                      const float* rowsum, float* loss, const int32_t* copy_ptr, const int32_t* copy_idx,
-                     hipStream_t s) {
+                     unsigned* g5max, unsigned* dfmax, hipStream_t s) {
   if (d > 256 || (rowsum && b->n_rows > 1024)) return DCUE_ERR_UNSUPPORTED;
   const bool gather = b->layout == DCUE_LAYOUT_GATHER;
   if ((!gather || copy_ptr) && (!fcW || d <= 128)) {  // multi-item workgroups
-    const ItemGradFc fc = {rowsum, loss, fcW, g5, acc5, y5, mean5, invstd5};
+    const ItemGradFc fc = {rowsum, loss, fcW, g5, acc5, y5, mean5, invstd5, g5max, dfmax};
     const bool wlds = fcW && d % 4 == 0;
     const size_t lds = wlds ? sizeof(float) * d * d : 0;
     // many items (catalogue M = B(1+N)): 16 per workgroup; a few (in-batch M = B): 4
@@ -930,7 +955,7 @@ int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df,
                 : item_grad_multi<1, false>(dfcopy, b, d, df, copy_ptr, copy_idx, fc, lds, s);
   }
   if (b->layout == DCUE_LAYOUT_GATHER && (long)b->n_rows * b->n_neg + 1 > kItemGradCap) return DCUE_ERR_UNSUPPORTED;
-  const ItemGradFc fc = {rowsum, loss, fcW, g5, acc5, y5, mean5, invstd5};
+  const ItemGradFc fc = {rowsum, loss, fcW, g5, acc5, y5, mean5, invstd5, g5max, dfmax};
   if (fcW && d <= kItemGradWLds && d % 4 == 0) {
     const size_t lds = sizeof(float) * d * d;
     static bool attr = false;
