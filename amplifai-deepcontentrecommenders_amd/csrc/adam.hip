@@ -67,7 +67,8 @@ __device__ __forceinline__ void window_bound(const AdamScalars* hs, int j0, int 
 }
 
 struct PackSeg {
-  long src, fwd, bwd, f16;  // floats: W in params; forward pack; dgrad pack (-1: none); split-f16 pack
+  long src, fwd, bwd, f16, f16b;  // floats: W in params; forward pack; dgrad pack (-1: none); split-f16
+                                 // forward and dgrad packs
   int cout, cin, ks;
 };
 struct PackArgs;
@@ -96,6 +97,13 @@ __device__ __forceinline__ void pack_store(const PackSeg& sg, long e, float w, f
   const long base = ((q * sg.cout + o) * 4 + (cc & 31) / 8) * 16 + (cc & 7);
   h16[base] = hi;
   h16[base + 8] = lo;
+  if (sg.f16b >= 0) {  // split-f16 dgrad operand: K = (reversed tap, o), columns cc
+    _Float16* b16 = reinterpret_cast<_Float16*>(wpack + sg.f16b);
+    const long qb = (sg.ks - 1 - k) * (sg.cout / 32) + o / 32;
+    const long bb = ((qb * sg.cin + cc) * 4 + (o & 31) / 8) * 16 + (o & 7);
+    b16[bb] = hi;
+    b16[bb + 8] = lo;
+  }
 }
 
 // Adam over the flat dense buffer with the conv-weight repack fused in: a float4 that lies in a
@@ -501,6 +509,7 @@ PackArgs pack_args(const dcue_model* md, const int64_t* poff) {
     sg.fwd = wl.conv_fwd[l];
     sg.bwd = l >= 2 ? wl.conv_bwd[l] : -1;
     sg.f16 = wl.conv_f16[l];
+    sg.f16b = l >= 2 ? wl.conv_f16b[l] : -1;
   }
   return pa;
 }

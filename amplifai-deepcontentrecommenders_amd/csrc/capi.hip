@@ -7,6 +7,7 @@
 //             BN1 -> wgrad_1 (+ bn0 grads without conv1 dgrad) -> user tower -> embedding rows
 //   adam      dense params + user table, then weight repack
 #include <math.h>
+#include <atomic>
 #include <string.h>
 
 #include "dcue_internal.h"
@@ -74,6 +75,9 @@ LaunchTag& launch_tag() {
   thread_local LaunchTag t;
   return t;
 }
+
+static std::atomic<int64_t> g_launches{0};
+void count_launch() { g_launches.fetch_add(1, std::memory_order_relaxed); }
 
 bool& capturing_step() {
   thread_local bool c = false;
@@ -536,6 +540,8 @@ extern "C" {
 
 int dcue_abi_version(void) { return DCUE_ABI_VERSION; }
 
+int64_t dcue_launch_count(void) { return dcue::g_launches.load(std::memory_order_relaxed); }
+
 int dcue_storage_dims(const dcue_dims* dims, dcue_dims* storage_host) {
   TRY(check_dims(dims));
   if (!storage_host) return DCUE_ERR_INVALID;
@@ -837,6 +843,10 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       ra.skip_scale = 1.0f / (float)layer_geom(l - 1).lp;
     }
     ra.wpack = m->wpack + wpack_offset(&m->dims, l, true);
+    ra.wpack16 = reinterpret_cast<const uint4*>(m->wpack + wpack_layout(&m->dims).conv_f16b[l]);
+    // the split-f16 dgrad's dz bound: max |g_l| (the previous dgrad / item gradient), y_l's range
+    ra.in_range = grng_at(w, l); ra.y_range = rng_at(w, l);
+    ra.kd_max = (float)kd_max * ra.invN;
     ra.out = w.g[l - 1];
     ra.out_acc = bn_acc(w.bnbacc, w.cmax, l - 1);
     ra.oy = w.y[l - 1]; ra.omean = w.mean[l - 1]; ra.oinvstd = w.invstd[l - 1];

@@ -6,9 +6,23 @@ namespace dcue {
 
 // dgrad of layer L: rows = (item, input position t' < Lin_L), slab = layer-L conv positions
 // [0, Lp*pool) carrying dz, taps reversed (PADL = ks-1-pad).
+// Split-f16 MFMA (conv_rows.h F16: three f16 products per 32-channel chunk, the dz slab scaled by a
+// power of two from the dz bound, range_stage) unless DCUE_DGRAD_F16=0 selects the exact-f32 path
+static bool dgrad_f16_on() {
+  static const bool on = [] {
+    const char* e = getenv("DCUE_DGRAD_F16");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <int L, int KC, int TW>
 static int dgrad_layer_tw(const RowsArgs& a, hipStream_t s) {
   constexpr LayerGeom gm = layer_geom(L);
+  static_assert(KC % 32 == 0, "split-f16 chunks are 32 channels");
+  if (a.wpack16 && a.in_range && dgrad_f16_on())
+    return run_rows<1, SRC_DZ, KC, gm.ks, gm.ks - 1 - gm.pad, gm.lp * gm.pool, gm.lin, 1, TW, gm.lp,
+                    gm.pool, true>(a, s);
   return run_rows<1, SRC_DZ, KC, gm.ks, gm.ks - 1 - gm.pad, gm.lp * gm.pool, gm.lin, 1, TW, gm.lp,
                   gm.pool>(a, s);
 }

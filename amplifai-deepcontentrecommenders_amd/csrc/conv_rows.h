@@ -53,12 +53,23 @@ struct ChanLds {
 // are at x = min and x = max (the ReLU outputs of layers >= 2 have min 0). Every workgroup of the
 // launch reads the same ranges, so all use the same S. Threads t < KC own channel t (chan_stage);
 // waves 0-3 reduce the bounds, and after the block barrier every thread forms S from the four.
+// The dgrad (SRC_DZ) operand is dz = a (g - kD sD - kD xhat sDx) (masked): |dz| <= |a| (max|g| +
+// kDmax (|sD| + max|xhat| |sDx|)), max|g| from the producer's epilogue (in_range), max|xhat| from
+// y_l's range -- the same bound as the split-f16 weight gradient's (conv_wgrad.hip).
 template <int SRC>
 __device__ __forceinline__ void range_stage(const RowsArgs& a, int KC, ChanLds& L) {
   const int t = threadIdx.x;
   if (t >= 256) return;  // waves 0-3 (uniform per wave)
   float bnd = 0.f;
-  if (t < KC && a.in_range) {
+  if (SRC == SRC_DZ) {
+    if (t < KC && a.in_range) {
+      const unsigned kg = a.in_range[t], ky = a.y_range ? a.y_range[t] : 0u;
+      const float gmax = kg ? ord_value(kg) : 0.f, ym = ky ? fmaxf(ord_value(ky), 0.f) : 0.f;
+      const float mu = L.v[0][t], av = L.v[1][t], iv = L.v[2][t];
+      const float xhm = fmaxf(fabsf(mu), fabsf(ym - mu)) * iv;
+      bnd = fabsf(av) * (gmax + a.kd_max * (fabsf(L.v[3][t]) + xhm * fabsf(L.v[4][t])));
+    }
+  } else if (t < KC && a.in_range) {
     const unsigned khi = a.in_range[t], knlo = a.in_range[kRngC + t];
     float hi = khi ? ord_value(khi) : 0.f;
     float lo = (SRC == SRC_ACT) ? 0.f : (knlo ? -ord_value(knlo) : 0.f);
@@ -459,7 +470,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (grb + j < total) {
-            float gv = acc[r][ct][j];
+            float gv = acc[r][ct][j] * sscale.inv;  // 1 on the f32 path; exact power of two on the split path
             if (a.skip && o < a.skip_n) gv += a.skip[((grb + j) / R) * a.skip_ld + o] * a.skip_scale;
             a.out[(grb + j) * nout + o] = gv;
             gmx[ct] = fmaxf(gmx[ct], fabsf(gv));

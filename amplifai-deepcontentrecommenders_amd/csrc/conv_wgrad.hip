@@ -646,7 +646,7 @@ __device__ __forceinline__ void wgrad16_body(const WgradArgs& a, int bx, int by,
 }
 
 template <int SRCX, int KS, int PAD, int LIN, int R, int POOL, int LP, bool EDGES>
-__global__ __launch_bounds__(256) void k_conv_wgrad16(WgradArgs a) {
+__global__ __launch_bounds__(256, 2) void k_conv_wgrad16(WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds16[];
   wgrad16_body<SRCX, KS, PAD, LIN, R, POOL, LP, EDGES>(a, blockIdx.x, blockIdx.y, blockIdx.z, lds16);
 }
@@ -659,7 +659,7 @@ __device__ __forceinline__ void wgrad16_multi_layer(const WgradMulti& w, int j, 
       w.a[j], b % kt, (b / kt) % ot, b / (kt * ot), lds);
 }
 
-__global__ __launch_bounds__(256) void k_conv_wgrad16_multi(WgradMulti w) {
+__global__ __launch_bounds__(256, 2) void k_conv_wgrad16_multi(WgradMulti w) {
   extern __shared__ __attribute__((aligned(16))) char lds16[];
   const int b = blockIdx.x;
   int j = 0;
@@ -1045,7 +1045,13 @@ int wgrad_nchunk(int layer, int M, int cout, int cin) {
     return (int)(n < 1 ? 1 : n);
   }
   const long tiles = ((gm.ks * cin + 127) / 128) * ((cout + 127) / 128);
-  long n = 256 / tiles;
+  // split-f16 kernels: two workgroups per CU (one's MFMAs and fill run while the other's stage
+  // loads are in flight); DCUE_W16_WGS_PER_CU=1 halves the chunks (A/B diagnostic)
+  static const long per_cu = [] {
+    const char* e = getenv("DCUE_W16_WGS_PER_CU");
+    return e && atoi(e) == 1 ? 1L : 2L;
+  }();
+  long n = (wgrad_f16_on() ? 256 * per_cu : 256) / tiles;
   if (n > (rows + 63) / 64) n = (rows + 63) / 64;
   const long cap = (8L << 20) / ((long)cout * gm.ks * cin);
   if (n > cap) n = cap;

@@ -38,12 +38,15 @@ struct LaunchTag {
   bool missed = false;  // a nested scope's launches bound another event: `stop` must be recorded
 };
 LaunchTag& launch_tag();
+// process-wide launch counter (dcue_launch_count)
+void count_launch();
 }  // namespace dcue
 
 // Every kernel launch of the library goes through here (see LaunchTag).
 #define DCUE_LAUNCH(kern, grid, block, shm, stream, ...)                                          \
   do {                                                                                            \
     ::dcue::LaunchTag& dcue_tag_ = ::dcue::launch_tag();                                          \
+    ::dcue::count_launch();                                                                       \
     if (dcue_tag_.stop) {                                                                         \
       hipExtLaunchKernelGGL(kern, grid, block, shm, stream, dcue_tag_.start, dcue_tag_.stop, 0,   \
                             __VA_ARGS__);                                                         \

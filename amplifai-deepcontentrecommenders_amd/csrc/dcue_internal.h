@@ -72,9 +72,11 @@ struct RowsArgs {
   // the raw track values (layer 1) or the previous layer's ReLU output (min 0) -- from which every
   // workgroup derives the same power-of-two operand scale; out_range: this layer's output maximum,
   // merged by the epilogue (nullable)
-  const unsigned* in_range;
+  const unsigned* in_range;  // dgrad (SRC_DZ): max |g_l| per channel instead (ordered keys)
   unsigned* out_range;
   unsigned* out_grange;  // dgrad: max |g_{l-1}| per channel (ordered keys), for the split-f16 wgrad
+  const unsigned* y_range;  // dgrad: y_l's range (its maximum), for the dz bound
+  float kd_max;             // dgrad: the largest copies(item) * invN of the batch
 };
 
 struct WgradArgs {
@@ -154,9 +156,11 @@ int launch_bn_eval(int C, const float* gamma, const float* rmean, const float* r
 // wpack = conv B operands (forward per layer, dgrad per layer >= 2). Dense weights are read in place.
 // conv_f16[l]: the forward B operand split into fp16 pairs w = hi + lo (hi = fp16(w), lo =
 // fp16(w - hi)) for the split-f16 MFMA forward (conv.hip), as halves
-// [k * cin/32 + c/32][cout][(c % 32) / 8][hi, lo][c % 8] -- one float slot per weight
+// [k * cin/32 + c/32][cout][(c % 32) / 8][hi, lo][c % 8] -- one float slot per weight;
+// conv_f16b[l] (l >= 2): the dgrad B operand the same way, K = (reversed tap, layer-l channel o),
+// columns = layer l-1's channels: [(ks-1-k) * cout/32 + o/32][cin][(o % 32) / 8][hi, lo][o % 8]
 struct WpackLayout {
-  long conv_fwd[6], conv_bwd[6], conv_f16[6];
+  long conv_fwd[6], conv_bwd[6], conv_f16[6], conv_f16b[6];
   long total;
 };
 inline WpackLayout wpack_layout(const dcue_dims* dm) {
@@ -172,6 +176,8 @@ inline WpackLayout wpack_layout(const dcue_dims* dm) {
     if (l >= 2) n += e;
     w.conv_f16[l] = n;  // cin is a multiple of 32 (128, or H in 32..256)
     n += e;
+    w.conv_f16b[l] = l >= 2 ? n : -1;  // cout too (H or d_s)
+    if (l >= 2) n += e;
   }
   w.total = n;
   return w;

@@ -98,12 +98,13 @@ class PlanConfig(ctypes.Structure):
 
 MT_STATE_BYTES = 624 * 4 + 16
 MAX_LOG_CAP = 256
-ABI_VERSION = 9
+ABI_VERSION = 10
 RANK_SPLIT, RANK_SINGLE = 0, 1
 
 _P = ctypes.c_void_p
 _SIGS = {
     "dcue_abi_version": ([], ctypes.c_int),
+    "dcue_launch_count": ([], ctypes.c_int64),
     "dcue_last_error": ([], ctypes.c_char_p),
     "dcue_storage_dims": ([ctypes.POINTER(Dims), ctypes.POINTER(Dims)], ctypes.c_int),
     "dcue_param_layout": ([ctypes.POINTER(Dims), _P], ctypes.c_int),

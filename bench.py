@@ -40,6 +40,7 @@ HBM_PEAK_GBS = 8000.0
 F16_PEAK_TFLOPS = 2500.0  # MI355X dense FP16/BF16 MFMA (no sparsity), MI355X_MICROARCH.md
 # conv forwards run on split-f16 MFMA (three f16 products per f32 product) unless DCUE_CONV_F16=0
 CONV_F16 = os.environ.get("DCUE_CONV_F16", "1")[:1] != "0"
+WGRAD_F16 = os.environ.get("DCUE_WGRAD_F16", "1")[:1] != "0"
 
 
 
@@ -437,6 +438,8 @@ def main():
         torch.cuda._sleep(1000)
         torch.cuda.synchronize()
 
+    launches = {}  # kernel launches per timed step, per phase (libdcue_hip's own count)
+
     def timed_phase(name, plan, step_fn, gpu_only=False):
         """W warm-up steps, then EXACTLY K timed steps between barrier + synchronize on both
         sides; max over ranks. Returns (seconds, host enqueue seconds, gpu-only ms or None)."""
@@ -456,10 +459,12 @@ def main():
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda._sleep(int(2.4e6 * args.steps))  # ~1 ms of GPU per step (2.4 GHz cycles)
             ev0.record()
+        l0 = nat.lib().dcue_launch_count()
         t0 = time.perf_counter()
         run(plan, lambda p, s: step_fn(p, args.warmup + s), args.steps, name + " timed")
         opt.flush()  # deferred user-table steps still pending are part of the timed work
         t_enq = time.perf_counter() - t0
+        launches[name] = (nat.lib().dcue_launch_count() - l0) / args.steps
         if gpu_only:
             ev1.record()
         mark(name + ": synchronize after the timed steps (every issued step's exchange pending)")
@@ -482,7 +487,10 @@ def main():
         conv1 = 2.0 * H * 128 * 4 * (M * 132)
         rows_slice = n_users_local / args.flush_every
         spec = {
-            nat.TIMED_CONV1_WGRAD: ("k_conv1_wgrad (conv-1 weight gradient, f32 MFMA 32x32x2)", "mfma", conv1),
+            nat.TIMED_CONV1_WGRAD: (("k_conv_wgrad16 layer 1 (conv-1 weight gradient, split-f16 MFMA 16x16x32 on "
+                                     "the raw fp16 table: two f16 products per f32 product, dz hi+lo x exact x; "
+                                     "peak = f16 dense peak / 2)") if WGRAD_F16 else
+                                    "k_conv1_wgrad (conv-1 weight gradient, f32 MFMA 32x32x2)", "mfma", conv1),
             nat.TIMED_CONV1_FWD: (("k_conv_rows<0,0> layer 1 (conv-1 forward + pool + BN partials, split-f16 "
                                    "MFMA 16x16x32: three f16 products per f32 product; peak = f16 dense peak / 3)")
                                   if CONV_F16 else
@@ -504,8 +512,12 @@ def main():
             ent = {"kernel": name, "bound": bound, "avg_ms": avg, "launches_timed": n,
                    "ms_per_step": avg * per_step, "critical_path": k != nat.TIMED_EMB_SLICE}
             if bound == "mfma":
-                split = k == nat.TIMED_CONV1_FWD and CONV_F16
-                peak = F16_PEAK_TFLOPS / 3.0 if split else F32_PEAK_TFLOPS
+                # split-f16 kernels: f32-equivalent FLOPs against the f16 peak over their products per
+                # f32 product (forward: 3; conv-1 weight gradient on the fp16 table: 2)
+                nprod = 3 if (k == nat.TIMED_CONV1_FWD and CONV_F16) else 2 if (
+                    k == nat.TIMED_CONV1_WGRAD and WGRAD_F16) else 0
+                split = nprod > 0
+                peak = F16_PEAK_TFLOPS / nprod if split else F32_PEAK_TFLOPS
                 ent.update(achieved=work / (avg * 1e-3) / 1e12, peak=peak,
                            unit="TFLOP/s (f32-equivalent)" if split else "TFLOP/s", algorithmic_flops=work)
                 ent["frac"] = ent["achieved"] / peak
@@ -518,7 +530,7 @@ def main():
         return out
 
     def traffic_for(kernel_name, mode):
-        tag = {"k_conv1_wgrad": "conv1_wgrad", "k_emb_flush_rows": "emb_flush_rows",
+        tag = {"k_conv1_wgrad": "conv1_wgrad", "k_conv_wgrad16": "conv1_wgrad16", "k_emb_flush_rows": "emb_flush_rows",
                "k_conv_rows<0,0>": "conv1_fwd"}.get(kernel_name.split(" ")[0])
         path = os.path.join(ROOT, "profiles", "pmc_%s_%s.json" % (tag, mode)) if tag else None
         if path and os.path.exists(path):
@@ -528,7 +540,7 @@ def main():
                 return None
         return None
 
-    def summary(dt, t_enq, kern, M, items_per_row, mode):
+    def summary(dt, t_enq, kern, M, items_per_row, mode, phase):
         rows = world * B * args.steps / dt
         ks = kernel_rooflines(kern, M, args.steps)
         # the roofline line names the largest kernel on the step's critical path (the caller's stream);
@@ -541,7 +553,8 @@ def main():
         roof["step_frac"] = rows / world * flops_row / (F32_PEAK_TFLOPS * 1e12)
         roof["step_flops_per_row"] = flops_row
         res = {"ms_per_step": dt / args.steps * 1e3, "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
-               "rows_per_s": rows, "triplets_per_s": rows * N, "roofline": roof, "kernels": ks}
+               "launches_per_step": launches.get(phase), "rows_per_s": rows, "triplets_per_s": rows * N,
+               "roofline": roof, "kernels": ks}
         ar = [k for k in ks if k["bound"] == "xgmi"]
         if ar:
             res["allreduce_ms_per_step"] = ar[0]["ms_per_step"]
@@ -558,14 +571,14 @@ def main():
     plan = make_plan(False)
     ub, ib = batches(args.warmup + args.steps)
     dt, t_enq, _, kern = timed_phase("inbatch_cold", plan, inbatch_step(ub, ib))
-    out["inbatch_cold"] = summary(dt, t_enq, kern, B, 1, "inbatch")
+    out["inbatch_cold"] = summary(dt, t_enq, kern, B, 1, "inbatch", "inbatch_cold")
     # ---- phase 2: every local user once (outside any timed region), then in-batch steady state
     warm = inbatch_step(warm_users, warm_items)
     run(plan, warm, warm_users.shape[0])
     if "inbatch" in modes:
         ub, ib = batches(args.warmup + args.steps)
         dt, t_enq, gpu_ms, kern = timed_phase("inbatch", plan, inbatch_step(ub, ib), gpu_only=args.gpu_only)
-        out["inbatch"] = summary(dt, t_enq, kern, B, 1, "inbatch")
+        out["inbatch"] = summary(dt, t_enq, kern, B, 1, "inbatch", "inbatch")
         if gpu_ms is not None:
             out["inbatch"]["gpu_only_ms_per_step"] = gpu_ms
     checks = {"after": [], "failed": []}
@@ -652,7 +665,7 @@ def main():
                 draw(s + 2)
             sched_step()
         dt, t_enq, _, kern = timed_phase("catalogue", cplan, cat_step)
-        out["catalogue"] = summary(dt, t_enq, kern, B * (1 + N), 1 + N, "catalogue")
+        out["catalogue"] = summary(dt, t_enq, kern, B * (1 + N), 1 + N, "catalogue", "catalogue")
         check_state(cplan, "catalogue")
         cplan.close()
     head = out.get("inbatch", out["inbatch_cold"])
@@ -666,11 +679,12 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": head["ms_per_step"],
         "host_enqueue_ms_per_step": head["host_enqueue_ms_per_step"],
+        "launches_per_step": head["launches_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32 (conv forwards: f32 values as split fp16 hi+lo pairs on f16 MFMA, f32 accumulate)"
-                 if CONV_F16 else "f32",
+        "dtype": ("f32 (conv forwards, input and weight gradients: f32 values as power-of-two-scaled split "
+                  "fp16 hi+lo pairs on f16 MFMA, f32 accumulate)") if CONV_F16 or WGRAD_F16 else "f32",
         "data": "synthetic",
         "rows_per_s": head["rows_per_s"],
         "auc_val": None,
@@ -689,7 +703,7 @@ def main():
         "roofline": head["roofline"],
         "kernels": head["kernels"],
         "inbatch_cold": {k: out["inbatch_cold"][k] for k in ("ms_per_step", "rows_per_s", "triplets_per_s",
-                                                             "host_enqueue_ms_per_step")},
+                                                             "host_enqueue_ms_per_step", "launches_per_step")},
     }
     if "allreduce_ms_per_step" in head:
         result["allreduce_ms_per_step"] = head["allreduce_ms_per_step"]

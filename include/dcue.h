@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DCUE_ABI_VERSION 9
+#define DCUE_ABI_VERSION 10
 #define DCUE_N_MELS 128
 #define DCUE_N_FRAMES 131
 #define DCUE_N_BN 6
@@ -148,6 +148,9 @@ typedef struct dcue_adam_args {
 int dcue_abi_version(void);
 /* The HIP call behind the most recent DCUE_ERR_HIP (file:line, call, HIP error), "" if none. */
 const char* dcue_last_error(void);
+/* Kernel launches the library has issued in this process (all threads and streams; a step replay
+ * through a captured graph counts none). Diagnostic: bench.py reports launches per step from it. */
+int64_t dcue_launch_count(void);
 /* Storage widths. Any conv_hidden / feature_dim in 1..256 is accepted (DCUENet takes any,
  * dcue/dcue.py:39-47). The library stores and computes them at the width rounded up to 32, 64, 128
  * or 256: every dense segment below is laid out for the storage dims (e.g. conv.layer5.weight is

@@ -15,7 +15,7 @@ HEADER = os.path.join(ROOT, "include", "dcue.h")
 
 def _declared():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|const char\s*\*)\s*(dcue_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char\s*\*)\s*(dcue_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_library_exports_header_symbols():
@@ -76,8 +76,8 @@ def test_layouts_match_reference_shapes(golden):
         assert off[s + 1] - off[s] < n + 4, name
     boff = nat.bn_layout(dims)
     assert boff[1] - boff[0] >= 128 and boff[-1] > 0
-    # conv packs only: forward, dgrad (layers 2-5) and the split-f16 forward copy
-    assert nat.wpack_floats(dims) == 2 * 128 * H * 4 + 3 * (2 * H * H * 4 + H * H * 2 + d * H)
+    # conv packs only: forward, dgrad (layers 2-5) and their split-f16 copies
+    assert nat.wpack_floats(dims) == 2 * 128 * H * 4 + 4 * (2 * H * H * 4 + H * H * 2 + d * H)
     assert nat.workspace_bytes(dims, 4, 3, 16) > 0
 
 
