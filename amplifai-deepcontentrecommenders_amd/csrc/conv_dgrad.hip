@@ -16,11 +16,15 @@ static bool dgrad_f16_on() {
   return on;
 }
 
+constexpr long kDgradF16MinRows = 8192;  // output rows M * Lin of a launch
+
 template <int L, int KC, int TW>
 static int dgrad_layer_tw(const RowsArgs& a, hipStream_t s) {
   constexpr LayerGeom gm = layer_geom(L);
   static_assert(KC % 32 == 0, "split-f16 chunks are 32 channels");
-  if (a.wpack16 && a.in_range && dgrad_f16_on())
+  // (small launches stay on f32: in-batch, the split's range stage and fill cost the one-tile
+  // workgroups 1-3 us each, rocprof; catalogue layer 2: 128 -> 54 us)
+  if (a.wpack16 && a.in_range && dgrad_f16_on() && (long)a.M * gm.lin >= kDgradF16MinRows)
     return run_rows<1, SRC_DZ, KC, gm.ks, gm.ks - 1 - gm.pad, gm.lp * gm.pool, gm.lin, 1, TW, gm.lp,
                     gm.pool, true>(a, s);
   return run_rows<1, SRC_DZ, KC, gm.ks, gm.ks - 1 - gm.pad, gm.lp * gm.pool, gm.lin, 1, TW, gm.lp,

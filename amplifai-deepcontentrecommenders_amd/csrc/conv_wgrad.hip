@@ -1025,6 +1025,13 @@ int launch_xhat0(int src, const void* tracks, const int32_t* item_track, int M, 
   return DCUE_OK;
 }
 
+// split-K chunk length of the split-f16 kernels: whole stages (so whole pool windows), (wgrad_nchunk
+// picks counts that leave no chunk empty)
+static long w16_rows_per_chunk(long rows, int nchunk) {
+  const long rpc = (rows + nchunk - 1) / nchunk;
+  return (rpc + kW16Rows - 1) / kW16Rows * kW16Rows;
+}
+
 int wgrad_nchunk(int layer, int M, int cout, int cin) {
   // one workgroup per CU (LDS-bound): at most 256 / tiles chunks, each of >= 64 rows; partial
   // blocks cost a write + a read of cout*ks*cin floats per chunk (layer 6: the fc, geometry of 5)
@@ -1052,9 +1059,25 @@ int wgrad_nchunk(int layer, int M, int cout, int cin) {
     return e && atoi(e) == 1 ? 1L : 2L;
   }();
   long n = (wgrad_f16_on() ? 256 * per_cu : 256) / tiles;
-  if (n > (rows + 63) / 64) n = (rows + 63) / 64;
+  if (!wgrad_f16_on()) {
+    if (n > (rows + 63) / 64) n = (rows + 63) / 64;
+  } else {
+    // at least DCUE_W16_MIN_STAGES (default 4) 64-row stages per chunk: each chunk costs a
+    // prologue, a partial block written and read back by the reduce, so short ones do not pay
+    // (A/B, GPU-only: 1, 2, 4 stages within noise in-batch; 4 the fastest catalogue, -8 us)
+    static const long min_stages = [] {
+      const char* e = getenv("DCUE_W16_MIN_STAGES");
+      const long v = e ? atol(e) : 0;
+      return v >= 1 && v <= 64 ? v : 4L;
+    }();
+    const long per = min_stages * kW16Rows;
+    if (n > (rows + per - 1) / per) n = (rows + per - 1) / per;
+  }
   const long cap = (8L << 20) / ((long)cout * gm.ks * cin);
   if (n > cap) n = cap;
+  if (n < 1) n = 1;
+  if (wgrad_f16_on())  // whole stages per chunk: no chunk left empty by the rounding
+    n = (rows + w16_rows_per_chunk(rows, (int)n) - 1) / w16_rows_per_chunk(rows, (int)n);
   return (int)(n < 1 ? 1 : n);
 }
 
@@ -1079,13 +1102,6 @@ static int wgrad_layer(const WgradArgs& a0, int nchunk, hipStream_t s) {
   DCUE_LAUNCH(kern, grid, dim3(256), LDS, s, a);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
-}
-
-// split-K chunk length of the split-f16 kernels: whole stages (so whole pool windows), and chunks
-// past the rows simply contribute zero partial blocks
-static long w16_rows_per_chunk(long rows, int nchunk) {
-  const long rpc = (rows + nchunk - 1) / nchunk;
-  return (rpc + kW16Rows - 1) / kW16Rows * kW16Rows;
 }
 
 template <int L, int SRCX>
