@@ -648,7 +648,11 @@ __device__ __forceinline__ void wgrad16_body(const WgradArgs& a, int bx, int by,
 template <int SRCX, int KS, int PAD, int LIN, int R, int POOL, int LP, bool EDGES>
 __global__ __launch_bounds__(256, 2) void k_conv_wgrad16(WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds16[];
-  wgrad16_body<SRCX, KS, PAD, LIN, R, POOL, LP, EDGES>(a, blockIdx.x, blockIdx.y, blockIdx.z, lds16);
+  // the kc tiles of one chunk read the same x rows and dz windows: consecutive logical blocks
+  // (kc tile fastest) on one XCD share its L2 instead of fetching them once per tile from HBM
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int L = xcd_swizzle(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+  wgrad16_body<SRCX, KS, PAD, LIN, R, POOL, LP, EDGES>(a, L % gx, (L / gx) % gy, L / (gx * gy), lds16);
 }
 
 template <int L>
@@ -661,7 +665,7 @@ __device__ __forceinline__ void wgrad16_multi_layer(const WgradMulti& w, int j, 
 
 __global__ __launch_bounds__(256, 2) void k_conv_wgrad16_multi(WgradMulti w) {
   extern __shared__ __attribute__((aligned(16))) char lds16[];
-  const int b = blockIdx.x;
+  const int b = xcd_swizzle(blockIdx.x, gridDim.x);  // a chunk's tiles on one XCD (k_conv_wgrad16)
   int j = 0;
   while (j + 1 < w.n && b >= w.start[j + 1]) ++j;
   switch (w.layer[j]) {

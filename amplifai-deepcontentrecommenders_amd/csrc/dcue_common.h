@@ -116,6 +116,14 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
+// XCD-aware block order (guide T1): blocks with equal id % 8 share an XCD (and its L2), so the
+// logical index L gives each such group a contiguous range -- consecutive L then share an L2.
+// Bijective for any nb. A placement guess only: a wrong one is slower, never wrong.
+__device__ __forceinline__ int xcd_swizzle(int b, int nb) {
+  const int x = b & 7, q = nb >> 3, r = nb & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

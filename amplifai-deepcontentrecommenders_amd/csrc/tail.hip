@@ -927,7 +927,13 @@ int launch_item_grad(const float* dfcopy, const dcue_batch* b, int d, float* df,
   const bool gather = b->layout == DCUE_LAYOUT_GATHER;
   if ((!gather || copy_ptr) && (!fcW || d <= 128)) {  // multi-item workgroups
     const ItemGradFc fc = {rowsum, loss, fcW, g5, acc5, y5, mean5, invstd5, g5max, dfmax};
-    const bool wlds = fcW && d % 4 == 0;
+    // W staged in LDS (64 KB per workgroup at d = 128), or read from L2 in the g5 loop
+    // (DCUE_ITEMGRAD_WLDS=0: A/B diagnostic)
+    static const bool wlds_on = [] {
+      const char* e = getenv("DCUE_ITEMGRAD_WLDS");
+      return !(e && e[0] == '0');
+    }();
+    const bool wlds = fcW && d % 4 == 0 && wlds_on;
     const size_t lds = wlds ? sizeof(float) * d * d : 0;
     // many items (catalogue M = B(1+N)): 16 per workgroup; a few (in-batch M = B): 4
     // (DCUE_ITEMGRAD_IT = 1, 2, 4 or 16 forces one: A/B diagnostic)

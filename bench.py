@@ -398,7 +398,8 @@ def main():
         except RuntimeError as e:  # reported in the line; the step then all-reduces from Python
             comm_error = str(e)
 
-    timed = [nat.TIMED_CONV1_WGRAD, nat.TIMED_CONV1_FWD, nat.TIMED_EMB_SLICE, nat.TIMED_ALLREDUCE]
+    timed = [nat.TIMED_CONV1_WGRAD, nat.TIMED_CONV1_FWD, nat.TIMED_EMB_SLICE, nat.TIMED_EMB_FLUSH,
+             nat.TIMED_ALLREDUCE]
     # every stride-th launch of each class is timed live (a timed launch costs its stream a few us)
     stride = max(1, min(args.timer_stride, args.steps // 4))
 
@@ -498,7 +499,10 @@ def main():
                                   "mfma", conv1),
             nat.TIMED_EMB_SLICE: ("k_emb_flush_rows (deferred user-table Adam, one rolling slice; user "
                                   "stream, beside the item tower: its duration includes waiting behind the "
-                                  "priority-2 critical-path kernels)", "hbm", 24.0 * rows_slice * E),
+                                  "priority-2 critical-path kernels)", "valu", 24.0 * rows_slice * E),
+            nat.TIMED_EMB_FLUSH: ("k_emb_flush (deferred user-table Adam, full-table flush at the phase end, "
+                                  "alone on its stream: the replay's uncontended per-element rate)", "valu",
+                                  24.0 * n_users_local * E),
             nat.TIMED_ALLREDUCE: ("RCCL all-reduce of the dense gradient (per bucket)", "xgmi", None),
         }
         out = []
@@ -507,10 +511,12 @@ def main():
                 continue
             name, bound, work = spec[k]
             avg = ms / n
-            # launches per step from the timer stride (every stride-th launch is timed)
-            per_step = n * stride / steps
+            # launches per step from the timer stride (every stride-th launch is timed); the full flush
+            # runs once per phase (opt.flush() after the timed steps)
+            per_step = 1.0 / steps if k == nat.TIMED_EMB_FLUSH else n * stride / steps
             ent = {"kernel": name, "bound": bound, "avg_ms": avg, "launches_timed": n,
-                   "ms_per_step": avg * per_step, "critical_path": k != nat.TIMED_EMB_SLICE}
+                   "ms_per_step": avg * per_step,
+                   "critical_path": k not in (nat.TIMED_EMB_SLICE, nat.TIMED_EMB_FLUSH)}
             if bound == "mfma":
                 # split-f16 kernels: f32-equivalent FLOPs against the f16 peak over their products per
                 # f32 product (forward: 3; conv-1 weight gradient on the fp16 table: 2)
@@ -521,11 +527,22 @@ def main():
                 ent.update(achieved=work / (avg * 1e-3) / 1e12, peak=peak,
                            unit="TFLOP/s (f32-equivalent)" if split else "TFLOP/s", algorithmic_flops=work)
                 ent["frac"] = ent["achieved"] / peak
-            elif bound == "hbm":
+            elif bound in ("hbm", "valu"):
+                # the user-table replay (k_emb_flush*) is classed "valu": correctly rounded sqrt / div
+                # per replayed element-step; its HBM fraction is informational
                 ent.update(achieved=work / (avg * 1e-3) / 1e9, peak=HBM_PEAK_GBS, unit="GB/s",
                            algorithmic_bytes=work)
-                ent["frac"] = ent["achieved"] / HBM_PEAK_GBS
+                ent["frac" if bound == "hbm" else "hbm_frac"] = ent["achieved"] / HBM_PEAK_GBS
             out.append(ent)
+        byk = {e["kernel"]: e for e in out}
+        sl = byk.get(spec[nat.TIMED_EMB_SLICE][0])
+        fl = byk.get(spec[nat.TIMED_EMB_FLUSH][0])
+        if sl is not None and fl is not None:
+            # same session: the slice's rows at the full flush's uncontended per-row rate, against its
+            # live duration on the user stream beside the priority-2 critical-path kernels
+            iso = fl["avg_ms"] * rows_slice / max(n_users_local, 1)
+            sl["isolated_ms_estimate"] = iso
+            sl["live_over_isolated"] = sl["avg_ms"] / iso if iso > 0 else None
         out.sort(key=lambda e: -e["ms_per_step"])
         return out
 

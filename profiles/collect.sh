@@ -7,7 +7,8 @@
 #    --stats; bench.py --profile-phase brackets that phase's timed steps with a marker kernel and
 #    summarize_pmc.py keeps only the dispatches between the marks (<tag>_<phase>_kernel_stats.csv)
 # 3. per mode, two --pmc passes (FETCH_SIZE, then WRITE_SIZE: they do not fit one TCC pass) over
-#    the conv-1 forward and weight gradient and the rolling user-table flush (+ the marker), summarised by
+#    the conv-1 forward, the conv weight gradients (conv 1; layers 2-5 + fc) and the rolling
+#    user-table flush (+ the marker), summarised by
 #    summarize_pmc.py (gfx950 FETCH_SIZE x2 correction, KB -> B) into pmc_<kernel>_<mode>.json
 set -euo pipefail
 TAG=${1:-rNN}
@@ -26,7 +27,7 @@ for PH in inbatch catalogue inbatch_cold; do
 done
 for PH in inbatch catalogue; do
   for C in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 180 rocprofv3 --pmc $C --kernel-include-regex 'k_conv1_wgrad|k_emb_flush_rows|k_conv_rows|spin_kernel' \
+    timeout -s KILL 180 rocprofv3 --pmc $C --kernel-include-regex 'k_conv1_wgrad|k_conv_wgrad16|k_emb_flush_rows|k_conv_rows|spin_kernel' \
       -f csv -d "$OUT/pmc_${PH}_$C" -o run -- python3 $ROOT/bench.py --no-cpu-baseline --no-eval --steps 40 \
       --warmup 5 --profile-phase $PH > "$OUT/pmc_${PH}_$C.log" 2>&1
   done

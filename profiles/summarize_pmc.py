@@ -21,7 +21,8 @@ import json
 import os
 import sys
 
-KERNELS = {"conv1_wgrad": "k_conv1_wgrad", "emb_flush_rows": "k_emb_flush_rows",
+KERNELS = {"conv1_wgrad": "k_conv1_wgrad", "conv1_wgrad16": "k_conv_wgrad16<0,",
+           "wgrad16_multi": "k_conv_wgrad16_multi", "emb_flush_rows": "k_emb_flush_rows",
            "conv1_fwd": "k_conv_rows<0, 0,"}
 MARK = "spin_kernel"
 
