@@ -742,6 +742,16 @@ int step_prologue(const dcue_model* m, const dcue_batch* b, void* ws, size_t ws_
   return launch_step_prologue(p, s);
 }
 
+// DCUE_FORK_ONCE=1: one fork point on the dgrad chain (after dgrad 3) for both weight-gradient
+// launches instead of two (A/B diagnostic: each launch-bound event costs the chain a gap)
+static bool fork_once() {
+  static const bool on = [] {
+    const char* e = getenv("DCUE_FORK_ONCE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws, size_t ws_bytes,
                   const float* dscores, float emb_grad_scale, const StepOpts& o, hipStream_t s) {
   Ctx c;
@@ -855,7 +865,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     ra.nout = H;
     // a fork point only where a side stream waits (wgrads of layers 3-5 after g_3, of layer 2
     // after g_2): every event bound to a launch costs the chain a gap before its next kernel
-    if (l - 1 == 3 || l - 1 == 2) {
+    if ((l - 1 == 3 && !fork_once()) || l - 1 == 2) {
       ForkAfter fk(sp, s, &ev_layer[l - 1]);
       TRY(launch_conv_dgrad(l, l == 5 ? D : H, ra, s));
       TRY(fk.done());
@@ -987,6 +997,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(launch_conv_wgrad_multi(mw, so));
     return fk.done();
   };
+  if (fork_once()) ev_layer[3] = ev_layer[2];
   TRY(issue_multi(3, 5, !c.res, sw[0], ev_layer[3], &tail[2]));
   TRY(issue_multi(2, 2, false, sw[1], ev_layer[2], &tail[3]));
   HPROF("capi:25");

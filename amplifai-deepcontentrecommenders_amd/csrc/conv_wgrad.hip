@@ -663,7 +663,8 @@ __device__ __forceinline__ void wgrad16_multi_layer(const WgradMulti& w, int j, 
       w.a[j], b % kt, (b / kt) % ot, b / (kt * ot), lds);
 }
 
-__global__ __launch_bounds__(256, 2) void k_conv_wgrad16_multi(WgradMulti w) {
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void k_conv_wgrad16_multi(WgradMulti w) {
   extern __shared__ __attribute__((aligned(16))) char lds16[];
   const int b = xcd_swizzle(blockIdx.x, gridDim.x);  // a chunk's tiles on one XCD (k_conv_wgrad16)
   int j = 0;
@@ -1246,7 +1247,9 @@ int launch_conv_wgrad_multi(WgradMulti w, hipStream_t s) {
   if (!attr) {
     DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_conv_wgrad_multi, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)(wgrad_lds_floats(1) * sizeof(float))));
-    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_conv_wgrad16_multi,
+    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_conv_wgrad16_multi<1>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kW16LdsB));
+    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_conv_wgrad16_multi<2>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kW16LdsB));
     attr = true;
   }
@@ -1267,7 +1270,18 @@ int launch_conv_wgrad_multi(WgradMulti w, hipStream_t s) {
     w.rstart[j + 1] = w.rstart[j] + (int)(((long)a.cout * gm.ks * a.cin + 127) / 128 + (a.cout + 127) / 128);
   }
   if (f16)
-    DCUE_LAUNCH(k_conv_wgrad16_multi, dim3((unsigned)w.start[w.n]), dim3(256), LDS, s, w);
+  {
+    // two workgroups per CU (the layer-5 / fc branch spills 148 B per lane at that register budget);
+    // DCUE_W16_MULTI_OCC=1: one, no spill (A/B diagnostic)
+    static const bool occ1 = [] {
+      const char* e = getenv("DCUE_W16_MULTI_OCC");
+      return e && e[0] == '1';
+    }();
+    if (occ1)
+      DCUE_LAUNCH(k_conv_wgrad16_multi<1>, dim3((unsigned)w.start[w.n]), dim3(256), LDS, s, w);
+    else
+      DCUE_LAUNCH(k_conv_wgrad16_multi<2>, dim3((unsigned)w.start[w.n]), dim3(256), LDS, s, w);
+  }
   else
     DCUE_LAUNCH(k_conv_wgrad_multi, dim3((unsigned)w.start[w.n]), dim3(256), LDS, s, w);
   DCUE_LAUNCH_CHECK();

@@ -193,8 +193,17 @@ def test_plan_at_bench_shape_against_oracle(mode, model_type, B, N, D, H):
             assert int(got) == int(ref), k
             continue
         tol = budget + 1e-4 * float(ref.abs().max()) if k in p else 1e-4 * float(ref.abs().max()) + 1e-6
-        assert float((got - ref).abs().max()) <= tol, "%s after %d steps: %.3e" % (
-            k, len(LRS), float((got - ref).abs().max()))
+        diff = (got - ref).abs()
+        assert float(diff.max()) <= tol, "%s after %d steps: %.3e" % (k, len(LRS), float(diff.max()))
+        if k in p and ref.numel() >= 64:
+            # Adam's step is ~lr * sign(g) wherever |g| stands above the rounding noise, so only
+            # elements whose gradient is ~0 -- or flips with a max-pool near-tie at M = 1,344 after
+            # the first step -- end up to the budget away: measured <= 11 % of a parameter's elements
+            # further than lr/4 from the oracle's trajectory, identically with the f32 backward
+            # (DCUE_WGRAD_F16=0 DCUE_DGRAD_F16=0). An extra, missing or wrong step moves nearly every
+            # element by ~lr, so at most 25 % may sit that far.
+            far = float((diff > 0.25 * min(LRS)).double().mean())
+            assert far <= 0.25, "%s after %d steps: %.1f%% of elements > lr/4 off" % (k, len(LRS), 100 * far)
     from test_gpu_parity import assert_storage_pads_zero
     assert_storage_pads_zero(net)
     plan.close()
