@@ -640,6 +640,30 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
                              (hipStream_t)stream);
 }
 
+int dcue_dcbr_step(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, const float* target,
+                   float* loss, void* ws, size_t ws_bytes, void* stream) {
+  // the item tower's train forward, the MSE head and the item tower's backward (dcue.h)
+  Ctx c;
+  TRY(init_ctx(&c, m));
+  if (!b || !t || !t->data || !target || !ws || !m->grads || !b->item_track) return DCUE_ERR_INVALID;
+  if (b->layout != DCUE_LAYOUT_CATALOGUE || b->n_neg != 0 || b->n_rows <= 0 || b->n_items != b->n_rows)
+    return DCUE_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  TRY(join_user_stream(s));
+  Ws w;
+  const int M = b->n_items;
+  if (carve(&m->dims, M, 0, M, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
+  carve(&m->dims, M, 0, M, ws, &w);
+  TRY(launch_item_counts(b, w.counts, s));
+  TRY(item_forward(c, w, t, b->item_track, M, (double)M, true, w.counts, nullptr, s, false, false, false,
+                   nullptr));
+  TRY(launch_mse_grad(w.f, target, M, m->dims.feature_dim, c.D, w.dfcopy, w.loss, s));
+  if (loss) DCUE_HIP_CHECK(hipMemcpyAsync(loss, w.loss, sizeof(float), hipMemcpyDeviceToDevice, s));
+  StepOpts o;
+  o.item_only = true;
+  return dcue::backward_impl(m, b, t, ws, ws_bytes, nullptr, 1.f, o, s);
+}
+
 }  // extern "C"
 
 namespace dcue {
@@ -757,9 +781,10 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   Ctx c;
   TRY(init_ctx(&c, m));
   HPROF("capi:11");
-  TRY(check_batch(b));
+  if (!o.item_only) TRY(check_batch(b));
   HPROF("capi:12");
-  if (!t || !t->data || !ws || !m->grads || !m->emb_grad || !m->emb_slot) return DCUE_ERR_INVALID;
+  if (!t || !t->data || !ws || !m->grads) return DCUE_ERR_INVALID;
+  if (!o.item_only && (!m->emb_grad || !m->emb_slot)) return DCUE_ERR_INVALID;
   Ws w;
   if (carve(&m->dims, b->n_rows, b->n_neg, b->n_items, nullptr, &w) > ws_bytes) return DCUE_ERR_WORKSPACE;
   carve(&m->dims, b->n_rows, b->n_neg, b->n_items, ws, &w);
@@ -786,7 +811,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   if (!o.prologue_done)  // the backward sums and the gradient maxima
     DCUE_HIP_CHECK(hipMemsetAsync(w.bnbacc, 0, sizeof(unsigned long long) * (6 * 2 * w.cmax * 2 + kGrngWords), s));
     HPROF("capi:13");
-  if (!o.fuse_score)  // else the fused score kernel already produced du / dfcopy
+  if (!o.fuse_score && !o.item_only)  // else the fused score kernel (or the MSE head) produced dfcopy
     TRY(launch_score_bwd(w.uf, w.f, b, D, dscores ? dscores : w.dhinge, w.cosv, w.norms, w.du,
                          w.dfcopy, s));
   // fork points on the chain are bound to its launches (ForkAfter): no record packets between them
@@ -1003,6 +1028,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   HPROF("capi:25");
   // user tower (userembedding.py:33-44 backward), the compact embedding rows, and -- when the step
   // carries it -- the user table's Adam step (it needs nothing from the item tower)
+  if (!o.item_only) {
   TRY(wait_point(su, ev_score));
   HPROF("capi:26");
   {
@@ -1054,11 +1080,12 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   }
   if (o.emb_adam) TRY(launch_adam(m, o.emb_adam, c.poff, su, !o.defer_flush_slice));
   HPROF("capi:32");
+  }  // !item_only
 
   // the join: wgrad stream 0 collects the user stream's and wgrad stream 1's tails, and the caller's
   // stream waits for it once (each cross-queue wait on a pending event costs the waiting queue
   // ≈4 µs, measured; on the side stream that time is slack, on the caller's it is the step's)
-  TRY(wait_point(sw[0], tail[1]));
+  if (tail[1]) TRY(wait_point(sw[0], tail[1]));
   HPROF("capi:33");
   TRY(wait_point(sw[0], tail[3]));
   HPROF("capi:34");

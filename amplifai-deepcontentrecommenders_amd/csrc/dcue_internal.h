@@ -389,7 +389,13 @@ struct StepOpts {
   // the step's per-item copy lists (gather layout, built by the plan's prologue; StepPrologue)
   const int32_t* copy_ptr = nullptr;
   const int32_t* copy_idx = nullptr;
+  // DCBR regression (dcue_dcbr_step): the item tower only -- dfcopy already holds dL/df, no score
+  // backward, no user tower, no embedding gradient
+  bool item_only = false;
 };
+// DCBR's MSE head: loss = sum over [M][d] of (f - y)^2 / (M d) (rows of width ld, the first d
+// columns), df = 2 (f - y) / (M d) into dfcopy ([M][ld], zero past d); deterministic
+int launch_mse_grad(const float* f, const float* y, int M, int d, int ld, float* df, float* loss, hipStream_t s);
 // A batch's model-independent item inputs, issued ahead of its step (plans): bn0's count-weighted
 // batch sums into the accumulator block `acc` (cleared, counts written, on the same stream before)
 // and bn0(x) zero-padded into xhat0 ([M+1][kXp][128] floats).

@@ -1066,3 +1066,41 @@ extern "C" int dcue_build_catalogue_batch(const int64_t* pos_items, const int64_
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
+
+namespace dcue {
+
+// DCBR's MSE head (torch.nn.MSELoss, reduction 'mean', over the [M][d] item factors; van den Oord
+// et al. 2013): one workgroup; thread t sums rows t, t+256, ... in row order, then a fixed tree
+// over the 256 partials (deterministic). df = 2 (f - y) / (M d) at the same time.
+__global__ __launch_bounds__(256) void k_mse_grad(const float* __restrict__ f, const float* __restrict__ y, int M,
+                                                  int d, int ld, float* __restrict__ df, float* loss) {
+  __shared__ float part[256];
+  const float scale = 2.f / ((float)M * (float)d);
+  float acc = 0.f;
+  for (int r = threadIdx.x; r < M; r += blockDim.x) {
+    float rs = 0.f;
+    for (int c = 0; c < ld; ++c) {
+      const long e = (long)r * ld + c;
+      const float diff = c < d ? f[e] - y[e] : 0.f;
+      rs = fmaf(diff, diff, rs);
+      df[e] = diff * scale;
+    }
+    acc += rs;
+  }
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) part[threadIdx.x] += part[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *loss = part[0] / ((float)M * (float)d);
+}
+
+int launch_mse_grad(const float* f, const float* y, int M, int d, int ld, float* df, float* loss, hipStream_t s) {
+  if (M <= 0 || d <= 0 || d > ld) return DCUE_ERR_INVALID;
+  DCUE_LAUNCH(k_mse_grad, dim3(1), dim3(256), 0, s, f, y, M, d, ld, df, loss);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+}  // namespace dcue

@@ -98,7 +98,7 @@ class PlanConfig(ctypes.Structure):
 
 MT_STATE_BYTES = 624 * 4 + 16
 MAX_LOG_CAP = 256
-ABI_VERSION = 10
+ABI_VERSION = 11
 RANK_SPLIT, RANK_SINGLE = 0, 1
 
 _P = ctypes.c_void_p
@@ -121,6 +121,11 @@ _SIGS = {
                       ctypes.c_size_t, ctypes.c_int32, ctypes.c_float, _P, _P, _P, _P, _P], ctypes.c_int),
     "dcue_train_backward": ([ctypes.POINTER(Model), ctypes.POINTER(Batch), ctypes.POINTER(Tracks), _P,
                              ctypes.c_size_t, _P, ctypes.c_float, _P], ctypes.c_int),
+    "dcue_wrmf_workspace_bytes": ([ctypes.c_int32, ctypes.c_int64, _P], ctypes.c_int),
+    "dcue_wrmf_half_step": ([_P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int32, _P, _P, _P, ctypes.c_float,
+                             ctypes.c_float, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "dcue_dcbr_step": ([ctypes.POINTER(Model), ctypes.POINTER(Batch), ctypes.POINTER(Tracks), _P, _P, _P,
+                        ctypes.c_size_t, _P], ctypes.c_int),
     "dcue_adam_step": ([ctypes.POINTER(Model), ctypes.POINTER(AdamArgs), _P], ctypes.c_int),
     "dcue_optimizer_step": ([ctypes.POINTER(Model), ctypes.POINTER(OptArgs), ctypes.POINTER(OptState), _P],
                             ctypes.c_int),

@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--modes", default="inbatch,catalogue",
+    ap.add_argument("--modes", default="inbatch,catalogue,dcbr",
                     help="comma list of phases after the cold one: inbatch (warm), catalogue")
     ap.add_argument("--users", type=int, default=100_000)
     ap.add_argument("--tracks", type=int, default=200_000)
@@ -193,6 +193,51 @@ def row_flops(args, items_per_row):
 
 
 # --------------------------------------------------------------------------------- evaluation
+def dcbr_phase(args, tracks, pair_user, pair_track, n_users, dev, M):
+    """BASELINE config 5 at this run's shape (no reference numbers exist: dcrecommend/dcbr is
+    unpublished): WRMF (factors = d, alpha 40, lambda 0.1) on the interactions -- one untimed
+    iteration, then two timed ALS iterations (users, then items) -- and the DCBR regression of the
+    item tower onto those factors, `warmup` + `steps` Adam steps over random M-item batches."""
+    from dcrecommend.dcbr import DCBR, WRMF
+    d = args.feature_dim
+    w = WRMF(factors=d, regularization=0.1, alpha=40.0, iterations=1, seed=0, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    w.fit(pair_user, pair_track, None, n_users=n_users, n_items=args.tracks)
+    torch.cuda.synchronize()
+    t_fit1 = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for _ in range(2):
+        w.half_step(w.user_factors, w.item_factors, w.by_user)
+        w.half_step(w.item_factors, w.user_factors, w.by_item)
+    torch.cuda.synchronize()
+    t_iter = (time.perf_counter() - t0) / 2
+    gen = torch.Generator(device="cpu").manual_seed(17)
+    n = args.warmup + args.steps
+    items = torch.randint(0, args.tracks, (n, M), generator=gen, dtype=torch.int32).to(dev)
+    model = DCBR(feature_dim=d, conv_hidden=args.hidden, lr=1e-4, device=dev)
+    targets = w.item_factors
+    losses = []
+    for s in range(args.warmup):
+        losses.append(model.step(tracks, items[s], targets[items[s].long()]))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.warmup, n):
+        losses.append(model.step(tracks, items[s], targets[items[s].long()]))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    nnz = int(pair_user.shape[0])
+    return {"workload": "WRMF d=%d over %d users x %d tracks, %d interactions; DCBR regression of the "
+                        "truedcuemel1dbn item tower (H=%d) onto the item factors, %d-item batches"
+                        % (d, n_users, args.tracks, nnz, args.hidden, M),
+            "wrmf_ms_per_iteration": t_iter * 1e3, "wrmf_rows_per_s": (n_users + args.tracks) / t_iter,
+            "wrmf_first_iteration_ms_incl_csr_build": t_fit1 * 1e3,
+            "regression_ms_per_step": dt / args.steps * 1e3, "regression_items_per_s": M * args.steps / dt,
+            "loss_first": float(losses[0]), "loss_last": float(losses[-1]),
+            "parity": "unpinned against the reference (never published); pinned against oracle/wrmf_oracle.py "
+                      "and the fp64 oracle item tower (tests/test_gpu_dcbr.py)"}
+
+
 def evaluate_val(args, net, tracks, pair_user, pair_track, split, n_users, dev):
     """Item factors of every track (eval tower), user factors of every user, then the split-weighted
     AUC / mAP of DCUE.score for an eval_pct sample of the users with train and val interactions."""
@@ -685,6 +730,11 @@ def main():
         out["catalogue"] = summary(dt, t_enq, kern, B * (1 + N), 1 + N, "catalogue", "catalogue")
         check_state(cplan, "catalogue")
         cplan.close()
+    # ---- phase 4 (N = 1): the DCBR path (BASELINE config 5): WRMF target factors of
+    # the same interactions, then the audio ConvNet regressing them (catalogue-sized item batches)
+    if "dcbr" in modes and world == 1 and args.feature_dim <= 128:
+        mark("dcbr phase")
+        out["dcbr"] = dcbr_phase(args, tracks, pair_user, pair_track, n_users_local, dev, B * (1 + N))
     head = out.get("inbatch", out["inbatch_cold"])
     E = args.user_embdim
     result = {
@@ -728,6 +778,8 @@ def main():
         result["gpu_only_ms_per_step"] = head["gpu_only_ms_per_step"]
     if "catalogue" in out:
         result["catalogue"] = out["catalogue"]
+    if "dcbr" in out:
+        result["dcbr"] = out["dcbr"]
     checks["finite"] = not checks["failed"]
     result["checks"] = checks
     # data parallelism's invariant: every rank steps the same dense replica (the exchange averaged

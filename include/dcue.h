@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DCUE_ABI_VERSION 10
+#define DCUE_ABI_VERSION 11
 #define DCUE_N_MELS 128
 #define DCUE_N_FRAMES 131
 #define DCUE_N_BN 6
@@ -200,6 +200,30 @@ int dcue_forward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
  * scaled by emb_grad_scale (1/world_size under user-sharded data parallelism). */
 int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, void* ws,
                         size_t ws_bytes, const float* dscores, float emb_grad_scale, void* stream);
+
+/* ------------------------------------------------------------ DCBR path (BASELINE config 5)
+ * The reference never published it (dcrecommend/dcbr is git-ignored, .gitignore:13;
+ * nn/dcue_orig.py:35 imports it and fails), so these restate the papers and are parity-unpinned
+ * against the reference (pinned against oracle/wrmf_oracle.py and the fp64 oracle item tower).
+ *
+ * WRMF (Hu, Koren, Volinsky 2008) half-step: every row r of `solve` [n_rows][dim] becomes
+ *   x_r = (F^T F + sum_{j in r} (c_rj - 1) f_j f_j^T + lambda I)^{-1} sum_{j in r} c_rj f_j,
+ *   c_rj = 1 + alpha * v_rj (v = values, or 1 when values == NULL),
+ * with F = `fixed` [n_fixed][dim] and row r's observed columns indices[indptr[r] .. indptr[r+1]).
+ * Rows without an observed column get x_r = 0. dim <= 128; lambda > 0. Alternate users and items
+ * (the item-side CSR is the transpose) for the ALS iterations. fp32 in-LDS Cholesky per row. */
+int dcue_wrmf_workspace_bytes(int32_t dim, int64_t n_fixed, size_t* bytes_host);
+int dcue_wrmf_half_step(float* solve, int64_t n_rows, const float* fixed, int64_t n_fixed, int32_t dim,
+                        const int64_t* indptr, const int32_t* indices, const float* values, float alpha,
+                        float lambda, void* ws, size_t ws_bytes, void* stream);
+/* DCBR regression step (van den Oord, Dieleman, Schrauwen 2013): the item tower's train forward over
+ * the batch's items (catalogue layout, n_neg = 0, n_rows = n_items = M; users unused), the MSE loss
+ * mean over [M][d] of (f - target)^2 (torch.nn.MSELoss; target [M][d_s] rows, columns past d
+ * ignored) into *loss (device, nullable), and its backward into the item tower's gradients in
+ * m->grads (the user-tower segments are left as they are). Workspace: dcue_workspace_bytes(dims, M,
+ * 0, M). BN running statistics update as in dcue_forward. */
+int dcue_dcbr_step(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t, const float* target,
+                   float* loss, void* ws, size_t ws_bytes, void* stream);
 
 /* optimizer.step() (nn/dcue.py:209, torch.optim.Adam semantics): dense params + every user row
  * (rows without a gradient this step still decay their moments and move, as the reference's dense

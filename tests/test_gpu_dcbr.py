@@ -1,0 +1,123 @@
+"""DCBR path on the MI355X (BASELINE config 5): the WRMF half-step and the audio-ConvNet regression
+step against the fp64 oracles (oracle/wrmf_oracle.py, oracle/dcue_oracle.py). Parity unpinned
+against the reference, which never published DCBR (its .gitignore:13).
+
+Tolerances: WRMF factors within 1e-4 of their max magnitude (fp32 Cholesky of a lambda-regularised
+system, against fp64 numpy); DCBR loss within 1e-4 relative and gradients within 1e-3 of their max
+(the golden tests' gradient tolerance: the conv backward runs on split-f16 MFMA).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _problem(seed, n_users, n_items, nnz, with_values):
+    rs = np.random.RandomState(seed)
+    rows = rs.randint(0, n_users - 10, nnz)  # the last 10 users have no pair: x = 0
+    cols = rs.randint(0, n_items, nnz)
+    keys = np.unique(rows * n_items + cols)
+    rows, cols = keys // n_items, keys % n_items
+    vals = rs.randint(1, 30, len(rows)).astype(np.float32) if with_values else None
+    return rows, cols, vals
+
+
+@pytest.mark.parametrize("dim,with_values", [(32, True), (128, False), (100, True), (7, False)])
+def test_wrmf_half_step_against_oracle(dim, with_values):
+    from dcrecommend.dcbr import WRMF, device_csr
+    from oracle import wrmf_oracle as W
+    n_users, n_items = 70, 90
+    rows, cols, vals = _problem(dim, n_users, n_items, 900, with_values)
+    alpha, lam = 3.0, 0.05
+    m = WRMF(factors=dim, regularization=lam, alpha=alpha, device=DEV)
+    rs = np.random.RandomState(7)
+    Y = rs.randn(n_items, dim).astype(np.float32) * 0.3
+    X = torch.zeros(n_users, dim, device=DEV)
+    csr = device_csr(torch.as_tensor(rows, device=DEV), torch.as_tensor(cols, device=DEV),
+                     None if vals is None else torch.as_tensor(vals, device=DEV), n_users)
+    m.half_step(X, torch.as_tensor(Y, device=DEV), csr)
+    torch.cuda.synchronize()
+    ip, ix, iv = W.csr(rows.astype(np.int64), cols, vals, n_users)
+    ref = W.half_step(Y, ip, ix, iv, alpha, lam)
+    got = X.double().cpu().numpy()
+    scale = np.abs(ref).max()
+    assert np.abs(got - ref).max() <= 1e-4 * scale, np.abs(got - ref).max() / scale
+    empty = np.setdiff1d(np.arange(n_users), rows)
+    assert np.all(got[empty] == 0.0)
+
+
+def test_wrmf_fit_monotone_against_oracle():
+    from dcrecommend.dcbr import WRMF
+    from oracle import wrmf_oracle as W
+    n_users, n_items, dim = 60, 80, 16
+    rows, cols, vals = _problem(11, n_users, n_items, 700, True)
+    m = WRMF(factors=dim, regularization=0.1, alpha=2.0, iterations=0, seed=3, device=DEV)
+    m.fit(rows, cols, vals, n_users=n_users, n_items=n_items)
+    X = m.user_factors.double().cpu().numpy()
+    Y = m.item_factors.double().cpu().numpy()
+    prev = W.objective(X, Y, rows, cols, vals, 2.0, 0.1)
+    ipu, ixu, ivu = W.csr(rows, cols, vals, n_users)
+    ipi, ixi, ivi = W.csr(cols, rows, vals, n_items)
+    for it in range(3):
+        m.half_step(m.user_factors, m.item_factors, m.by_user)
+        m.half_step(m.item_factors, m.user_factors, m.by_item)
+        X = W.half_step(Y, ipu, ixu, ivu, 2.0, 0.1)
+        Y = W.half_step(X, ipi, ixi, ivi, 2.0, 0.1)
+        cur = m.loss()
+        ref = W.objective(X, Y, rows, cols, vals, 2.0, 0.1)
+        assert cur <= prev * (1 + 1e-6), "iteration %d: objective rose %.6g -> %.6g" % (it, prev, cur)
+        assert abs(cur - ref) <= 1e-4 * abs(ref), (cur, ref)
+        prev = cur
+
+
+@pytest.mark.parametrize("model_type,d,H", [("truedcuemel1dbn", 32, 64), ("truedcuemel1dbn", 100, 128),
+                                            ("truedcuemel1dres", 32, 40)])
+def test_dcbr_step_against_fp64_oracle(model_type, d, H):
+    from dcrecommend.dcbr import DCBR
+    from oracle import dcue_oracle as O
+    from oracle import wrmf_oracle as W
+    torch.manual_seed(5)
+    m = DCBR(feature_dim=d, conv_hidden=H, model_type=model_type, lr=1e-3, device=DEV)
+    torch.manual_seed(5)
+    p, b = O.init_params(d, H, 1, 1, model_type)
+    gen = torch.Generator().manual_seed(9)
+    n_tracks, M = 20, 12
+    X = torch.randn(n_tracks, 128, 131, generator=gen)
+    table = m.net._spectro_table(X.to(DEV)).contiguous()
+    items = torch.randint(0, n_tracks, (M,), generator=gen)
+    target = torch.randn(M, d, generator=gen) * 0.5
+    loss = m.loss_and_grads(table, items.to(DEV), target.to(DEV))
+    torch.cuda.synchronize()
+    p64 = {k: v.double() for k, v in p.items()}
+    b64 = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in b.items()}
+    ref_loss, grads, _ = W.dcbr_loss_and_grads(p64, b64, X[items].double(), target.double())
+    assert abs(float(loss) - float(ref_loss)) <= 1e-4 * abs(float(ref_loss))
+    named = dict(m.net.named_parameters())
+    for k, g_ref in grads.items():
+        got = named[k].grad.double().cpu()
+        scale = float(g_ref.abs().max())
+        if scale == 0.0:
+            continue
+        err = float((got - g_ref).abs().max()) / scale
+        assert err <= 1e-3, "grad %s: %.3e of max" % (k, err)
+    # the user tower is not part of the DCBR step: its gradients stay zero
+    assert float(named["user_embd.linear1.weight"].grad.abs().max()) == 0.0
+
+
+def test_dcbr_training_reduces_loss():
+    from dcrecommend.dcbr import DCBR
+    torch.manual_seed(1)
+    m = DCBR(feature_dim=32, conv_hidden=64, lr=3e-3, device=DEV)
+    gen = torch.Generator().manual_seed(2)
+    X = torch.randn(16, 128, 131, generator=gen)
+    table = m.net._spectro_table(X.to(DEV)).half().contiguous()
+    items = torch.arange(16, dtype=torch.int32, device=DEV)
+    target = (torch.randn(16, 32, generator=gen) * 0.5).to(DEV)
+    losses = [float(m.step(table, items, target)) for _ in range(40)]
+    assert all(np.isfinite(losses))
+    assert losses[-1] < 0.5 * losses[0], losses[::8]
+    pred = m.predict(table, items)
+    assert pred.shape == (16, 32) and bool(torch.isfinite(pred).all())
