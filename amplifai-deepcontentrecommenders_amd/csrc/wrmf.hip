@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256) void k_wrmf_solve(float* __restrict__ X, long 
   extern __shared__ __attribute__((aligned(16))) wacc_t wl[];
   wacc_t* A = wl;                                  // [dim][kWrmfPitch], lower triangle used
   wacc_t* bv = A + kWrmfMaxDim * kWrmfPitch;       // b, then x
-  __shared__ wacc_t dg[kWrmfMaxDim];               // L's diagonal
+  __shared__ wacc_t dg[kWrmfMaxDim];               // 1 / L's diagonal
   float* st = reinterpret_cast<float*>(bv + kWrmfMaxDim);  // [kWrmfStage][dim] staged f_j
   float* cs = st + kWrmfStage * kWrmfMaxDim;       // [kWrmfStage] c_j - 1
   const int t = threadIdx.x;
@@ -94,10 +94,8 @@ __global__ __launch_bounds__(256) void k_wrmf_solve(float* __restrict__ X, long 
       continue;
     }
     // A = G + lambda I (lower triangle and diagonal), b = 0
-    for (int e = t; e < dim * dim; e += blockDim.x) {
-      const int i = e / dim, j = e - i * dim;
-      if (j <= i) A[i * kWrmfPitch + j] = G[e] + (i == j ? (wacc_t)lambda : 0.0);
-    }
+    for (int i = t >> 4; i < dim; i += 16)
+      for (int j = t & 15; j <= i; j += 16) A[i * kWrmfPitch + j] = G[i * dim + j] + (i == j ? (wacc_t)lambda : 0.0);
     for (int c = t; c < dim; c += blockDim.x) bv[c] = 0.0;
     __syncthreads();
     // the row's observed factors: A += (c - 1) f f^T, b += c f, kWrmfStage at a time
@@ -129,7 +127,7 @@ __global__ __launch_bounds__(256) void k_wrmf_solve(float* __restrict__ X, long 
     for (int k = 0; k < dim; ++k) {
       const wacc_t piv = sqrt(A[k * kWrmfPitch + k]);
       const wacc_t inv = 1.0 / piv;
-      if (t == 0) dg[k] = piv;
+      if (t == 0) dg[k] = inv;  // the solves multiply by 1 / L[k][k]
       for (int i = k + 1 + t; i < dim; i += blockDim.x) A[i * kWrmfPitch + k] *= inv;
       __syncthreads();
       // 16 x 16 threads over (row, column) of the trailing lower triangle
@@ -141,12 +139,13 @@ __global__ __launch_bounds__(256) void k_wrmf_solve(float* __restrict__ X, long 
       __syncthreads();
     }
     // L y = b, then L^T x = y: wave 0 alone, lane l holding entries l and l + 64 in registers (no
-    // barriers; y_k / x_k broadcast by shuffle from the owning lane)
+    // barriers; y_k / x_k broadcast by shuffle from the owning lane; x/L[k][k] as x * (1/L[k][k]),
+    // one rounding more than the division, far below the fp32 output's)
     if (t < 64) {
       wacc_t v0 = t < dim ? bv[t] : 0.0, v1 = t + 64 < dim ? bv[t + 64] : 0.0;
       for (int k = 0; k < dim; ++k) {
         const wacc_t own = k < 64 ? v0 : v1;
-        const wacc_t yk = __shfl(own, k & 63, 64) / dg[k];
+        const wacc_t yk = __shfl(own, k & 63, 64) * dg[k];
         if (t == (k & 63)) {
           if (k < 64) v0 = yk; else v1 = yk;
         }
@@ -155,7 +154,7 @@ __global__ __launch_bounds__(256) void k_wrmf_solve(float* __restrict__ X, long 
       }
       for (int k = dim - 1; k >= 0; --k) {
         const wacc_t own = k < 64 ? v0 : v1;
-        const wacc_t xk = __shfl(own, k & 63, 64) / dg[k];
+        const wacc_t xk = __shfl(own, k & 63, 64) * dg[k];
         if (t == (k & 63)) {
           if (k < 64) v0 = xk; else v1 = xk;
         }
