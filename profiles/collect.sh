@@ -33,3 +33,10 @@ for PH in inbatch catalogue; do
   done
 done
 python3 "$ROOT/profiles/summarize_pmc.py" "$OUT" "$TAG"
+# keep the summaries and rocprofv3's own --stats tables; drop the raw traces (gpurun copies back at
+# most 64 MiB of gpurun_out/)
+for PH in inbatch catalogue inbatch_cold; do
+  f=$(find "$OUT/stats_$PH" -name '*kernel_stats.csv' | head -n 1)
+  [ -n "$f" ] && cp "$f" "$OUT/${TAG}_${PH}_rocprof_kernel_stats.csv"
+done
+rm -rf "$OUT"/stats_inbatch "$OUT"/stats_catalogue "$OUT"/stats_inbatch_cold "$OUT"/pmc_*_FETCH_SIZE "$OUT"/pmc_*_WRITE_SIZE
