@@ -445,6 +445,46 @@ __device__ __forceinline__ void wgrad16_body(const WgradArgs& a, int bx, int by,
   uint2 xr16[XRAW ? FR : 1];
   uint32_t xvalid = 0;
   auto issue = [&](int rb) {
+    if constexpr (R >= RCH && TRACK) {
+      // layer 1: a stage's rows span at most two items, ia = rb / R and ia + 1 -- one division, two
+      // item-id loads and two row bases per stage instead of one of each per row (32-bit offsets
+      // for the pooled operands; the table's needs 64 bits)
+      const int ia = rb / R, ra = (ia + 1) * R;  // ra: the first row of item ia + 1
+      const int ib = min(ia + 1, a.M - 1);
+      const float ca = (!RAW && a.counts) ? a.counts[ia] : 1.f, cb = (!RAW && a.counts) ? a.counts[ib] : 1.f;
+#pragma unroll
+      for (int j = 0; j < FW; ++j) {
+        int rw = rb + (slot + 8 * j) * POOL;
+        rw = rw < r_end ? rw : rb;
+        const bool nb = rw >= ra;
+        const int t0 = rw - (nb ? ra : ra - R);
+        const int base = ((nb ? ib : ia) * LP + t0 / POOL) * cout + oc;
+        wg[j] = ld4(a.g_l + base);
+        if constexpr (!RAW) {
+          wy[j] = ld4(a.y_l + base);
+          wid[j] = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
+          wcnt[j] = nb ? cb : ca;
+        }
+      }
+      const long ta = a.item_track[ia], tb = a.item_track[ib];
+      uint32_t vm = 0;
+#pragma unroll
+      for (int j = 0; j < FR; ++j) {
+        const int row = rb + slot + 8 * j;
+        const int rowc = row < r_end ? row : rb;
+        const bool nb = rowc >= ra;
+        const int p = rowc - (nb ? ra : ra - R) + kx - PAD;
+        vm |= (row < r_end && kc_ok && p >= 0 && p < LIN) ? (1u << j) : 0u;
+        const int pc = p < 0 ? 0 : (p >= LIN ? LIN - 1 : p);
+        const long e = ((nb ? tb : ta) * kFrames + pc) * kMels + cx;
+        if constexpr (XRAW)
+          xr16[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.xsrc) + e);
+        else
+          xr[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + e);
+      }
+      xvalid = vm;
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < FW; ++j) {
       int rw = rb + (slot + 8 * j) * POOL;
@@ -519,7 +559,13 @@ __device__ __forceinline__ void wgrad16_body(const WgradArgs& a, int bx, int by,
       if (do_bias) {
         bacc[0].x += d[0]; bacc[0].y += d[1]; bacc[0].z += d[2]; bacc[0].w += d[3];
         if constexpr (EDGES) {  // t = 0, 1 (first window), R-2, R-1 (last): static indices only
-          const int t0 = rw - (rw / R) * R;
+          int t0;
+          if constexpr (R >= RCH) {  // as in issue(): at most two items per stage
+            const int ra = (rb / R + 1) * R;
+            t0 = rw - (rw >= ra ? ra : ra - R);
+          } else {
+            t0 = rw - (rw / R) * R;
+          }
           const bool first = t0 == 0, last = t0 == R - POOL;
           float e1[4], e2[4], e3[4], e4[4];
 #pragma unroll
