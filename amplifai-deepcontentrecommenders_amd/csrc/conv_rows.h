@@ -611,6 +611,11 @@ static int choose_tw(long rows, int twmax) {
   // CU. Every workgroup streams the layer's whole packed weights from L2, so one-tile workgroups
   // re-read them 4x as often; measured at M = 1,344 (tw_sweep.sh): layer-2 dgrad 179 -> 105 us,
   // layer-2 forward 86 -> 65 us against the pass-count model's TW = 1.
+  // Every workgroup also streams the layer's whole packed weights (256 KB of split-f16 B operand
+  // for conv 1) from L2, so the largest launches take eight tiles per workgroup once that still
+  // leaves two workgroups per CU: catalogue conv-1 forward (M = 1,344: 11k tiles), forced-TW A/B
+  // 0.578 -> 0.556 ms per catalogue step; TW = 2 0.748 ms.
+  if (twmax >= 8 && tiles >= 8 * 2 * kCUs) return 8;
   if (twmax >= 4 && tiles >= 4 * 2 * kCUs) return 4;
   int best = 1;
   long best_cost = -1;
