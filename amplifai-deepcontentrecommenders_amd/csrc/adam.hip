@@ -437,10 +437,9 @@ int launch_emb_flush(const dcue_model* md, hipStream_t s) {
   return DCUE_OK;
 }
 
-int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* poff, hipStream_t s,
-                bool flush_slice, long dense_lo, long dense_hi) {
-  // host scalars as torch.optim.Adam forms them from Python floats (double), each rounded once to
-  // float where the CPU kernel takes it as a float scalar
+// host scalars as torch.optim.Adam forms them from Python floats (double), each rounded once to
+// float where the CPU kernel takes it as a float scalar
+static AdamScalars form_scalars(const dcue_adam_args* a) {
   const double bc1 = 1.0 - pow(a->beta1, (double)a->step);
   const double bc2 = 1.0 - pow(a->beta2, (double)a->step);
   const double w = 1.0 - a->beta1;
@@ -454,6 +453,105 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
   sc.eps = (float)a->eps;
   sc.wd = (float)a->weight_decay;
   sc.inv_bc2_sqrt = 1.0f / sc.bc2_sqrt;  // IEEE single division on the host: RN(1/bc2_sqrt)
+  return sc;
+}
+
+// bn0's gradients + Adam over segments [0, DCUE_SEG_LATE) in one launch (dcue_internal.h Bn0Adam):
+// workgroup c owns input channel c -- W1[:, c, :] (gradient, Adam, repack), bn0's gamma/beta[c] --
+// and workgroups 0 / 1 conv 1's bias and bn1's gamma/beta (whose gradients the conv-1 weight
+// gradient already wrote). Gradient arithmetic: bn0_elem, as k_bn0_grads; Adam: adam_elem, as the
+// dense sweep -- the plan's fused step and an eager backward + dcue_adam_step agree bit for bit.
+struct Bn0AdamDev {
+  float *p, *m, *v, *g;
+  long o_w1, o_cb1, o_g0, o_b0, o_g1, o_b1;  // -1: no such segment (towers without BatchNorm)
+  AdamScalars sc;
+  PackSeg seg1;
+  float* wpack;
+};
+
+__device__ __forceinline__ void adam_at(const Bn0AdamDev& a, long idx, float gr) {
+  float pp = a.p[idx], mm = a.m[idx], vv = a.v[idx];
+  adam_elem(pp, gr, mm, vv, a.sc);
+  a.p[idx] = pp;
+  a.m[idx] = mm;
+  a.v[idx] = vv;
+}
+
+__global__ __launch_bounds__(256) void k_bn0_grads_adam(const float* __restrict__ G, const float* __restrict__ E,
+                                                        const float* gamma0, const float* beta0, const float* mean0,
+                                                        const float* invstd0, int H, float* dgamma0, float* dbeta0,
+                                                        Bn0AdamDev a) {
+  critical_path_priority();
+  __shared__ float rg[256], rb[256];
+  const int c = blockIdx.x, t = threadIdx.x;
+  const Bn0Chan ch = bn0_chan(gamma0, beta0, mean0, invstd0, c);
+  float dg = 0.f, db = 0.f;
+  for (int e = t; e < 4 * H; e += blockDim.x) {
+    const int o = e >> 2, k = e & 3;
+    const long wi = ((long)o * kMels + c) * 4 + k;
+    const long idx = a.o_w1 + wi;
+    float pp = a.p[idx];
+    const float gw = bn0_elem(G, E, H, ch, o, k, c, pp, dg, db);  // reads the pre-step weight
+    a.g[idx] = gw;
+    float mm = a.m[idx], vv = a.v[idx];
+    adam_elem(pp, gw, mm, vv, a.sc);
+    a.p[idx] = pp;
+    a.m[idx] = mm;
+    a.v[idx] = vv;
+    pack_store(a.seg1, wi, pp, a.wpack);
+  }
+  if (c == 0)
+    for (int o = t; o < H; o += blockDim.x) {
+      a.g[a.o_cb1 + o] = E[o];
+      adam_at(a, a.o_cb1 + o, E[o]);
+    }
+  if (c == 1 && a.o_g1 >= 0)
+    for (int o = t; o < H; o += blockDim.x) {
+      adam_at(a, a.o_g1 + o, a.g[a.o_g1 + o]);
+      adam_at(a, a.o_b1 + o, a.g[a.o_b1 + o]);
+    }
+  rg[t] = dg;
+  rb[t] = db;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) {
+      rg[t] += rg[t + off];
+      rb[t] += rb[t + off];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    dgamma0[c] = rg[0];
+    dbeta0[c] = rb[0];
+    if (a.o_g0 >= 0) {
+      adam_at(a, a.o_g0 + c, rg[0]);
+      adam_at(a, a.o_b0 + c, rb[0]);
+    }
+  }
+}
+
+int launch_bn0_grads_adam(const float* G, const float* E, const float* gamma0, const float* beta0,
+                          const float* mean0, const float* invstd0, int H, float* dgamma0, float* dbeta0,
+                          const Bn0Adam& a, hipStream_t s) {
+  const dcue_model* md = a.md;
+  if (!md->params || !md->grads || !md->exp_avg || !md->exp_avg_sq || a.args.grad_div > 1.0) return DCUE_ERR_INVALID;
+  Bn0AdamDev d;
+  d.p = md->params; d.m = md->exp_avg; d.v = md->exp_avg_sq; d.g = md->grads;
+  d.o_w1 = a.poff[2]; d.o_cb1 = a.poff[3];
+  d.o_g0 = a.bn ? a.poff[0] : -1; d.o_b0 = a.bn ? a.poff[1] : -1;
+  d.o_g1 = a.bn ? a.poff[4] : -1; d.o_b1 = a.bn ? a.poff[5] : -1;
+  d.sc = form_scalars(&a.args);
+  d.seg1 = pack_args(md, a.poff).seg[0];
+  d.wpack = md->wpack;
+  DCUE_LAUNCH(k_bn0_grads_adam, dim3(kMels), dim3(256), 0, s, G, E, gamma0, beta0, mean0, invstd0, H, dgamma0,
+              dbeta0, d);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* poff, hipStream_t s,
+                bool flush_slice, long dense_lo, long dense_hi) {
+  const AdamScalars sc = form_scalars(a);
   const float gdiv = a->grad_div > 1.0 ? (float)a->grad_div : 0.f;
   const int parts = a->parts ? a->parts : (DCUE_ADAM_DENSE | DCUE_ADAM_EMBEDDING);
   const long n = dense_hi >= 0 ? dense_hi : poff[DCUE_N_DENSE_SEGMENTS];

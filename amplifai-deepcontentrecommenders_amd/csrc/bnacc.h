@@ -81,6 +81,8 @@ struct BnPublish {
   float *rmean, *rvar;            // running statistics
   int64_t* nbt;                   // num_batches_tracked
   int C;
+  float* beta_out;                // nullable: the step's beta, snapshotted for the backward (a split
+                                  // plan's Adam may update the parameter while side streams still read it)
 };
 
 __device__ __forceinline__ void bn_publish(const BnPublish& p, int tid) {
@@ -88,6 +90,7 @@ __device__ __forceinline__ void bn_publish(const BnPublish& p, int tid) {
   const BnChan s = bn_chan_train(p.acc, p.C, tid, p.count, p.inv_count);
   p.mean[tid] = s.mean;
   p.invstd[tid] = s.invstd;
+  if (p.beta_out) p.beta_out[tid] = p.beta ? p.beta[tid] : 0.f;
   p.a[tid] = p.gamma[tid] * s.invstd;
   const float momentum = 0.1f;
   p.rmean[tid] = (1.f - momentum) * p.rmean[tid] + momentum * s.mean;

@@ -210,6 +210,7 @@ struct Ws {
   float* counts;
   int32_t *copy_ptr, *copy_idx;  // gather layout: per-item copy lists (StepPrologue), M <= kCopyListMaxItems
   float *mean[6], *invstd[6], *a[6];
+  float* bcp[6];  // the step's BN betas as the forward used them (BnPublish::beta_out)
   // exact BN sums (bnacc.h), [6 layers][2 sums][Cmax][2 words]: forward stats, backward sums
   unsigned long long *bnacc, *bnbacc;
   // the forward's value ranges (split-f16 operand scales, conv_rows.h / conv_wgrad.hip): [6 layers]
@@ -269,6 +270,7 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
     w->mean[l] = ar.take<float>(C);
     w->invstd[l] = ar.take<float>(C);
     w->a[l] = ar.take<float>(C);
+    w->bcp[l] = ar.take<float>(C);
   }
   w->cmax = Cmax > D ? Cmax : D;
   w->nfwd = 6L * 2 * w->cmax * 2 + kRngWords;
@@ -354,6 +356,9 @@ struct Ctx {
   // scratch sink in the towers without BN
   const float* gamma(const Ws& w, int l) const;
   const float* beta(const Ws& w, int l) const;
+  // the backward's view of BN l's beta: the forward's snapshot (the parameter itself may already be
+  // stepping: split plans run Adam over bn1 beside the layer-2 weight gradient that reads it)
+  const float* beta_bwd(const Ws& w, int l) const { return bn ? w.bcp[l] : w.zeros; }
   float* dgamma(const Ws& w, int l) const;
   float* dbeta(const Ws& w, int l) const;
 };
@@ -407,6 +412,7 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     p.gamma = c.gamma(w, l);
     p.beta = c.beta(w, l);
     p.mean = w.mean[l]; p.invstd = w.invstd[l]; p.a = w.a[l];
+    p.beta_out = w.bcp[l];
     p.rmean = c.rmean(l); p.rvar = c.rvar(l); p.nbt = m->bn_batches + l;
     p.C = bn_channels(&m->dims, l);
     return p;
@@ -766,6 +772,14 @@ int step_prologue(const dcue_model* m, const dcue_batch* b, void* ws, size_t ws_
   return launch_step_prologue(p, s);
 }
 
+static bool fuse_late_adam_on() {
+  static const bool on = [] {
+    const char* e = getenv("DCUE_FUSE_LATE_ADAM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // DCUE_FORK_ONCE=1: one fork point on the dgrad chain (after dgrad 3) for both weight-gradient
 // launches instead of two (A/B diagnostic: each launch-bound event costs the chain a gap)
 static bool fork_once() {
@@ -825,6 +839,9 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   // backward chain (it needs only the forward's input statistics); waited for just before that kernel
   hipEvent_t ev_x0 = nullptr;
   const bool f16w = wgrad_f16_on();  // split-f16 weight gradients (conv_wgrad.hip)
+  // split plans: Adam over bn0 / conv 1 / bn1 rides in the bn0-gradient launch (adam.hip
+  // k_bn0_grads_adam) instead of a launch of its own behind it (DCUE_FUSE_LATE_ADAM=0: separate)
+  const bool fuse_late = o.dense_split && o.dense_split->grad_div <= 1.0 && fuse_late_adam_on();
   // the largest copy count of an item (in-batch: a positive drawn by every other row), the
   // split-f16 dz bounds' kD factor
   const double kd_max = b->layout == DCUE_LAYOUT_GATHER ? 1.0 + (double)B * N : 1.0;
@@ -913,7 +930,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     wa.item_track = b->item_track;
     wa.x_mean = w.mean[l - 1];
     wa.x_a = l == 1 ? w.invstd[0] : w.a[l - 1];
-    wa.x_beta = l == 1 ? nullptr : c.beta(w, l - 1);
+    wa.x_beta = l == 1 ? nullptr : c.beta_bwd(w, l - 1);
     wa.g_l = w.g[l]; wa.y_l = w.y[l]; wa.idx_l = w.idx[l];
     wa.mean_l = w.mean[l]; wa.invstd_l = w.invstd[l]; wa.a_l = w.a[l];
     wa.dz_acc = bn_acc(w.bnbacc, w.cmax, l); wa.dgamma = c.dgamma(w, l); wa.dbeta = c.dbeta(w, l);
@@ -947,6 +964,13 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
                             c.Gd(seg_conv_b(l)), w.G, w.S, so));
     ForkAfter fk(sp, so, tail);
     const bool graw = f16w && src == SRC_TRACK_F16;  // G over the raw fp16 input (conv_wgrad.hip)
+    if (fuse_late) {  // split plans: bn0's gradients and Adam over [0, DCUE_SEG_LATE) in one launch
+      Bn0Adam ba;
+      ba.md = m; ba.poff = c.poff; ba.args = *o.dense_split; ba.bn = c.bn;
+      TRY(launch_bn0_grads_adam(w.G, w.S, c.gamma(w, 0), c.beta(w, 0), graw ? w.mean[0] : nullptr,
+                                graw ? w.invstd[0] : nullptr, H, c.dgamma(w, 0), c.dbeta(w, 0), ba, so));
+      return fk.done();
+    }
     TRY(launch_bn0_grads(w.G, w.S, c.P(seg_conv_w(1)), c.gamma(w, 0), c.beta(w, 0),
                          graw ? w.mean[0] : nullptr, graw ? w.invstd[0] : nullptr, H,
                          c.Gd(seg_conv_w(1)), c.dgamma(w, 0), c.dbeta(w, 0),
@@ -984,7 +1008,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       mw.layer[j] = 6;
       WgradArgs& wa = mw.a[j];
       wa.xsrc = w.y[5];
-      wa.x_mean = w.mean[5]; wa.x_a = w.a[5]; wa.x_beta = c.beta(w, 5);
+      wa.x_mean = w.mean[5]; wa.x_a = w.a[5]; wa.x_beta = c.beta_bwd(w, 5);
       wa.g_l = w.df;
       wa.M = M; wa.cout = D; wa.cin = D;
       wa.wpart = w.wpm[4]; wa.bpart = w.bpm[4];
@@ -1002,7 +1026,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       WgradArgs& wa = mw.a[j];
       wa.xsrc = w.y[l - 1];
       wa.item_track = b->item_track;
-      wa.x_mean = w.mean[l - 1]; wa.x_a = w.a[l - 1]; wa.x_beta = c.beta(w, l - 1);
+      wa.x_mean = w.mean[l - 1]; wa.x_a = w.a[l - 1]; wa.x_beta = c.beta_bwd(w, l - 1);
       wa.g_l = w.g[l]; wa.y_l = w.y[l]; wa.idx_l = w.idx[l];
       wa.mean_l = w.mean[l]; wa.invstd_l = w.invstd[l]; wa.a_l = w.a[l];
       wa.dz_acc = bn_acc(w.bnbacc, w.cmax, l); wa.dgamma = c.dgamma(w, l); wa.dbeta = c.dbeta(w, l);
@@ -1105,7 +1129,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       TRY(launch_adam(m, &dense, c.poff, su, true, late, -1));
       TRY(fk.done());
     }
-    TRY(launch_adam(m, &dense, c.poff, s, true, 0, late));
+    if (!fuse_late) TRY(launch_adam(m, &dense, c.poff, s, true, 0, late));
   } else {
     TRY(wait_point(s, joined));
   }

@@ -1353,30 +1353,23 @@ int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int n
 //   dW1[o][c][k] = gamma0[c] G + beta0[c] S,   dgamma0[c] = sum_{o,k} W1 G,   dbeta0[c] = sum_{o,k} W1 S.
 // With mean0 set, G holds the contraction with the raw fp16 input instead (the split-f16 weight
 // gradient's exact operand): sum dz1 * xhat0 = invstd0 (G - mean0 S) over the same rows.
+// The per-element arithmetic is bn0_elem (explicit fmaf): k_bn0_grads_adam (adam.hip, built without
+// contraction) repeats it bit for bit.
 __global__ __launch_bounds__(256) void k_bn0_grads(const float* __restrict__ G, const float* __restrict__ E,
                                                    const float* __restrict__ W1, const float* gamma0,
                                                    const float* beta0, const float* mean0,
                                                    const float* invstd0, int H, float* dW1,
                                                    float* dgamma0, float* dbeta0, float* db1) {
   critical_path_priority();
-  // E = the five layer-1 bias-partial sums [5][H]: sum dz1 and its parts at t = 0, 1, R-2, R-1.
-  // Tap k of conv row t reads input t+k-2 (zero padding at t+k-2 < 0 or > 130), so
-  //   S[0] = e0-e1-e2, S[1] = e0-e1, S[2] = e0-e4, S[3] = e0-e3-e4;  db1 = e0.
   __shared__ float rg[256], rb[256];
   const int c = blockIdx.x, t = threadIdx.x;
-  const float ga = gamma0[c], be = beta0[c];
-  const float m0 = mean0 ? mean0[c] : 0.f, i0 = mean0 ? invstd0[c] : 1.f;
+  const Bn0Chan ch = bn0_chan(gamma0, beta0, mean0, invstd0, c);
   float dg = 0.f, db = 0.f;
   for (int e = t; e < 4 * H; e += blockDim.x) {  // e = o*4 + k: dW1[o][c][k] layout
     const int o = e >> 2, k = e & 3;
-    const float e0 = E[o], e1 = E[H + o], e2 = E[2 * H + o], e3 = E[3 * H + o], e4 = E[4 * H + o];
-    const float sv = k == 0 ? e0 - e1 - e2 : k == 1 ? e0 - e1 : k == 2 ? e0 - e4 : e0 - e3 - e4;
-    const float gr = G[(size_t)o * 4 * kMels + k * kMels + c];
-    const float gv = mean0 ? i0 * (gr - m0 * sv) : gr;
-    const float w = W1[((size_t)o * kMels + c) * 4 + k];
-    dg += w * gv;
-    db += w * sv;
-    dW1[((size_t)o * kMels + c) * 4 + k] = ga * gv + be * sv;
+    const long wi = ((long)o * kMels + c) * 4 + k;
+    const float w = W1[wi];
+    dW1[wi] = bn0_elem(G, E, H, ch, o, k, c, w, dg, db);
   }
   if (c == 0)
     for (int o = t; o < H; o += blockDim.x) db1[o] = E[o];

@@ -138,6 +138,49 @@ int wgrad_nchunk(int layer, int M, int cout, int cin);
 int launch_conv1_dx(const WgradArgs& a, float* dx1, hipStream_t s);
 int launch_wgrad_reduce(int layer, const float* wpart, const float* bpart, int nchunk, int cout,
                         int cin, float* dW, float* db, float* G_tmp, float* E_tmp, hipStream_t s);
+// One channel's bn0 constants and one dW1 element (k_bn0_grads and the fused k_bn0_grads_adam share
+// them, so the two compute identical bits: explicit fmaf, no reliance on contraction flags).
+// E = the five layer-1 bias-partial sums [5][H]: sum dz1 and its parts at t = 0, 1, R-2, R-1. Tap k
+// of conv row t reads input t+k-2 (zero padding at t+k-2 < 0 or > 130), so
+//   S[0] = e0-e1-e2, S[1] = e0-e1, S[2] = e0-e4, S[3] = e0-e3-e4;  db1 = e0.
+struct Bn0Chan {
+  float ga, be, m0, i0;
+  bool raw;
+};
+__device__ __forceinline__ Bn0Chan bn0_chan(const float* gamma0, const float* beta0, const float* mean0,
+                                            const float* invstd0, int c) {
+  Bn0Chan r;
+  r.ga = gamma0[c];
+  r.be = beta0[c];
+  r.raw = mean0 != nullptr;
+  r.m0 = r.raw ? mean0[c] : 0.f;
+  r.i0 = r.raw ? invstd0[c] : 1.f;
+  return r;
+}
+__device__ __forceinline__ float bn0_elem(const float* __restrict__ G, const float* __restrict__ E, int H,
+                                          const Bn0Chan& ch, int o, int k, int c, float w, float& dg, float& db) {
+  const float e0 = E[o], e1 = E[H + o], e2 = E[2 * H + o], e3 = E[3 * H + o], e4 = E[4 * H + o];
+  const float sv = k == 0 ? (e0 - e1) - e2 : k == 1 ? e0 - e1 : k == 2 ? e0 - e4 : (e0 - e3) - e4;
+  const float gr = G[(size_t)o * 4 * kMels + k * kMels + c];
+  const float gv = ch.raw ? ch.i0 * fmaf(-ch.m0, sv, gr) : gr;
+  dg = fmaf(w, gv, dg);
+  db = fmaf(w, sv, db);
+  return fmaf(ch.ga, gv, ch.be * sv);
+}
+// split plans (StepOpts::dense_split): bn0's gradients and, in the same launch, Adam over segments
+// [0, DCUE_SEG_LATE) -- bn0, conv 1 (with its weight repack), bn1 -- every one of which this
+// kernel's workgroups complete (workgroup c owns input channel c; workgroups 0 / 1 conv 1's bias and
+// bn1). p == nullptr: gradients only (as k_bn0_grads).
+struct Bn0Adam {
+  const dcue_model* md;              // p / m / v / grads / wpack
+  const int64_t* poff;               // segment offsets (reference order)
+  dcue_adam_args args;               // the dense Adam step (host values; the launcher forms scalars)
+  bool bn;                           // towers with BatchNorm: bn0 / bn1 segments exist
+};
+int launch_bn0_grads_adam(const float* G, const float* E, const float* gamma0, const float* beta0,
+                          const float* mean0, const float* invstd0, int H, float* dgamma0, float* dbeta0,
+                          const Bn0Adam& a, hipStream_t s);
+
 // mean0 / invstd0 (nullable): G is the contraction with the raw input (split-f16 path, fp16 table)
 int launch_bn0_grads(const float* G, const float* E, const float* W1, const float* gamma0,
                      const float* beta0, const float* mean0, const float* invstd0, int H, float* dW1,
