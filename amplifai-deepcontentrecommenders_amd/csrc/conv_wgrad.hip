@@ -693,6 +693,9 @@ __device__ __forceinline__ void wgrad16_body(const WgradArgs& a, int bx, int by,
 
 template <int SRCX, int KS, int PAD, int LIN, int R, int POOL, int LP, bool EDGES>
 __global__ __launch_bounds__(256, 2) void k_conv_wgrad16(WgradArgs a) {
+  // the conv-1 weight gradient is the step's tail on the caller's stream: its waves take the issue
+  // slots the side-stream weight gradients (priority 0) share with it
+  critical_path_priority();
   extern __shared__ __attribute__((aligned(16))) char lds16[];
   // the kc tiles of one chunk read the same x rows and dz windows: consecutive logical blocks
   // (kc tile fastest) on one XCD share its L2 instead of fetching them once per tile from HBM
