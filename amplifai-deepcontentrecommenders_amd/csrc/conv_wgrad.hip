@@ -727,6 +727,340 @@ __global__ __launch_bounds__(256, OCC) void k_conv_wgrad16_multi(WgradMulti w) {
   }
 }
 
+// ------------------------------------------------ tap-fused split-f16 conv-1 weight gradient
+// dW1[o][k*128 + c] for one 64-channel o tile and ALL four taps in one workgroup of 8 waves: wave w
+// owns tap k = w & 3 and o half w >> 2 (32 o x 128 c, 2 x 8 MFMA tiles). The kc-tiled kernel above
+// builds a stage's dz windows once per kc tile (four times, one per tap) and its x rows once per
+// tap; here the dz windows are built once per o tile and the x rows once: the x image holds, item
+// by item, the input positions the stage's conv rows read -- each item's rows plus KS - 1 halo
+// positions -- so tap k's B fragment of conv row r is image row r + k + (KS - 1) * (items of the
+// stage before r's), a per-lane row address in the transposed read. dz rows are 128 B (64 o);
+// x rows 256 B (the 128 mels).
+constexpr int kW16tO = 64;   // o per workgroup
+constexpr int kW16tThreads = 512;
+template <int R, int KS>
+constexpr int w16t_img_rows() { return kW16Rows + (KS - 1) * (R >= kW16Rows ? 2 : kW16Rows / R + 2); }
+template <int R, int KS>
+constexpr size_t w16t_lds_bytes(bool xraw) {
+  return (size_t)2 * kW16Rows * 128 + (size_t)(xraw ? 1 : 2) * w16t_img_rows<R, KS>() * 256 +
+         (size_t)(kW16tO + 128) * sizeof(int);
+}
+// 16-byte chunk ch (of 8) of 128-byte dz row r: a transposed read's 32-lane half touches rows
+// r0 + {0..3} + {0, 8}, two chunks each -- row bits 1 and 3 spread them over all 64 banks
+__device__ __forceinline__ int w16_off128(int r, int ch) { return 128 * r + 16 * (ch ^ ((r & 2) | ((r >> 1) & 4))); }
+
+template <int SRCX, int KS, int PAD, int LIN, int R, int POOL, int LP>
+__device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz, char* lds) {
+  constexpr int RCH = kW16Rows;
+  constexpr int NB = 5;  // bias + the four edge sums (layer 1)
+  constexpr int HALO = KS - 1;
+  constexpr int IMG = w16t_img_rows<R, KS>();
+  constexpr int FX = (IMG + 15) / 16;  // x image rows per thread (16 row slots x 32 channel quads)
+  static_assert(KS == 4 && POOL == 4 && R % POOL == 0, "8 waves = 4 taps x 2 o halves; 16 windows per stage");
+  constexpr bool TWO = R >= RCH;  // a stage spans at most two items
+  constexpr bool XRAW = SRCX == SRC_TRACK_F16;
+  static_assert(SRCX == SRC_TRACK_F16 || SRCX == SRC_TRACK_F32, "layer 1: x is the track table");
+  char* dzh = lds;
+  char* dzl = dzh + RCH * 128;
+  char* xh = dzl + RCH * 128;
+  char* xl = xh + IMG * 256;
+  int* exp_o = reinterpret_cast<int*>(xh + (XRAW ? 1 : 2) * IMG * 256);
+  int* exp_c = exp_o + kW16tO;
+  float (*bsum)[NB][kW16tO] = reinterpret_cast<float (*)[NB][kW16tO]>(lds);  // after the last stage
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int kx = wave & 3, oh = wave >> 2;  // this wave's tap and o half
+  const int cout = a.cout, cin = a.cin, kcn = KS * cin;
+  const int obase = by * kW16tO;
+  const int total = a.M * R;  // rows (the host keeps M * R below 2^30)
+  const int r_begin = bz * a.rows_per_chunk;  // a multiple of RCH
+  const int r_end = min(r_begin + a.rows_per_chunk, total);
+
+  f32x4 acc[2][8];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 bacc[NB];
+#pragma unroll
+  for (int e = 0; e < NB; ++e) bacc[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  // dz: threads 0..255, window slot ws (16 per stage) x o quad q (16); x: every thread, row slot
+  // xs (16) x mel quad cq (32)
+  const bool dzt = tid < 256;
+  const int q = tid & 15, ws = (tid >> 4) & 15;
+  const int o = obase + 4 * q;
+  const bool o_ok = o < cout;
+  const int oc = o_ok ? o : 0;
+  const int cq = tid & 31, xs = tid >> 5;
+  const int cx = 4 * cq;
+  float mu[4] = {}, iv[4] = {}, av[4] = {}, sd[4] = {}, sdx[4] = {};
+  {
+    const float4 m4 = ld4(a.mean_l + oc), i4 = ld4(a.invstd_l + oc), a4 = ld4(a.a_l + oc);
+    mu[0] = m4.x; mu[1] = m4.y; mu[2] = m4.z; mu[3] = m4.w;
+    iv[0] = i4.x; iv[1] = i4.y; iv[2] = i4.z; iv[3] = i4.w;
+    av[0] = a4.x; av[1] = a4.y; av[2] = a4.z; av[3] = a4.w;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sd[s] = (float)acc_sum(a.dz_acc, cout, 0, oc + s);
+      sdx[s] = (float)acc_sum(a.dz_acc, cout, 1, oc + s);
+    }
+  }
+  if (by == 0 && bz == 0 && tid < cout) {  // BN_1 = gamma * xhat + beta: dbeta = sum g, dgamma = sum g * xhat
+    a.dbeta[tid] = (float)acc_sum(a.dz_acc, cout, 0, tid);
+    a.dgamma[tid] = (float)acc_sum(a.dz_acc, cout, 1, tid);
+  }
+  const float4 xmu = ld4(a.x_mean + cx), xsc = ld4(a.x_a + cx);
+  const float4 xbe = a.x_beta ? ld4(a.x_beta + cx) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float xm[4] = {xmu.x, xmu.y, xmu.z, xmu.w}, xs_[4] = {xsc.x, xsc.y, xsc.z, xsc.w};
+  const float xb[4] = {xbe.x, xbe.y, xbe.z, xbe.w};
+  // column scales as wgrad16_body: scaled dz = cas g - count (cA + xhat cB), scaled x = (src - xm) xas + xbs
+  float cas[4], cA[4], cB[4], xas[4], xbs[4];
+  {
+    int eo[4], ec[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float gmax = w16_key(a.g_range, oc + s);
+      const float ym = fmaxf(w16_key(a.y_range, oc + s), 0.f);
+      const float xhm = fmaxf(fabsf(mu[s]), fabsf(ym - mu[s])) * iv[s];
+      const float bo = fabsf(av[s]) * (gmax + a.kd_max * (fabsf(sd[s]) + xhm * fabsf(sdx[s])));
+      eo[s] = o_ok ? w16_exp(bo) : 0;
+      const float lo = -w16_key(a.x_range + kRngC, cx + s), hi = w16_key(a.x_range, cx + s);
+      const float bx_ = fmaxf(fabsf((lo - xm[s]) * xs_[s] + xb[s]), fabsf((hi - xm[s]) * xs_[s] + xb[s]));
+      ec[s] = XRAW ? 0 : w16_exp(bx_);
+      const float so = ldexpf(1.f, eo[s]), sx = ldexpf(1.f, ec[s]);
+      cas[s] = av[s] * so;
+      cA[s] = av[s] * a.invN * sd[s] * so;
+      cB[s] = av[s] * a.invN * sdx[s] * so;
+      xas[s] = xs_[s] * sx;
+      xbs[s] = xb[s] * sx;
+    }
+    if (tid < 16)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) exp_o[4 * q + s] = eo[s];
+    if (xs == 0)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) exp_c[4 * cq + s] = ec[s];
+  }
+  __syncthreads();
+
+  // raw operands of one stage, loaded branch-free: the thread's dz window (g, y, argmax bytes, the
+  // item's count) and its x image rows xs, xs + 16, ...
+  float4 wg = make_float4(0.f, 0.f, 0.f, 0.f), wy = wg;
+  uint32_t wid = 0;
+  float wcnt = 1.f;
+  float4 xr[XRAW ? 1 : FX];
+  uint2 xr16[XRAW ? FX : 1];
+  uint32_t xvalid = 0;
+  auto issue = [&](int rb) {
+    const int i0 = rb / R, D = rb - i0 * R;  // the stage starts D rows into item i0
+    if (dzt) {
+      int rw = rb + ws * POOL;
+      rw = rw < r_end ? rw : rb;
+      const int ii = rw / R, t0 = rw - ii * R;
+      const int base = (ii * LP + t0 / POOL) * cout + oc;
+      wg = ld4(a.g_l + base);
+      wy = ld4(a.y_l + base);
+      wid = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
+      wcnt = a.counts ? a.counts[ii] : 1.f;
+    }
+    const long t_a = a.item_track[i0], t_b = a.item_track[min(i0 + 1, a.M - 1)];
+    uint32_t vm = 0;
+#pragma unroll
+    for (int j = 0; j < FX; ++j) {
+      const int jr = xs + 16 * j;  // image row
+      int k;                       // items after i0
+      if constexpr (TWO)
+        k = jr + D >= R + HALO ? 1 : 0;
+      else
+        k = (jr + D) / (R + HALO);
+      const int i = i0 + k;
+      const int p = jr + D - k * (R + HALO) - PAD;  // input position in item i
+      const bool ok = jr < IMG && i < a.M && p >= 0 && p < LIN;
+      vm |= ok ? (1u << j) : 0u;
+      long trk;
+      if constexpr (TWO)
+        trk = k ? t_b : t_a;
+      else
+        trk = a.item_track[ok ? i : i0];
+      const long e = (trk * kFrames + (ok ? p : 0)) * kMels + cx;
+      if constexpr (XRAW)
+        xr16[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.xsrc) + e);
+      else
+        xr[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + e);
+    }
+    xvalid = vm;
+  };
+
+  // fragment read offsets: lane 4q'+p of its 16-lane group g supplies row (8g + 4h + q') of the
+  // k-step, columns 4p..4p+3 of the 16-column tile
+  const int fq = l16 >> 2, fp = l16 & 3;
+  if (r_begin < r_end) issue(r_begin);
+  for (int rb = r_begin; rb < r_end; rb += RCH) {
+    if (dzt) {  // dz: BN_1's backward for the thread's window, scaled, split, written to its rows
+      const int rw = rb + ws * POOL;
+      const bool wv = rw < r_end && o_ok;
+      const float gv[4] = {wg.x, wg.y, wg.z, wg.w}, yv[4] = {wy.x, wy.y, wy.z, wy.w};
+      float d[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const float xh_ = (yv[s] - mu[s]) * iv[s];
+        const float v = cas[s] * gv[s] - wcnt * (cA[s] + xh_ * cB[s]);
+        d[s] = (wv && yv[s] > 0.f) ? v : 0.f;
+      }
+      bacc[0].x += d[0]; bacc[0].y += d[1]; bacc[0].z += d[2]; bacc[0].w += d[3];
+      {  // t = 0, 1 (first window), R-2, R-1 (last window)
+        const int t0 = rw - (rw / R) * R;
+        const bool first = t0 == 0, last = t0 == R - POOL;
+        float e1[4], e2[4], e3[4], e4[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const uint32_t r = (wid >> (8 * s)) & 0xffu;
+          e1[s] = (first && r == 0u) ? d[s] : 0.f;
+          e2[s] = (first && r == 1u) ? d[s] : 0.f;
+          e3[s] = (last && r == (uint32_t)(POOL - 2)) ? d[s] : 0.f;
+          e4[s] = (last && r == (uint32_t)(POOL - 1)) ? d[s] : 0.f;
+        }
+        bacc[1].x += e1[0]; bacc[1].y += e1[1]; bacc[1].z += e1[2]; bacc[1].w += e1[3];
+        bacc[2].x += e2[0]; bacc[2].y += e2[1]; bacc[2].z += e2[2]; bacc[2].w += e2[3];
+        bacc[3].x += e3[0]; bacc[3].y += e3[1]; bacc[3].z += e3[2]; bacc[3].w += e3[3];
+        bacc[4].x += e4[0]; bacc[4].y += e4[1]; bacc[4].z += e4[2]; bacc[4].w += e4[3];
+      }
+      const w16_h4 h = {(_Float16)d[0], (_Float16)d[1], (_Float16)d[2], (_Float16)d[3]};
+      const w16_h4 l = {(_Float16)(d[0] - (float)h[0]), (_Float16)(d[1] - (float)h[1]),
+                        (_Float16)(d[2] - (float)h[2]), (_Float16)(d[3] - (float)h[3])};
+      const uint2 hb = __builtin_bit_cast(uint2, h), lb = __builtin_bit_cast(uint2, l);
+#pragma unroll
+      for (int jp = 0; jp < POOL; ++jp) {
+        const uint32_t m0 = ((wid & 0xffu) == (uint32_t)jp ? 0x0000ffffu : 0u) |
+                            (((wid >> 8) & 0xffu) == (uint32_t)jp ? 0xffff0000u : 0u);
+        const uint32_t m1 = (((wid >> 16) & 0xffu) == (uint32_t)jp ? 0x0000ffffu : 0u) |
+                            ((wid >> 24) == (uint32_t)jp ? 0xffff0000u : 0u);
+        const int off = w16_off128(ws * POOL + jp, q >> 1) + 8 * (q & 1);
+        *reinterpret_cast<uint2*>(dzh + off) = make_uint2(hb.x & m0, hb.y & m1);
+        *reinterpret_cast<uint2*>(dzl + off) = make_uint2(lb.x & m0, lb.y & m1);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < FX; ++j) {  // x image (zero padding and past-the-batch rows are zeros)
+      const int jr = xs + 16 * j;
+      if (jr < IMG) {
+        const bool ok = (xvalid >> j) & 1u;
+        const int off = w16_off(jr, cq >> 1) + 8 * (cq & 1);
+        if constexpr (XRAW) {
+          *reinterpret_cast<uint2*>(xh + off) = ok ? xr16[j] : make_uint2(0u, 0u);
+        } else {
+          const float x[4] = {xr[j].x, xr[j].y, xr[j].z, xr[j].w};
+          float v[4];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) v[s] = ok ? (x[s] - xm[s]) * xas[s] + xbs[s] : 0.f;
+          w16_split_store(xh, xl, off, make_float4(v[0], v[1], v[2], v[3]));
+        }
+      }
+    }
+    __syncthreads();
+    const int i0 = rb / R;
+    const int lb = (i0 + 1) * R - rb;  // the stage row where item i0 + 1 starts (TWO)
+    if (rb + RCH < r_end) issue(rb + RCH);  // next stage's loads fly while the MFMAs run
+#pragma unroll
+    for (int ks = 0; ks < RCH / 32; ++ks) {
+      const int r0 = 32 * ks + 8 * g + fq;  // this lane's conv rows: r0 (first read), r0 + 4 (second)
+      w16_h8 ah[2], al[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int ch = 4 * oh + 2 * m + (fp >> 1);
+        const int o0 = w16_off128(r0, ch) + 8 * (fp & 1), o1 = w16_off128(r0 + 4, ch) + 8 * (fp & 1);
+        const w16_h4 h0 = w16_tr(dzh, o0), h1 = w16_tr(dzh, o1), l0 = w16_tr(dzl, o0), l1 = w16_tr(dzl, o1);
+        ah[m] = w16_h8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        al[m] = w16_h8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+      }
+      int img0, img1;  // the image rows tap kx reads for conv rows r0, r0 + 4
+      if constexpr (TWO) {
+        img0 = r0 + kx + (r0 >= lb ? HALO : 0);
+        img1 = r0 + 4 + kx + (r0 + 4 >= lb ? HALO : 0);
+      } else {
+        img0 = r0 + kx + HALO * ((rb + r0) / R - i0);
+        img1 = r0 + 4 + kx + HALO * ((rb + r0 + 4) / R - i0);
+      }
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        const int ch = 2 * n + (fp >> 1);
+        const int ob0 = w16_off(img0, ch) + 8 * (fp & 1), ob1 = w16_off(img1, ch) + 8 * (fp & 1);
+        const w16_h4 h0 = w16_tr(xh, ob0), h1 = w16_tr(xh, ob1);
+        const w16_h8 bh = w16_h8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        if constexpr (XRAW) {
+#pragma unroll
+          for (int m = 0; m < 2; ++m) {
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[m], bh, acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[m], bh, acc[m][n], 0, 0, 0);
+          }
+        } else {
+          const w16_h4 l0 = w16_tr(xl, ob0), l1 = w16_tr(xl, ob1);
+          const w16_h8 bl = w16_h8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+#pragma unroll
+          for (int m = 0; m < 2; ++m) {
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[m], bh, acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[m], bl, acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[m], bh, acc[m][n], 0, 0, 0);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // partial block -> wpart[z][o][kx * cin + c], unscaled; D lane map: o = 4g + reg, c = l16
+  float* wp = a.wpart + (size_t)bz * cout * kcn;
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    const int cl = 16 * n + l16;
+    const int ecn = exp_c[cl];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ol = 32 * oh + 16 * m + 4 * g + j;
+        if (obase + ol < cout) wp[(size_t)(obase + ol) * kcn + kx * cin + cl] = ldexpf(acc[m][n][j], -(exp_o[ol] + ecn));
+      }
+  }
+  // bias (+ edge) partials of the tile's 64 channels: the 16 window slots, summed in order (the
+  // operand images are free: the last stage ended with a barrier)
+  if (dzt)
+#pragma unroll
+    for (int e = 0; e < NB; ++e) st4(&bsum[ws][e][4 * q], bacc[e]);
+  __syncthreads();
+  if (tid < kW16tO && obase + tid < cout) {
+    const int eo = exp_o[tid];
+#pragma unroll
+    for (int e = 0; e < NB; ++e) {
+      float v = 0.f;
+#pragma unroll
+      for (int sl = 0; sl < 16; ++sl) v += bsum[sl][e][tid];
+      a.bpart[((size_t)bz * NB + e) * cout + obase + tid] = ldexpf(v, -eo);
+    }
+  }
+}
+
+template <int SRCX, int KS, int PAD, int LIN, int R, int POOL, int LP>
+__global__ __launch_bounds__(kW16tThreads, 1) void k_conv_wgrad16t(WgradArgs a) {
+  critical_path_priority();  // the step's tail on the caller's stream, as k_conv_wgrad16
+  extern __shared__ __attribute__((aligned(16))) char lds16t[];
+  // a chunk's o tiles read the same x rows: consecutive logical blocks (o tile fastest) on one XCD
+  const int ot = (a.cout + kW16tO - 1) / kW16tO;
+  const int L = xcd_swizzle(blockIdx.x, gridDim.x);
+  wgrad16t_body<SRCX, KS, PAD, LIN, R, POOL, LP>(a, L % ot, L / ot, lds16t);
+}
+
+// whether layer 1's split-f16 weight gradient runs tap-fused (DCUE_W16_TAPFUSED=0: kc-tiled)
+static bool wgrad16t_on() {
+  static const bool on = [] {
+    const char* e = getenv("DCUE_W16_TAPFUSED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // whether the weight gradients run on split-f16 MFMA (DCUE_WGRAD_F16=0: the f32-MFMA kernels)
 bool wgrad_f16_on() {
   static const bool on = [] {
@@ -1105,7 +1439,9 @@ int wgrad_nchunk(int layer, int M, int cout, int cin) {
     if (n > (wins + 4 * kW1Win - 1) / (4 * kW1Win)) n = (wins + 4 * kW1Win - 1) / (4 * kW1Win);
     return (int)(n < 1 ? 1 : n);
   }
-  const long tiles = ((gm.ks * cin + 127) / 128) * ((cout + 127) / 128);
+  const long tiles = layer == 1 && wgrad_f16_on() && wgrad16t_on()
+                        ? (cout + kW16tO - 1) / kW16tO  // k_conv_wgrad16t: 64 o x all taps
+                        : ((gm.ks * cin + 127) / 128) * ((cout + 127) / 128);
   // split-f16 kernels: two workgroups per CU (one's MFMAs and fill run while the other's stage
   // loads are in flight); DCUE_W16_WGS_PER_CU=1 halves the chunks (A/B diagnostic)
   static const long per_cu = [] {
@@ -1158,10 +1494,34 @@ static int wgrad_layer(const WgradArgs& a0, int nchunk, hipStream_t s) {
   return DCUE_OK;
 }
 
+template <int SRCX>
+static int wgrad16t_layer1(const WgradArgs& a0, int nchunk, hipStream_t s) {
+  constexpr LayerGeom gm = layer_geom(1);
+  constexpr int R = gm.lp * gm.pool;
+  constexpr size_t LDS = w16t_lds_bytes<R, gm.ks>(SRCX == SRC_TRACK_F16);
+  auto kern = k_conv_wgrad16t<SRCX, gm.ks, gm.pad, gm.lin, R, gm.pool, gm.lp>;
+  if (a0.cin != kMels) return DCUE_ERR_INVALID;  // the x image rows are the 128 mels
+  static bool attr = false;
+  if (!attr) {
+    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS));
+    attr = true;
+  }
+  WgradArgs a = a0;
+  const long rows = (long)a.M * R;
+  if (rows >= (1L << 30)) return DCUE_ERR_UNSUPPORTED;  // 32-bit row indices
+  a.rows_per_chunk = (int)w16_rows_per_chunk(rows, nchunk);
+  const unsigned ot = (unsigned)((a.cout + kW16tO - 1) / kW16tO);
+  DCUE_LAUNCH(kern, dim3(ot * (unsigned)nchunk), dim3(kW16tThreads), LDS, s, a);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
 template <int L, int SRCX>
 static int wgrad16_layer(const WgradArgs& a0, int nchunk, hipStream_t s) {
   constexpr LayerGeom gm = layer_geom(L);
   constexpr int R = gm.lp * gm.pool;
+  if constexpr (L == 1)
+    if (wgrad16t_on()) return wgrad16t_layer1<SRCX>(a0, nchunk, s);
   auto kern = k_conv_wgrad16<SRCX, gm.ks, gm.pad, gm.lin, R, gm.pool, gm.lp, L == 1>;
   static bool attr = false;
   if (!attr) {
