@@ -727,15 +727,15 @@ __global__ __launch_bounds__(256, OCC) void k_conv_wgrad16_multi(WgradMulti w) {
   }
 }
 
-// ------------------------------------------------ tap-fused split-f16 conv-1 weight gradient
-// dW1[o][k*128 + c] for one 64-channel o tile and ALL four taps in one workgroup of 8 waves: wave w
+// ------------------------------------------------ tap-fused split-f16 weight gradient (layers 1, 2)
+// dW[o][k*128 + c] for one 64-channel o tile and ALL four taps in one workgroup of 8 waves: wave w
 // owns tap k = w & 3 and o half w >> 2 (32 o x 128 c, 2 x 8 MFMA tiles). The kc-tiled kernel above
 // builds a stage's dz windows once per kc tile (four times, one per tap) and its x rows once per
 // tap; here the dz windows are built once per o tile and the x rows once: the x image holds, item
 // by item, the input positions the stage's conv rows read -- each item's rows plus KS - 1 halo
 // positions -- so tap k's B fragment of conv row r is image row r + k + (KS - 1) * (items of the
 // stage before r's), a per-lane row address in the transposed read. dz rows are 128 B (64 o);
-// x rows 256 B (the 128 mels).
+// x rows 256 B (cin = 128: the mels, or layer 2's input at H = 128).
 constexpr int kW16tO = 64;   // o per workgroup
 constexpr int kW16tThreads = 512;
 template <int R, int KS>
@@ -752,14 +752,16 @@ __device__ __forceinline__ int w16_off128(int r, int ch) { return 128 * r + 16 *
 template <int SRCX, int KS, int PAD, int LIN, int R, int POOL, int LP>
 __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz, char* lds) {
   constexpr int RCH = kW16Rows;
-  constexpr int NB = 5;  // bias + the four edge sums (layer 1)
+  constexpr bool TRACK = SRCX == SRC_TRACK_F16 || SRCX == SRC_TRACK_F32;
+  constexpr bool EDGES = TRACK;  // layer 1
+  constexpr int NB = EDGES ? 5 : 1;  // bias (+ the four edge sums)
   constexpr int HALO = KS - 1;
   constexpr int IMG = w16t_img_rows<R, KS>();
   constexpr int FX = (IMG + 15) / 16;  // x image rows per thread (16 row slots x 32 channel quads)
   static_assert(KS == 4 && POOL == 4 && R % POOL == 0, "8 waves = 4 taps x 2 o halves; 16 windows per stage");
   constexpr bool TWO = R >= RCH;  // a stage spans at most two items
   constexpr bool XRAW = SRCX == SRC_TRACK_F16;
-  static_assert(SRCX == SRC_TRACK_F16 || SRCX == SRC_TRACK_F32, "layer 1: x is the track table");
+  static_assert(TRACK || SRCX == SRC_ACT, "x: the track table (layer 1) or y_{l-1}");
   char* dzh = lds;
   char* dzl = dzh + RCH * 128;
   char* xh = dzl + RCH * 128;
@@ -807,7 +809,7 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
       sdx[s] = (float)acc_sum(a.dz_acc, cout, 1, oc + s);
     }
   }
-  if (by == 0 && bz == 0 && tid < cout) {  // BN_1 = gamma * xhat + beta: dbeta = sum g, dgamma = sum g * xhat
+  if (by == 0 && bz == 0 && tid < cout) {  // BN_l = gamma * xhat + beta: dbeta = sum g, dgamma = sum g * xhat
     a.dbeta[tid] = (float)acc_sum(a.dz_acc, cout, 0, tid);
     a.dgamma[tid] = (float)acc_sum(a.dz_acc, cout, 1, tid);
   }
@@ -826,7 +828,14 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
       const float xhm = fmaxf(fabsf(mu[s]), fabsf(ym - mu[s])) * iv[s];
       const float bo = fabsf(av[s]) * (gmax + a.kd_max * (fabsf(sd[s]) + xhm * fabsf(sdx[s])));
       eo[s] = o_ok ? w16_exp(bo) : 0;
-      const float lo = -w16_key(a.x_range + kRngC, cx + s), hi = w16_key(a.x_range, cx + s);
+      float lo, hi;
+      if constexpr (TRACK) {
+        lo = -w16_key(a.x_range + kRngC, cx + s);
+        hi = w16_key(a.x_range, cx + s);
+      } else {  // a ReLU output
+        lo = 0.f;
+        hi = fmaxf(w16_key(a.x_range, cx + s), 0.f);
+      }
       const float bx_ = fmaxf(fabsf((lo - xm[s]) * xs_[s] + xb[s]), fabsf((hi - xm[s]) * xs_[s] + xb[s]));
       ec[s] = XRAW ? 0 : w16_exp(bx_);
       const float so = ldexpf(1.f, eo[s]), sx = ldexpf(1.f, ec[s]);
@@ -865,7 +874,11 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
       wid = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
       wcnt = a.counts ? a.counts[ii] : 1.f;
     }
-    const long t_a = a.item_track[i0], t_b = a.item_track[min(i0 + 1, a.M - 1)];
+    long t_a = 0, t_b = 0;
+    if constexpr (TRACK && TWO) {
+      t_a = a.item_track[i0];
+      t_b = a.item_track[min(i0 + 1, a.M - 1)];
+    }
     uint32_t vm = 0;
 #pragma unroll
     for (int j = 0; j < FX; ++j) {
@@ -879,16 +892,20 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
       const int p = jr + D - k * (R + HALO) - PAD;  // input position in item i
       const bool ok = jr < IMG && i < a.M && p >= 0 && p < LIN;
       vm |= ok ? (1u << j) : 0u;
-      long trk;
-      if constexpr (TWO)
-        trk = k ? t_b : t_a;
-      else
-        trk = a.item_track[ok ? i : i0];
-      const long e = (trk * kFrames + (ok ? p : 0)) * kMels + cx;
-      if constexpr (XRAW)
-        xr16[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.xsrc) + e);
-      else
-        xr[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + e);
+      if constexpr (TRACK) {
+        long trk;
+        if constexpr (TWO)
+          trk = k ? t_b : t_a;
+        else
+          trk = a.item_track[ok ? i : i0];
+        const long e = (trk * kFrames + (ok ? p : 0)) * kMels + cx;
+        if constexpr (XRAW)
+          xr16[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.xsrc) + e);
+        else
+          xr[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + e);
+      } else {
+        xr[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + (((long)(ok ? i : i0) * LIN + (ok ? p : 0)) * cin + cx));
+      }
     }
     xvalid = vm;
   };
@@ -910,7 +927,7 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
         d[s] = (wv && yv[s] > 0.f) ? v : 0.f;
       }
       bacc[0].x += d[0]; bacc[0].y += d[1]; bacc[0].z += d[2]; bacc[0].w += d[3];
-      {  // t = 0, 1 (first window), R-2, R-1 (last window)
+      if constexpr (EDGES) {  // t = 0, 1 (first window), R-2, R-1 (last window)
         const int t0 = rw - (rw / R) * R;
         const bool first = t0 == 0, last = t0 == R - POOL;
         float e1[4], e2[4], e3[4], e4[4];
@@ -923,9 +940,9 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
           e4[s] = (last && r == (uint32_t)(POOL - 1)) ? d[s] : 0.f;
         }
         bacc[1].x += e1[0]; bacc[1].y += e1[1]; bacc[1].z += e1[2]; bacc[1].w += e1[3];
-        bacc[2].x += e2[0]; bacc[2].y += e2[1]; bacc[2].z += e2[2]; bacc[2].w += e2[3];
-        bacc[3].x += e3[0]; bacc[3].y += e3[1]; bacc[3].z += e3[2]; bacc[3].w += e3[3];
-        bacc[4].x += e4[0]; bacc[4].y += e4[1]; bacc[4].z += e4[2]; bacc[4].w += e4[3];
+        bacc[2 % NB].x += e2[0]; bacc[2 % NB].y += e2[1]; bacc[2 % NB].z += e2[2]; bacc[2 % NB].w += e2[3];
+        bacc[3 % NB].x += e3[0]; bacc[3 % NB].y += e3[1]; bacc[3 % NB].z += e3[2]; bacc[3 % NB].w += e3[3];
+        bacc[4 % NB].x += e4[0]; bacc[4 % NB].y += e4[1]; bacc[4 % NB].z += e4[2]; bacc[4 % NB].w += e4[3];
       }
       const w16_h4 h = {(_Float16)d[0], (_Float16)d[1], (_Float16)d[2], (_Float16)d[3]};
       const w16_h4 l = {(_Float16)(d[0] - (float)h[0]), (_Float16)(d[1] - (float)h[1]),
@@ -1044,21 +1061,13 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
 
 template <int SRCX, int KS, int PAD, int LIN, int R, int POOL, int LP>
 __global__ __launch_bounds__(kW16tThreads, 1) void k_conv_wgrad16t(WgradArgs a) {
-  critical_path_priority();  // the step's tail on the caller's stream, as k_conv_wgrad16
+  // layer 1 is the step's tail on the caller's stream (as k_conv_wgrad16); layer 2 a side stream's
+  if constexpr (SRCX != SRC_ACT) critical_path_priority();
   extern __shared__ __attribute__((aligned(16))) char lds16t[];
   // a chunk's o tiles read the same x rows: consecutive logical blocks (o tile fastest) on one XCD
   const int ot = (a.cout + kW16tO - 1) / kW16tO;
   const int L = xcd_swizzle(blockIdx.x, gridDim.x);
   wgrad16t_body<SRCX, KS, PAD, LIN, R, POOL, LP>(a, L % ot, L / ot, lds16t);
-}
-
-// whether layer 1's split-f16 weight gradient runs tap-fused (DCUE_W16_TAPFUSED=0: kc-tiled)
-static bool wgrad16t_on() {
-  static const bool on = [] {
-    const char* e = getenv("DCUE_W16_TAPFUSED");
-    return !(e && e[0] == '0');
-  }();
-  return on;
 }
 
 // whether the weight gradients run on split-f16 MFMA (DCUE_WGRAD_F16=0: the f32-MFMA kernels)
@@ -1068,6 +1077,18 @@ bool wgrad_f16_on() {
     return !(e && e[0] == '0');
   }();
   return on;
+}
+
+// the layers whose split-f16 weight gradient runs tap-fused (k_conv_wgrad16t): 1 and 2, whose
+// inputs have 128 channels (layer 2 at H = 128). DCUE_W16_TAPFUSED=0: neither, =1: layer 1 only
+// (A/B; the kc-tiled k_conv_wgrad16 / multi kernel otherwise)
+static bool w16t_layer(int layer, int cin) {
+  static const int mode = [] {
+    const char* e = getenv("DCUE_W16_TAPFUSED");
+    return e ? atoi(e) : 2;
+  }();
+  if (!wgrad_f16_on() || cin != kMels) return false;
+  return layer == 1 ? mode >= 1 : (layer == 2 && mode >= 2);
 }
 
 // Layer-1 weight gradient (the step's largest MFMA kernel). The GEMM is
@@ -1439,7 +1460,7 @@ int wgrad_nchunk(int layer, int M, int cout, int cin) {
     if (n > (wins + 4 * kW1Win - 1) / (4 * kW1Win)) n = (wins + 4 * kW1Win - 1) / (4 * kW1Win);
     return (int)(n < 1 ? 1 : n);
   }
-  const long tiles = layer == 1 && wgrad_f16_on() && wgrad16t_on()
+  const long tiles = w16t_layer(layer, cin)
                         ? (cout + kW16tO - 1) / kW16tO  // k_conv_wgrad16t: 64 o x all taps
                         : ((gm.ks * cin + 127) / 128) * ((cout + 127) / 128);
   // split-f16 kernels: two workgroups per CU (one's MFMAs and fill run while the other's stage
@@ -1460,7 +1481,14 @@ int wgrad_nchunk(int layer, int M, int cout, int cin) {
       const long v = e ? atol(e) : 0;
       return v >= 1 && v <= 64 ? v : 4L;
     }();
-    const long per = min_stages * kW16Rows;
+    // DCUE_W16T_MIN_STAGES: the same for the tap-fused conv-1 kernel (A/B diagnostic)
+    static const long min_stages_t = [] {
+      const char* e = getenv("DCUE_W16T_MIN_STAGES");
+      const long v = e ? atol(e) : 0;
+      return v >= 1 && v <= 64 ? v : 0L;
+    }();
+    const bool fused = w16t_layer(layer, cin);
+    const long per = (fused && min_stages_t ? min_stages_t : min_stages) * kW16Rows;
     if (n > (rows + per - 1) / per) n = (rows + per - 1) / per;
   }
   const long cap = (8L << 20) / ((long)cout * gm.ks * cin);
@@ -1494,13 +1522,13 @@ static int wgrad_layer(const WgradArgs& a0, int nchunk, hipStream_t s) {
   return DCUE_OK;
 }
 
-template <int SRCX>
-static int wgrad16t_layer1(const WgradArgs& a0, int nchunk, hipStream_t s) {
-  constexpr LayerGeom gm = layer_geom(1);
+template <int L, int SRCX>
+static int wgrad16t_launch(const WgradArgs& a0, int nchunk, hipStream_t s) {
+  constexpr LayerGeom gm = layer_geom(L);
   constexpr int R = gm.lp * gm.pool;
   constexpr size_t LDS = w16t_lds_bytes<R, gm.ks>(SRCX == SRC_TRACK_F16);
   auto kern = k_conv_wgrad16t<SRCX, gm.ks, gm.pad, gm.lin, R, gm.pool, gm.lp>;
-  if (a0.cin != kMels) return DCUE_ERR_INVALID;  // the x image rows are the 128 mels
+  if (a0.cin != kMels || a0.cout % 4) return DCUE_ERR_INVALID;  // x image rows: 128 channels
   static bool attr = false;
   if (!attr) {
     DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS));
@@ -1521,7 +1549,7 @@ static int wgrad16_layer(const WgradArgs& a0, int nchunk, hipStream_t s) {
   constexpr LayerGeom gm = layer_geom(L);
   constexpr int R = gm.lp * gm.pool;
   if constexpr (L == 1)
-    if (wgrad16t_on()) return wgrad16t_layer1<SRCX>(a0, nchunk, s);
+    if (w16t_layer(1, a0.cin)) return wgrad16t_launch<1, SRCX>(a0, nchunk, s);
   auto kern = k_conv_wgrad16<SRCX, gm.ks, gm.pad, gm.lin, R, gm.pool, gm.lp, L == 1>;
   static bool attr = false;
   if (!attr) {
@@ -1665,6 +1693,14 @@ int launch_conv_wgrad_multi(WgradMulti w, hipStream_t s) {
   w.start[0] = 0;
   w.rstart[0] = 0;
   if (w.n < 1 || w.n > kWgradMultiMax) return DCUE_ERR_INVALID;
+  if (w.n == 1 && w.layer[0] == 2 && w16t_layer(2, w.a[0].cin)) {  // layer 2 alone: tap-fused + its reduce
+    const WgradArgs& a = w.a[0];
+    TRY((wgrad16t_launch<2, SRC_ACT>(a, w.nchunk[0], s)));
+    w.rstart[1] = (int)(((long)a.cout * 4 * a.cin + 127) / 128 + (a.cout + 127) / 128);
+    DCUE_LAUNCH(k_wgrad_reduce_multi, dim3((unsigned)w.rstart[1]), dim3(256), 0, s, w);
+    DCUE_LAUNCH_CHECK();
+    return DCUE_OK;
+  }
   for (int j = 0; j < w.n; ++j) {
     if (w.layer[j] < 2 || w.layer[j] > 6) return DCUE_ERR_INVALID;
     WgradArgs& a = w.a[j];
