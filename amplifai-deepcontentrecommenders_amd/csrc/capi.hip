@@ -8,6 +8,7 @@
 //   adam      dense params + user table, then weight repack
 #include <math.h>
 #include <atomic>
+#include <functional>
 #include <string.h>
 
 #include "dcue_internal.h"
@@ -42,12 +43,22 @@ SidePool* side_pool() {
       const char* e = getenv("DCUE_SIDE_PRIO");
       return e && e[0] == 'l';
     }();
+    // DCUE_USER_PRIO=high: the user stream (st[0]) at the device's greatest priority, so its short
+    // user-tower GEMMs are dispatched between the item tower's conv workgroups (A/B knob)
+    static const bool user_high = [] {
+      const char* e = getenv("DCUE_USER_PRIO");
+      return e && e[0] == 'h';
+    }();
     int least = 0, greatest = 0;
-    if (low && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
-    for (auto& s : p.st)
-      if ((low ? hipStreamCreateWithPriority(&s, hipStreamNonBlocking, least)
-               : hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess)
+    if ((low || user_high) && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
+    for (int i = 0; i < 3; ++i) {
+      hipStream_t& s = p.st[i];
+      const bool prio = low || (user_high && i == 0);
+      const int pr = (user_high && i == 0) ? greatest : least;
+      if ((prio ? hipStreamCreateWithPriority(&s, hipStreamNonBlocking, pr)
+                : hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess)
         return nullptr;
+    }
     for (auto& e : p.ev)
       if (hipEventCreateWithFlags(&e, sync_event_flags()) != hipSuccess) return nullptr;
   }
@@ -399,7 +410,7 @@ int init_ctx(Ctx* c, const dcue_model* m) {
 int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t* item_track, int M,
                  double copies, bool train, const float* counts, float* f_out, hipStream_t s,
                  bool acc_cleared = false, bool stats_done = false, bool clear_bn0 = false,
-                 hipEvent_t before_l2 = nullptr) {
+                 hipEvent_t before_l2 = nullptr, const std::function<int()>* after_l1 = nullptr) {
   const dcue_model* m = c.m;
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
   // one BN's finalize/publish record for its first consumer (train) -- bnacc.h
@@ -463,6 +474,7 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     TRY(timer_begin(&tsc, l == 1 ? DCUE_TIMED_CONV1_FWD : -1, s));
     TRY(launch_conv_fwd(l, l == 1 ? kMels : c.H, l == 1 ? src : SRC_ACT, a, s));
     TRY(timer_end(&tsc));
+    if (l == 1 && after_l1) TRY((*after_l1)());
   }
   if (c.res) {  // fc on [tp1, tp2, tp3, tp4, bn5(y5)] (truedcuemel1dres.py:93-97)
     TRY(launch_timepool(w.y, w.mean, w.a, c.bn ? c.P(seg_bn_b(1)) : nullptr, c.bn ? c.P(seg_bn_b(2)) : nullptr,
@@ -698,21 +710,33 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   HPROF("capi:3");
   if (!o.prologue_done) TRY(batch_counts(b, w, s));
   HPROF("capi:4");
-  TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s,
-                   o.prologue_done, o.input_stats_done && o.prologue_done, o.clear_bn0, o.wait_late));
-  TRY(wait_point(su, ev_in));
-  HPROF("capi:5");
-  if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
-  HPROF("capi:6");
   hipEvent_t ev_uf = nullptr;
-  {
-    ForkAfter fk(sp, su, &ev_uf);
-    TRY(user_forward(c, w, b->users, b->n_rows, nullptr, su));
-    HPROF("capi:7");
-    TRY(fk.done());
-    HPROF("capi:8");
-  }
-  if (o.flush_slice_step >= 0 && m->emb_step) TRY(launch_emb_flush_rows(m, o.flush_slice_step, su));
+  // the user tower on su: emb rows brought up to date, then the two GEMMs (+ the rolling flush slice)
+  const std::function<int()> user_part = [&]() -> int {
+    TRY(wait_point(su, ev_in));
+    HPROF("capi:5");
+    if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
+    HPROF("capi:6");
+    {
+      ForkAfter fk(sp, su, &ev_uf);
+      TRY(user_forward(c, w, b->users, b->n_rows, nullptr, su));
+      HPROF("capi:7");
+      TRY(fk.done());
+      HPROF("capi:8");
+    }
+    if (o.flush_slice_step >= 0 && m->emb_step) TRY(launch_emb_flush_rows(m, o.flush_slice_step, su));
+    return DCUE_OK;
+  };
+  // DCUE_USER_EARLY=1: the user tower is issued right after conv 1 instead of after the whole item
+  // tower, so the host's issue order does not hold it behind four conv launches (A/B knob)
+  static const bool early = [] {
+    const char* e = getenv("DCUE_USER_EARLY");
+    return e && e[0] == '1';
+  }();
+  TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s,
+                   o.prologue_done, o.input_stats_done && o.prologue_done, o.clear_bn0, o.wait_late,
+                   early ? &user_part : nullptr));
+  if (!early) TRY(user_part());
   TRY(wait_point(s, ev_uf));
   HPROF("capi:9");
   if (o.fuse_score) {
