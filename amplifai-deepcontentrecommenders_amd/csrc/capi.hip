@@ -410,7 +410,8 @@ int init_ctx(Ctx* c, const dcue_model* m) {
 int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t* item_track, int M,
                  double copies, bool train, const float* counts, float* f_out, hipStream_t s,
                  bool acc_cleared = false, bool stats_done = false, bool clear_bn0 = false,
-                 hipEvent_t before_l2 = nullptr, const std::function<int()>* after_l1 = nullptr) {
+                 hipEvent_t before_l2 = nullptr, const std::function<int()>* after_l1 = nullptr,
+                 dcue_comm* sync_bn = nullptr) {
   const dcue_model* m = c.m;
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
   // one BN's finalize/publish record for its first consumer (train) -- bnacc.h
@@ -448,6 +449,10 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
                          w.invstd[l], w.a[l], s));
     TRY(launch_input_stats(src, t->data, item_track, nullptr, M, nullptr, rng_at(w, 0), s));
   }
+  // SyncBN: each layer's batch sums over every rank before their first consumer (the next launch on
+  // this stream finalizes them); the counts are already the global ones (forward_impl)
+  const bool sync = train && c.bn && sync_bn;
+  if (sync) TRY(comm_allreduce_u64(sync_bn, bn_acc(w.bnacc, w.cmax, 0), 4L * w.cmax, s));
   for (int l = 1; l <= 5; ++l) {
     // the previous step's late-segment Adam (split plans, StepOpts::dense_split) ran on the user
     // stream: conv 2 is the first kernel on this stream to read those parameters
@@ -474,6 +479,7 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     TRY(timer_begin(&tsc, l == 1 ? DCUE_TIMED_CONV1_FWD : -1, s));
     TRY(launch_conv_fwd(l, l == 1 ? kMels : c.H, l == 1 ? src : SRC_ACT, a, s));
     TRY(timer_end(&tsc));
+    if (sync) TRY(comm_allreduce_u64(sync_bn, bn_acc(w.bnacc, w.cmax, l), 4L * w.cmax, s));
     if (l == 1 && after_l1) TRY((*after_l1)());
   }
   if (c.res) {  // fc on [tp1, tp2, tp3, tp4, bn5(y5)] (truedcuemel1dres.py:93-97)
@@ -700,7 +706,8 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   carve(&m->dims, b->n_rows, b->n_neg, b->n_items, ws, &w);
   if (o.acc) rebase_acc(&w, o.acc);
   if (o.counts) w.counts = const_cast<float*>(o.counts);
-  const double copies = (double)b->n_rows * (1 + b->n_neg);
+  // SyncBN: BatchNorm normalises over every rank's copies (same B, N on each rank)
+  const double copies = (double)b->n_rows * (1 + b->n_neg) * (o.sync_bn ? comm_world(o.sync_bn) : 1);
   SidePool* sp = side_pool();
   if (!sp) return DCUE_ERR_HIP;
   hipStream_t su = sp->st[0];
@@ -735,7 +742,7 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   }();
   TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s,
                    o.prologue_done, o.input_stats_done && o.prologue_done, o.clear_bn0, o.wait_late,
-                   early ? &user_part : nullptr));
+                   early ? &user_part : nullptr, o.sync_bn));
   if (!early) TRY(user_part());
   TRY(wait_point(s, ev_uf));
   HPROF("capi:9");
@@ -830,7 +837,9 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   if (o.counts) w.counts = const_cast<float*>(o.counts);
   const int B = b->n_rows, N = b->n_neg, M = b->n_items;
   const int H = c.H, D = c.D, E = c.E;
-  const double copies = (double)B * (1 + N);
+  const double copies = (double)B * (1 + N) * (o.sync_bn ? comm_world(o.sync_bn) : 1);  // (SyncBN: global)
+  const bool sync = o.sync_bn && c.bn;
+  const int bn_world = sync ? comm_world(o.sync_bn) : 0;
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
   if (o.fuse_score && dscores) return DCUE_ERR_INVALID;
   // the item gradients' copy lists: the plan's (current slot), else the workspace's (eager steps and
@@ -904,6 +913,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
                          cptr, cidx, grng_at(w, 5), grng_at(w, 6), s));
     HPROF("capi:15");
   }
+  if (sync) TRY(comm_allreduce_u64(o.sync_bn, bn_acc(w.bnbacc, w.cmax, 5), 4L * w.cmax, s));
   for (int l = 5; l >= 2; --l) {  // dgrad chain: g_l (+ BN_l sums) -> g_{l-1} (+ BN_{l-1} sums)
     const LayerGeom gm = layer_geom(l);
     RowsArgs ra = {};
@@ -934,9 +944,15 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     if ((l - 1 == 3 && !fork_once()) || l - 1 == 2) {
       ForkAfter fk(sp, s, &ev_layer[l - 1]);
       TRY(launch_conv_dgrad(l, l == 5 ? D : H, ra, s));
+      if (sync) {  // the weight gradients forked here read the summed BN_{l-1} sums: the fork point
+                   // is recorded after the exchange instead of bound to the launch
+        TRY(comm_allreduce_u64(o.sync_bn, bn_acc(w.bnbacc, w.cmax, l - 1), 4L * w.cmax, s));
+        launch_tag().missed = true;
+      }
       TRY(fk.done());
     } else {
       TRY(launch_conv_dgrad(l, l == 5 ? D : H, ra, s));
+      if (sync) TRY(comm_allreduce_u64(o.sync_bn, bn_acc(w.bnbacc, w.cmax, l - 1), 4L * w.cmax, s));
     }
     HPROF("capi:16");
   }
@@ -959,6 +975,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     wa.mean_l = w.mean[l]; wa.invstd_l = w.invstd[l]; wa.a_l = w.a[l];
     wa.dz_acc = bn_acc(w.bnbacc, w.cmax, l); wa.dgamma = c.dgamma(w, l); wa.dbeta = c.dbeta(w, l);
     wa.invN = c.bn ? (float)(1.0 / (copies * gm.lp)) : 0.f;
+    wa.bn_world = bn_world;
     wa.counts = w.counts;
     wa.M = M; wa.cout = C; wa.cin = cin;
     wa.wpart = w.wpart[ps]; wa.bpart = w.bpart[ps];
@@ -1055,6 +1072,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       wa.mean_l = w.mean[l]; wa.invstd_l = w.invstd[l]; wa.a_l = w.a[l];
       wa.dz_acc = bn_acc(w.bnbacc, w.cmax, l); wa.dgamma = c.dgamma(w, l); wa.dbeta = c.dbeta(w, l);
       wa.invN = c.bn ? (float)(1.0 / (copies * gm.lp)) : 0.f;
+      wa.bn_world = bn_world;
       wa.counts = w.counts;
       wa.M = M; wa.cout = l == 5 ? D : H; wa.cin = H;
       wa.wpart = w.wpm[l - 2]; wa.bpart = w.bpm[l - 2];

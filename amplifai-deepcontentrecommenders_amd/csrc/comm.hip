@@ -17,7 +17,11 @@
 #include "dcue_internal.h"
 
 struct dcue_comm {
-  ncclComm_t nc = nullptr;
+  ncclComm_t nc = nullptr;         // RCCL transport (dcue_comm_create)
+  dcue_host_allreduce_fn host_fn = nullptr;  // host transport (dcue_comm_create_host)
+  void* host_ctx = nullptr;
+  void* hbuf = nullptr;            // pinned staging of the host transport
+  size_t hbuf_bytes = 0;
   int world = 1, rank = 0;
   hipStream_t stream = nullptr;  // the exchange's own stream (beside the step's side streams)
   hipEvent_t ev_tail = nullptr;  // the caller's stream at the step's end
@@ -47,9 +51,34 @@ __global__ __launch_bounds__(256) void k_div_world(float* __restrict__ buf, long
     buf[i] = __fdiv_rn(buf[i], w);  // grad.div_(world)
 }
 
+// Host transport: the comm's stream is drained (it has waited for whatever produced `buf`), the
+// buffer is staged through pinned host memory, the caller's function sums it over the ranks, and
+// the result goes back, all before this returns. The plan's exchange keeps its stream/event order,
+// so the same library code runs over either transport.
+static int host_allreduce(dcue_comm* c, void* buf, long n, int dtype) {
+  const size_t bytes = (size_t)n * (dtype == DCUE_COMM_U64 ? 8 : 4);
+  if (bytes > c->hbuf_bytes) {
+    if (c->hbuf) DCUE_HIP_CHECK(hipHostFree(c->hbuf));
+    c->hbuf = nullptr;
+    c->hbuf_bytes = 0;
+    DCUE_HIP_CHECK(hipHostMalloc(&c->hbuf, bytes, hipHostMallocDefault));
+    c->hbuf_bytes = bytes;
+  }
+  DCUE_HIP_CHECK(hipMemcpyAsync(c->hbuf, buf, bytes, hipMemcpyDeviceToHost, c->stream));
+  DCUE_HIP_CHECK(hipStreamSynchronize(c->stream));
+  if (c->host_fn(c->host_ctx, c->hbuf, (int64_t)n, dtype) != 0) {
+    set_last_error("dcue_comm host transport: the all-reduce callback failed", hipSuccess, __FILE__, __LINE__);
+    return DCUE_ERR_HIP;
+  }
+  DCUE_HIP_CHECK(hipMemcpyAsync(buf, c->hbuf, bytes, hipMemcpyHostToDevice, c->stream));
+  DCUE_HIP_CHECK(hipStreamSynchronize(c->stream));
+  return DCUE_OK;
+}
+
 // Sum all-reduce of n floats in place on the comm's stream; timed as DCUE_TIMED_ALLREDUCE.
 int comm_allreduce_sum(dcue_comm* c, float* buf, long n) {
   if (n <= 0) return DCUE_OK;
+  if (c->host_fn) return host_allreduce(c, buf, n, DCUE_COMM_F32);
   hipEvent_t a = nullptr, b = nullptr;
   if (timer_take_turn(DCUE_TIMED_ALLREDUCE)) {
     a = timer_event();
@@ -66,6 +95,20 @@ int comm_allreduce_sum(dcue_comm* c, float* buf, long n) {
 }
 
 int comm_world(const dcue_comm* c) { return c->world; }
+
+int comm_allreduce_u64(dcue_comm* c, unsigned long long* buf, long n, hipStream_t s) {
+  if (n <= 0) return DCUE_OK;
+  DCUE_HIP_CHECK(hipEventRecord(c->ev_tail, s));
+  DCUE_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_tail, 0));
+  if (c->host_fn) {
+    TRY(host_allreduce(c, buf, n, DCUE_COMM_U64));
+  } else {
+    DCUE_NCCL_CHECK(ncclAllReduce(buf, buf, (size_t)n, ncclUint64, ncclSum, c->nc, c->stream));
+  }
+  DCUE_HIP_CHECK(hipEventRecord(c->ev_done, c->stream));
+  DCUE_HIP_CHECK(hipStreamWaitEvent(s, c->ev_done, 0));
+  return DCUE_OK;
+}
 
 // The plan's exchange (dcue_plan_set_comm): `side_done` marks the side streams' join (the flat
 // gradient is final past `late` floats), the caller's stream `s` is at the step's end. Returns with
@@ -124,10 +167,32 @@ extern "C" int dcue_comm_create(const void* id_host, int32_t world, int32_t rank
   return DCUE_OK;
 }
 
+extern "C" int dcue_comm_create_host(int32_t world, int32_t rank, dcue_host_allreduce_fn fn, void* ctx,
+                                     dcue_comm** comm_host) {
+  if (!fn || !comm_host || world < 1 || rank < 0 || rank >= world) return DCUE_ERR_INVALID;
+  *comm_host = nullptr;
+  dcue_comm* c = new dcue_comm;
+  c->world = world;
+  c->rank = rank;
+  c->host_fn = fn;
+  c->host_ctx = ctx;
+  int st = DCUE_OK;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) st = DCUE_ERR_HIP;
+  if (!st && hipEventCreateWithFlags(&c->ev_tail, sync_event_flags()) != hipSuccess) st = DCUE_ERR_HIP;
+  if (!st && hipEventCreateWithFlags(&c->ev_done, sync_event_flags()) != hipSuccess) st = DCUE_ERR_HIP;
+  if (st) {
+    dcue_comm_destroy(c);
+    return st;
+  }
+  *comm_host = c;
+  return DCUE_OK;
+}
+
 extern "C" int dcue_comm_destroy(dcue_comm* c) {
   if (!c) return DCUE_OK;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->nc) (void)ncclCommDestroy(c->nc);
+  if (c->hbuf) (void)hipHostFree(c->hbuf);
   if (c->ev_tail) (void)hipEventDestroy(c->ev_tail);
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
   if (c->stream) (void)hipStreamDestroy(c->stream);

@@ -74,8 +74,8 @@ __device__ __forceinline__ void wgrad_body(const WgradArgs& a, int bx, int by, i
   }
   if (!RAW && bx == 0 && by == 0 && bz == 0 && tid < cout) {
     // BN_l = gamma * xhat + beta: dbeta = sum g, dgamma = sum g * xhat
-    a.dbeta[tid] = (float)acc_sum(a.dz_acc, cout, 0, tid);
-    a.dgamma[tid] = (float)acc_sum(a.dz_acc, cout, 1, tid);
+    a.dbeta[tid] = (float)(acc_sum(a.dz_acc, cout, 0, tid) * bn_grad_scale(a));
+    a.dgamma[tid] = (float)(acc_sum(a.dz_acc, cout, 1, tid) * bn_grad_scale(a));
   }
   const float4 xmu = ld4(a.x_mean + cx), xsc = ld4(a.x_a + cx);
   const float4 xbe = a.x_beta ? ld4(a.x_beta + cx) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -380,8 +380,8 @@ __device__ __forceinline__ void wgrad16_body(const WgradArgs& a, int bx, int by,
   }
   if (!RAW && bx == 0 && by == 0 && bz == 0 && tid < cout) {
     // BN_l = gamma * xhat + beta: dbeta = sum g, dgamma = sum g * xhat
-    a.dbeta[tid] = (float)acc_sum(a.dz_acc, cout, 0, tid);
-    a.dgamma[tid] = (float)acc_sum(a.dz_acc, cout, 1, tid);
+    a.dbeta[tid] = (float)(acc_sum(a.dz_acc, cout, 0, tid) * bn_grad_scale(a));
+    a.dgamma[tid] = (float)(acc_sum(a.dz_acc, cout, 1, tid) * bn_grad_scale(a));
   }
   const float4 xmu = ld4(a.x_mean + cx), xsc = ld4(a.x_a + cx);
   const float4 xbe = a.x_beta ? ld4(a.x_beta + cx) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -810,8 +810,8 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
     }
   }
   if (by == 0 && bz == 0 && tid < cout) {  // BN_l = gamma * xhat + beta: dbeta = sum g, dgamma = sum g * xhat
-    a.dbeta[tid] = (float)acc_sum(a.dz_acc, cout, 0, tid);
-    a.dgamma[tid] = (float)acc_sum(a.dz_acc, cout, 1, tid);
+    a.dbeta[tid] = (float)(acc_sum(a.dz_acc, cout, 0, tid) * bn_grad_scale(a));
+    a.dgamma[tid] = (float)(acc_sum(a.dz_acc, cout, 1, tid) * bn_grad_scale(a));
   }
   const float4 xmu = ld4(a.x_mean + cx), xsc = ld4(a.x_a + cx);
   const float4 xbe = a.x_beta ? ld4(a.x_beta + cx) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1205,8 +1205,8 @@ __global__ __launch_bounds__(512, DCUE_W1_WGS) void k_conv1_wgrad(WgradArgs a) {
   };
 
   if (chunk == 0 && ktile == 0 && otile == 0 && tid < cout) {  // BN1's gamma/beta gradients
-    a.dbeta[tid] = (float)acc_sum(a.dz_acc, cout, 0, tid);
-    a.dgamma[tid] = (float)acc_sum(a.dz_acc, cout, 1, tid);
+    a.dbeta[tid] = (float)(acc_sum(a.dz_acc, cout, 0, tid) * bn_grad_scale(a));
+    a.dgamma[tid] = (float)(acc_sum(a.dz_acc, cout, 1, tid) * bn_grad_scale(a));
   }
 
   // ---- MFMA: lane (hl = lane >> 5, l32) holds A[o = l32][row 2h + hl] and B[row 2h + hl][kc = l32]

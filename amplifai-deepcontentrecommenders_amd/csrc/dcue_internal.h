@@ -80,6 +80,7 @@ struct RowsArgs {
 };
 
 struct WgradArgs {
+  int bn_world;               // SyncBN (> 1): dz sums are over the ranks; BN_l's dgamma/dbeta get 1/world
   const void* xsrc;           // layer input: tracks (l=1) or y_{l-1} [M][Lin][cin]
   const int32_t* item_track;
   const float* x_mean;        // x = (src - mean) * a + beta ; l=1 uses xhat0 (a = invstd0, beta = 0)
@@ -106,6 +107,9 @@ struct WgradArgs {
   const unsigned* g_range;    // max |g_l| per channel (ordered keys of |g|), from its producer
   float kd_max;               // the largest copies(item) * invN of the batch
 };
+// SyncBN: BN_l's dgamma / dbeta come from sums over every rank; DDP then averages them, so each rank
+// contributes 1/world of the global sum (torch SyncBatchNorm: local sums, averaged by DDP). x1 otherwise.
+__device__ __forceinline__ double bn_grad_scale(const WgradArgs& a) { return a.bn_world > 1 ? 1.0 / a.bn_world : 1.0; }
 
 // weight gradients of n conv layers (of 2..5) in one launch, then their chunk sums in a second one
 // (the host fills n, layer[], a[], nchunk[], dW[], db[]; the launcher derives the block ranges)
@@ -347,6 +351,9 @@ void timer_add_recorded(int cls, hipEvent_t a, hipEvent_t b);
 // after the caller's stream `s`; `s` then waits for both
 int comm_exchange_step(dcue_comm* c, float* grad, long late, long n, hipEvent_t side_done, hipStream_t s);
 int comm_world(const dcue_comm* c);
+// SyncBN: n uint64 words (exact fixed-point BN accumulators, bnacc.h) summed over the ranks in place,
+// ordered on `s` (through the comm's stream, so every collective of a rank runs in issue order)
+int comm_allreduce_u64(dcue_comm* c, unsigned long long* buf, long n, hipStream_t s);
 int comm_divide(const dcue_comm* c, float* grad, long n, hipStream_t s);
 // whether this occurrence of a timed class is one to time (every stride-th; for intervals timed by
 // event records rather than a bound launch, e.g. the RCCL exchange)
@@ -400,6 +407,7 @@ int join_user_stream(hipStream_t s);
 
 // ------------------------------------------------------------- step implementation (capi.hip)
 struct StepOpts {
+  dcue_comm* sync_bn = nullptr;  // SyncBN: BatchNorm sums all-reduced over this communicator's ranks
   bool prologue_done = false;  // counts written + accumulators cleared by the prologue
   bool fuse_score = false;     // train forward also runs the hinge backward (k_score_fused)
   const dcue_adam_args* emb_adam = nullptr;  // backward: also step the user table (parts = EMBEDDING)

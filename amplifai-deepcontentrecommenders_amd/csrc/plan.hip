@@ -51,6 +51,7 @@ struct dcue_plan {
   int pending_flush = -1;         // step whose rolling-flush slice the next launch issues
   hipStream_t last_stream = nullptr;  // the caller's stream of the last launch
   dcue_comm* comm = nullptr;      // data-parallel exchange between backward and Adam (plan_step)
+  bool sync_bn = false;           // SyncBN over `comm` (dcue_plan_set_sync_bn)
   long late = 0, n_dense = 0;     // flat-gradient floats: end of bn0/conv1/bn1, total
   int comm_world = 1;
 };
@@ -143,6 +144,7 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   const bool ahead = prepared && items_src == p->ahead_items[cur];
   p->ahead_items[cur] = nullptr;
   StepOpts o;
+  o.sync_bn = p->sync_bn ? p->comm : nullptr;
   o.prologue_done = true;
   o.fuse_score = true;
   o.emb_adam = emb_adam;
@@ -389,12 +391,29 @@ extern "C" int dcue_plan_set_comm(dcue_plan* p, dcue_comm* comm) {
   if (!p || p->exec) return DCUE_ERR_INVALID;  // eager plans only
   p->comm = comm;
   p->comm_world = 1;
-  if (!comm) return DCUE_OK;
+  if (!comm) {
+    p->sync_bn = false;
+    return DCUE_OK;
+  }
   int64_t off[DCUE_N_DENSE_SEGMENTS + 1];
   TRY(dcue_param_layout(&p->model.dims, off));
   p->late = off[DCUE_SEG_LATE];
   p->n_dense = off[DCUE_N_DENSE_SEGMENTS];
   p->comm_world = dcue::comm_world(comm);
+  return DCUE_OK;
+}
+
+extern "C" int dcue_plan_set_sync_bn(dcue_plan* p, int32_t on) {
+  if (!p || p->exec) return DCUE_ERR_INVALID;
+  if (!on) {
+    p->sync_bn = false;
+    return DCUE_OK;
+  }
+  if (!p->comm) return DCUE_ERR_INVALID;  // bind the communicator first
+  // the f32 conv-1 weight-gradient path materialises bn0(x) one step ahead on a side stream, before
+  // this step's sums are exchanged; SyncBN runs on the split-f16 weight gradients (the default)
+  if (!dcue::wgrad_f16_on()) return DCUE_ERR_UNSUPPORTED;
+  p->sync_bn = true;
   return DCUE_OK;
 }
 

@@ -98,7 +98,9 @@ class PlanConfig(ctypes.Structure):
 
 MT_STATE_BYTES = 624 * 4 + 16
 MAX_LOG_CAP = 256
-ABI_VERSION = 11
+ABI_VERSION = 12
+COMM_F32, COMM_U64 = 0, 1  # dcue_host_allreduce_fn dtypes
+HOST_ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32)
 RANK_SPLIT, RANK_SINGLE = 0, 1
 
 _P = ctypes.c_void_p
@@ -156,9 +158,12 @@ _SIGS = {
     "dcue_check_ids": ([_P, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_int32, _P], ctypes.c_int),
     "dcue_comm_unique_id": ([_P], ctypes.c_int),
     "dcue_comm_create": ([_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "dcue_comm_create_host": ([ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.POINTER(ctypes.c_void_p)],
+                              ctypes.c_int),
     "dcue_comm_destroy": ([_P], ctypes.c_int),
     "dcue_comm_allreduce_mean": ([_P, _P, ctypes.c_int64, _P], ctypes.c_int),
     "dcue_plan_set_comm": ([_P, _P], ctypes.c_int),
+    "dcue_plan_set_sync_bn": ([_P, ctypes.c_int32], ctypes.c_int),
     "dcue_timer_enable": ([ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
     "dcue_timer_read": ([ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)],
                         ctypes.c_int),

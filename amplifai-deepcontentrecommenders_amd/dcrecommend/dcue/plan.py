@@ -187,6 +187,14 @@ class TrainPlan:
                   "dcue_plan_set_comm")
         self._comm = comm  # keep the communicator alive while bound
 
+    def set_sync_bn(self, on=True):
+        """SyncBN over the bound communicator's ranks (dcue_plan_set_sync_bn): every train-mode
+        BatchNorm of the item tower normalises over the global batch -- torch's
+        convert_sync_batchnorm + DDP semantics. Bind the communicator first (set_comm)."""
+        if self._handle is None:
+            raise RuntimeError("TrainPlan was closed")
+        nat.check(self._lib.dcue_plan_set_sync_bn(self._handle, 1 if on else 0), "dcue_plan_set_sync_bn")
+
     def wait_side(self, stream):
         """`stream` (a torch.cuda.Stream or raw handle) waits until the side-stream part of the last
         launched step is in: the flat gradient is then final past its first SEG_LATE segments

@@ -12,8 +12,11 @@ Two ways to run the exchange:
   the whole data-parallel step -- sample, forward, backward, the two-bucket all-reduce overlapped
   with the conv-1 weight gradient, Adam with the divide by W fused in -- stays ONE host call
   (TrainPlan.step), exactly as the single-GPU step.
+* HostComm + TrainPlan.set_comm: the same native plan step and exchange code, with the library
+  handing each bucket to a torch.distributed all-reduce on the host (gloo): for several ranks that
+  share one GPU, which RCCL does not allow (tests), not for speed.
 * allreduce_mean_overlapped_ over a torch.distributed group: the same buckets from Python (gloo
-  on CPU tests, or several ranks sharing one GPU, which RCCL does not allow).
+  on CPU tests, or several ranks sharing one GPU).
 
 BatchNorm running statistics are per replica during training, as under DDP without SyncBN; DDP's
 default broadcast_buffers makes every rank use rank 0's buffers, which broadcast_buffers_ does
@@ -173,3 +176,35 @@ class NativeComm:
             self.close()
         except Exception:
             pass
+
+
+class HostComm(NativeComm):
+    """A libdcue_hip communicator whose transport is a torch.distributed group on the host
+    (dcue_comm_create_host): the plan's native exchange -- both buckets, their event order, Adam's
+    divide by the world size -- runs unchanged, each bucket summed by `dist.all_reduce` on a CPU view
+    of the library's pinned staging buffer. uint64 buffers are summed as int64 (the same bits: two's
+    complement addition wraps identically)."""
+
+    def __init__(self, group=None):
+        from . import _native as nat
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self._group = group
+
+        def _allreduce(ctx, host_buf, n, dtype):
+            try:
+                ct = ctypes.c_float if dtype == nat.COMM_F32 else ctypes.c_int64
+                arr = (ct * int(n)).from_address(host_buf)
+                t = torch.frombuffer(arr, dtype=torch.float32 if dtype == nat.COMM_F32 else torch.int64)
+                dist.all_reduce(t, group=self._group)
+                return 0
+            except Exception as e:  # reported through the library's error path (non-zero)
+                print("HostComm all-reduce failed: %r" % (e,), flush=True)
+                return 1
+
+        self._cb = nat.HOST_ALLREDUCE_FN(_allreduce)  # kept alive as long as the communicator
+        handle = ctypes.c_void_p()
+        nat.check(nat.lib().dcue_comm_create_host(self.world, self.rank, self._cb, None, ctypes.byref(handle)),
+                  "dcue_comm_create_host")
+        self.handle = handle
+        self._lib = nat.lib()

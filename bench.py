@@ -75,6 +75,9 @@ def parse():
     ap.add_argument("--profile-phase", choices=["inbatch_cold", "inbatch", "catalogue"],
                     help="under `rocprofv3 --kernel-trace`: bracket this phase's timed steps with a "
                          "marker kernel (profiles/summarize_pmc.py keeps what lies between)")
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="N > 1 with the native exchange: SyncBN over the ranks (dcue_plan_set_sync_bn); "
+                         "default per-replica BatchNorm (DDP semantics)")
     ap.add_argument("--py-exchange", action="store_true",
                     help="N>1: all-reduce from Python over torch.distributed instead of the plan's RCCL")
     ap.add_argument("--stall-s", type=float, default=180.0,
@@ -453,6 +456,8 @@ def main():
                          optimizer=opt)
         if comm is not None:
             plan.set_comm(comm)
+            if args.sync_bn:
+                plan.set_sync_bn(True)
         return plan
 
     def run(plan, step_fn, n, phase="warm-up"):
@@ -766,6 +771,7 @@ def main():
                                 "torch.distributed (%s) from Python%s" % (
                                     backend, "; native RCCL failed: " + comm_error if comm_error else ""))
                                if world > 1 else None,
+                   "batchnorm": "sync (global batch)" if (comm is not None and args.sync_bn) else "per replica",
                    "process_group_world": dist.get_world_size() if world > 1 else 1},
         "roofline": head["roofline"],
         "kernels": head["kernels"],

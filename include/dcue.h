@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DCUE_ABI_VERSION 11
+#define DCUE_ABI_VERSION 12
 #define DCUE_N_MELS 128
 #define DCUE_N_FRAMES 131
 #define DCUE_N_BN 6
@@ -385,6 +385,17 @@ typedef struct dcue_comm dcue_comm;
 int dcue_comm_unique_id(void* id_host); /* rank 0: DCUE_COMM_ID_BYTES bytes */
 /* A communicator over `world` ranks on the current HIP device (collective: every rank calls it). */
 int dcue_comm_create(const void* id_host, int32_t world, int32_t rank, dcue_comm** comm_host);
+/* A communicator whose transport is the caller's: `fn(ctx, host_buf, n, dtype)` must replace the n
+ * elements at host_buf (DCUE_COMM_F32: float, DCUE_COMM_U64: uint64, two's-complement wrap) by their
+ * sum over the ranks and return 0. The library drains its stream and stages the buffer through pinned
+ * host memory around each call, so a plan step blocks the host at every exchange point; it runs the
+ * same exchange code (buckets, event order, Adam's divide) as the RCCL transport. For ranks that
+ * cannot share an RCCL communicator -- several ranks on one GPU over gloo (tests) -- not for speed. */
+#define DCUE_COMM_F32 0
+#define DCUE_COMM_U64 1
+typedef int (*dcue_host_allreduce_fn)(void* ctx, void* host_buf, int64_t n, int32_t dtype);
+int dcue_comm_create_host(int32_t world, int32_t rank, dcue_host_allreduce_fn fn, void* ctx,
+                          dcue_comm** comm_host);
 int dcue_comm_destroy(dcue_comm* comm);
 /* In-place mean over the ranks of n floats, ordered on `stream` (sum all-reduce, then / world). */
 int dcue_comm_allreduce_mean(dcue_comm* comm, float* buf, int64_t n, void* stream);
@@ -398,6 +409,17 @@ int dcue_comm_allreduce_mean(dcue_comm* comm, float* buf, int64_t n, void* strea
  * grad_div 0). Collective order is the same on every rank. The plan must have been created with
  * emb_grad_scale = 1/world. */
 int dcue_plan_set_comm(dcue_plan* plan, dcue_comm* comm);
+/* SyncBN (on != 0; the bound communicator's ranks): every train-mode BatchNorm of the item
+ * tower normalises over the whole global batch. Its exact fixed-point sums (forward: count-weighted
+ * sum and sum of squares; backward: sum g and sum g*xhat) are all-reduced over the ranks between
+ * their producer and first consumer, so the statistics -- and the running statistics -- are the same
+ * on every rank and do not depend on the order of the ranks. BN gamma/beta gradients enter the
+ * exchange as 1/world of the global sum each, so after the DDP mean they equal torch
+ * SyncBatchNorm + DDP's (the mean of the per-rank local sums). 11 small collectives per step (6 BN
+ * layers forward, bn5..bn1 backward; bn0 has no input gradient, its gamma/beta gradients stay local).
+ * Requires a bound communicator (DCUE_ERR_INVALID otherwise) and the split-f16 weight gradients
+ * (DCUE_ERR_UNSUPPORTED under DCUE_WGRAD_F16=0). Unbinding the communicator turns it off. */
+int dcue_plan_set_sync_bn(dcue_plan* plan, int32_t on);
 
 /* ------------------------------------------------------------------- live kernel timing */
 /* enable = n > 0: every n-th launch of the kernel class (also inside plans created afterwards)
