@@ -259,7 +259,6 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
   const long i0 = gr0 / R, i1 = (gr1 - 1) / R;
   const long elo = i0 * RX + (gr0 - i0 * R);
   const int nslab = (int)(i1 * RX + (gr1 - 1 - i1 * R) + KS - elo);
-  (void)MAXI;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, l16 = lane & 15;
@@ -307,6 +306,16 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
     const int nfill = nslab * C4;
     const int c = 4 * (threadIdx.x % C4);
     __shared__ ChanLds chl;
+    // the track ids of the workgroup's items (uniform: scalar loads issued before anything else), so
+    // the slab's row loads do not wait on a per-slot item_track load first; rows of one workgroup
+    // span at most two items whenever ROWS <= R (MAXI == 2)
+    constexpr bool kTrack = SRC == SRC_TRACK_F16 || SRC == SRC_TRACK_F32;
+    long trk_lo = 0, trk_hi = 0;
+    const bool trk_pre = kTrack && MAXI <= 2 && !a.trk_vector;
+    if (trk_pre) {
+      trk_lo = a.item_track[i0];
+      trk_hi = a.item_track[min(i1, (long)M - 1)];
+    }
     int pp[FB];
     bool ok[FB];
     Raw raw[FB];
@@ -326,9 +335,14 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
       long trk[FB];
 #pragma unroll
       for (int j = 0; j < FB; ++j) trk[j] = 0;
-      if constexpr (SRC == SRC_TRACK_F16 || SRC == SRC_TRACK_F32) {
+      if constexpr (kTrack) {
+        if (trk_pre) {
 #pragma unroll
-        for (int j = 0; j < FB; ++j) trk[j] = a.item_track[ii[j]];
+          for (int j = 0; j < FB; ++j) trk[j] = ii[j] == i0 ? trk_lo : trk_hi;
+        } else {
+#pragma unroll
+          for (int j = 0; j < FB; ++j) trk[j] = a.item_track[ii[j]];
+        }
       }
 #pragma unroll
       for (int j = 0; j < FB; ++j) raw[j] = slab_load<SRC, KC, LIN, LPL, POOLL>(a, ii[j], pp[j], c, trk[j]);
