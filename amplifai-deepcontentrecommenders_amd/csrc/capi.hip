@@ -1165,7 +1165,19 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     dcue_adam_args dense = *o.dense_split;
     dense.parts = DCUE_ADAM_DENSE;
     const long late = c.poff[DCUE_SEG_LATE];
-    TRY(wait_point(su, joined));
+    // the user stream waits for the two weight-gradient streams' tails itself (its own tail is in
+    // stream order) instead of for `joined`, which is one cross-queue hop further (wgrad stream 1 ->
+    // wgrad stream 0 -> here); DCUE_LATE_JOIN=hop restores the hop (A/B)
+    static const bool hop = [] {
+      const char* e = getenv("DCUE_LATE_JOIN");
+      return e && e[0] == 'h';
+    }();
+    if (hop) {
+      TRY(wait_point(su, joined));
+    } else {
+      TRY(wait_point(su, tail[2]));
+      TRY(wait_point(su, tail[3]));
+    }
     {
       ForkAfter fk(sp, su, o.late_done);
       TRY(launch_adam(m, &dense, c.poff, su, true, late, -1));
