@@ -484,21 +484,39 @@ __global__ __launch_bounds__(256) void k_bn0_grads_adam(const float* __restrict_
   critical_path_priority();
   __shared__ float rg[256], rb[256];
   const int c = blockIdx.x, t = threadIdx.x;
+  // the parameter, gradient and moment buffers never alias G / E (workspace): restrict lets every
+  // element's loads issue before the first element's stores (one memory round instead of one per
+  // element); the per-element arithmetic and the order of the dg / db sums are unchanged
+  float* __restrict__ P = a.p;
+  float* __restrict__ Mo = a.m;
+  float* __restrict__ V = a.v;
+  float* __restrict__ Gd = a.g;
+  // bn0's gamma / beta state of this channel, loaded up front (thread 0 steps them last)
+  float pg = 0.f, mg = 0.f, vg = 0.f, pb = 0.f, mb = 0.f, vb = 0.f;
+  if (t == 0 && a.o_g0 >= 0) {
+    pg = P[a.o_g0 + c]; mg = Mo[a.o_g0 + c]; vg = V[a.o_g0 + c];
+    pb = P[a.o_b0 + c]; mb = Mo[a.o_b0 + c]; vb = V[a.o_b0 + c];
+  }
   const Bn0Chan ch = bn0_chan(gamma0, beta0, mean0, invstd0, c);
   float dg = 0.f, db = 0.f;
-  for (int e = t; e < 4 * H; e += blockDim.x) {
-    const int o = e >> 2, k = e & 3;
-    const long wi = ((long)o * kMels + c) * 4 + k;
-    const long idx = a.o_w1 + wi;
-    float pp = a.p[idx];
-    const float gw = bn0_elem(G, E, H, ch, o, k, c, pp, dg, db);  // reads the pre-step weight
-    a.g[idx] = gw;
-    float mm = a.m[idx], vv = a.v[idx];
-    adam_elem(pp, gw, mm, vv, a.sc);
-    a.p[idx] = pp;
-    a.m[idx] = mm;
-    a.v[idx] = vv;
-    pack_store(a.seg1, wi, pp, a.wpack);
+  constexpr int kMaxIt = 4;  // 4H <= 1024 = 4 x 256 threads (H <= 256)
+#pragma unroll
+  for (int it = 0; it < kMaxIt; ++it) {
+    const int e = t + 256 * it;
+    if (e < 4 * H) {
+      const int o = e >> 2, k = e & 3;
+      const long wi = ((long)o * kMels + c) * 4 + k;
+      const long idx = a.o_w1 + wi;
+      float pp = P[idx];
+      const float gw = bn0_elem(G, E, H, ch, o, k, c, pp, dg, db);  // reads the pre-step weight
+      Gd[idx] = gw;
+      float mm = Mo[idx], vv = V[idx];
+      adam_elem(pp, gw, mm, vv, a.sc);
+      P[idx] = pp;
+      Mo[idx] = mm;
+      V[idx] = vv;
+      pack_store(a.seg1, wi, pp, a.wpack);
+    }
   }
   if (c == 0)
     for (int o = t; o < H; o += blockDim.x) {
@@ -524,8 +542,10 @@ __global__ __launch_bounds__(256) void k_bn0_grads_adam(const float* __restrict_
     dgamma0[c] = rg[0];
     dbeta0[c] = rb[0];
     if (a.o_g0 >= 0) {
-      adam_at(a, a.o_g0 + c, rg[0]);
-      adam_at(a, a.o_b0 + c, rb[0]);
+      adam_elem(pg, rg[0], mg, vg, a.sc);
+      adam_elem(pb, rb[0], mb, vb, a.sc);
+      P[a.o_g0 + c] = pg; Mo[a.o_g0 + c] = mg; V[a.o_g0 + c] = vg;
+      P[a.o_b0 + c] = pb; Mo[a.o_b0 + c] = mb; V[a.o_b0 + c] = vb;
     }
   }
 }
@@ -534,6 +554,7 @@ int launch_bn0_grads_adam(const float* G, const float* E, const float* gamma0, c
                           const float* mean0, const float* invstd0, int H, float* dgamma0, float* dbeta0,
                           const Bn0Adam& a, hipStream_t s) {
   const dcue_model* md = a.md;
+  if (H > 256) return DCUE_ERR_UNSUPPORTED;  // k_bn0_grads_adam: 4H elements over 4 x 256 threads
   if (!md->params || !md->grads || !md->exp_avg || !md->exp_avg_sq || a.args.grad_div > 1.0) return DCUE_ERR_INVALID;
   Bn0AdamDev d;
   d.p = md->params; d.m = md->exp_avg; d.v = md->exp_avg_sq; d.g = md->grads;

@@ -1021,6 +1021,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   hipEvent_t tail[4] = {};  // caller's stream, user stream, wgrad streams 0 and 1
   // layer 1 (the step's tail) follows the chain on the caller's stream, issued right away
   if (ev_x0) TRY(wait_point(s, ev_x0));
+  if (o.wait_inputs) TRY(wait_point(s, o.wait_inputs));
   TRY(issue_wgrad(1, s, 2, &tail[0]));
   HPROF("capi:22");
 

@@ -409,6 +409,8 @@ int join_user_stream(hipStream_t s);
 
 // ------------------------------------------------------------- step implementation (capi.hip)
 struct StepOpts {
+  hipEvent_t wait_inputs = nullptr;  // plans: the next step's prepared inputs; the caller's stream
+                                     // waits for it before the conv-1 weight gradient
   dcue_comm* sync_bn = nullptr;  // SyncBN: BatchNorm sums all-reduced over this communicator's ranks
   bool prologue_done = false;  // counts written + accumulators cleared by the prologue
   bool fuse_score = false;     // train forward also runs the hinge backward (k_score_fused)

@@ -48,6 +48,7 @@ struct dcue_plan {
   long launches = 0;
   hipEvent_t tails[2] = {};       // the last launched step's end (StepOpts::tails)
   hipEvent_t late_done = nullptr; // the last split step's late-segment Adam (StepOpts::dense_split)
+  hipEvent_t inputs_ready = nullptr;  // the next step's inputs (prologue + lookahead) on wgrad stream 0
   int pending_flush = -1;         // step whose rolling-flush slice the next launch issues
   hipStream_t last_stream = nullptr;  // the caller's stream of the last launch
   dcue_comm* comm = nullptr;      // data-parallel exchange between backward and Adam (plan_step)
@@ -143,6 +144,18 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   const bool prepared = p->ahead_items[cur] != nullptr;
   const bool ahead = prepared && items_src == p->ahead_items[cur];
   p->ahead_items[cur] = nullptr;
+  // The next step's inputs (slot nxt: prologue at this launch's start, lookahead after its score
+  // kernel) are made on wgrad stream 0, which split plans never join back into the caller's stream.
+  // The caller's stream waits for them inside this step's backward, just before the conv-1 weight
+  // gradient -- a point that already idles behind the layer-2 dgrad's bound fork event and is long
+  // after the lookahead finished -- so the next launch's conv 1 is ordered after them.
+  // DCUE_INPUTS_WAIT=start waits at the next launch's start instead, =0 not at all (A/B only).
+  static const int inputs_wait = [] {
+    const char* e = getenv("DCUE_INPUTS_WAIT");
+    return !e ? 1 : e[0] == '0' ? 0 : e[0] == 's' ? 2 : 1;
+  }();
+  if (p->inputs_ready && inputs_wait == 2) TRY(wait_point(s, p->inputs_ready));
+  p->inputs_ready = nullptr;
   StepOpts o;
   o.sync_bn = p->sync_bn ? p->comm : nullptr;
   o.prologue_done = true;
@@ -179,6 +192,11 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
     p->ahead_items[nxt] = p->next_items;
   }
   p->next_items = nullptr;
+  TRY(fork_point(sp, sa, &p->inputs_ready));  // slot nxt's inputs, for the next launch
+  if (inputs_wait == 1) {
+    o.wait_inputs = p->inputs_ready;
+    p->inputs_ready = nullptr;
+  }
   TRY(backward_impl(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, nullptr, p->cfg.emb_grad_scale, o, s));
   HPROF("plan:5");
   p->pending_flush = o.defer_flush_slice ? emb_adam->step : -1;
