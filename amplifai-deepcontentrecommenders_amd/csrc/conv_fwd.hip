@@ -1,7 +1,5 @@
 // Forward convolutions of the item tower (k_conv_rows MODE 0): the launch dispatch per layer and
 // input width. Kernel body: conv_rows.h.
-#include <cstdlib>
-
 #include "conv_rows.h"
 
 namespace dcue {
@@ -44,13 +42,7 @@ static int fwd_kc(int kc, int src, const RowsArgs& a, hipStream_t s) {
   }
 }
 
-int launch_conv_fwd(int layer, int kc, int src, const RowsArgs& a0, hipStream_t s) {
-  static const int trk_vec = [] {
-    const char* e = getenv("DCUE_ROWS_TRK_VEC");
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
-  RowsArgs a = a0;
-  a.trk_vector = trk_vec;
+int launch_conv_fwd(int layer, int kc, int src, const RowsArgs& a, hipStream_t s) {
   switch (layer) {
     case 1: return fwd_kc<1>(kc, src, a, s);
     case 2: return fwd_kc<2>(kc, src, a, s);

@@ -310,11 +310,11 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
     // the slab's row loads do not wait on a per-slot item_track load first; rows of one workgroup
     // span at most two items whenever ROWS <= R (MAXI == 2)
     constexpr bool kTrack = SRC == SRC_TRACK_F16 || SRC == SRC_TRACK_F32;
-    long trk_lo = 0, trk_hi = 0;
-    const bool trk_pre = kTrack && MAXI <= 2 && !a.trk_vector;
-    if (trk_pre) {
-      trk_lo = a.item_track[i0];
-      trk_hi = a.item_track[min(i1, (long)M - 1)];
+    constexpr bool trk_pre = kTrack && MAXI <= 2;  // compile-time: no second fill path (VGPRs)
+    int trk_lo = 0, trk_hi = 0;                    // uniform: SGPRs
+    if constexpr (trk_pre) {
+      trk_lo = __builtin_amdgcn_readfirstlane(a.item_track[i0]);
+      trk_hi = __builtin_amdgcn_readfirstlane(a.item_track[min(i1, (long)M - 1)]);
     }
     int pp[FB];
     bool ok[FB];
@@ -335,14 +335,12 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
       long trk[FB];
 #pragma unroll
       for (int j = 0; j < FB; ++j) trk[j] = 0;
-      if constexpr (kTrack) {
-        if (trk_pre) {
+      if constexpr (trk_pre) {
 #pragma unroll
-          for (int j = 0; j < FB; ++j) trk[j] = ii[j] == i0 ? trk_lo : trk_hi;
-        } else {
+        for (int j = 0; j < FB; ++j) trk[j] = ii[j] == i0 ? trk_lo : trk_hi;
+      } else if constexpr (kTrack) {
 #pragma unroll
-          for (int j = 0; j < FB; ++j) trk[j] = a.item_track[ii[j]];
-        }
+        for (int j = 0; j < FB; ++j) trk[j] = a.item_track[ii[j]];
       }
 #pragma unroll
       for (int j = 0; j < FB; ++j) raw[j] = slab_load<SRC, KC, LIN, LPL, POOLL>(a, ii[j], pp[j], c, trk[j]);

@@ -37,8 +37,6 @@ enum SlabSrc { SRC_TRACK_F16 = 0, SRC_TRACK_F32 = 1, SRC_ACT = 2, SRC_DZ = 3 };
 struct RowsArgs {
   const void* src;            // tracks [n_tracks][131][128] | y_{l-1} [M][Lin][KC] | g_l [M][Lp_l][KC]
   const int32_t* item_track;  // tracks only
-  int trk_vector;             // tracks: 1 = per-slot item_track loads (A/B: DCUE_ROWS_TRK_VEC=1); 0 = the
-                              // workgroup's (at most two) track ids loaded once, up front
   const float* in_mean;       // forward BN apply: (x - mean) * a + beta  (in_bn.acc == null)
   const float* in_a;
   const float* in_beta;
