@@ -681,7 +681,7 @@ int dcue_dcbr_step(const dcue_model* m, const dcue_batch* b, const dcue_tracks* 
   TRY(launch_item_counts(b, w.counts, s));
   TRY(item_forward(c, w, t, b->item_track, M, (double)M, true, w.counts, nullptr, s, false, false, false,
                    nullptr));
-  TRY(launch_mse_grad(w.f, target, M, m->dims.feature_dim, c.D, w.dfcopy, w.loss, s));
+  TRY(launch_mse_grad(w.f, target, M, m->dims.feature_dim, c.D, w.dfcopy, w.rowsum, w.loss, s));
   if (loss) DCUE_HIP_CHECK(hipMemcpyAsync(loss, w.loss, sizeof(float), hipMemcpyDeviceToDevice, s));
   StepOpts o;
   o.item_only = true;
@@ -706,6 +706,7 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   carve(&m->dims, b->n_rows, b->n_neg, b->n_items, ws, &w);
   if (o.acc) rebase_acc(&w, o.acc);
   if (o.counts) w.counts = const_cast<float*>(o.counts);
+  if (o.y1) w.y[1] = o.y1;
   // SyncBN: BatchNorm normalises over every rank's copies (same B, N on each rank)
   const double copies = (double)b->n_rows * (1 + b->n_neg) * (o.sync_bn ? comm_world(o.sync_bn) : 1);
   SidePool* sp = side_pool();
@@ -835,6 +836,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   carve(&m->dims, b->n_rows, b->n_neg, b->n_items, ws, &w);
   if (o.acc) rebase_acc(&w, o.acc);
   if (o.counts) w.counts = const_cast<float*>(o.counts);
+  if (o.y1) w.y[1] = o.y1;
   const int B = b->n_rows, N = b->n_neg, M = b->n_items;
   const int H = c.H, D = c.D, E = c.E;
   const double copies = (double)B * (1 + N) * (o.sync_bn ? comm_world(o.sync_bn) : 1);  // (SyncBN: global)

@@ -445,10 +445,17 @@ struct StepOpts {
   // DCBR regression (dcue_dcbr_step): the item tower only -- dfcopy already holds dL/df, no score
   // backward, no user tower, no embedding gradient
   bool item_only = false;
+  // split plans: conv 1's output y_1 per plan slot (step parity). The layer-2 weight gradient of step
+  // t reads y_1 on a side stream that the caller's stream does not join before step t+1's conv 1
+  // writes it; alternating buffers keep that write off the one being read (step t+2's conv 1 is
+  // ordered after it: its stream waited for step t's late Adam before step t+1's conv 2)
+  float* y1 = nullptr;
 };
 // DCBR's MSE head: loss = sum over [M][d] of (f - y)^2 / (M d) (rows of width ld, the first d
-// columns), df = 2 (f - y) / (M d) into dfcopy ([M][ld], zero past d); deterministic
-int launch_mse_grad(const float* f, const float* y, int M, int d, int ld, float* df, float* loss, hipStream_t s);
+// columns), df = 2 (f - y) / (M d) into dfcopy ([M][ld], zero past d); rowsq [M]: the per-row sums
+// (scratch); deterministic
+int launch_mse_grad(const float* f, const float* y, int M, int d, int ld, float* df, float* rowsq, float* loss,
+                    hipStream_t s);
 // A batch's model-independent item inputs, issued ahead of its step (plans): bn0's count-weighted
 // batch sums into the accumulator block `acc` (cleared, counts written, on the same stream before)
 // and bn0(x) zero-padded into xhat0 ([M+1][kXp][128] floats).

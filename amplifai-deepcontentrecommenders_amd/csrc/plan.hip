@@ -43,6 +43,7 @@ struct dcue_plan {
   // lookahead (dcue_plan_set_next): each slot's conv-1 wgrad X operand, the items its bn0 sums and
   // xhat0 were prepared from (nullptr: not prepared), and the announced next batch
   float* xh[2] = {};
+  float* y1[2] = {};  // conv 1's output per slot (split plans, StepOpts::y1)
   const int32_t* ahead_items[2] = {};
   const int32_t* next_items = nullptr;
   long launches = 0;
@@ -173,6 +174,7 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   o.tails = p->tails;
   o.wait_late = p->late_done;  // the previous split step's late Adam, before conv 2
   o.dense_split = dense_split;
+  if (dense_split) o.y1 = p->y1[cur];
   hipEvent_t late_done = nullptr;
   o.late_done = &late_done;
   // the previous step's rolling-flush slice runs after this step's user tower (StepOpts)
@@ -254,8 +256,10 @@ extern "C" int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const 
     // lookahead slots (plans of BatchNorm towers): xhat0 per slot
     const bool look = dcue::tower_has_bn(&m->dims);
     const size_t bxh = look ? al(sizeof(float) * (size_t)(M + 1) * dcue::kXp * dcue::kMels) : 0;
+    // conv 1's output per slot (StepOpts::y1): [M][33][H_s] floats
+    const size_t by1 = al(sizeof(float) * (size_t)M * dcue::layer_geom(1).lp * dcue::st_hidden(&m->dims));
     void* mem = nullptr;
-    DCUE_HIP_CHECK(hipMalloc(&mem, 2 * (bneg + bcnt + bacc + bxh + bptr + bidx) + bmt));
+    DCUE_HIP_CHECK(hipMalloc(&mem, 2 * (bneg + bcnt + bacc + bxh + bptr + bidx + by1) + bmt));
     dcue_plan* p = new dcue_plan;
     p->model = *m;
     p->batch = *b;
@@ -274,6 +278,7 @@ extern "C" int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const 
         p->copy_ptr[i] = (int32_t*)q; q += bptr;
         p->copy_idx[i] = (int32_t*)q; q += bidx;
       }
+      p->y1[i] = (float*)q; q += by1;
     }
     p->mt_ahead = (dcue_mt_state*)q;
     p->nacc = nacc;

@@ -1070,23 +1070,45 @@ extern "C" int dcue_build_catalogue_batch(const int64_t* pos_items, const int64_
 namespace dcue {
 
 // DCBR's MSE head (torch.nn.MSELoss, reduction 'mean', over the [M][d] item factors; van den Oord
-// et al. 2013): one workgroup; thread t sums rows t, t+256, ... in row order, then a fixed tree
-// over the 256 partials (deterministic). df = 2 (f - y) / (M d) at the same time.
-__global__ __launch_bounds__(256) void k_mse_grad(const float* __restrict__ f, const float* __restrict__ y, int M,
-                                                  int d, int ld, float* __restrict__ df, float* loss) {
-  __shared__ float part[256];
+// et al. 2013), in two launches:
+//   k_mse_rows  one wave per row (4 rows per 256-thread workgroup, a grid over the rows): lane l
+//               reads columns 4l..4l+3 (+256 ...) as float4 -- the row's 4*ld bytes in one coalesced
+//               pass -- writes df = 2 (f - y) / (M d) and the row's sum of squares (lane partials,
+//               then a fixed butterfly: deterministic) into rowsq[r]
+//   k_mse_loss  one workgroup: thread t sums rowsq[t], rowsq[t + 256], ... in order, then a fixed
+//               tree; loss = sum / (M d)
+// ld (the storage width) is a multiple of 4 (32, 64, 128 or 256).
+__global__ __launch_bounds__(256) void k_mse_rows(const float* __restrict__ f, const float* __restrict__ y, int M,
+                                                  int d, int ld, float* __restrict__ df, float* __restrict__ rowsq) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= M) return;
   const float scale = 2.f / ((float)M * (float)d);
   float acc = 0.f;
-  for (int r = threadIdx.x; r < M; r += blockDim.x) {
-    float rs = 0.f;
-    for (int c = 0; c < ld; ++c) {
-      const long e = (long)r * ld + c;
-      const float diff = c < d ? f[e] - y[e] : 0.f;
-      rs = fmaf(diff, diff, rs);
-      df[e] = diff * scale;
-    }
-    acc += rs;
+  for (int c = lane * 4; c < ld; c += 256) {
+    const long e = (long)r * ld + c;
+    const float4 fv = *reinterpret_cast<const float4*>(f + e);
+    const float4 yv = *reinterpret_cast<const float4*>(y + e);
+    float4 dv;
+    dv.x = c + 0 < d ? fv.x - yv.x : 0.f;
+    dv.y = c + 1 < d ? fv.y - yv.y : 0.f;
+    dv.z = c + 2 < d ? fv.z - yv.z : 0.f;
+    dv.w = c + 3 < d ? fv.w - yv.w : 0.f;
+    acc = fmaf(dv.x, dv.x, acc);
+    acc = fmaf(dv.y, dv.y, acc);
+    acc = fmaf(dv.z, dv.z, acc);
+    acc = fmaf(dv.w, dv.w, acc);
+    *reinterpret_cast<float4*>(df + e) = make_float4(dv.x * scale, dv.y * scale, dv.z * scale, dv.w * scale);
   }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (lane == 0) rowsq[r] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_mse_loss(const float* __restrict__ rowsq, int M, int d, float* loss) {
+  __shared__ float part[256];
+  float acc = 0.f;
+  for (int r = threadIdx.x; r < M; r += blockDim.x) acc += rowsq[r];
   part[threadIdx.x] = acc;
   __syncthreads();
   for (int off = 128; off > 0; off >>= 1) {
@@ -1096,9 +1118,12 @@ __global__ __launch_bounds__(256) void k_mse_grad(const float* __restrict__ f, c
   if (threadIdx.x == 0) *loss = part[0] / ((float)M * (float)d);
 }
 
-int launch_mse_grad(const float* f, const float* y, int M, int d, int ld, float* df, float* loss, hipStream_t s) {
-  if (M <= 0 || d <= 0 || d > ld) return DCUE_ERR_INVALID;
-  DCUE_LAUNCH(k_mse_grad, dim3(1), dim3(256), 0, s, f, y, M, d, ld, df, loss);
+int launch_mse_grad(const float* f, const float* y, int M, int d, int ld, float* df, float* rowsq, float* loss,
+                    hipStream_t s) {
+  if (M <= 0 || d <= 0 || d > ld || (ld & 3)) return DCUE_ERR_INVALID;
+  DCUE_LAUNCH(k_mse_rows, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, f, y, M, d, ld, df, rowsq);
+  DCUE_LAUNCH_CHECK();
+  DCUE_LAUNCH(k_mse_loss, dim3(1), dim3(256), 0, s, rowsq, M, d, loss);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }

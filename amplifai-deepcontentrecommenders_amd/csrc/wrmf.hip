@@ -211,12 +211,10 @@ int dcue_wrmf_half_step(float* solve, int64_t n_rows, const float* fixed, int64_
   DCUE_LAUNCH_CHECK();
   if (n_rows == 0) return DCUE_OK;
   const size_t lds = wrmf_solve_lds_bytes();
-  static bool attr = false;
-  if (!attr) {
-    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_wrmf_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds));
-    attr = true;
-  }
+  // the dynamic-LDS limit is a per-device function attribute: set it on every call (cheap), so a
+  // process that also solves on another device gets it there too
+  DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_wrmf_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds));
   const long grid = n_rows < 4096 ? n_rows : 4096;  // grid-stride over rows
   DCUE_LAUNCH(k_wrmf_solve, dim3((unsigned)grid), dim3(256), lds, s, solve, (long)n_rows, fixed, (int)dim, G,
               indptr, indices, values, alpha, lambda);

@@ -35,11 +35,13 @@ class DCBR:
         self.feature_dim = feature_dim
         self._target = None
 
-    def _padded_target(self, target):
-        M, d = target.shape
+    def _padded_target(self, target, M):
+        nat.require_gpu(target, "target")
+        if target.dim() != 2 or tuple(target.shape) != (M, self.feature_dim):
+            raise ValueError("target must be [%d, %d] (one row per item), got %s"
+                             % (M, self.feature_dim, tuple(target.shape)))
+        d = self.feature_dim
         ds = self.net._ds
-        if d != self.feature_dim:
-            raise ValueError("target must be [M, %d], got %s" % (self.feature_dim, tuple(target.shape)))
         if self._target is None or self._target.shape[0] < M:
             self._target = torch.zeros((M, ds), dtype=torch.float32, device=target.device)
         t = self._target[:M]
@@ -53,7 +55,7 @@ class DCBR:
         nat.require_gpu(item_track, "item_track")
         item_track = item_track.to(torch.int32).contiguous()
         M = item_track.shape[0]
-        tgt = self._padded_target(target.to(torch.float32))
+        tgt = self._padded_target(target.to(torch.float32), M)
         ws = net._workspace(M, 0, M)
         users = torch.zeros(M, dtype=torch.int64, device=item_track.device)
         batch = nat.Batch(M, 0, M, nat.LAYOUT_CATALOGUE, users.data_ptr(), item_track.data_ptr(), None)
@@ -75,6 +77,8 @@ class DCBR:
     @torch.no_grad()
     def predict(self, tracks, item_track):
         """Eval-mode item factors [M, feature_dim] (running BN statistics)."""
+        nat.require_gpu(tracks, "tracks")
+        nat.require_gpu(item_track, "item_track")
         self.net.eval()
         try:
             out = torch.empty((item_track.shape[0], self.net._ds), dtype=torch.float32, device=tracks.device)

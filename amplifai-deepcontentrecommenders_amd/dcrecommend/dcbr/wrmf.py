@@ -56,6 +56,10 @@ class WRMF:
     def half_step(self, solve, fixed, csr):
         """solve[r] <- the WRMF least-squares solution of row r with `fixed` held (in place)."""
         indptr, indices, values = csr
+        if indptr.numel() != solve.shape[0] + 1:
+            raise ValueError("the CSR has %d rows, the solved factors %d" % (indptr.numel() - 1, solve.shape[0]))
+        if solve.shape[1] != self.factors or fixed.shape[1] != self.factors:
+            raise ValueError("factor matrices must be [n, %d]" % self.factors)
         ws = self._workspace(fixed.shape[0])
         nat.check(nat.lib().dcue_wrmf_half_step(
             nat.ptr(solve), solve.shape[0], nat.ptr(fixed), fixed.shape[0], self.factors, nat.ptr(indptr),
@@ -74,9 +78,15 @@ class WRMF:
         v = None if values is None else torch.as_tensor(values, device=self.device)
         n_users = int(u.max()) + 1 if n_users is None else int(n_users)
         n_items = int(i.max()) + 1 if n_items is None else int(n_items)
+        # every index is a row of the other side's factors: the solver gathers them unchecked
+        if int(u.min()) < 0 or int(u.max()) >= n_users or int(i.min()) < 0 or int(i.max()) >= n_items:
+            raise ValueError("user / item indices must lie in [0, n_users) / [0, n_items)")
         self.by_user = device_csr(u, i, v, n_users)
         self.by_item = device_csr(i, u, v, n_items)
-        if self.user_factors is None or self.user_factors.shape[0] != n_users:
+        # (re)initialise unless both factor sets already have this problem's shapes (a refit with a
+        # different item count must not keep item factors the CSRs index past)
+        if (self.user_factors is None or self.user_factors.shape[0] != n_users
+                or self.item_factors.shape[0] != n_items):
             self.init_factors(n_users, n_items)
         for _ in range(self.iterations):
             self.half_step(self.user_factors, self.item_factors, self.by_user)
