@@ -67,14 +67,17 @@ __device__ __forceinline__ void window_bound(const AdamScalars* hs, int j0, int 
 }
 
 struct PackSeg {
-  long src, fwd, bwd, f16, f16b;  // floats: W in params; forward pack; dgrad pack (-1: none); split-f16
-                                 // forward and dgrad packs
+  long src, fwd, bwd, f16, f16b;  // floats: W in params; f32 forward pack (-1: none); dgrad pack (-1:
+                                 // none); split-f16 forward and dgrad packs
   int cout, cin, ks;
+  int cinp;  // the split-f16 forward pack's K per tap: cin rounded up to 32 (the text conv's word width)
 };
 struct PackArgs;
 PackArgs pack_args(const dcue_model* md, const int64_t* poff);
+// conv layers 1..5, then the text conv (text tower; an empty segment otherwise)
+constexpr int kPackSegs = 6;
 struct PackArgs {
-  PackSeg seg[5];
+  PackSeg seg[kPackSegs];
 };
 
 // Packed position of element e of conv segment sg (W[o][c][k], k fastest): the forward B operand
@@ -84,7 +87,7 @@ __device__ __forceinline__ void pack_store(const PackSeg& sg, long e, float w, f
   const long o = e / ((long)sg.cin * ks);
   const long rem = e - o * sg.cin * ks;
   const long cc = rem / ks, k = rem - cc * ks;
-  wpack[sg.fwd + (((k * (sg.cin / 4) + cc / 4) * sg.cout + o) * 4 + (cc & 3))] = w;
+  if (sg.fwd >= 0) wpack[sg.fwd + (((k * (sg.cin / 4) + cc / 4) * sg.cout + o) * 4 + (cc & 3))] = w;
   if (sg.bwd >= 0) {
     const long kr = sg.ks - 1 - k;
     wpack[sg.bwd + (((kr * (sg.cout / 4) + o / 4) * sg.cin + cc) * 4 + (o & 3))] = w;
@@ -93,7 +96,7 @@ __device__ __forceinline__ void pack_store(const PackSeg& sg, long e, float w, f
   const _Float16 hi = (_Float16)w;
   const _Float16 lo = (_Float16)(w - (float)hi);
   _Float16* h16 = reinterpret_cast<_Float16*>(wpack + sg.f16);
-  const long q = k * (sg.cin / 32) + cc / 32;
+  const long q = k * (sg.cinp / 32) + cc / 32;
   const long base = ((q * sg.cout + o) * 4 + (cc & 31) / 8) * 16 + (cc & 7);
   h16[base] = hi;
   h16[base + 8] = lo;
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(256) void k_adam_dense_pack(float* __restrict__ p, 
     st4(p + 4 * i, pp); st4(m + 4 * i, mm); st4(v + 4 * i, vv);
     const long e0 = 4 * i;
 #pragma unroll
-    for (int q = 0; q < 5; ++q) {
+    for (int q = 0; q < kPackSegs; ++q) {
       const PackSeg& sg = pa.seg[q];
       const long len = (long)sg.cout * sg.cin * sg.ks;
       if (e0 >= sg.src && e0 < sg.src + len) {
@@ -629,13 +632,23 @@ PackArgs pack_args(const dcue_model* md, const int64_t* poff) {
     sg.bwd = l >= 2 ? wl.conv_bwd[l] : -1;
     sg.f16 = wl.conv_f16[l];
     sg.f16b = l >= 2 ? wl.conv_f16b[l] : -1;
+    sg.cinp = sg.cin;
   }
+  PackSeg& tx = pa.seg[5];  // text.conv.weight [C_s][E_w][3]: the split-f16 forward operand only
+  tx.cin = md->dims.word_dim;
+  tx.cinp = st_word(&md->dims);
+  tx.cout = st_text(&md->dims);
+  tx.ks = 3;
+  tx.src = poff[28];
+  tx.fwd = tx.bwd = tx.f16b = -1;
+  tx.f16 = wl.text_f16;
+  if (!tower_text(&md->dims)) tx.cout = tx.cin = 0;  // empty: no element lies in it
   return pa;
 }
 
 int launch_pack(const dcue_model* md, const int64_t* poff, hipStream_t s) {
   const PackArgs pa = pack_args(md, poff);
-  DCUE_LAUNCH(k_pack, dim3(64, 5), dim3(256), 0, s, md->params, md->wpack, pa);
+  DCUE_LAUNCH(k_pack, dim3(64, kPackSegs), dim3(256), 0, s, md->params, md->wpack, pa);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }

@@ -167,6 +167,7 @@ struct TimepoolArgs {
   const float* beta[6];  // nullable (0)
   BnPublish p5;          // train + BN: BN_5 from its accumulators (this kernel is its first consumer)
   int M, H, HL, D;       // y_l channel stride H (storage); xfc block width HL (the reference's H)
+  int off5, ld;          // bn5(y5)'s first column and the row stride of xfc
   float* xfc;
 };
 
@@ -188,10 +189,10 @@ __global__ __launch_bounds__(256) void k_timepool(TimepoolArgs t) {
   }
   if (i == 0) bn_publish(t.p5, threadIdx.x);
   __syncthreads();
-  const int FI = 4 * HL + D;
-  for (int col = threadIdx.x; col < FI; col += blockDim.x) {
+  for (int cc = threadIdx.x; cc < 4 * HL + D; cc += blockDim.x) {
+    const int col = cc < 4 * HL ? cc : t.off5 + (cc - 4 * HL);
     float v;
-    if (col < 4 * HL) {
+    if (cc < 4 * HL) {
       const int l = col / HL + 1, c = col - (l - 1) * HL;
       const int lp = layer_geom(l).lp;
       const float mu = t.mean[l][c], sc = t.a[l][c], be = t.beta[l] ? t.beta[l][c] : 0.f;
@@ -200,16 +201,16 @@ __global__ __launch_bounds__(256) void k_timepool(TimepoolArgs t) {
       for (int q = 0; q < lp; ++q) acc += (yl[(long)q * H] - mu) * sc + be;
       v = acc / (float)lp;
     } else {
-      const int c = col - 4 * HL;
+      const int c = cc - 4 * HL;
       v = (t.y[5][(long)i * D + c] - m5[c]) * a5[c] + (t.beta[5] ? t.beta[5][c] : 0.f);
     }
-    t.xfc[(long)i * FI + col] = v;
+    t.xfc[(long)i * t.ld + col] = v;
   }
 }
 
 int launch_timepool(float* const* y, float* const* mean, float* const* a, const float* beta1, const float* beta2,
                     const float* beta3, const float* beta4, const float* beta5, const BnPublish& p5, int M, int H,
-                    int HL, int D, float* xfc, hipStream_t s) {
+                    int HL, int D, int off5, int ld, float* xfc, hipStream_t s) {
   if (D > 256) return DCUE_ERR_UNSUPPORTED;
   TimepoolArgs t = {};
   for (int l = 1; l <= 5; ++l) {
@@ -220,6 +221,7 @@ int launch_timepool(float* const* y, float* const* mean, float* const* a, const 
   t.beta[1] = beta1; t.beta[2] = beta2; t.beta[3] = beta3; t.beta[4] = beta4; t.beta[5] = beta5;
   t.p5 = p5;
   t.M = M; t.H = H; t.HL = HL; t.D = D;
+  t.off5 = off5; t.ld = ld;
   t.xfc = xfc;
   DCUE_LAUNCH(k_timepool, dim3((unsigned)M), dim3(256), 0, s, t);
   DCUE_LAUNCH_CHECK();

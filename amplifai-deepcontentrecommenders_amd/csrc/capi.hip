@@ -158,7 +158,11 @@ int check_dims(const dcue_dims* d) {
     return DCUE_ERR_INVALID;
   // any width up to 256 (run at its storage width, dcue_common.h); the user tower's E up to 1024
   if (d->conv_hidden > 256 || d->feature_dim > 256 || d->user_embdim > 1024) return DCUE_ERR_UNSUPPORTED;
-  if (d->tower < DCUE_TOWER_BN || d->tower > DCUE_TOWER_RESBN) return DCUE_ERR_INVALID;
+  if (d->tower < DCUE_TOWER_BN || d->tower > DCUE_TOWER_TEXT) return DCUE_ERR_INVALID;
+  if (d->tower == DCUE_TOWER_TEXT) {  // text.hip's limits: uint8 argmax positions, float4 word rows
+    if (d->text_dim <= 0 || d->word_dim <= 0 || d->text_len < 2 || d->text_pad < 0) return DCUE_ERR_INVALID;
+    if (d->text_dim > 256 || d->word_dim > 1024 || d->word_dim % 4 || d->text_len > 128) return DCUE_ERR_UNSUPPORTED;
+  }
   return DCUE_OK;
 }
 
@@ -183,6 +187,9 @@ void param_sizes(const dcue_dims* d, long* sz) {
   sz[s++] = E;
   sz[s++] = D * E;  // user_embd.linear2.weight
   sz[s++] = D;
+  const long CT = st_text(d);  // 0 outside the text tower: empty segments
+  sz[s++] = CT * d->word_dim * 3;  // text.conv.weight [C_s][E_w][3]
+  sz[s++] = CT;                    // text.conv.bias
 }
 
 void param_offsets(const dcue_dims* d, int64_t* off) {
@@ -249,8 +256,11 @@ struct Ws {
   // = 1, beta 0) and the BN parameter gradients go to a scratch sink
   float *ones, *zeros, *sink;
   // res towers: the fc input [M][4H + d] (time-pooled blocks 1-4, then block 5) and the gradient
-  // of the four time-pooled outputs [M][4H]
+  // of the four time-pooled outputs [M][4H]; text tower: the fc input [M][text_dim + d] (text
+  // features, then block 5) and the text features' gradient [M][C_s]
   float *xfc, *dtp;
+  uint8_t* tidx;  // text tower: [M][C_s] the max-over-positions argmax (255: no gradient)
+  float* twpart;  // text tower: the text conv's weight-gradient chunk partials
 };
 
 // the accumulator block's parts: [6][2][Cmax][2] forward sums, then the same for the backward
@@ -334,7 +344,8 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   w->S = ar.take<float>(5L * H);  // the five layer-1 bias partial sums E[5][H]
   w->xhat0 = ar.take<float>((long)(M + 1) * kXp * kMels);  // + a zero item
   w->dx1 = ar.take<float>((long)M * layer_geom(1).lp * H);
-  w->ones = w->zeros = w->sink = w->xfc = w->dtp = nullptr;
+  w->ones = w->zeros = w->sink = w->xfc = w->dtp = w->twpart = nullptr;
+  w->tidx = nullptr;
   if (!tower_has_bn(d)) {
     w->ones = ar.take<float>(w->cmax);
     w->zeros = ar.take<float>(w->cmax);
@@ -343,6 +354,13 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   if (tower_res(d)) {
     w->xfc = ar.take<float>((long)M * fc_in(d));
     w->dtp = ar.take<float>((long)M * 4 * d->conv_hidden);  // the fc input's block columns: reference H
+  }
+  if (tower_text(d)) {
+    const long CT = st_text(d);
+    w->xfc = ar.take<float>((long)M * fc_in(d));
+    w->dtp = ar.take<float>((long)M * CT);
+    w->tidx = ar.take<uint8_t>((long)M * CT);
+    w->twpart = ar.take<float>((long)text_wgrad_nchunk(M) * (CT * d->word_dim * 3 + CT));
   }
   return ar.used + 256;
 }
@@ -358,7 +376,10 @@ struct Ctx {
   int H, D, E;   // storage widths (H, d padded to 32/64/128/256) and E
   int HL;        // the reference's conv_hidden: column width of the res towers' time-pooled blocks
   bool bn, res;  // tower variant (dcue_dims.tower)
-  int FI;        // fc input width: D, or 4H + D in the res towers
+  bool text;     // the mixed audio + text tower (text.hip)
+  int FI;        // fc input width: D, 4H + D in the res towers, text_dim + D in the text tower
+  int off5;      // first fc-input column of bn5(y5)
+  int CT;        // text tower: storage channels of the text branch
   const float* P(int seg) const { return m->params + poff[seg]; }
   float* Gd(int seg) const { return m->grads + poff[seg]; }
   float* rmean(int l) const { return m->bn_stats + boff[2 * l]; }
@@ -383,6 +404,7 @@ float* Ctx::dbeta(const Ws& w, int l) const { return bn ? Gd(seg_bn_b(l)) : w.si
 int seg_conv_w(int l) { return 2 + 4 * (l - 1); }
 int seg_conv_b(int l) { return 3 + 4 * (l - 1); }
 constexpr int SEG_FC_W = 22, SEG_FC_B = 23, SEG_L1_W = 24, SEG_L1_B = 25, SEG_L2_W = 26, SEG_L2_B = 27;
+constexpr int SEG_TX_W = 28, SEG_TX_B = 29;
 
 int init_ctx(Ctx* c, const dcue_model* m) {
   int st = check_dims(&m->dims);
@@ -401,8 +423,26 @@ int init_ctx(Ctx* c, const dcue_model* m) {
   c->E = m->dims.user_embdim;
   c->bn = tower_has_bn(&m->dims);
   c->res = tower_res(&m->dims);
+  c->text = tower_text(&m->dims);
   c->FI = fc_in(&m->dims);
+  c->off5 = fc_off5(&m->dims);
+  c->CT = st_text(&m->dims);
+  if (c->text && (!m->words || m->n_words <= 0)) return DCUE_ERR_INVALID;
   return DCUE_OK;
+}
+
+// the text branch's operands (text tower); t->tokens must be set
+TextBranch text_branch(const Ctx& c, const dcue_tracks* t) {
+  const dcue_dims* d = &c.m->dims;
+  TextBranch tb;
+  tb.tokens = t->tokens;
+  tb.words = c.m->words;
+  tb.words_exp = c.m->words_exp;
+  tb.wpack16 = c.m->wpack + wpack_layout(d).text_f16;
+  tb.bias = c.P(SEG_TX_B);
+  tb.T = d->text_len; tb.E = d->word_dim; tb.EP = st_word(d); tb.C = c.CT; tb.Creal = d->text_dim;
+  tb.pad = d->text_pad;
+  return tb;
 }
 
 // Item tower forward. train: batch statistics (weighted by counts, accumulated exactly by the
@@ -413,6 +453,7 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
                  hipEvent_t before_l2 = nullptr, const std::function<int()>* after_l1 = nullptr,
                  dcue_comm* sync_bn = nullptr) {
   const dcue_model* m = c.m;
+  if (c.text && !t->tokens) return DCUE_ERR_INVALID;
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
   // one BN's finalize/publish record for its first consumer (train) -- bnacc.h
   auto bn_of = [&](int l) {
@@ -482,10 +523,12 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     if (sync) TRY(comm_allreduce_u64(sync_bn, bn_acc(w.bnacc, w.cmax, l), 4L * w.cmax, s));
     if (l == 1 && after_l1) TRY((*after_l1)());
   }
-  if (c.res) {  // fc on [tp1, tp2, tp3, tp4, bn5(y5)] (truedcuemel1dres.py:93-97)
+  if (c.res || c.text) {  // fc on [tp1, tp2, tp3, tp4, bn5(y5)] (truedcuemel1dres.py:93-97) or [s, bn5(y5)]
     TRY(launch_timepool(w.y, w.mean, w.a, c.bn ? c.P(seg_bn_b(1)) : nullptr, c.bn ? c.P(seg_bn_b(2)) : nullptr,
                         c.bn ? c.P(seg_bn_b(3)) : nullptr, c.bn ? c.P(seg_bn_b(4)) : nullptr,
-                        c.bn ? c.P(seg_bn_b(5)) : nullptr, bn_of(5), M, c.H, c.HL, c.D, w.xfc, s));
+                        c.bn ? c.P(seg_bn_b(5)) : nullptr, bn_of(5), M, c.H, c.res ? c.HL : 0, c.D, c.off5,
+                        c.FI, w.xfc, s));
+    if (c.text) TRY(launch_text_fwd(text_branch(c, t), item_track, M, w.xfc, c.FI, w.tidx, s));
     TGemmArgs g = {};
     g.M = M; g.N = c.D; g.K = c.FI;
     g.A = w.xfc; g.sam = c.FI; g.sak = 1;
@@ -888,23 +931,24 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
                      copies * kFrames, w.xhat0, sw[1]));
     TRY(fk.done());
   }
-  if (c.res) {  // df; then the fc input gradient split: g5 = df W[:, 4H:] (+ BN5's sums) and the
-                // time-pooled blocks' dtp = df W[:, :4H]
+  if (c.text && !t->tokens) return DCUE_ERR_INVALID;
+  if (c.res || c.text) {  // df; then the fc input gradient split: g5 = df W[:, off5:] (+ BN5's sums) and
+                          // the time-pooled blocks' dtp = df W[:, :4H] (text: the text features' df W[:, :C])
     TRY(launch_item_grad(w.dfcopy, b, D, w.df, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                          o.fuse_score ? w.rowsum : nullptr, w.loss, cptr, cidx, nullptr, grng_at(w, 6), s));
     TGemmArgs g = {};
     g.M = M; g.N = D; g.K = D;
     g.A = w.df; g.sam = D; g.sak = 1;
-    g.B = c.P(SEG_FC_W) + 4 * c.HL; g.sbk = c.FI; g.sbn = 1;
+    g.B = c.P(SEG_FC_W) + c.off5; g.sbk = c.FI; g.sbn = 1;
     g.C = w.g[5]; g.scm = D; g.scn = 1;
     g.colacc = bn_acc(w.bnbacc, w.cmax, 5); g.xy = w.y[5]; g.xmean = w.mean[5]; g.xinvstd = w.invstd[5];
     g.colmax = grng_at(w, 5);
     TRY(launch_tgemm(0, 0, g, s));
     g = TGemmArgs{};
-    g.M = M; g.N = 4 * c.HL; g.K = D;
+    g.M = M; g.N = c.off5; g.K = D;
     g.A = w.df; g.sam = D; g.sak = 1;
     g.B = c.P(SEG_FC_W); g.sbk = c.FI; g.sbn = 1;
-    g.C = w.dtp; g.scm = 4 * c.HL; g.scn = 1;
+    g.C = w.dtp; g.scm = c.text ? c.CT : 4 * c.HL; g.scn = 1;
     ForkAfter fk(sp, s, &ev_layer[5]);
     TRY(launch_tgemm(0, 0, g, s));
     TRY(fk.done());
@@ -1027,8 +1071,8 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   TRY(issue_wgrad(1, s, 2, &tail[0]));
   HPROF("capi:22");
 
-  if (c.res) {  // fc weight gradient of the res towers: dW[n][k] = sum_m df[m][n] xfc[m][k], db = sum df
-    // over the concatenated fc input (the other towers' fc rides in the layer 3-5 launch, below)
+  if (c.res || c.text) {  // fc weight gradient of the res / text towers: dW[n][k] = sum_m df[m][n] xfc[m][k],
+    // db = sum df over the concatenated fc input (the other towers' fc rides in the layer 3-5 launch, below)
     TRY(wait_point(sw[1], ev_layer[5]));
     HPROF("capi:23");
     TGemmArgs g = {};
@@ -1039,6 +1083,10 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     g.B = w.xfc; g.sbk = c.FI; g.sbn = 1;
     TRY(launch_tgemm(0, 0, g, sw[1]));
     HPROF("capi:24");
+    // the text conv's weight and bias gradients (the max routes each gradient to one position)
+    if (c.text)
+      TRY(launch_text_wgrad(text_branch(c, t), b->item_track, M, w.dtp, w.tidx, w.twpart, c.Gd(SEG_TX_W),
+                            c.Gd(SEG_TX_B), sw[1]));
   }
   // (wgrad of layer l reads g_l, which dgrad l+1 produced: ev_layer[l]) layers 5..3 in one launch
   // on wgrad stream 0 once dgrad 4 is done (beside dgrad 3-2); layer 2 on wgrad stream 1 (behind
@@ -1092,7 +1140,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     return fk.done();
   };
   if (fork_once()) ev_layer[3] = ev_layer[2];
-  TRY(issue_multi(3, 5, !c.res, sw[0], ev_layer[3], &tail[2]));
+  TRY(issue_multi(3, 5, !c.res && !c.text, sw[0], ev_layer[3], &tail[2]));
   TRY(issue_multi(2, 2, false, sw[1], ev_layer[2], &tail[3]));
   HPROF("capi:25");
   // user tower (userembedding.py:33-44 backward), the compact embedding rows, and -- when the step

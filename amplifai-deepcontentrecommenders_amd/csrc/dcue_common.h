@@ -66,8 +66,10 @@ constexpr int kWave = 64;
 
 // Tower variant (dcue_dims.tower): BatchNorm present, time-pooled skips into the fc
 __host__ __device__ inline bool tower_has_bn(const dcue_dims* d) {
-  return d->tower == DCUE_TOWER_BN || d->tower == DCUE_TOWER_RESBN;
+  return d->tower == DCUE_TOWER_BN || d->tower == DCUE_TOWER_RESBN || d->tower == DCUE_TOWER_TEXT;
 }
+// the mixed audio + text item tower (BASELINE config 4, text.hip)
+__host__ __device__ inline bool tower_text(const dcue_dims* d) { return d->tower == DCUE_TOWER_TEXT; }
 __host__ __device__ inline bool tower_res(const dcue_dims* d) {
   return d->tower == DCUE_TOWER_RES || d->tower == DCUE_TOWER_RESBN;
 }
@@ -84,8 +86,23 @@ __host__ __device__ inline int st_feature(const dcue_dims* d) { return storage_w
 // fc input width: d, or 4H + d with the four time-pooled block outputs (truedcuemel1dres.py:63-64).
 // The time-pooled blocks keep the reference's H columns each (the fc weight is then a view of its
 // padded [d_s][4H + d_s] segment); only the block-5 part is padded.
+// The text tower's fc input is [s ; bn5(y5)]: the text features' text_dim columns (unpadded, as the
+// res towers' pooled blocks) before the d_s audio columns.
 __host__ __device__ inline int fc_in(const dcue_dims* d) {
-  return tower_res(d) ? 4 * d->conv_hidden + st_feature(d) : st_feature(d);
+  return tower_res(d) ? 4 * d->conv_hidden + st_feature(d)
+       : tower_text(d) ? d->text_dim + st_feature(d) : st_feature(d);
+}
+// columns of the fc input before bn5(y5): the res towers' pooled blocks or the text features
+__host__ __device__ inline int fc_off5(const dcue_dims* d) {
+  return tower_res(d) ? 4 * d->conv_hidden : tower_text(d) ? d->text_dim : 0;
+}
+// text branch storage widths: channels C_s (64, 128 or 256: the forward's 64-channel column tiles)
+// and the word width rounded up to the 32-channel MFMA k-step (the split-f16 weight pack's K)
+__host__ __device__ inline int st_text(const dcue_dims* d) {
+  return !tower_text(d) ? 0 : d->text_dim <= 64 ? 64 : storage_width(d->text_dim);
+}
+__host__ __device__ inline int st_word(const dcue_dims* d) {
+  return !tower_text(d) ? 0 : (d->word_dim + 31) / 32 * 32;
 }
 
 // Per-layer geometry of the default item tower (truedcuemel1dbn.py:25-61).

@@ -206,8 +206,12 @@ int launch_bn_eval(int C, const float* gamma, const float* rmean, const float* r
 // [k * cin/32 + c/32][cout][(c % 32) / 8][hi, lo][c % 8] -- one float slot per weight;
 // conv_f16b[l] (l >= 2): the dgrad B operand the same way, K = (reversed tap, layer-l channel o),
 // columns = layer l-1's channels: [(ks-1-k) * cout/32 + o/32][cin][(o % 32) / 8][hi, lo][o % 8]
+// text_f16: the text conv's split-f16 B operand (text.hip), K = (tap, word channel padded to st_word),
+// [k * EWs/32 + c/32][C_s][(c % 32) / 8][hi, lo][c % 8] halves (zero past word_dim: the caller
+// zero-fills wpack once); -1 outside the text tower
 struct WpackLayout {
   long conv_fwd[6], conv_bwd[6], conv_f16[6], conv_f16b[6];
+  long text_f16;
   long total;
 };
 inline WpackLayout wpack_layout(const dcue_dims* dm) {
@@ -225,6 +229,11 @@ inline WpackLayout wpack_layout(const dcue_dims* dm) {
     n += e;
     w.conv_f16b[l] = l >= 2 ? n : -1;  // cout too (H or d_s)
     if (l >= 2) n += e;
+  }
+  w.text_f16 = -1;
+  if (tower_text(dm)) {
+    w.text_f16 = n;
+    n += 3L * st_word(dm) * st_text(dm);
   }
   w.total = n;
   return w;
@@ -316,9 +325,30 @@ int launch_bn_identity(float* const* mean, float* const* invstd, float* const* a
 // res towers: xfc[i] = [mean_t bn_1(y_1), ..., mean_t bn_4(y_4), bn_5(y_5)] (truedcuemel1dres.py:93-97);
 // p5 (train, BN): BN_5 finalized from its accumulators here (block 0 publishes it)
 // H: storage width of y_1..y_4; HL: the reference's H, the column width of each block in xfc
+// text tower (HL = 0): only bn5(y5), at columns [off5, off5 + D) of rows ld wide (res: off5 = 4 HL,
+// ld = 4 HL + D)
 int launch_timepool(float* const* y, float* const* mean, float* const* a, const float* beta1, const float* beta2,
                     const float* beta3, const float* beta4, const float* beta5, const BnPublish& p5, int M, int H,
-                    int HL, int D, float* xfc, hipStream_t s);
+                    int HL, int D, int off5, int ld, float* xfc, hipStream_t s);
+// Text branch of the mixed item tower (text.hip): the token table, frozen word vectors, the text conv's
+// split-f16 weight pack and bias, widths (C = storage channels, Creal = the reference's text_dim)
+struct TextBranch {
+  const int32_t* tokens;  // [n_tracks][T]
+  const float* words;     // [V][E]
+  int words_exp;
+  const float* wpack16;   // WpackLayout::text_f16
+  const float* bias;      // [C]
+  int T, E, EP, C, Creal, pad;
+};
+// s[i][o] (o < Creal) -> out[i * ld + o] (the fc input's text columns), argmax -> tidx [M][C]
+int launch_text_fwd(const TextBranch& tb, const int32_t* item_track, int M, float* out, long ld, uint8_t* tidx,
+                    hipStream_t s);
+// chunk partials of the text conv's weight / bias gradients (wpart: text_wgrad_nchunk(M) x (C E 3 + C)
+// floats) and their chunk-ordered sums into dW [C][E][3], db [C]; dt [M][C] = dL/ds (read where
+// tidx != 255)
+int text_wgrad_nchunk(int M);
+int launch_text_wgrad(const TextBranch& tb, const int32_t* item_track, int M, const float* dt, const uint8_t* tidx,
+                      float* wpart, float* dW, float* db, hipStream_t s);
 // SGD / Ranger over the dense buffer and the user table (optim.hip)
 int launch_opt(const dcue_model* m, const dcue_opt_args* a, const dcue_opt_state* st, long n_dense,
                hipStream_t s);

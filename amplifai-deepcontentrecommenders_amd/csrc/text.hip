@@ -1,0 +1,351 @@
+// Text branch of the mixed audio + text item tower (BASELINE config 4: "DCUE + language-model-pretrained
+// text tower (bio/lyrics), d=256, mixed audio+text item encoder") -- gfx950.
+//
+// The reference never published this path: its text item set imports a `WordEmbeddings` module
+// that does not exist (reference datasets/dcuelmitemset.py:8), so only the data contract is pinned
+// by the reference: one sentence of token ids per track, BOS + sentence + EOS, cut to
+// max_sentence_length + 1 and right-padded with PAD (dcuelmitemset.py:40-56). The encoder is this
+// build's choice, parity-unpinned against the reference and pinned against
+// oracle/text_oracle.py (torch-CPU):
+//
+//   e[i][t]   = words[tokens[track_i][t]]                    frozen word vectors [V][E] (the
+//                                                            LM-pretrained part, caller supplied)
+//   z[i][t]   = Conv1d(E -> C, k = 3, pad = 1)(e[i])[t]      text.conv.{weight [C][E][3], bias [C]}
+//   s[i][o]   = relu(max over t with tokens[t] != PAD of z[i][t][o])
+//   f[i]      = fc([s[i] ; bn5(y5[i])])                      conv.fc: Linear(C + d -> d)
+//
+// Kernels:
+//   k_text_fwd     the conv as a row-GEMM on split-f16 MFMA (v_mfma_f32_16x16x32_f16, three per f32
+//                  product as the audio forwards, conv_rows.h): a workgroup owns IPW items x 64 output
+//                  channels, 4 waves x 16 channels over all of the items' T positions; the items' word
+//                  vectors are gathered 32 channels at a time into LDS (hi/lo halves, register-
+//                  prefetched one chunk ahead), the B operand (the packed split-f16 text weights) comes
+//                  from L2. The epilogue adds the bias, takes the masked max over t in registers and
+//                  across the wave's four row groups, applies the ReLU and writes s into the fc input
+//                  xfc[:, :C] plus the argmax position (255: no gradient) for the backward.
+//   k_text_wgrad   dW[o][c][k] = sum_i g[i][o] e[i][t*(i,o) + k - 1][c] -- the max routes each (item,
+//                  channel) gradient to one position, so the weight gradient is a gathered sum, not a
+//                  dense GEMM over positions (3 x C x E FMAs per item instead of 3 x C x E x T). A
+//                  workgroup owns 32 word channels x all C output channels over a chunk of items: the
+//                  chunk's word-vector slices staged in LDS once, 3 x C/8 fp32 accumulators per thread,
+//                  exact fp32 FMAs in item order (deterministic).
+//   k_text_wreduce the chunk partials in chunk order, and db[o] = sum_i g[i][o] in item order.
+#include "dcue_internal.h"
+
+namespace dcue {
+
+typedef _Float16 t16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kTextKC = 32;        // word channels per K chunk (one MFMA k-step)
+constexpr int kTextRowH = 72;      // LDS row: [hi x 32][lo x 32][pad x 8] halves = 144 B (conflict-free)
+constexpr int kTextNoGrad = 255;   // argmax code: no gradient (ReLU off, or no valid position)
+
+struct TextFwdArgs {
+  const int32_t* tokens;      // [n_tracks][T]
+  const int32_t* item_track;  // [M]
+  const float* words;         // [V][E]
+  float xscale, inv_xscale;   // 2^words_exp and its inverse (exact): the word values' split-f16 scale
+  const uint4* wpack;         // [3 * EP/32][C][4][hi x 8, lo x 8] halves (uint4 = 8 halves)
+  const float* bias;          // [C]
+  int M, T, E, EP, C, Creal, pad;
+  float* out;                 // s[i][o] at out[i * ld + o], o < Creal
+  long ld;
+  uint8_t* tidx;              // [M][C]
+};
+
+// Split f32 -> (hi, lo) fp16 halves: hi = fp16(v), lo = fp16(v - hi) (v - hi is exact in f32).
+__device__ __forceinline__ void split4(const float4& v, _Float16* hi, _Float16* lo) {
+  const float a[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const _Float16 h = (_Float16)a[q];
+    hi[q] = h;
+    lo[q] = (_Float16)(a[q] - (float)h);
+  }
+}
+
+template <int TB, int IPW>
+__global__ __launch_bounds__(256) void k_text_fwd(TextFwdArgs a) {
+  constexpr int TP = TB * 16;       // conv positions computed per item (T rounded up)
+  constexpr int RS = TP + 2;        // staged rows per item: token positions -1 .. TP
+  constexpr int NROW = IPW * RS;
+  constexpr int PASSES = (NROW * (kTextKC / 4) + 255) / 256;
+  __shared__ __attribute__((aligned(16))) _Float16 xs[2][NROW * kTextRowH];
+  __shared__ int32_t tok[NROW];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int i0 = blockIdx.x * IPW;
+  const int o0 = blockIdx.y * 64 + wv * 16;
+  // the items' token rows (row r' = position r' - 1; -1 outside the sentence or the batch)
+  for (int r = tid; r < NROW; r += 256) {
+    const int s = r / RS, t = r - s * RS - 1;
+    const int i = i0 + s;
+    tok[r] = (i < a.M && t >= 0 && t < a.T) ? a.tokens[(long)a.item_track[i] * a.T + t] : -1;
+  }
+  __syncthreads();
+  const int nchunk = a.EP / kTextKC;
+  float4 pre[PASSES];
+  auto load_chunk = [&](int cb) {
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p) {
+      const int e = tid + 256 * p;
+      const int r = e >> 3, q = e & 7;
+      const int c = cb * kTextKC + 4 * q;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < NROW && c < a.E) {
+        const int tk = tok[r];
+        if (tk >= 0) v = *reinterpret_cast<const float4*>(a.words + (long)tk * a.E + c);
+      }
+      pre[p] = v;
+    }
+  };
+  auto store_chunk = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p) {
+      const int e = tid + 256 * p;
+      const int r = e >> 3, q = e & 7;
+      if (r < NROW) {
+        float4 v = pre[p];
+        v.x *= a.xscale; v.y *= a.xscale; v.z *= a.xscale; v.w *= a.xscale;  // exact (power of two)
+        _Float16 hi[4], lo[4];
+        split4(v, hi, lo);
+        _Float16* row = &xs[buf][r * kTextRowH];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          row[4 * q + j] = hi[j];
+          row[kTextKC + 4 * q + j] = lo[j];
+        }
+      }
+    }
+  };
+  f32x4 acc[IPW][TB];
+#pragma unroll
+  for (int s = 0; s < IPW; ++s)
+#pragma unroll
+    for (int b = 0; b < TB; ++b) acc[s][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  load_chunk(0);
+  store_chunk(0);
+  __syncthreads();
+  const int col = o0 + (lane & 15), g = lane >> 4;
+  for (int cb = 0; cb < nchunk; ++cb) {
+    if (cb + 1 < nchunk) load_chunk(cb + 1);  // in flight under this chunk's MFMAs
+    const _Float16* xb = xs[cb & 1];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const long q = (long)k * nchunk + cb;
+      const uint4* wp = a.wpack + ((q * a.C + col) * 4 + g) * 2;
+      const uint4 wh = wp[0], wl = wp[1];
+      const t16x8 bh = *reinterpret_cast<const t16x8*>(&wh);
+      const t16x8 bl = *reinterpret_cast<const t16x8*>(&wl);
+#pragma unroll
+      for (int s = 0; s < IPW; ++s)
+#pragma unroll
+        for (int b = 0; b < TB; ++b) {
+          // conv row t = 16b + (lane & 15) reads token t + k - 1 = staged row t + k
+          const _Float16* rp = xb + (s * RS + 16 * b + (lane & 15) + k) * kTextRowH + 8 * g;
+          const t16x8 ah = *reinterpret_cast<const t16x8*>(rp);
+          const t16x8 al = *reinterpret_cast<const t16x8*>(rp + kTextKC);
+          acc[s][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc[s][b], 0, 0, 0);
+          acc[s][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc[s][b], 0, 0, 0);
+          acc[s][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[s][b], 0, 0, 0);
+        }
+    }
+    if (cb + 1 < nchunk) store_chunk((cb + 1) & 1);
+    __syncthreads();
+  }
+  // epilogue: bias, masked first-max over the positions, ReLU
+  const float bo = a.bias[col];
+#pragma unroll
+  for (int s = 0; s < IPW; ++s) {
+    const int i = i0 + s;
+    float best = -INFINITY;
+    int bi = kTextNoGrad;
+#pragma unroll
+    for (int b = 0; b < TB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int t = 16 * b + 4 * g + j;
+        const int tk = tok[s * RS + t + 1];
+        const float v = acc[s][b][j] * a.inv_xscale + bo;
+        if (t < a.T && tk >= 0 && tk != a.pad && v > best) {
+          best = v;
+          bi = t;
+        }
+      }
+    // the four row groups of this column: larger value, the earlier position on a tie
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {
+      const float ob = __shfl_xor(best, off, 64);
+      const int oi = __shfl_xor(bi, off, 64);
+      if (ob > best || (ob == best && oi < bi)) {
+        best = ob;
+        bi = oi;
+      }
+    }
+    if (g == 0 && i < a.M) {
+      const bool on = best > 0.f;
+      if (col < a.Creal) a.out[(long)i * a.ld + col] = on ? best : 0.f;
+      a.tidx[(long)i * a.C + col] = (uint8_t)(on ? bi : kTextNoGrad);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------- weight gradient
+struct TextWgradArgs {
+  const int32_t* tokens;
+  const int32_t* item_track;
+  const float* words;
+  const float* dt;       // [M][C] dL/ds (before the ReLU / max routing)
+  const uint8_t* tidx;   // [M][C]
+  int M, T, E, C;
+  int items_per_chunk;
+  float* wpart;          // [nchunk][C * E * 3 + C]: the chunk's dW ([C][E][3]) and db partials
+};
+
+constexpr int kTextWIB = 4;  // items staged per pass
+
+// thread t: word channel c = 32 * blockIdx.x + (t & 31), output channels o = (t >> 5) + 8 j, j < C/8
+template <int OPT>
+__global__ __launch_bounds__(256) void k_text_wgrad(TextWgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float tw_lds[];
+  const int RS = a.T + 2;  // staged rows: positions -1 .. T
+  float* xsl = tw_lds;                                  // [kTextWIB][RS][33]
+  float* gs = xsl + kTextWIB * RS * 33;                 // [kTextWIB][C]
+  int* ts = reinterpret_cast<int*>(gs + kTextWIB * a.C);  // [kTextWIB][C]
+  const int tid = threadIdx.x, cl = tid & 31, og = tid >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  const int ib = blockIdx.y * a.items_per_chunk;
+  const int ie = min(a.M, ib + a.items_per_chunk);
+  float acc[OPT][3], bacc[OPT];
+#pragma unroll
+  for (int j = 0; j < OPT; ++j) acc[j][0] = acc[j][1] = acc[j][2] = bacc[j] = 0.f;
+  for (int i0 = ib; i0 < ie; i0 += kTextWIB) {
+    const int ni = min(kTextWIB, ie - i0);
+    __syncthreads();  // the previous pass's readers are done
+    for (int e = tid; e < ni * RS * 32; e += 256) {
+      const int s = e / (RS * 32), rem = e - s * RS * 32;
+      const int r = rem >> 5, cc = rem & 31;
+      const int t = r - 1, ch = blockIdx.x * 32 + cc;
+      float v = 0.f;
+      if (t >= 0 && t < a.T && ch < a.E) {
+        const int tk = a.tokens[(long)a.item_track[i0 + s] * a.T + t];
+        v = a.words[(long)tk * a.E + ch];
+      }
+      xsl[(s * RS + r) * 33 + cc] = v;
+    }
+    for (int e = tid; e < ni * a.C; e += 256) {
+      const int s = e / a.C, o = e - s * a.C;
+      const int ti = a.tidx[(long)(i0 + s) * a.C + o];
+      ts[e] = ti;
+      gs[e] = ti == kTextNoGrad ? 0.f : a.dt[(long)(i0 + s) * a.C + o];
+    }
+    __syncthreads();
+    for (int s = 0; s < ni; ++s)
+#pragma unroll
+      for (int j = 0; j < OPT; ++j) {
+        const int o = og + 8 * j;
+        const int ti = ts[s * a.C + o];
+        if (ti != kTextNoGrad) {  // uniform over the 32 lanes of one o
+          const float gv = gs[s * a.C + o];
+          bacc[j] += gv;  // db's partial, in item order
+          const float* xr = xsl + (s * RS + ti) * 33 + cl;  // staged row ti + k = position ti + k - 1
+          acc[j][0] = fmaf(gv, xr[0], acc[j][0]);
+          acc[j][1] = fmaf(gv, xr[33], acc[j][1]);
+          acc[j][2] = fmaf(gv, xr[66], acc[j][2]);
+        }
+      }
+  }
+  const long n = (long)a.C * a.E * 3;
+  float* wp = a.wpart + (long)blockIdx.y * (n + a.C);  // chunk block: dW partial, then db partial
+  if (c < a.E) {
+#pragma unroll
+    for (int j = 0; j < OPT; ++j) {
+      const int o = og + 8 * j;
+      float* d = wp + ((long)o * a.E + c) * 3;
+      d[0] = acc[j][0];
+      d[1] = acc[j][1];
+      d[2] = acc[j][2];
+    }
+  }
+  if (blockIdx.x == 0 && cl == 0) {
+#pragma unroll
+    for (int j = 0; j < OPT; ++j) wp[n + og + 8 * j] = bacc[j];
+  }
+}
+
+// the chunk partials [nchunk][n + C] (dW then db per chunk) summed in chunk order
+__global__ __launch_bounds__(256) void k_text_wreduce(const float* __restrict__ wpart, int nchunk, long n, int C,
+                                                      float* __restrict__ dW, float* __restrict__ db) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n + C) return;
+  float s = 0.f;
+  for (int z = 0; z < nchunk; ++z) s += wpart[(long)z * (n + C) + e];
+  if (e < n)
+    dW[e] = s;
+  else
+    db[e - n] = s;
+}
+
+template <int TB, int IPW>
+static int launch_text_fwd_t(const TextFwdArgs& a, hipStream_t s) {
+  dim3 grid((unsigned)((a.M + IPW - 1) / IPW), (unsigned)(a.C / 64));
+  DCUE_LAUNCH((k_text_fwd<TB, IPW>), grid, dim3(256), 0, s, a);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+int launch_text_fwd(const TextBranch& tb, const int32_t* item_track, int M, float* out, long ld, uint8_t* tidx,
+                    hipStream_t s) {
+  TextFwdArgs a;
+  a.tokens = tb.tokens; a.item_track = item_track; a.words = tb.words;
+  a.xscale = ldexpf(1.f, tb.words_exp); a.inv_xscale = ldexpf(1.f, -tb.words_exp);
+  a.wpack = reinterpret_cast<const uint4*>(tb.wpack16);
+  a.bias = tb.bias;
+  a.M = M; a.T = tb.T; a.E = tb.E; a.EP = tb.EP; a.C = tb.C; a.Creal = tb.Creal; a.pad = tb.pad;
+  a.out = out; a.ld = ld; a.tidx = tidx;
+  if (tb.C % 64 || tb.T < 1 || tb.T > 128 || tb.E % 4 || tb.EP % kTextKC || tb.EP < tb.E) return DCUE_ERR_INVALID;
+  if (tb.T <= 16) return launch_text_fwd_t<1, 8>(a, s);
+  if (tb.T <= 32) return launch_text_fwd_t<2, 4>(a, s);
+  if (tb.T <= 64) return launch_text_fwd_t<4, 2>(a, s);
+  return launch_text_fwd_t<8, 1>(a, s);
+}
+
+int text_wgrad_nchunk(int M) {
+  const int n = M / 8;
+  return n < 1 ? 1 : (n > 32 ? 32 : n);
+}
+
+template <int OPT>
+static int launch_text_wgrad_t(const TextWgradArgs& a, int nchunk, hipStream_t s) {
+  const size_t lds = sizeof(float) * ((size_t)kTextWIB * (a.T + 2) * 33 + (size_t)kTextWIB * a.C) +
+                     sizeof(int) * (size_t)kTextWIB * a.C;
+  dim3 grid((unsigned)((a.E + 31) / 32), (unsigned)nchunk);
+  DCUE_LAUNCH((k_text_wgrad<OPT>), grid, dim3(256), lds, s, a);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+int launch_text_wgrad(const TextBranch& tb, const int32_t* item_track, int M, const float* dt, const uint8_t* tidx,
+                      float* wpart, float* dW, float* db, hipStream_t s) {
+  TextWgradArgs a;
+  a.tokens = tb.tokens; a.item_track = item_track; a.words = tb.words;
+  a.dt = dt; a.tidx = tidx;
+  a.M = M; a.T = tb.T; a.E = tb.E; a.C = tb.C;
+  const int nchunk = text_wgrad_nchunk(M);
+  a.items_per_chunk = (M + nchunk - 1) / nchunk;
+  a.wpart = wpart;
+  int st;
+  switch (tb.C) {
+    case 64: st = launch_text_wgrad_t<8>(a, nchunk, s); break;
+    case 128: st = launch_text_wgrad_t<16>(a, nchunk, s); break;
+    case 256: st = launch_text_wgrad_t<32>(a, nchunk, s); break;
+    default: return DCUE_ERR_INVALID;
+  }
+  if (st) return st;
+  const long n = (long)tb.C * tb.E * 3;
+  DCUE_LAUNCH(k_text_wreduce, dim3((unsigned)((n + tb.C + 255) / 256)), dim3(256), 0, s, wpart, nchunk, n, tb.C,
+              dW, db);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+}  // namespace dcue

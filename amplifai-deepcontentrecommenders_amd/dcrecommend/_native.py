@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("DCUE_HIP_LIB", os.path.join(_PKG_ROOT, "lib", "libdcu
 N_MELS = 128
 N_FRAMES = 131
 N_BN = 6
-N_DENSE_SEGMENTS = 28
+N_DENSE_SEGMENTS = 30
 SEG_LATE = 6  # DCUE_SEG_LATE: bn0, conv layer 1, bn1 come first in the flat layout
 ERR_UNSUPPORTED = 2
 LAYOUT_CATALOGUE = 0
@@ -29,20 +29,24 @@ DENSE_NAMES = (["conv.bn0.weight", "conv.bn0.bias"]
                + [n for l in range(1, 6) for n in ("conv.layer%d.weight" % l, "conv.layer%d.bias" % l,
                                                    "conv.bn%d.weight" % l, "conv.bn%d.bias" % l)]
                + ["conv.fc.weight", "conv.fc.bias", "user_embd.linear1.weight",
-                  "user_embd.linear1.bias", "user_embd.linear2.weight", "user_embd.linear2.bias"])
+                  "user_embd.linear1.bias", "user_embd.linear2.weight", "user_embd.linear2.bias"]
+               # the mixed audio + text tower's text conv (BASELINE config 4; empty segments otherwise)
+               + ["text.conv.weight", "text.conv.bias"])
 
 
 class Dims(ctypes.Structure):
     _fields_ = [("conv_hidden", ctypes.c_int32), ("feature_dim", ctypes.c_int32),
                 ("user_embdim", ctypes.c_int32), ("tower", ctypes.c_int32),
-                ("n_users", ctypes.c_int64)]
+                ("n_users", ctypes.c_int64), ("text_dim", ctypes.c_int32), ("word_dim", ctypes.c_int32),
+                ("text_len", ctypes.c_int32), ("text_pad", ctypes.c_int32)]
 
 
 class Model(ctypes.Structure):
     _fields_ = [("dims", Dims)] + [(n, ctypes.c_void_p) for n in (
         "params", "grads", "exp_avg", "exp_avg_sq", "emb", "emb_exp_avg", "emb_exp_avg_sq",
         "emb_grad", "emb_slot", "bn_stats", "bn_batches", "wpack", "emb_rows", "emb_step", "emb_log")] + [
-        ("emb_log_cap", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+        ("emb_log_cap", ctypes.c_int32), ("reserved", ctypes.c_int32), ("words", ctypes.c_void_p),
+        ("n_words", ctypes.c_int64), ("words_exp", ctypes.c_int32), ("reserved2", ctypes.c_int32)]
 
 
 class Batch(ctypes.Structure):
@@ -53,7 +57,7 @@ class Batch(ctypes.Structure):
 
 class Tracks(ctypes.Structure):
     _fields_ = [("data", ctypes.c_void_p), ("n_tracks", ctypes.c_int64), ("dtype", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("reserved", ctypes.c_int32), ("tokens", ctypes.c_void_p)]
 
 
 class AdamArgs(ctypes.Structure):
@@ -98,7 +102,7 @@ class PlanConfig(ctypes.Structure):
 
 MT_STATE_BYTES = 624 * 4 + 16
 MAX_LOG_CAP = 256
-ABI_VERSION = 12
+ABI_VERSION = 13
 COMM_F32, COMM_U64 = 0, 1  # dcue_host_allreduce_fn dtypes
 HOST_ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32)
 RANK_SPLIT, RANK_SINGLE = 0, 1
@@ -216,11 +220,30 @@ def require_gpu(t, name):
         raise RuntimeError("%s must be a GPU tensor (the DCUE path runs only on the MI355X)" % name)
 
 
-TOWERS = {"truedcuemel1dbn": 0, "truedcuemel1d": 1, "truedcuemel1dres": 2, "truedcuemel1dresbn": 3}
+TOWERS = {"truedcuemel1dbn": 0, "truedcuemel1d": 1, "truedcuemel1dres": 2, "truedcuemel1dresbn": 3,
+          "truedcuemel1dbntext": 4}
+TEXT_TOWER = "truedcuemel1dbntext"
 
 
-def make_dims(conv_hidden, feature_dim, user_embdim, n_users, model_type="truedcuemel1dbn"):
-    return Dims(conv_hidden, feature_dim, user_embdim, TOWERS[model_type], n_users)
+def make_dims(conv_hidden, feature_dim, user_embdim, n_users, model_type="truedcuemel1dbn", text=None):
+    """text = (text_dim, word_dim, text_len, pad_idx) for the text tower (BASELINE config 4)."""
+    t = tuple(text) if model_type == TEXT_TOWER else (0, 0, 0, 0)
+    return Dims(conv_hidden, feature_dim, user_embdim, TOWERS[model_type], n_users, *t)
+
+
+def text_storage(text_dim):
+    """The text branch's storage channels (64, 128 or 256: text.hip's column tiles)."""
+    return 64 if text_dim <= 64 else 128 if text_dim <= 128 else 256
+
+
+def words_exponent(words):
+    """dcue_model.words_exp: the power of two that puts max |word value| in [2^13, 2^15) before the
+    kernels' fp16 hi/lo split (include/dcue.h)."""
+    import math
+    m = float(words.detach().abs().max()) if words.numel() else 0.0
+    if not m > 0.0 or not math.isfinite(m):
+        return 0
+    return max(-60, min(60, 14 - math.frexp(m)[1]))
 
 
 def storage_dims(dims):
@@ -236,13 +259,17 @@ def segment_shapes(dims):
     sd = storage_dims(dims)
     Hs, Ds, E, H = sd.conv_hidden, sd.feature_dim, sd.user_embdim, dims.conv_hidden
     res = dims.tower in (TOWERS["truedcuemel1dres"], TOWERS["truedcuemel1dresbn"])
+    text = dims.tower == TOWERS[TEXT_TOWER]
+    CTs = text_storage(dims.text_dim) if text else 0
     cin = [N_MELS, Hs, Hs, Hs, Hs]
     cout = [Hs, Hs, Hs, Hs, Ds]
     ks = [4, 4, 4, 2, 1]
     shapes = [(N_MELS,), (N_MELS,)]
     for l in range(5):
         shapes += [(cout[l], cin[l], ks[l]), (cout[l],), (cout[l],), (cout[l],)]
-    shapes += [(Ds, 4 * H + Ds if res else Ds), (Ds,), (E, E), (E,), (Ds, E), (Ds,)]
+    fi = 4 * H + Ds if res else dims.text_dim + Ds if text else Ds
+    shapes += [(Ds, fi), (Ds,), (E, E), (E,), (Ds, E), (Ds,)]
+    shapes += [(CTs, dims.word_dim if text else 0, 3), (CTs,)]
     return shapes
 
 

@@ -17,7 +17,13 @@ from torch import nn
 from dcrecommend import _native as nat
 
 REFERENCE_TYPES = ("truedcuemel1d", "truedcuemel1dres", "truedcuemel1dbn", "truedcuemel1dresbn")
-SUPPORTED_TYPES = REFERENCE_TYPES
+# BASELINE config 4: the mixed audio + text item encoder (no reference code: the reference's text item
+# set imports a WordEmbeddings module it never published, datasets/dcuelmitemset.py:8)
+TEXT_TYPE = nat.TEXT_TOWER
+SUPPORTED_TYPES = REFERENCE_TYPES + (TEXT_TYPE,)
+# the text tower's extra dict_args keys and their defaults (config 4: d = 256; 300-d word vectors;
+# one sentence of at most 63 tokens + BOS/EOS per track, dcuelmitemset.py:40-56)
+TEXT_DEFAULTS = {"text_dim": 256, "word_dim": 300, "text_len": 64, "n_words": 20000, "pad_idx": 0}
 
 # conv stack shared by the towers, truedcuemel1dbn.py:25-61: (kernel, padding) per layer
 _CONV = ((4, 2), (4, 2), (4, 2), (2, 1), (1, 0))
@@ -28,9 +34,9 @@ class _ItemTower(nn.Module):
     four towers DCUENet wires (dcue/dcue.py:49-59): truedcuemel1dbn (default), truedcuemel1d (no
     BatchNorm), truedcuemel1dres / truedcuemel1dresbn (time-pooled skips into fc(4H + d -> d))."""
 
-    def __init__(self, feature_dim, conv_hidden, model_type="truedcuemel1dbn"):
+    def __init__(self, feature_dim, conv_hidden, model_type="truedcuemel1dbn", text_dim=0):
         super().__init__()
-        bn = model_type in ("truedcuemel1dbn", "truedcuemel1dresbn")
+        bn = model_type in ("truedcuemel1dbn", "truedcuemel1dresbn", TEXT_TYPE)
         res = model_type in ("truedcuemel1dres", "truedcuemel1dresbn")
         chans = [nat.N_MELS] + [conv_hidden] * 4 + [feature_dim]
         # construction order = RNG consumption order of the reference constructors (BN draws nothing)
@@ -40,7 +46,9 @@ class _ItemTower(nn.Module):
             if l < 5:
                 k, pad = _CONV[l]
                 self.add_module("layer%d" % (l + 1), nn.Conv1d(chans[l], chans[l + 1], k, 1, pad, bias=True))
-        self.fc = nn.Linear(4 * conv_hidden + feature_dim if res else feature_dim, feature_dim)
+        # res towers: fc(4H + d -> d); the text tower: fc(text_dim + d -> d) over [text features ; audio]
+        fi = 4 * conv_hidden + feature_dim if res else text_dim + feature_dim if model_type == TEXT_TYPE else feature_dim
+        self.fc = nn.Linear(fi, feature_dim)
         for l in range(1, 6):
             nn.init.kaiming_uniform_(getattr(self, "layer%d" % l).weight, nonlinearity="relu")
         nn.init.xavier_uniform_(self.fc.weight)
@@ -54,6 +62,21 @@ class _ItemTower(nn.Module):
         if net is None:
             raise RuntimeError("item tower is only callable through its DCUENet")
         return net.item_features(X)
+
+
+class _TextTower(nn.Module):
+    """The text branch of the mixed item tower (BASELINE config 4; csrc/text.hip): frozen word vectors
+    `embeddings` [n_words, word_dim] -- the language-model-pretrained part, supplied by the caller
+    through load_state_dict (never fetched; random N(0, 1) until then) -- and `conv`, a
+    Conv1d(word_dim -> text_dim, kernel 3, padding 1) whose outputs are max-pooled over each sentence's
+    non-PAD positions and passed through a ReLU."""
+
+    def __init__(self, n_words, word_dim, text_dim):
+        super().__init__()
+        self.embeddings = nn.Embedding(n_words, word_dim)
+        self.embeddings.weight.requires_grad_(False)
+        self.conv = nn.Conv1d(word_dim, text_dim, 3, 1, 1, bias=True)
+        nn.init.kaiming_uniform_(self.conv.weight, nonlinearity="relu")
 
 
 class _UserTower(nn.Module):
@@ -78,21 +101,19 @@ class _StepFunction(torch.autograd.Function):
     """Train-mode forward through the C ABI; backward feeds dL/dscores to dcue_train_backward."""
 
     @staticmethod
-    def forward(ctx, anchor, net, u, X, N):
-        scores, uf, f, _ = net._native_forward(u, X, N, train=True, margin=0.0)
+    def forward(ctx, anchor, net, u, X, N, tokens=None):
+        scores, uf, f, _ = net._native_forward(u, X, N, train=True, margin=0.0, tokens=tokens)
         ctx.net = net
-        ctx.batch_key = (u, X, N)
         ctx.mark_non_differentiable(uf, f)
         return scores, uf, f
 
     @staticmethod
     def backward(ctx, dscores, duf, df):
-        u, X, N = ctx.batch_key
         net = ctx.net
         if duf is not None and bool(torch.any(duf != 0)) or df is not None and bool(torch.any(df != 0)):
             raise RuntimeError("DCUENet backward supports gradients through the scores only")
         net._native_backward(dscores.contiguous().float())
-        return None, None, None, None, None
+        return None, None, None, None, None, None
 
 
 class DCUENet(nn.Module):
@@ -105,10 +126,17 @@ class DCUENet(nn.Module):
         self.user_embdim = dict_args["user_embdim"]
         self.user_count = dict_args["user_count"]
         self.model_type = dict_args["model_type"]
-        if self.model_type not in REFERENCE_TYPES:
+        if self.model_type not in SUPPORTED_TYPES:
             raise ValueError("{} is not a recognized model type!".format(self.model_type))
-        self.conv = _ItemTower(self.feature_dim, self.conv_hidden, self.model_type)
+        self.is_text = self.model_type == TEXT_TYPE
+        if self.is_text:
+            for k, v in TEXT_DEFAULTS.items():
+                setattr(self, k, int(dict_args.get(k, v)))
+        self.conv = _ItemTower(self.feature_dim, self.conv_hidden, self.model_type,
+                               self.text_dim if self.is_text else 0)
         self.user_embd = _UserTower(self.user_count, self.user_embdim, self.feature_dim)
+        if self.is_text:
+            self.text = _TextTower(self.n_words, self.word_dim, self.text_dim)
         self.sim = nn.CosineSimilarity(dim=1)
         self.conv._owner = weakref.ref(self)
         self.user_embd._owner = weakref.ref(self)
@@ -131,7 +159,7 @@ class DCUENet(nn.Module):
     def _flatten(self, device):
         """Move every dense parameter/buffer into the flat buffers the C ABI addresses."""
         dims = nat.make_dims(self.conv_hidden, self.feature_dim, self.user_embdim, self.user_count,
-                             self.model_type)
+                             self.model_type, self._text_dims())
         poff = nat.param_layout(dims)
         boff = nat.bn_layout(dims)
         shapes = nat.segment_shapes(dims)
@@ -163,14 +191,27 @@ class DCUENet(nn.Module):
         emb = self.user_embd.embeddings.weight
         emb._dcue_owner = weakref.ref(self)
         slot = torch.full((max(self.user_count, 1),), -1, dtype=torch.int32, device=device)
-        wpack = torch.empty(nat.wpack_floats(dims), dtype=torch.float32, device=device)
+        # zero-filled once: the text weights' split-f16 pack has zero K padding past word_dim
+        wpack = torch.zeros(nat.wpack_floats(dims), dtype=torch.float32, device=device)
         self._flat = dict(dims=dims, poff=poff, boff=boff, shapes=shapes, P=P, G=G, stats=stats, nbt=nbt, slot=slot,
                           wpack=wpack, emb_grad=torch.zeros(0, device=device),
                           emb_rows=torch.zeros(0, dtype=torch.int64, device=device), m=None, v=None,
                           em=None, ev=None)
         self._ws = None
         self._ds = nat.storage_dims(dims).feature_dim
+        self._words_key = None
         self._repack()
+
+    def _text_dims(self):
+        return (self.text_dim, self.word_dim, self.text_len, self.pad_idx) if self.is_text else None
+
+    def _words_exp(self):
+        """dcue_model.words_exp of the (frozen) word vectors, recomputed when they are rewritten."""
+        w = self.text.embeddings.weight
+        key = (w.data_ptr(), w._version)
+        if self._words_key != key:
+            self._words_exp_v, self._words_key = nat.words_exponent(w), key
+        return self._words_exp_v
 
     def _repack(self):
         """Refresh the MFMA-packed conv weights from the flat parameters."""
@@ -181,7 +222,8 @@ class DCUENet(nn.Module):
     def _conv_versions(self):
         # each nn.Parameter keeps its own version counter (setting .data does not share P's), so the
         # conv weights' counters are what records a host-side write to them
-        return tuple(getattr(self.conv, "layer%d" % l).weight._version for l in range(1, 6))
+        v = tuple(getattr(self.conv, "layer%d" % l).weight._version for l in range(1, 6))
+        return v + ((self.text.conv.weight._version,) if self.is_text else ())
 
     def _sync_plan(self):
         """Order torch's current stream after the last plan step's side-stream Adam work
@@ -216,6 +258,10 @@ class DCUENet(nn.Module):
         m.emb_slot = fl["slot"].data_ptr()
         m.bn_stats, m.bn_batches, m.wpack = fl["stats"].data_ptr(), fl["nbt"].data_ptr(), fl["wpack"].data_ptr()
         m.emb_rows = fl["emb_rows"].data_ptr() if fl["emb_rows"].numel() else None
+        if self.is_text:
+            w = self.text.embeddings.weight
+            nat.require_gpu(w, "text.embeddings.weight")
+            m.words, m.n_words, m.words_exp = w.data_ptr(), w.shape[0], self._words_exp()
         opt = self._deferred_opt() if getattr(self, "_deferred_opt", None) is not None else None
         if opt is not None and adam_state is None:
             adam_state = opt._adam_state()  # the deferred user-table Adam replays inside forwards
@@ -272,9 +318,24 @@ class DCUENet(nn.Module):
                   "dcue_transpose_spectrograms")
         return out
 
+    def _tracks(self, tracks, tokens=None):
+        """dcue_tracks of an HBM track table (+ the text tower's [n_tracks, text_len] token table)."""
+        tr = nat.Tracks(tracks.data_ptr(), tracks.shape[0], 0 if tracks.dtype == torch.float16 else 1, 0)
+        if self.is_text:
+            if tokens is None:
+                raise ValueError("the text tower needs each track's token ids (tokens [n_tracks, %d])" % self.text_len)
+            nat.require_gpu(tokens, "tokens")
+            if tokens.dtype != torch.int32 or tuple(tokens.shape) != (tracks.shape[0], self.text_len) \
+                    or not tokens.is_contiguous():
+                raise ValueError("tokens must be a contiguous int32 [%d, %d] tensor, got %s %s"
+                                 % (tracks.shape[0], self.text_len, tokens.dtype, tuple(tokens.shape)))
+            tr.tokens = tokens.data_ptr()
+        return tr
+
     def native_forward(self, users, tracks, item_track, n_neg, layout, neg_item=None, train=True,
-                       margin=0.2, copy_outputs=True):
-        """Forward over an HBM-resident track table. Returns (scores, user_feat, item_feat, loss).
+                       margin=0.2, copy_outputs=True, tokens=None):
+        """Forward over an HBM-resident track table (text tower: and its token table). Returns
+        (scores, user_feat, item_feat, loss).
 
         copy_outputs=False returns views into the workspace (no copy; overwritten by the next call)."""
         fl = self._require_device()
@@ -283,12 +344,12 @@ class DCUENet(nn.Module):
         ws = self._workspace(B, n_neg, M)
         batch = nat.Batch(B, n_neg, M, layout, users.data_ptr(), item_track.data_ptr(),
                           neg_item.data_ptr() if neg_item is not None else None)
-        tr = nat.Tracks(tracks.data_ptr(), tracks.shape[0], 0 if tracks.dtype == torch.float16 else 1, 0)
+        tr = self._tracks(tracks, tokens)
         model = self._model_struct()
         nat.check(nat.lib().dcue_forward(ctypes.byref(model), ctypes.byref(batch), ctypes.byref(tr),
                                          nat.ptr(ws), ws.numel(), int(bool(train)), float(margin),
                                          None, None, None, None, nat.stream_handle()), "dcue_forward")
-        self._last = (users, tracks, item_track, n_neg, layout, neg_item)
+        self._last = (users, tracks, item_track, n_neg, layout, neg_item, tokens)
         key = (B, n_neg, M)
         if fl.get("out_key") != key:
             fl["out_off"], fl["out_key"] = nat.workspace_outputs(fl["dims"], B, n_neg, M), key
@@ -305,12 +366,12 @@ class DCUENet(nn.Module):
         """Backward of the last train-mode native_forward: writes the flat grads + compact
         embedding rows (emb_grad/emb_slot)."""
         fl = self._require_device()
-        users, tracks, item_track, n_neg, layout, neg_item = self._last
+        users, tracks, item_track, n_neg, layout, neg_item, tokens = self._last
         B, M = users.shape[0], item_track.shape[0]
         ws = self._workspace(B, n_neg, M)
         batch = nat.Batch(B, n_neg, M, layout, users.data_ptr(), item_track.data_ptr(),
                           neg_item.data_ptr() if neg_item is not None else None)
-        tr = nat.Tracks(tracks.data_ptr(), tracks.shape[0], 0 if tracks.dtype == torch.float16 else 1, 0)
+        tr = self._tracks(tracks, tokens)
         model = self._model_struct()
         nat.check(nat.lib().dcue_train_backward(ctypes.byref(model), ctypes.byref(batch), ctypes.byref(tr),
                                                 nat.ptr(ws), ws.numel(), nat.ptr(dscores),
@@ -341,19 +402,31 @@ class DCUENet(nn.Module):
         dense[users[first].long()] = rows[slots[first].long()]
         return dense
 
-    def _native_forward(self, u, X, N, train, margin):
+    def _token_table(self, tokens, M):
+        if not self.is_text:
+            return None
+        if tokens is None:
+            raise ValueError("the text tower's forward needs the items' token ids")
+        nat.require_gpu(tokens, "tokens")
+        t = tokens.reshape(M, -1).to(torch.int32).contiguous()
+        if t.shape[1] != self.text_len:
+            raise ValueError("token rows must hold text_len = %d ids, got %d" % (self.text_len, t.shape[1]))
+        return t
+
+    def _native_forward(self, u, X, N, train, margin, tokens=None):
         B = X.shape[0] // (1 + N)
         table = self._spectro_table(X)
-        self._table_keepalive = table
+        tok = self._token_table(tokens, X.shape[0])
+        self._table_keepalive = (table, tok)
         item_track = torch.arange(X.shape[0], dtype=torch.int32, device=X.device)
         return self.native_forward(u.to(torch.int64).contiguous(), table, item_track, N,
-                                   nat.LAYOUT_CATALOGUE, None, train=train, margin=margin)
+                                   nat.LAYOUT_CATALOGUE, None, train=train, margin=margin, tokens=tok)
 
     def _native_backward(self, dscores):
         self.native_backward(dscores)
 
     # --------------------------------------------------------------------- reference API
-    def item_features(self, X):
+    def item_features(self, X, tokens=None):
         fl = self._require_device()
         table = self._spectro_table(X)
         M = table.shape[0]
@@ -361,7 +434,7 @@ class DCUENet(nn.Module):
         if self.training:
             raise NotImplementedError("DCUENet.conv(X) in train mode is only reachable through forward()")
         ws = self._workspace(1, 0, M)
-        tr = nat.Tracks(table.data_ptr(), M, 1, 0)
+        tr = self._tracks(table, self._token_table(tokens, M))
         item_track = torch.arange(M, dtype=torch.int32, device=table.device)
         nat.check(nat.lib().dcue_item_tower_eval(ctypes.byref(self._model_struct()), ctypes.byref(tr),
                                                  nat.ptr(item_track), M, nat.ptr(ws), ws.numel(),
@@ -380,8 +453,9 @@ class DCUENet(nn.Module):
                   "dcue_user_tower")
         return out[:, :self.feature_dim].reshape(*shape, self.feature_dim)
 
-    def forward(self, u, pos, neg=None):
-        """dcue/dcue.py:70-108 -> (scores [B,N], user feats [B,d], pos feats [B,d], neg feats [B,N,d])."""
+    def forward(self, u, pos, neg=None, pos_text=None, neg_text=None):
+        """dcue/dcue.py:70-108 -> (scores [B,N], user feats [B,d], pos feats [B,d], neg feats [B,N,d]).
+        The text tower (config 4) also takes the items' token ids: pos_text [B, T], neg_text [B, N, T]."""
         self._require_device()
         if neg is None:
             # reference quirk (dcue/dcue.py:101-108): neg_featvects is never bound on this path
@@ -390,8 +464,13 @@ class DCUENet(nn.Module):
         X = torch.empty((B * (1 + N), nat.N_MELS, nat.N_FRAMES), dtype=torch.float32, device=pos.device)
         X[:B].copy_(pos)
         X[B:].copy_(neg.reshape(B * N, nat.N_MELS, nat.N_FRAMES))
+        tok = None
+        if self.is_text:
+            if pos_text is None or neg_text is None:
+                raise ValueError("the text tower's forward needs pos_text [B, T] and neg_text [B, N, T]")
+            tok = torch.cat([pos_text.reshape(B, -1), neg_text.reshape(B * N, -1)], 0)
         if self.training and torch.is_grad_enabled():
-            scores, uf, f = _StepFunction.apply(self._anchor, self, u, X, N)
+            scores, uf, f = _StepFunction.apply(self._anchor, self, u, X, N, tok)
         else:
-            scores, uf, f, _ = self._native_forward(u, X, N, train=self.training, margin=0.0)
+            scores, uf, f, _ = self._native_forward(u, X, N, train=self.training, margin=0.0, tokens=tok)
         return scores, uf, f[:B], f[B:].reshape(B, N, self.feature_dim)

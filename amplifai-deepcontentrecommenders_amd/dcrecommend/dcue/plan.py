@@ -22,16 +22,17 @@ from dcrecommend.check import StepCheck, enabled_by_env
 class TrainPlan:
 
     def __init__(self, net, tracks, n_rows, n_neg, mt_state=None, item_track=None, margin=0.2,
-                 emb_grad_scale=1.0, graph=False, optimizer=None, check=None):
+                 emb_grad_scale=1.0, graph=False, optimizer=None, check=None, tokens=None):
         """tracks: HBM track table [n_tracks][131][128] (fp16/fp32). In-batch mode (mt_state given):
         positives are items 0..B-1 of item_track, negatives drawn in-graph. Otherwise item_track holds
-        B*(1+N) items in catalogue order (datasets/dcuedataset.py:242-250)."""
+        B*(1+N) items in catalogue order (datasets/dcuedataset.py:242-250). tokens: the text tower's
+        [n_tracks][text_len] int32 token table (BASELINE config 4), bound like `tracks`."""
         fl = net._require_device()
         dev = fl["P"].device
         B, N = int(n_rows), int(n_neg)
         self.inbatch = mt_state is not None
         M = B if self.inbatch else B * (1 + N)
-        self.net, self.tracks = net, tracks
+        self.net, self.tracks, self.tokens = net, tracks, tokens
         self.users = torch.zeros(B, dtype=torch.int64, device=dev)
         self.item_track = torch.zeros(M, dtype=torch.int32, device=dev)
         if item_track is not None:
@@ -52,7 +53,7 @@ class TrainPlan:
         batch = nat.Batch(B, N, M, nat.LAYOUT_GATHER if self.inbatch else nat.LAYOUT_CATALOGUE,
                           self.users.data_ptr(), self.item_track.data_ptr(),
                           self.neg_item.data_ptr() if self.inbatch else None)
-        tr = nat.Tracks(tracks.data_ptr(), tracks.shape[0], 0 if tracks.dtype == torch.float16 else 1, 0)
+        tr = net._tracks(tracks, tokens)
         flags = (nat.PLAN_SAMPLE_INBATCH if self.inbatch else 0) | (nat.PLAN_GRAPH if graph else 0)
         cfg = nat.PlanConfig(flags, float(margin),
                              float(emb_grad_scale), 0, mt_state.data_ptr() if self.inbatch else None)

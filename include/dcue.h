@@ -27,12 +27,14 @@
 extern "C" {
 #endif
 
-#define DCUE_ABI_VERSION 12
+#define DCUE_ABI_VERSION 13
 #define DCUE_N_MELS 128
 #define DCUE_N_FRAMES 131
 #define DCUE_N_BN 6
-/* dense parameter segments, reference order (DCUENet.named_parameters(), minus the embedding) */
-#define DCUE_N_DENSE_SEGMENTS 28
+/* dense parameter segments, reference order (DCUENet.named_parameters(), minus the embeddings):
+ * 28 of the reference's DCUENet, then the text tower's text.conv.{weight, bias} (empty in the
+ * audio-only towers) */
+#define DCUE_N_DENSE_SEGMENTS 30
 
 typedef enum {
   DCUE_OK = 0,
@@ -48,11 +50,20 @@ typedef enum {
  *   RES   truedcuemel1dres   no BN; each block's output also time-averaged (AvgPool1d over all its
  *                            positions) and concatenated with the last block: fc(4H + d -> d)
  *   RESBN truedcuemel1dresbn RES with the BN tower's BatchNorms (the averages taken after each BN)
- * In the towers without BN the segments of the BN parameters are empty (dcue_param_layout). */
+ * In the towers without BN the segments of the BN parameters are empty (dcue_param_layout).
+ *   TEXT  BASELINE config 4, the mixed audio + text item encoder (no reference code: the reference's
+ *         text item set, datasets/dcuelmitemset.py:8, imports a WordEmbeddings module it never
+ *         published; this build's encoder): the BN tower's audio stack plus a text
+ *         branch over each track's sentence of token ids (BOS + sentence + EOS, PAD-padded to
+ *         text_len, dcuelmitemset.py:40-56): frozen word vectors [n_words][word_dim] (the
+ *         LM-pretrained part, caller supplied: dcue_model.words), Conv1d(word_dim -> text_dim, k 3,
+ *         pad 1), max over the non-PAD positions, ReLU; f = fc([s ; bn5(y5)]) with fc(text_dim + d -> d).
+ *         The text positions' token ids come from dcue_tracks.tokens. */
 #define DCUE_TOWER_BN 0
 #define DCUE_TOWER_PLAIN 1
 #define DCUE_TOWER_RES 2
 #define DCUE_TOWER_RESBN 3
+#define DCUE_TOWER_TEXT 4
 
 typedef struct dcue_dims {
   int32_t conv_hidden; /* H: nn/dcue.py:45 conv_hidden (1..256; stored padded, dcue_storage_dims) */
@@ -60,6 +71,11 @@ typedef struct dcue_dims {
   int32_t user_embdim; /* E: u_embdim (<= 1024) */
   int32_t tower;       /* DCUE_TOWER_* */
   int64_t n_users;     /* rows of the (local shard of the) user table */
+  /* DCUE_TOWER_TEXT only (0 otherwise): */
+  int32_t text_dim;    /* C: text features (1..256; stored at 64/128/256 channels) */
+  int32_t word_dim;    /* E_w: word-vector width (4..1024, a multiple of 4) */
+  int32_t text_len;    /* T: token positions per track (max_sentence_length + 1; 2..128) */
+  int32_t text_pad;    /* PAD token id: positions holding it are left out of the max */
 } dcue_dims;
 
 /* Deferred user-table Adam (optional, selected by dcue_model.emb_step != NULL).
@@ -101,6 +117,13 @@ typedef struct dcue_model {
   dcue_emb_log* emb_log; /* deferred mode: header + history (dcue_emb_log_bytes) */
   int32_t emb_log_cap;   /* deferred mode: the log's history capacity (1..DCUE_MAX_LOG_CAP) */
   int32_t reserved;
+  /* DCUE_TOWER_TEXT: the frozen word vectors text.embeddings.weight [n_words][word_dim] (never
+   * updated by the library) and the power of two 2^words_exp the kernels scale them by before their
+   * fp16 hi/lo split (exact; choose it so max |word value| * 2^words_exp lies in [2^13, 2^15)) */
+  const float* words;
+  int64_t n_words;
+  int32_t words_exp;
+  int32_t reserved2;
 } dcue_model;
 
 #define DCUE_MAX_LOG_CAP 256
@@ -129,6 +152,7 @@ typedef struct dcue_tracks {
   int64_t n_tracks;
   int32_t dtype;     /* 0 = fp16, 1 = fp32 */
   int32_t reserved;
+  const int32_t* tokens;  /* DCUE_TOWER_TEXT: [n_tracks][text_len] token ids (< n_words) */
 } dcue_tracks;
 
 #define DCUE_ADAM_DENSE 1     /* flat dense params, then the conv-weight repack */

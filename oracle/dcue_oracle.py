@@ -61,7 +61,7 @@ def param_names(model_type="truedcuemel1dbn"):
     return names
 
 
-def init_params(feature_dim, conv_hidden, user_embdim, user_count, model_type="truedcuemel1dbn"):
+def init_params(feature_dim, conv_hidden, user_embdim, user_count, model_type="truedcuemel1dbn", fc_in=None):
     """Create parameters + BN buffers consuming torch's global CPU RNG in reference order.
 
     Order of RNG use in the reference constructors: each Conv1d/Linear default reset
@@ -94,7 +94,7 @@ def init_params(feature_dim, conv_hidden, user_embdim, user_count, model_type="t
             default_reset(w, bias)
             p["conv.layer%d.weight" % (l + 1)] = w
             p["conv.layer%d.bias" % (l + 1)] = bias
-    fi = 4 * H + d if is_res(model_type) else d
+    fi = fc_in if fc_in is not None else 4 * H + d if is_res(model_type) else d
     fcw, fcb = torch.empty(d, fi), torch.empty(d)
     default_reset(fcw, fcb)
     for l in range(1, 6):

@@ -70,6 +70,9 @@ def test_layouts_match_reference_shapes(golden):
     dims = nat.make_dims(H, d, 300, int(g["n_users"]))
     off = nat.param_layout(dims)
     for s, name in enumerate(nat.DENSE_NAMES):
+        if name.startswith("text."):  # the text tower's segments: empty in the audio-only towers
+            assert off[s + 1] == off[s], name
+            continue
         n = g["init." + name].size
         assert off[s] % 4 == 0
         assert off[s + 1] - off[s] >= n, name
@@ -183,3 +186,64 @@ def test_check_mode_disabled_by_default(monkeypatch):
     assert not check.enabled_by_env()
     monkeypatch.setenv("DCUE_CHECK", "1")
     assert check.enabled_by_env()
+
+
+@pytest.mark.parametrize("td,wd,t,d", [(256, 300, 64, 256), (100, 64, 20, 100), (40, 128, 128, 32)])
+def test_text_tower_layout(td, wd, t, d):
+    """The mixed audio + text tower (BASELINE config 4): its parameters -- the BN tower with
+    fc(text_dim + d -> d), the text conv [text_dim][word_dim][3] -- are corners of the flat segments
+    (text channels stored at 64 / 128 / 256), the frozen word vectors stay outside the flat buffer,
+    and the split-f16 text weight pack is 3 x word_dim (rounded up to 32) x the storage channels."""
+    from dcrecommend import _native as nat
+    from dcrecommend.dcue.dcue import DCUENet
+    args = {"feature_dim": d, "conv_hidden": 64, "user_embdim": 300, "user_count": 10,
+            "model_type": "truedcuemel1dbntext", "text_dim": td, "word_dim": wd, "text_len": t,
+            "n_words": 50, "pad_idx": 0}
+    torch.manual_seed(0)
+    net = DCUENet(args)
+    dims = nat.make_dims(64, d, 300, 10, "truedcuemel1dbntext", (td, wd, t, 0))
+    off, shapes = nat.param_layout(dims), nat.segment_shapes(dims)
+    named = dict(net.named_parameters())
+    assert named["conv.fc.weight"].shape == (d, td + d)
+    assert named["text.conv.weight"].shape == (td, wd, 3)
+    assert "text.embeddings.weight" not in nat.DENSE_NAMES
+    for s, name in enumerate(nat.DENSE_NAMES):
+        p = named[name]
+        n = int(np.prod(shapes[s]))
+        assert n <= off[s + 1] - off[s] < n + 4, name
+        assert all(a >= b for a, b in zip(shapes[s], p.shape)), name
+    cts = nat.text_storage(td)
+    assert shapes[nat.DENSE_NAMES.index("text.conv.weight")] == (cts, wd, 3)
+    plain = nat.wpack_floats(nat.make_dims(64, d, 300, 10, "truedcuemel1dbn"))
+    assert nat.wpack_floats(dims) == plain + 3 * ((wd + 31) // 32 * 32) * cts
+
+
+def test_text_tower_rejects_bad_dims():
+    from dcrecommend import _native as nat
+    for text, err in (((300, 300, 64, 0), "UNSUPPORTED"), ((256, 302, 64, 0), "UNSUPPORTED"),
+                      ((256, 300, 129, 0), "UNSUPPORTED"), ((256, 300, 1, 0), "INVALID")):
+        with pytest.raises(RuntimeError, match=err):
+            nat.param_layout(nat.make_dims(64, 256, 300, 10, "truedcuemel1dbntext", text))
+
+
+def test_text_oracle_contract():
+    """oracle/text_oracle.py: token rows in the reference's shape (dcuelmitemset.py:40-56: BOS,
+    sentence, EOS, PAD) and a forward whose PAD positions never win the max."""
+    from oracle import text_oracle as TO
+    gen = torch.Generator().manual_seed(0)
+    tok = TO.sentences(gen, 50, 16, 30, pad_idx=0, min_len=0)
+    assert tok.shape == (50, 16) and bool((tok[:, 0] == 1).all())
+    for row in tok:
+        L = int((row != 0).sum())
+        assert int(row[L - 1]) == 2 and bool((row[L:] == 0).all()) and bool((row[1:L - 1] >= 3).all())
+    torch.manual_seed(1)
+    p, _ = TO.init_params(32, 32, 8, 4, 16, 12, 30)
+    s = TO.text_features(p, tok, 0)
+    assert s.shape == (50, 16) and bool((s >= 0).all())
+    # PAD positions changed to anything: the features do not move unless a real neighbour reads them
+    emb = p["text.embeddings.weight"].clone()
+    p["text.embeddings.weight"][0] = 0.0
+    s0 = TO.text_features(p, tok, 0)
+    p["text.embeddings.weight"] = emb
+    full = tok[:, -1] != 0  # no PAD at all: identical
+    assert torch.equal(s0[full], s[full])
