@@ -528,7 +528,12 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
                         c.bn ? c.P(seg_bn_b(3)) : nullptr, c.bn ? c.P(seg_bn_b(4)) : nullptr,
                         c.bn ? c.P(seg_bn_b(5)) : nullptr, bn_of(5), M, c.H, c.res ? c.HL : 0, c.D, c.off5,
                         c.FI, w.xfc, s));
-    if (c.text) TRY(launch_text_fwd(text_branch(c, t), item_track, M, w.xfc, c.FI, w.tidx, s));
+    if (c.text) {
+      TimerScope tsc;
+      TRY(timer_begin(&tsc, DCUE_TIMED_TEXT_FWD, s));
+      TRY(launch_text_fwd(text_branch(c, t), item_track, M, w.xfc, c.FI, w.tidx, s));
+      TRY(timer_end(&tsc));
+    }
     TGemmArgs g = {};
     g.M = M; g.N = c.D; g.K = c.FI;
     g.A = w.xfc; g.sam = c.FI; g.sak = 1;

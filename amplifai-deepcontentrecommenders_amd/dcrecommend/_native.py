@@ -92,6 +92,7 @@ TIMED_EMB_FLUSH = 2
 TIMED_ADAM_EMBED = 3
 TIMED_ALLREDUCE = 4
 TIMED_EMB_SLICE = 5
+TIMED_TEXT_FWD = 6
 COMM_ID_BYTES = 128
 
 

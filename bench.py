@@ -49,8 +49,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--modes", default="inbatch,catalogue,dcbr",
-                    help="comma list of phases after the cold one: inbatch (warm), catalogue")
+    ap.add_argument("--modes", default="inbatch,catalogue,text,dcbr",
+                    help="comma list of phases after the cold one: inbatch (warm), catalogue, text "
+                         "(config 4's mixed audio + text tower), dcbr (config 5)")
+    ap.add_argument("--text-dim", type=int, default=256)
+    ap.add_argument("--text-feature-dim", type=int, default=256, help="config 4: d = 256")
+    ap.add_argument("--word-dim", type=int, default=300)
+    ap.add_argument("--text-len", type=int, default=64)
+    ap.add_argument("--n-words", type=int, default=20000)
     ap.add_argument("--users", type=int, default=100_000)
     ap.add_argument("--tracks", type=int, default=200_000)
     ap.add_argument("--interactions", type=int, default=5_000_000)
@@ -66,6 +72,9 @@ def parse():
     ap.add_argument("--flush-every", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-eval", action="store_true", help="skip AUC@val after the timed steps")
+    ap.add_argument("--no-f32-probe", action="store_true",
+                    help="skip the exact-f32 comparison run (DCUE_CONV_F16=0 DCUE_WGRAD_F16=0 "
+                         "DCUE_DGRAD_F16=0, in-batch + catalogue, in a child process)")
     ap.add_argument("--eval-pct", type=float, default=0.025, help="users sampled for AUC@val (eval_pct)")
     ap.add_argument("--timer-stride", type=int, default=8,
                     help="time every n-th launch of the roofline kernels live (HIP events)")
@@ -188,6 +197,57 @@ def item_flops(H, d):
     return 2 * (128 * 4 * H * 132 + H * 4 * H * 34 + H * 4 * H * 9 + H * 2 * H * 3 + H * d + d * d)
 
 
+def text_conv_flops(T, E, C):
+    """Forward FLOPs of the text conv per item: T positions x (3 taps x E) x C."""
+    return 2.0 * T * 3 * E * C
+
+
+def synthetic_sentences(n, T, n_words, device, seed, pad=0, bos=1, eos=2):
+    """[n][T] int32 token rows in the reference's shape (datasets/dcuelmitemset.py:40-56): BOS, a
+    sentence of 1..T-2 random word ids (>= 3), EOS, then PAD."""
+    gen = torch.Generator(device=device).manual_seed(seed)
+    lens = torch.randint(1, T - 1, (n, 1), generator=gen, device=device)
+    pos = torch.arange(T, device=device).unsqueeze(0)
+    words = torch.randint(3, n_words, (n, T), generator=gen, device=device, dtype=torch.int32)
+    tok = torch.where(pos <= lens, words, torch.full_like(words, pad))
+    tok[:, 0] = bos
+    tok.scatter_(1, lens + 1, eos)
+    return tok.to(torch.int32).contiguous()
+
+
+DGRAD_F16 = os.environ.get("DCUE_DGRAD_F16", "1")[:1] != "0"
+
+
+def executed_work(args, items_per_row, M):
+    """The FLOPs one row's step actually executes and their time at the ceiling of the arithmetic
+    that runs them: forwards on split-f16 MFMA (3 f16 products per f32 product: 2500/3
+    TFLOP/s f32-equivalent), the conv-1 weight gradient on the raw fp16 table (2 products: 2500/2),
+    the other weight gradients split-f16 (2500/3), input gradients of layers 5..2 split-f16 where a
+    launch writes >= 8,192 rows (catalogue layers 2-3) and f32 MFMA (157.3) otherwise, the user tower
+    f32 MFMA; conv 1's input gradient is never computed (§4.2). Returns (flops, seconds) per row."""
+    H, d, E = args.hidden, args.feature_dim, args.user_embdim
+    lp_in = {2: 33, 3: 8, 4: 2, 5: 1}  # rows of g_{l-1} written by layer l's dgrad, per item
+    f = {1: 2 * 128 * 4 * H * 132, 2: 2 * H * 4 * H * 34, 3: 2 * H * 4 * H * 9, 4: 2 * H * 2 * H * 3,
+         5: 2 * H * d, "fc": 2 * d * d}
+    fwd_peak = F16_PEAK_TFLOPS / 3 if CONV_F16 else F32_PEAK_TFLOPS
+    w16 = F16_PEAK_TFLOPS / 3 if WGRAD_F16 else F32_PEAK_TFLOPS
+    w1 = F16_PEAK_TFLOPS / 2 if WGRAD_F16 else F32_PEAK_TFLOPS
+    flops = t = 0.0
+    for k, v in f.items():
+        flops += v
+        t += v / (fwd_peak * 1e12)                                   # forward
+        flops += v
+        t += v / ((w1 if k == 1 else w16) * 1e12)                    # weight gradient
+        if k != 1:                                                   # input gradient (none for conv 1)
+            split = DGRAD_F16 and k in lp_in and M * lp_in[k] >= 8192
+            flops += v
+            t += v / ((F16_PEAK_TFLOPS / 3 if split else F32_PEAK_TFLOPS) * 1e12)
+    flops *= items_per_row
+    t *= items_per_row
+    u = 3 * 2 * (E * E + E * d)
+    return flops + u, t + u / (F32_PEAK_TFLOPS * 1e12)
+
+
 def row_flops(args, items_per_row):
     """SURVEY §8(d) canonical work per row: 3 x forward (fwd + bwd) of the item tower over the
     row's items plus the user tower (1.462 GFLOP catalogue, 70.4 MFLOP compact in-batch)."""
@@ -299,6 +359,25 @@ def evaluate_val(args, net, tracks, pair_user, pair_track, split, n_users, dev):
             "users": int(len(sample)), "candidates": int(n_tracks), "factors_s": t_factors, "rank_s": t_rank,
             "item_tower_s": t_items, "item_tower_tflops": flops * n_tracks / t_items / 1e12,
             "note": "random-init model after the bench steps on synthetic data: AUC ~0.5 is expected"}
+
+
+def exact_f32_probe(args):
+    """What the split-f16 emulation buys: the same in-batch and catalogue steps with every conv on
+    exact f32 MFMA (DCUE_CONV_F16=0 DCUE_WGRAD_F16=0 DCUE_DGRAD_F16=0; the library reads them at load,
+    so in a child process, after this one's timed phases)."""
+    env = dict(os.environ, DCUE_CONV_F16="0", DCUE_WGRAD_F16="0", DCUE_DGRAD_F16="0")
+    cmd = [sys.executable, os.path.abspath(__file__), "--modes", "inbatch,catalogue", "--no-eval",
+           "--no-cpu-baseline", "--no-f32-probe", "--steps", str(args.steps), "--warmup", str(args.warmup),
+           "--users", str(args.users), "--tracks", str(args.tracks), "--interactions", str(args.interactions)]
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+        line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+        d = json.loads(line)
+        return {"ms_per_step": d["ms_per_step"], "catalogue_ms_per_step": d.get("catalogue", {}).get("ms_per_step"),
+                "inbatch_cold_ms_per_step": d["inbatch_cold"]["ms_per_step"],
+                "env": "DCUE_CONV_F16=0 DCUE_WGRAD_F16=0 DCUE_DGRAD_F16=0 (every conv on f32 MFMA 16x16x4 / 32x32x2)"}
+    except (subprocess.SubprocessError, IndexError, ValueError, KeyError) as e:
+        return {"error": "%s: %s" % (type(e).__name__, str(e)[:200])}
 
 
 def cpu_model():
@@ -447,7 +526,7 @@ def main():
             comm_error = str(e)
 
     timed = [nat.TIMED_CONV1_WGRAD, nat.TIMED_CONV1_FWD, nat.TIMED_EMB_SLICE, nat.TIMED_EMB_FLUSH,
-             nat.TIMED_ALLREDUCE]
+             nat.TIMED_ALLREDUCE, nat.TIMED_TEXT_FWD]
     # every stride-th launch of each class is timed live (a timed launch costs its stream a few us)
     stride = max(1, min(args.timer_stride, args.steps // 4))
 
@@ -491,11 +570,12 @@ def main():
 
     launches = {}  # kernel launches per timed step, per phase (libdcue_hip's own count)
 
-    def timed_phase(name, plan, step_fn, gpu_only=False):
+    def timed_phase(name, plan, step_fn, gpu_only=False, optim=None):
         """W warm-up steps, then EXACTLY K timed steps between barrier + synchronize on both
         sides; max over ranks. Returns (seconds, host enqueue seconds, gpu-only ms or None)."""
+        optim = opt if optim is None else optim
         run(plan, step_fn, args.warmup, name + " warm-up")
-        opt.flush()
+        optim.flush()
         mark(name + ": barrier before the timed steps")
         if world > 1:
             dist.barrier()
@@ -513,7 +593,7 @@ def main():
         l0 = nat.lib().dcue_launch_count()
         t0 = time.perf_counter()
         run(plan, lambda p, s: step_fn(p, args.warmup + s), args.steps, name + " timed")
-        opt.flush()  # deferred user-table steps still pending are part of the timed work
+        optim.flush()  # deferred user-table steps still pending are part of the timed work
         t_enq = time.perf_counter() - t0
         launches[name] = (nat.lib().dcue_launch_count() - l0) / args.steps
         if gpu_only:
@@ -554,6 +634,11 @@ def main():
                                   "alone on its stream: the replay's uncontended per-element rate)", "valu",
                                   24.0 * n_users_local * E),
             nat.TIMED_ALLREDUCE: ("RCCL all-reduce of the dense gradient (per bucket)", "xgmi", None),
+            nat.TIMED_TEXT_FWD: ("k_text_fwd (config 4 text conv: word-vector gather + Conv1d(%d -> %d, k 3) "
+                                 "over %d positions + masked max, split-f16 MFMA 16x16x32: three f16 products "
+                                 "per f32 product; peak = f16 dense peak / 3)"
+                                 % (args.word_dim, args.text_dim, args.text_len), "mfma",
+                                 M * text_conv_flops(args.text_len, args.word_dim, args.text_dim)),
         }
         out = []
         for k, (ms, n) in kern.items():
@@ -570,7 +655,7 @@ def main():
             if bound == "mfma":
                 # split-f16 kernels: f32-equivalent FLOPs against the f16 peak over their products per
                 # f32 product (forward: 3; conv-1 weight gradient on the fp16 table: 2)
-                nprod = 3 if (k == nat.TIMED_CONV1_FWD and CONV_F16) else 2 if (
+                nprod = 3 if ((k == nat.TIMED_CONV1_FWD and CONV_F16) or k == nat.TIMED_TEXT_FWD) else 2 if (
                     k == nat.TIMED_CONV1_WGRAD and WGRAD_F16) else 0
                 split = nprod > 0
                 peak = F16_PEAK_TFLOPS / nprod if split else F32_PEAK_TFLOPS
@@ -616,9 +701,16 @@ def main():
         roof = dict(mf[0]) if mf else {}
         if roof:
             roof["traffic"] = traffic_for(roof["kernel"], mode)
+        # the step against the ceiling of the arithmetic it runs (FLOP-weighted over split-f16 and f32
+        # MFMA, executed FLOPs: conv 1's input gradient is elided); the canonical SURVEY §8(d) figure
+        # (3 x forward, f32 peak) beside it
         flops_row = row_flops(args, items_per_row)
-        roof["step_frac"] = rows / world * flops_row / (F32_PEAK_TFLOPS * 1e12)
+        ex_flops, ex_t = executed_work(args, items_per_row, M)
+        roof["step_frac"] = rows / world * ex_t
+        roof["step_flops_executed_per_row"] = ex_flops
+        roof["step_ceiling_tflops"] = ex_flops / ex_t / 1e12
         roof["step_flops_per_row"] = flops_row
+        roof["canonical_tflops_per_gpu"] = rows / world * flops_row / 1e12
         res = {"ms_per_step": dt / args.steps * 1e3, "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
                "launches_per_step": launches.get(phase), "rows_per_s": rows, "triplets_per_s": rows * N,
                "roofline": roof, "kernels": ks}
@@ -735,7 +827,75 @@ def main():
         out["catalogue"] = summary(dt, t_enq, kern, B * (1 + N), 1 + N, "catalogue", "catalogue")
         check_state(cplan, "catalogue")
         cplan.close()
-    # ---- phase 4 (N = 1): the DCBR path (BASELINE config 5): WRMF target factors of
+    # ---- phase 4: BASELINE config 4, the mixed audio + text item tower at d = 256,
+    # in-batch steps as phase 2 on the same users, tracks and interactions, each track with a synthetic
+    # sentence (BOS + words + EOS + PAD) and random 300-d word vectors in place of the LM-pretrained
+    # ones (caller-supplied; none can be fetched here)
+    if "text" in modes:
+        mark("text phase")
+        Dt = args.text_feature_dim
+        torch.manual_seed(0)
+        tnet = DCUENet({"feature_dim": Dt, "conv_hidden": args.hidden, "user_embdim": args.user_embdim,
+                        "user_count": n_users_local, "model_type": "truedcuemel1dbntext",
+                        "text_dim": args.text_dim, "word_dim": args.word_dim, "text_len": args.text_len,
+                        "n_words": args.n_words, "pad_idx": 0}).to(dev)
+        tnet.train()
+        with torch.no_grad():
+            tnet.text.embeddings.weight.copy_(torch.randn(args.n_words, args.word_dim, generator=gen, device=dev) * 0.3)
+        tokens = synthetic_sentences(args.tracks, args.text_len, args.n_words, dev, seed=77)
+        topt = NativeAdam(tnet.parameters(), 1e-5, (0.9, 0.99), 1e-8, 0, defer_embedding=defer,
+                          flush_every=args.flush_every)
+        tsched = CyclicLRWithRestarts(topt, B, epoch_size=epoch_size, restart_period=30, t_mult=2, policy="cosine")
+        tsched.step()
+        tplan = TrainPlan(tnet, tracks, B, N, mt_state=mt, emb_grad_scale=1.0 / world, optimizer=topt,
+                          tokens=tokens)
+        if comm is not None:
+            tplan.set_comm(comm)
+
+        def text_step(users_b, items_b):
+            def fn(plan, s):
+                if world > 1 and comm is None:
+                    plan.launch(users_b[s], items_b[s])
+                    D.allreduce_mean_overlapped_(plan, tnet._flat["G"], D.late_grad_floats(tnet))
+                    topt.step()
+                else:
+                    if s + 1 < users_b.shape[0]:
+                        plan.set_next(items_b[s + 1])
+                    plan.step(users_b[s], items_b[s])
+                try:
+                    tsched.batch_step()
+                except StopIteration:
+                    tsched.step()
+                    tsched.batch_step()
+            return fn
+        ub, ib = batches(args.warmup + args.steps)
+        dt, t_enq, _, kern = timed_phase("text", tplan, text_step(ub, ib), optim=topt)
+        rows = world * B * args.steps / dt
+        ks = kernel_rooflines(kern, B, args.steps)
+        tk = [k for k in ks if k["kernel"].startswith("k_text_fwd")]
+        troof = dict(tk[0]) if tk else {}
+        tflops_row = 3 * (item_flops(args.hidden, Dt) + 2.0 * args.text_dim * Dt
+                          + text_conv_flops(args.text_len, args.word_dim, args.text_dim)) \
+            + 3 * 2 * (args.user_embdim ** 2 + args.user_embdim * Dt)
+        troof["step_flops_per_row"] = tflops_row
+        tnet._sync_plan()
+        topt.flush()
+        out["text"] = {
+            "workload": "DCUE truedcuemel1dbntext (config 4): d=%d H=%d E=%d + text Conv1d(%d -> %d, k 3) over "
+                        "%d-token sentences of a %d-word vocabulary, fc(%d + %d -> %d); %d users x %d tracks, "
+                        "in-batch N=%d" % (Dt, args.hidden, args.user_embdim, args.word_dim, args.text_dim,
+                                           args.text_len, args.n_words, args.text_dim, Dt, Dt, args.users,
+                                           args.tracks, N),
+            "ms_per_step": dt / args.steps * 1e3, "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
+            "launches_per_step": launches.get("text"), "rows_per_s": rows, "triplets_per_s": rows * N,
+            "roofline": troof, "kernels": ks, "last_loss": float(tplan.loss),
+            "finite": bool(torch.isfinite(tnet._flat["P"]).all()) and bool(torch.isfinite(tplan.loss)),
+            "data": "synthetic: random word vectors (N(0, 0.09)) stand in for the LM-pretrained ones",
+            "parity": "unpinned against the reference (its text encoder was never published, "
+                      "datasets/dcuelmitemset.py:8); pinned against oracle/text_oracle.py (tests/test_gpu_text.py)"}
+        tplan.close()
+        del tplan, topt, tnet, tokens
+    # ---- phase 5 (N = 1): the DCBR path (BASELINE config 5): WRMF target factors of
     # the same interactions, then the audio ConvNet regressing them (catalogue-sized item batches)
     if "dcbr" in modes and world == 1 and args.feature_dim <= 128:
         mark("dcbr phase")
@@ -784,6 +944,8 @@ def main():
         result["gpu_only_ms_per_step"] = head["gpu_only_ms_per_step"]
     if "catalogue" in out:
         result["catalogue"] = out["catalogue"]
+    if "text" in out:
+        result["text"] = out["text"]
     if "dcbr" in out:
         result["dcbr"] = out["dcbr"]
     checks["finite"] = not checks["failed"]
@@ -806,6 +968,8 @@ def main():
         result["eval"] = ev
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, n_users_local)
+    if rank == 0 and world == 1 and not args.no_f32_probe:
+        result["exact_f32"] = exact_f32_probe(args)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if comm is not None:

@@ -456,7 +456,8 @@ int dcue_plan_set_sync_bn(dcue_plan* plan, int32_t on);
 #define DCUE_TIMED_ADAM_EMBED 3  /* dense user-table Adam sweep */
 #define DCUE_TIMED_ALLREDUCE 4    /* a plan's RCCL gradient exchange (each bucket's all-reduce) */
 #define DCUE_TIMED_EMB_SLICE 5    /* deferred user-table Adam: one step's rolling-flush slice */
-#define DCUE_N_TIMED 6
+#define DCUE_TIMED_TEXT_FWD 6     /* text tower: the text conv forward (k_text_fwd, config 4) */
+#define DCUE_N_TIMED 7
 int dcue_timer_enable(int32_t kernel, int32_t enable);
 int dcue_timer_read(int32_t kernel, double* total_ms_host, int64_t* launches_host);
 
