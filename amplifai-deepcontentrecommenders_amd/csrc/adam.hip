@@ -1,6 +1,7 @@
 // torch.optim.Adam over the flat dense buffer and the user table, plus the weight repack -- gfx950.
 // Reference: optim.Adam as built at nn/dcue.py:143-147 and stepped at :209 (CPU single-tensor path).
 #include "dcue_internal.h"
+#include "tgemm.h"
 
 namespace dcue {
 
@@ -270,7 +271,11 @@ __global__ __launch_bounds__(256) void k_emb_flush(float* __restrict__ p, float*
       const float4 p4 = ld4(p + 4 * i);
       float pp[4] = {p4.x, p4.y, p4.z, p4.w}, mm[4] = {m4.x, m4.y, m4.z, m4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
       replay_run<4>(pp, mm, vv, hs, max(from + 1, lo), T, cap, b, gz);
-      st4(p + 4 * i, make_float4(pp[0], pp[1], pp[2], pp[3]));
+      // a long-idle element's replay leaves p bit-identical (adam_replay.h): no store then (the
+      // flush's HBM traffic is p, m, v read and written; most rows skip a sixth of it)
+      if ((__float_as_uint(pp[0]) ^ __float_as_uint(p4.x)) | (__float_as_uint(pp[1]) ^ __float_as_uint(p4.y)) |
+          (__float_as_uint(pp[2]) ^ __float_as_uint(p4.z)) | (__float_as_uint(pp[3]) ^ __float_as_uint(p4.w)))
+        st4(p + 4 * i, make_float4(pp[0], pp[1], pp[2], pp[3]));
       st4(m + 4 * i, make_float4(mm[0], mm[1], mm[2], mm[3]));
       st4(v + 4 * i, make_float4(vv[0], vv[1], vv[2], vv[3]));
     }
@@ -322,7 +327,9 @@ __global__ __launch_bounds__(256) void k_emb_flush_rows(float* __restrict__ p, f
       const float4 p4 = ld4(p + off);
       float pp[4] = {p4.x, p4.y, p4.z, p4.w}, mm[4] = {m4.x, m4.y, m4.z, m4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
       replay_run<4>(pp, mm, vv, hs, from_s[i] + 1, T, cap, b, gz);
-      st4(p + off, make_float4(pp[0], pp[1], pp[2], pp[3]));
+      if ((__float_as_uint(pp[0]) ^ __float_as_uint(p4.x)) | (__float_as_uint(pp[1]) ^ __float_as_uint(p4.y)) |
+          (__float_as_uint(pp[2]) ^ __float_as_uint(p4.z)) | (__float_as_uint(pp[3]) ^ __float_as_uint(p4.w)))
+        st4(p + off, make_float4(pp[0], pp[1], pp[2], pp[3]));  // long-idle: p unchanged, no store
       st4(m + off, make_float4(mm[0], mm[1], mm[2], mm[3]));
       st4(v + off, make_float4(vv[0], vv[1], vv[2], vv[3]));
     }
@@ -362,6 +369,7 @@ int launch_emb_flush_rows(const dcue_model* md, int step, hipStream_t s) {
 
 
 
+static AdamScalars form_scalars(const dcue_adam_args* a);
 // Step t for the rows that have a gradient (emb_rows from the backward); records step t's scalars.
 __global__ __launch_bounds__(256) void k_adam_touched(float* __restrict__ p, float* __restrict__ m,
                                                       float* __restrict__ v,
@@ -396,6 +404,167 @@ __global__ __launch_bounds__(256) void k_adam_touched(float* __restrict__ p, flo
     log_hist(hdr)[t % cap] = s;
     hdr->step_done = t;
   }
+}
+
+// k_emb_grad (tail.hip) and k_adam_touched in one launch: workgroup b owns batch row b; a repeated
+// user's first row sums the user's rows in batch order (the compact gradient, as k_emb_grad), and
+// the same workgroup then steps the user's table row (as k_adam_touched: missed zero-gradient steps
+// replayed first -- normally none -- then adam_elem). Workgroup 0 records the step's scalars.
+__global__ __launch_bounds__(256) void k_emb_grad_adam(const float* __restrict__ de, const int64_t* users, int B,
+                                                       int E, float scale, float* __restrict__ emb_grad,
+                                                       int32_t* slot, int64_t* emb_rows, float* __restrict__ p,
+                                                       float* __restrict__ m, float* __restrict__ v,
+                                                       int32_t* emb_step, dcue_emb_log* hdr, int t, AdamScalars s,
+                                                       float gz) {
+  const int b = blockIdx.x;
+  const int64_t u = users[b];
+  const int cap = hdr->cap, F = hdr->flush_step;
+  if (b == 0 && threadIdx.x == 0) {
+    hdr->n_touched = B;
+    hdr->grad_step = t;
+  }
+  bool first = true;
+  for (int r = 0; r < b; ++r) first &= users[r] != u;
+  if (!first) {
+    if (threadIdx.x == 0) emb_rows[b] = -1;
+  } else {
+    const int from = max(emb_step[u], F);
+    const AdamScalars* hist = log_hist(hdr);
+    float* pr = p + u * E;
+    float* mr = m + u * E;
+    float* vr = v + u * E;
+    for (int k = threadIdx.x; k < E; k += blockDim.x) {
+      float gsum = 0.f;
+      for (int r = b; r < B; ++r)
+        if (users[r] == u) gsum += de[(long)r * E + k];
+      const float g = gsum * scale;
+      emb_grad[(long)b * E + k] = g;
+      float pp = pr[k], mm = mr[k], vv = vr[k];
+      for (int j = from + 1; j < t; ++j) adam_replay(pp, mm, vv, hist[j % cap], gz);  // normally none
+      adam_elem(pp, g, mm, vv, s);
+      pr[k] = pp; mr[k] = mm; vr[k] = vv;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      slot[u] = b;
+      emb_rows[b] = u;
+      emb_step[u] = t;
+    }
+  }
+  if (b == 0 && threadIdx.x == 0) {
+    log_hist(hdr)[t % cap] = s;
+    hdr->step_done = t;
+  }
+}
+
+int launch_emb_grad_adam(const dcue_model* md, const dcue_adam_args* a, const float* de, const int64_t* users, int B,
+                         float scale, hipStream_t s) {
+  if (!md->emb_step || !md->emb_rows || !md->emb_log) return DCUE_ERR_INVALID;
+  const AdamScalars sc = form_scalars(a);
+  DCUE_LAUNCH(k_emb_grad_adam, dim3((unsigned)B), dim3(256), 0, s, de, users, B, md->dims.user_embdim, scale,
+              md->emb_grad, md->emb_slot, md->emb_rows, md->emb, md->emb_exp_avg, md->emb_exp_avg_sq, md->emb_step,
+              md->emb_log, a->step, sc, 0.f);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+// ------------------------------------------------------------------- fused user-tower forward
+// userembedding.py:33-44 for 16 users per workgroup, in one launch: (deferred mode) the rows brought
+// current, then h1 = relu(E[u]) W1^T + b1 and uf = relu(h1) W2^T + b2. Replaces k_emb_sync and two
+// k_tgemm launches with the same arithmetic:
+//  * sync: each row replays its missed zero-gradient steps with replay_run (bound over the live window
+//    [lo, T], a superset of the row's own: still exact, adam_replay.h); a row listed twice in the batch
+//    is claimed by one workgroup (CAS on its clock, INT_MIN = in progress, as k_emb_sync) and any other
+//    workgroup that reads it waits, bounded, for the claimer's release of the clock;
+//  * the GEMMs are tgemm_block's 16 x 64 blocks (tgemm.h), two at a time (threads 0-255 / 256-511),
+//    so h1 and uf are bit-identical to the k_tgemm launches. h1 goes through global memory: written
+//    and read back by this workgroup's own waves only (one CU's L1), ordered by the block barrier.
+struct UserFwdArgs {
+  TGemmArgs g1, g2;
+  float *p, *m, *v;        // the table and its Adam moments (deferred mode)
+  dcue_emb_log* hdr;
+  int32_t* emb_step;       // null: dense mode, every row already current
+  const int64_t* users;
+  int B, E;
+  unsigned* fail;          // set when a wait for another workgroup's claim gave up (never expected)
+};
+
+__global__ __launch_bounds__(512) void k_user_fwd(UserFwdArgs a) {
+  __shared__ TgLds L[2];
+  __shared__ AdamScalars hs[DCUE_MAX_LOG_CAP];
+  __shared__ ReplayBound sb;
+  __shared__ int from_s[16], claim_s[16];
+  const int t = threadIdx.x, half = t >> 8, th = t & 255;
+  const int r0 = blockIdx.x * 16, nr = min(16, a.B - r0);
+  if (a.emb_step) {
+    const int T = a.hdr->step_done, F = a.hdr->flush_step, cap = a.hdr->cap;
+    if (t < nr) {
+      const int64_t u = a.users[r0 + t];
+      const int old = a.emb_step[u];
+      int from = T, claimed = 0;
+      if (old != INT_MIN && max(old, F) < T && atomicCAS(&a.emb_step[u], old, INT_MIN) == old) {
+        from = max(old, F);
+        claimed = 1;
+      }
+      from_s[t] = from;
+      claim_s[t] = claimed;
+    }
+    const int lo = max(F + 1, T - cap + 1);
+    const AdamScalars* hist = log_hist(a.hdr);
+    for (int j = lo + t; j <= T; j += blockDim.x) hs[j % cap] = hist[j % cap];
+    __syncthreads();
+    if (lo <= T) window_bound(hs, lo, T, cap, 0.f, &sb);
+    __syncthreads();
+    const ReplayBound b = sb;
+    for (int e = t; e < nr * a.E; e += blockDim.x) {
+      const int i = e / a.E, k = e - i * a.E;
+      if (!claim_s[i]) continue;
+      const long off = a.users[r0 + i] * a.E + k;
+      float mm[1] = {a.m[off]}, vv[1] = {a.v[off]};
+      if (b.nd && idle_moments(mm[0], vv[0])) continue;  // fixed point (idle_moments)
+      float pp[1] = {a.p[off]};
+      replay_run<1>(pp, mm, vv, hs, from_s[i] + 1, T, cap, b, 0.f);
+      a.p[off] = pp[0]; a.m[off] = mm[0]; a.v[off] = vv[0];
+    }
+    __syncthreads();
+    if (t < nr) {
+      int32_t* clk = a.emb_step + a.users[r0 + t];
+      if (claim_s[t]) {
+        __threadfence();  // the row's replayed values before its clock (other workgroups wait on it)
+        __hip_atomic_store(clk, T, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        unsigned spins = 0;
+        while (__hip_atomic_load(clk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == INT_MIN) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1u << 22)) {
+            if (a.fail) atomicOr(a.fail, 1u);
+            break;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+    }
+    __syncthreads();
+  }
+  // GEMM 1: the N / 64 column blocks two at a time (an out-of-range block stores nothing)
+  const int gy1 = (a.g1.N + 63) / 64, gy2 = (a.g2.N + 63) / 64;
+  for (int by = half; by < gy1 + (gy1 & 1); by += 2) tgemm_block<1, 0, 1, 0>(a.g1, blockIdx.x, by, L[half], th);
+  __syncthreads();
+  for (int by = half; by < gy2 + (gy2 & 1); by += 2) tgemm_block<1, 0, 1, 0>(a.g2, blockIdx.x, by, L[half], th);
+}
+
+int launch_user_fwd(const dcue_model* md, const TGemmArgs& g1, const TGemmArgs& g2, const int64_t* users, int B,
+                    hipStream_t s) {
+  if (g1.sak != 1 || g1.sbn == 1 || g2.sak != 1 || g2.sbn == 1 || !g1.arow || g2.arow) return DCUE_ERR_INVALID;
+  UserFwdArgs a;
+  a.g1 = g1; a.g2 = g2;
+  a.p = md->emb; a.m = md->emb_exp_avg; a.v = md->emb_exp_avg_sq;
+  a.hdr = md->emb_log; a.emb_step = md->emb_step;
+  a.users = users; a.B = B; a.E = md->dims.user_embdim;
+  a.fail = nullptr;
+  DCUE_LAUNCH(k_user_fwd, dim3((unsigned)((B + 15) / 16)), dim3(512), 0, s, a);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
 }
 
 __global__ void k_emb_log_init(dcue_emb_log* hdr, int cap, int step) {

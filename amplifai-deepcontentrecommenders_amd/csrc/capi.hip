@@ -573,6 +573,23 @@ int user_forward(const Ctx& c, const Ws& w, const int64_t* users, int B, float* 
   return launch_tgemm(1, 0, g, s);
 }
 
+// the same, with the deferred rows' sync in one launch (k_user_fwd): the train forward's user tower
+int user_forward_fused(const Ctx& c, const Ws& w, const int64_t* users, int B, hipStream_t s) {
+  const dcue_model* m = c.m;
+  TGemmArgs g1 = {}, g2 = {};
+  g1.M = B; g1.N = c.E; g1.K = c.E;
+  g1.A = m->emb; g1.sam = c.E; g1.sak = 1; g1.arow = users;
+  g1.B = c.P(SEG_L1_W); g1.sbk = 1; g1.sbn = c.E;
+  g1.bias = c.P(SEG_L1_B);
+  g1.C = w.h1; g1.scm = c.E; g1.scn = 1;
+  g2.M = B; g2.N = c.D; g2.K = c.E;
+  g2.A = w.h1; g2.sam = c.E; g2.sak = 1;
+  g2.B = c.P(SEG_L2_W); g2.sbk = 1; g2.sbn = c.E;
+  g2.bias = c.P(SEG_L2_B);
+  g2.C = w.uf; g2.scm = c.D; g2.scn = 1;
+  return launch_user_fwd(m, g1, g2, users, B, s);
+}
+
 // whether a gather batch gets per-item copy lists (the prologue's histogram path)
 bool copy_lists(const dcue_batch* b) {
   return b->layout == DCUE_LAYOUT_GATHER && b->n_items <= kCopyListMaxItems;
@@ -771,11 +788,10 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   const std::function<int()> user_part = [&]() -> int {
     TRY(wait_point(su, ev_in));
     HPROF("capi:5");
-    if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
-    HPROF("capi:6");
     {
+      // the deferred rows' sync and the two GEMMs in one launch (k_user_fwd)
       ForkAfter fk(sp, su, &ev_uf);
-      TRY(user_forward(c, w, b->users, b->n_rows, nullptr, su));
+      TRY(user_forward_fused(c, w, b->users, b->n_rows, su));
       HPROF("capi:7");
       TRY(fk.done());
       HPROF("capi:8");
@@ -1154,23 +1170,22 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   TRY(wait_point(su, ev_score));
   HPROF("capi:26");
   {
-    TGemmArgs g = {};
+    // two launches of two independent GEMMs each (launch_tgemm_pair; the same blocks as four
+    // launch_tgemm calls, so the same bits): (dW2, dh1) from du, then (dW1, de) from dh1
+    TGemmArgs g = {}, h = {};
     // dW2[n][k] = sum_b du[b][n] relu(h1)[b][k]; db2[n] = sum_b du[b][n]
     g.M = D; g.N = E; g.K = B;
     g.A = w.du; g.sam = 1; g.sak = D;
     g.B = w.h1; g.sbk = E; g.sbn = 1;
     g.C = c.Gd(SEG_L2_W); g.scm = E; g.scn = 1;
     g.rowsum = c.Gd(SEG_L2_B);
-    TRY(launch_tgemm(0, 1, g, su));
-    HPROF("capi:27");
     // dh1 = (du W2) * (h1 > 0)
-    g = TGemmArgs{};
-    g.M = B; g.N = E; g.K = D;
-    g.A = w.du; g.sam = D; g.sak = 1;
-    g.B = c.P(SEG_L2_W); g.sbk = E; g.sbn = 1;
-    g.C = w.dh1; g.scm = E; g.scn = 1;
-    g.cmask = w.h1; g.smm = E; g.smn = 1;
-    TRY(launch_tgemm(0, 0, g, su));
+    h.M = B; h.N = E; h.K = D;
+    h.A = w.du; h.sam = D; h.sak = 1;
+    h.B = c.P(SEG_L2_W); h.sbk = E; h.sbn = 1;
+    h.C = w.dh1; h.scm = E; h.scn = 1;
+    h.cmask = w.h1; h.smm = E; h.smn = 1;
+    TRY(launch_tgemm_pair(g, h, su));
     HPROF("capi:28");
     // dW1[n][k] = sum_b dh1[b][n] relu(E[u_b])[k]; db1[n] = sum_b dh1[b][n]
     g = TGemmArgs{};
@@ -1179,41 +1194,54 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     g.B = m->emb; g.sbk = E; g.sbn = 1; g.brow = b->users;
     g.C = c.Gd(SEG_L1_W); g.scm = E; g.scn = 1;
     g.rowsum = c.Gd(SEG_L1_B);
-    TRY(launch_tgemm(0, 1, g, su));
-    HPROF("capi:29");
     // de = (dh1 W1) * (E[u_b] > 0)
-    g = TGemmArgs{};
-    g.M = B; g.N = E; g.K = E;
-    g.A = w.dh1; g.sam = E; g.sak = 1;
-    g.B = c.P(SEG_L1_W); g.sbk = E; g.sbn = 1;
-    g.C = w.de; g.scm = E; g.scn = 1;
-    g.cmask = m->emb; g.smm = E; g.smn = 1; g.cmrow = b->users;
-    TRY(launch_tgemm(0, 0, g, su));
+    h = TGemmArgs{};
+    h.M = B; h.N = E; h.K = E;
+    h.A = w.dh1; h.sam = E; h.sak = 1;
+    h.B = c.P(SEG_L1_W); h.sbk = E; h.sbn = 1;
+    h.C = w.de; h.scm = E; h.scn = 1;
+    h.cmask = m->emb; h.smm = E; h.smn = 1; h.cmrow = b->users;
+    TRY(launch_tgemm_pair(g, h, su));
     HPROF("capi:30");
   }
   // the step's end joins the user stream here: its Adam part (and the rolling flush slice) below
   // needs nothing more from this step and runs on into the next one, ordered on this stream
+  // deferred user-table Adam with the step (plans): the compact rows and their Adam step in one
+  // launch (k_emb_grad_adam: each distinct user's workgroup sums its rows, then steps them)
+  const bool emb_fused = o.emb_adam && m->emb_step && o.defer_flush_slice;
   {
     ForkAfter fk(sp, su, &tail[1]);
-    TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, m->emb_rows,
-                        m->emb_step ? m->emb_log : nullptr, su));
+    if (emb_fused)
+      TRY(launch_emb_grad_adam(m, o.emb_adam, w.de, b->users, B, emb_grad_scale, su));
+    else
+      TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, m->emb_rows,
+                          m->emb_step ? m->emb_log : nullptr, su));
     TRY(fk.done());
     HPROF("capi:31");
   }
-  if (o.emb_adam) TRY(launch_adam(m, o.emb_adam, c.poff, su, !o.defer_flush_slice));
+  if (o.emb_adam && !emb_fused) TRY(launch_adam(m, o.emb_adam, c.poff, su, !o.defer_flush_slice));
   HPROF("capi:32");
   }  // !item_only
 
   // the join: wgrad stream 0 collects the user stream's and wgrad stream 1's tails, and the caller's
   // stream waits for it once (each cross-queue wait on a pending event costs the waiting queue
-  // ≈4 µs, measured; on the side stream that time is slack, on the caller's it is the step's)
-  if (tail[1]) TRY(wait_point(sw[0], tail[1]));
-  HPROF("capi:33");
-  TRY(wait_point(sw[0], tail[3]));
-  HPROF("capi:34");
+  // ≈4 µs, measured; on the side stream that time is slack, on the caller's it is the step's).
+  // Split plans need no join (their late Adam waits for the two weight-gradient tails itself, and
+  // nothing else reads `joined`): its two waits and one record are host time saved on every step
+  // (DCUE_LATE_JOIN=hop keeps it, for the A/B below).
+  static const bool hop = [] {
+    const char* e = getenv("DCUE_LATE_JOIN");
+    return e && e[0] == 'h';
+  }();
   hipEvent_t joined = nullptr;
-  TRY(fork_point(sp, sw[0], &joined));
-  HPROF("capi:35");
+  if (!o.dense_split || hop) {
+    if (tail[1]) TRY(wait_point(sw[0], tail[1]));
+    HPROF("capi:33");
+    TRY(wait_point(sw[0], tail[3]));
+    HPROF("capi:34");
+    TRY(fork_point(sp, sw[0], &joined));
+    HPROF("capi:35");
+  }
   if (o.dense_split) {
     // split dense Adam: the late segments (every gradient the side streams made) on the user stream
     // once they are in, bn0 / conv 1 / bn1 on this stream behind its conv-1 tail; this stream does
@@ -1224,10 +1252,6 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     // the user stream waits for the two weight-gradient streams' tails itself (its own tail is in
     // stream order) instead of for `joined`, which is one cross-queue hop further (wgrad stream 1 ->
     // wgrad stream 0 -> here); DCUE_LATE_JOIN=hop restores the hop (A/B)
-    static const bool hop = [] {
-      const char* e = getenv("DCUE_LATE_JOIN");
-      return e && e[0] == 'h';
-    }();
     if (hop) {
       TRY(wait_point(su, joined));
     } else {

@@ -291,6 +291,13 @@ struct TGemmArgs {
   unsigned* colmax;  // nullable: max |C| per column (ordered keys), the split-f16 wgrad's dz bound
 };
 int launch_tgemm(int ta, int tb, const TGemmArgs& g, hipStream_t s);
+// the user tower's forward in one launch (adam.hip k_user_fwd): deferred mode's row sync, then g1
+// (h1 = relu(E[users]) W1^T + b1) and g2 (uf = relu(h1) W2^T + b2) as launch_tgemm(1, 0, .) computes them
+int launch_user_fwd(const dcue_model* md, const TGemmArgs& g1, const TGemmArgs& g2, const int64_t* users, int B,
+                    hipStream_t s);
+// two independent GEMMs in one launch: g1 as launch_tgemm(0, 1, .) with a k-strided A, g2 as
+// launch_tgemm(0, 0, .) with a k-contiguous A; both with n-contiguous B (the user tower's backward)
+int launch_tgemm_pair(const TGemmArgs& g1, const TGemmArgs& g2, hipStream_t s);
 
 int launch_score_fwd(const float* uf, const float* f, const dcue_batch* b, int d, float margin,
                      float* scores, float* cosv, float* norms, float* hinge, float* loss,
@@ -319,6 +326,11 @@ int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float s
 int launch_adam(const dcue_model* m, const dcue_adam_args* a, const int64_t* poff, hipStream_t s,
                 bool flush_slice = true, long dense_lo = 0, long dense_hi = -1);
 int launch_emb_flush_rows(const dcue_model* m, int step, hipStream_t s);
+// deferred mode: launch_emb_grad + the user-table part of launch_adam (k_adam_touched) in one launch
+// (k_emb_grad_adam, adam.hip): the same compact rows and the same per-element Adam arithmetic; the
+// rolling-flush slice is left to the caller (plans issue it during the next step)
+int launch_emb_grad_adam(const dcue_model* m, const dcue_adam_args* a, const float* de, const int64_t* users, int B,
+                         float scale, hipStream_t s);
 // BN-free towers: mean 0, invstd = a = 1 for the six BN layers, plus the ones / zeros arrays
 int launch_bn_identity(float* const* mean, float* const* invstd, float* const* a, float* ones, float* zeros,
                        int cmax, int H, int D, hipStream_t s);

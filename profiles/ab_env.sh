@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B/C... of runtime environment switches in one GPU session: alternating bench runs, one per
-# variant per round (variant "-" = no extra environment).
+# variant per round (variant "-" = no extra environment). STEPS / WARMUP (default: the driver's
+# 20 / 5) and BENCH_EXTRA pass through to bench.py.
 #   gpurun -- 'bash profiles/ab_env.sh <tag> <rounds> <modes> "<env 1>" "<env 2>" ...'
 set -uo pipefail
 TAG=$1; ROUNDS=$2; MODES=$3; shift 3
@@ -12,7 +13,7 @@ for r in $(seq 1 $ROUNDS); do
   for E in "$@"; do
     i=$((i + 1))
     EV=$([ "$E" = "-" ] && echo "DCUE_AB_VARIANT=$i" || echo "$E")
-    env $EV timeout -k 10 200 python3 $ROOT/bench.py --no-cpu-baseline --no-eval --steps 200 --warmup 20 \
+    env $EV timeout -k 10 200 python3 $ROOT/bench.py --no-cpu-baseline --no-eval --no-f32-probe --steps ${STEPS:-20} --warmup ${WARMUP:-5} \
       --modes $MODES ${BENCH_EXTRA:-} > "$OUT/v${i}_$r.log" 2>&1 || exit 1
     python3 - "$OUT/v${i}_$r.log" "$EV" <<'PY' >> "$OUT/summary.txt"
 import json, sys
