@@ -939,8 +939,9 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   hipEvent_t ev_x0 = nullptr;
   const bool f16w = wgrad_f16_on();  // split-f16 weight gradients (conv_wgrad.hip)
   // split plans: Adam over bn0 / conv 1 / bn1 rides in the bn0-gradient launch (adam.hip
-  // k_bn0_grads_adam) instead of a launch of its own behind it (DCUE_FUSE_LATE_ADAM=0: separate)
-  const bool fuse_late = o.dense_split && o.dense_split->grad_div <= 1.0 && fuse_late_adam_on();
+  // k_bn0_grads_adam) instead of a launch of its own behind it (DCUE_FUSE_LATE_ADAM=0: separate);
+  // not under an exchange, whose Adam must wait for the all-reduced gradient
+  const bool fuse_late = o.dense_split && !o.comm && o.dense_split->grad_div <= 1.0 && fuse_late_adam_on();
   // the largest copy count of an item (in-batch: a positive drawn by every other row), the
   // split-f16 dz bounds' kD factor
   const double kd_max = b->layout == DCUE_LAYOUT_GATHER ? 1.0 + (double)B * N : 1.0;
@@ -1234,6 +1235,25 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     return e && e[0] == 'h';
   }();
   hipEvent_t joined = nullptr;
+  if (o.dense_split && o.comm) {
+    // data parallelism, split: each bucket's Adam waits only for its all-reduce (comm_exchange_split):
+    // the late segments' (every side stream's gradient) on the comm stream, then bn0 / conv 1 / bn1 on
+    // this stream after the early bucket; *late_done (the late Adam) is what the next forward's conv 2
+    // waits for, as without an exchange
+    dcue_adam_args dense = *o.dense_split;
+    dense.parts = DCUE_ADAM_DENSE;
+    const long late = c.poff[DCUE_SEG_LATE], n = c.poff[kSeg];
+    const hipEvent_t side[3] = {tail[1], tail[2], tail[3]};
+    hipEvent_t ld = ring_event(sp);
+    TRY(comm_exchange_split(o.comm, m, &dense, c.poff, late, n, side, 3, ld, s));
+    if (o.late_done) *o.late_done = ld;
+    TRY(launch_adam(m, &dense, c.poff, s, true, 0, late));
+    if (o.tails) {
+      o.tails[0] = tail[0];
+      o.tails[1] = nullptr;
+    }
+    return DCUE_OK;
+  }
   if (!o.dense_split || hop) {
     if (tail[1]) TRY(wait_point(sw[0], tail[1]));
     HPROF("capi:33");

@@ -124,6 +124,21 @@ int comm_exchange_step(dcue_comm* c, float* grad, long late, long n, hipEvent_t 
   return DCUE_OK;
 }
 
+int comm_exchange_split(dcue_comm* c, const dcue_model* m, const dcue_adam_args* dense, const int64_t* poff,
+                        long late, long n, const hipEvent_t* side, int nside, hipEvent_t late_done, hipStream_t s) {
+  for (int i = 0; i < nside; ++i)
+    if (side[i]) DCUE_HIP_CHECK(hipStreamWaitEvent(c->stream, side[i], 0));
+  TRY(comm_allreduce_sum(c, m->grads + late, n - late));
+  TRY(launch_adam(m, dense, poff, c->stream, true, late, n));  // the late segments' Adam, divide fused
+  DCUE_HIP_CHECK(hipEventRecord(late_done, c->stream));
+  DCUE_HIP_CHECK(hipEventRecord(c->ev_tail, s));
+  DCUE_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_tail, 0));
+  TRY(comm_allreduce_sum(c, m->grads, late));
+  DCUE_HIP_CHECK(hipEventRecord(c->ev_done, c->stream));
+  DCUE_HIP_CHECK(hipStreamWaitEvent(s, c->ev_done, 0));
+  return DCUE_OK;
+}
+
 // grad[0:n) /= world on `s` (DDP's grad.div_(world)), for steps whose optimizer does not fold the
 // divide into its sweep (plan launches followed by a separate optimizer call)
 int comm_divide(const dcue_comm* c, float* grad, long n, hipStream_t s) {
@@ -197,6 +212,26 @@ extern "C" int dcue_comm_destroy(dcue_comm* c) {
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+  return DCUE_OK;
+}
+
+extern "C" int dcue_comm_allgather(dcue_comm* c, float* buf, int64_t count, void* stream) {
+  if (!c || (!buf && count > 0) || count < 0) return DCUE_ERR_INVALID;
+  if (count == 0 || c->world == 1) return DCUE_OK;
+  hipStream_t s = (hipStream_t)stream;
+  DCUE_HIP_CHECK(hipEventRecord(c->ev_tail, s));
+  DCUE_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_tail, 0));
+  const size_t part = sizeof(float) * (size_t)count;
+  if (c->host_fn) {  // exact: every part is its owner's values plus zeros
+    if (c->rank > 0) DCUE_HIP_CHECK(hipMemsetAsync(buf, 0, part * c->rank, c->stream));
+    if (c->rank + 1 < c->world)
+      DCUE_HIP_CHECK(hipMemsetAsync(buf + (size_t)count * (c->rank + 1), 0, part * (c->world - c->rank - 1), c->stream));
+    TRY(host_allreduce(c, buf, count * c->world, DCUE_COMM_F32));
+  } else {
+    DCUE_NCCL_CHECK(ncclAllGather(buf + (size_t)count * c->rank, buf, (size_t)count, ncclFloat, c->nc, c->stream));
+  }
+  DCUE_HIP_CHECK(hipEventRecord(c->ev_done, c->stream));
+  DCUE_HIP_CHECK(hipStreamWaitEvent(s, c->ev_done, 0));
   return DCUE_OK;
 }
 

@@ -392,6 +392,12 @@ void timer_add_recorded(int cls, hipEvent_t a, hipEvent_t b);
 // RCCL exchange of a plan step (comm.hip): bucket grad[late:n) once `side_done`, then grad[0:late)
 // after the caller's stream `s`; `s` then waits for both
 int comm_exchange_step(dcue_comm* c, float* grad, long late, long n, hipEvent_t side_done, hipStream_t s);
+// the split plans' exchange (StepOpts::comm): the comm stream waits for the side streams' points
+// side[0..nside), all-reduces grad[late:n), runs Adam over it (dense, grad_div = world) and records
+// *late_done; then, after the caller's stream `s`, all-reduces grad[0:late), and `s` waits for it.
+// The caller then runs Adam over [0, late) on `s`.
+int comm_exchange_split(dcue_comm* c, const dcue_model* m, const dcue_adam_args* dense, const int64_t* poff,
+                        long late, long n, const hipEvent_t* side, int nside, hipEvent_t late_done, hipStream_t s);
 int comm_world(const dcue_comm* c);
 // SyncBN: n uint64 words (exact fixed-point BN accumulators, bnacc.h) summed over the ranks in place,
 // ordered on `s` (through the comm's stream, so every collective of a rank runs in issue order)
@@ -492,6 +498,11 @@ struct StepOpts {
   // writes it; alternating buffers keep that write off the one being read (step t+2's conv 1 is
   // ordered after it: its stream waited for step t's late Adam before step t+1's conv 2)
   float* y1 = nullptr;
+  // split plans with a communicator (data parallelism): the exchange runs inside the backward -- the
+  // late bucket all-reduced on the comm stream once the side streams' gradients are in and Adam over
+  // it right there (dense_split's grad_div = world), bn0 / conv 1 / bn1 after the early bucket on the
+  // caller's stream -- so each Adam waits only for its own bucket (comm_exchange_split)
+  dcue_comm* comm = nullptr;
 };
 // DCBR's MSE head: loss = sum over [M][d] of (f - y)^2 / (M d) (rows of width ld, the first d
 // columns), df = 2 (f - y) / (M d) into dfcopy ([M][ld], zero past d); rowsq [M]: the per-row sums

@@ -175,6 +175,7 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   o.wait_late = p->late_done;  // the previous split step's late Adam, before conv 2
   o.dense_split = dense_split;
   if (dense_split) o.y1 = p->y1[cur];
+  o.comm = dense_split ? p->comm : nullptr;  // the exchange inside the backward (comm_exchange_split)
   hipEvent_t late_done = nullptr;
   o.late_done = &late_done;
   // the previous step's rolling-flush slice runs after this step's user tower (StepOpts)
@@ -206,6 +207,16 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   p->last_stream = s;
   ++p->launches;
   return DCUE_OK;
+}
+
+// DCUE_SPLIT_COMM=0: data-parallel plan steps keep the unsplit exchange (both buckets, then the whole
+// dense Adam on the caller's stream) -- the A/B of comm_exchange_split
+bool split_comm_on() {
+  static const bool on = [] {
+    const char* e = getenv("DCUE_SPLIT_COMM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 // DCUE_SPLIT_ADAM=0 keeps the whole dense Adam on the caller's stream after the join (A/B)
@@ -391,7 +402,10 @@ extern "C" int dcue_plan_step(dcue_plan* p, const int64_t* users_src, const int3
   dcue_adam_args emb = *adam, dense = *adam;
   emb.parts = DCUE_ADAM_EMBEDDING;
   dense.parts = DCUE_ADAM_DENSE;
-  if (!p->comm && split_adam_on()) {  // one GPU: the dense Adam split over two streams (StepOpts)
+  if (split_adam_on() && (!p->comm || split_comm_on())) {
+    // the dense Adam split over two streams (StepOpts); with a communicator each part after its own
+    // bucket's all-reduce (comm_exchange_split), the divide by the world size fused into the sweep
+    if (p->comm) dense.grad_div = p->comm_world;
     TRY(issue_eager(p, users_src, item_track_src, (hipStream_t)stream, &emb, &dense));
     HPROF("plan_step:issue");
     return DCUE_OK;

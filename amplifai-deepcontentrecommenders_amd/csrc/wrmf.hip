@@ -19,7 +19,9 @@
 //                  registers (thread t owns G[t & 127][(t >> 7) * 64 + 0..63]); partials [chunk][d][d]
 //   k_wrmf_gram_reduce  the chunk partials in a fixed order (deterministic)
 //   k_wrmf_solve   one workgroup per row (grid-stride): A = G + lambda I + the row's rank-1 terms
-//                  and b in LDS, then an in-LDS Cholesky A = L L^T and the two triangular solves.
+//                  and b in LDS, then an in-LDS blocked Cholesky A = L L^T (16-column steps: a
+//                  register-resident diagonal factor, a panel solve, a rank-16 trailing update --
+//                  three barriers per 16 columns) and the two blocked triangular solves.
 // All of it in fp64: A's condition number is max eig(G + ...)/lambda, 1e4-1e6 for typical lambda,
 // which an fp32 Cholesky (or an fp32 Gram matrix) turns into 1e-3 relative errors. dim <= 128: A
 // is [128][129] doubles (132 KB, one workgroup per CU); the factors stay fp32 in HBM.
@@ -121,50 +123,116 @@ __global__ __launch_bounds__(256) void k_wrmf_solve(float* __restrict__ X, long 
       }
       __syncthreads();
     }
-    // Cholesky, right-looking, two barriers per column: every thread reads the pivot, the column
-    // below it is scaled, then the trailing lower triangle loses the column's outer product. The
-    // diagonal of L goes to dg[] (A[k][k] stays the pivot's square until every thread has read it)
-    for (int k = 0; k < dim; ++k) {
-      const wacc_t piv = sqrt(A[k * kWrmfPitch + k]);
-      const wacc_t inv = 1.0 / piv;
-      if (t == 0) dg[k] = inv;  // the solves multiply by 1 / L[k][k]
-      for (int i = k + 1 + t; i < dim; i += blockDim.x) A[i * kWrmfPitch + k] *= inv;
-      __syncthreads();
-      // 16 x 16 threads over (row, column) of the trailing lower triangle
-      for (int i = k + 1 + (t >> 4); i < dim; i += 16) {
-        const wacc_t lik = A[i * kWrmfPitch + k];
-        for (int j = k + 1 + (t & 15); j <= i; j += 16)
-          A[i * kWrmfPitch + j] = fma(-lik, A[j * kWrmfPitch + k], A[i * kWrmfPitch + j]);
-      }
-      __syncthreads();
-    }
-    // L y = b, then L^T x = y: wave 0 alone, lane l holding entries l and l + 64 in registers (no
-    // barriers; y_k / x_k broadcast by shuffle from the owning lane; x/L[k][k] as x * (1/L[k][k]),
-    // one rounding more than the division, far below the fp32 output's)
-    if (t < 64) {
-      wacc_t v0 = t < dim ? bv[t] : 0.0, v1 = t + 64 < dim ? bv[t + 64] : 0.0;
-      for (int k = 0; k < dim; ++k) {
-        const wacc_t own = k < 64 ? v0 : v1;
-        const wacc_t yk = __shfl(own, k & 63, 64) * dg[k];
-        if (t == (k & 63)) {
-          if (k < 64) v0 = yk; else v1 = yk;
-        }
-        if (t > k && t < dim) v0 = fma(-A[t * kWrmfPitch + k], yk, v0);
-        if (t + 64 > k && t + 64 < dim) v1 = fma(-A[(t + 64) * kWrmfPitch + k], yk, v1);
-      }
-      for (int k = dim - 1; k >= 0; --k) {
-        const wacc_t own = k < 64 ? v0 : v1;
-        const wacc_t xk = __shfl(own, k & 63, 64) * dg[k];
-        if (t == (k & 63)) {
-          if (k < 64) v0 = xk; else v1 = xk;
-        }
-        if (t < k) v0 = fma(-A[k * kWrmfPitch + t], xk, v0);
-        if (t + 64 < k) v1 = fma(-A[k * kWrmfPitch + t + 64], xk, v1);
-      }
-      if (t < dim) bv[t] = v0;
-      if (t + 64 < dim) bv[t + 64] = v1;
-    }
+    // Pad to D16 = dim rounded up to 16 with the identity (x = 0 there), then a blocked right-looking
+    // Cholesky A = L L^T, 16 columns per step, three barriers per step instead of two per column:
+    //  (1) wave 0 factors the 16 x 16 diagonal block in registers (lane i holds row i; pivots and
+    //      columns broadcast by shuffles, no barrier); 1 / L[k][k] goes to dg[];
+    //  (2) every row below solves its 16 panel entries against that block (one thread per row);
+    //  (3) the trailing lower triangle takes the panel's rank-16 update (16 x 16 thread tiles).
+    const int D16 = (dim + 15) & ~15;
+    for (int i = dim + (t >> 4); i < D16; i += 16)
+      for (int j = t & 15; j <= i; j += 16) A[i * kWrmfPitch + j] = i == j ? 1.0 : 0.0;
+    for (int c = dim + t; c < D16; c += blockDim.x) bv[c] = 0.0;
     __syncthreads();
+    const int ti = t >> 4, tj = t & 15;
+    for (int k0 = 0; k0 < D16; k0 += 16) {
+      if (t < 64) {
+        const int i = t & 15;
+        wacc_t row[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) row[j] = j <= i ? A[(k0 + i) * kWrmfPitch + k0 + j] : 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const wacc_t piv = sqrt(__shfl(row[k], k, 64));
+          const wacc_t inv = 1.0 / piv;
+          if (i == k) row[k] = piv;
+          if (i > k) row[k] *= inv;
+#pragma unroll
+          for (int j = k + 1; j < 16; ++j) {
+            const wacc_t ljk = __shfl(row[k], j, 64);  // L[j][k], scaled above
+            if (i >= j) row[j] = fma(-row[k], ljk, row[j]);
+          }
+          if (t == k) dg[k0 + k] = inv;
+        }
+        if (t < 16) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j)
+            if (j <= i) A[(k0 + i) * kWrmfPitch + k0 + j] = row[j];
+        }
+      }
+      __syncthreads();
+      for (int r = k0 + 16 + t; r < D16; r += blockDim.x) {  // panel: L[r][k0..k0+15]
+        wacc_t x[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) x[j] = A[r * kWrmfPitch + k0 + j];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          wacc_t v = x[j];
+#pragma unroll
+          for (int q = 0; q < j; ++q) v = fma(-x[q], A[(k0 + j) * kWrmfPitch + k0 + q], v);
+          x[j] = v * dg[k0 + j];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) A[r * kWrmfPitch + k0 + j] = x[j];
+      }
+      __syncthreads();
+      const int nb2 = (D16 - k0 - 16) >> 4;  // trailing 16-row blocks
+      for (int bi = 0; bi < nb2; ++bi)
+        for (int bj = 0; bj <= bi; ++bj) {
+          const int i = k0 + 16 + 16 * bi + ti, j = k0 + 16 + 16 * bj + tj;
+          if (j > i) continue;
+          wacc_t acc = A[i * kWrmfPitch + j];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc = fma(-A[i * kWrmfPitch + k0 + q], A[j * kWrmfPitch + k0 + q], acc);
+          A[i * kWrmfPitch + j] = acc;
+        }
+      __syncthreads();
+    }
+    // L y = b, then L^T x = y, blocked the same way: wave 0 solves a diagonal block (lane i holds
+    // entry i, the solved entries broadcast by shuffles), then every thread removes the block's
+    // contribution from the remaining rows (below for L, above for L^T)
+    for (int k0 = 0; k0 < D16; k0 += 16) {
+      if (t < 64) {
+        const int i = t & 15;
+        wacc_t y = bv[k0 + i];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const wacc_t yk = __shfl(y, k, 64) * dg[k0 + k];
+          if (i == k) y = yk;
+          else if (i > k) y = fma(-A[(k0 + i) * kWrmfPitch + k0 + k], yk, y);
+        }
+        if (t < 16) bv[k0 + i] = y;
+      }
+      __syncthreads();
+      for (int r = k0 + 16 + t; r < D16; r += blockDim.x) {
+        wacc_t v = bv[r];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v = fma(-A[r * kWrmfPitch + k0 + q], bv[k0 + q], v);
+        bv[r] = v;
+      }
+      __syncthreads();
+    }
+    for (int k0 = D16 - 16; k0 >= 0; k0 -= 16) {
+      if (t < 64) {
+        const int i = t & 15;
+        wacc_t x = bv[k0 + i];
+#pragma unroll
+        for (int k = 15; k >= 0; --k) {
+          const wacc_t xk = __shfl(x, k, 64) * dg[k0 + k];
+          if (i == k) x = xk;
+          else if (i < k) x = fma(-A[(k0 + k) * kWrmfPitch + k0 + i], xk, x);  // L^T[i][k] = L[k][i]
+        }
+        if (t < 16) bv[k0 + i] = x;
+      }
+      __syncthreads();
+      for (int r = t; r < k0; r += blockDim.x) {
+        wacc_t v = bv[r];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v = fma(-A[(k0 + q) * kWrmfPitch + r], bv[k0 + q], v);
+        bv[r] = v;
+      }
+      __syncthreads();
+    }
     for (int c = t; c < dim; c += blockDim.x) X[r * dim + c] = (float)bv[c];
     __syncthreads();  // bv and A are rewritten by the next row
   }

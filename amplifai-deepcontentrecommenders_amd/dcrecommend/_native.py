@@ -167,6 +167,7 @@ _SIGS = {
                               ctypes.c_int),
     "dcue_comm_destroy": ([_P], ctypes.c_int),
     "dcue_comm_allreduce_mean": ([_P, _P, ctypes.c_int64, _P], ctypes.c_int),
+    "dcue_comm_allgather": ([_P, _P, ctypes.c_int64, _P], ctypes.c_int),
     "dcue_plan_set_comm": ([_P, _P], ctypes.c_int),
     "dcue_plan_set_sync_bn": ([_P, ctypes.c_int32], ctypes.c_int),
     "dcue_timer_enable": ([ctypes.c_int32, ctypes.c_int32], ctypes.c_int),

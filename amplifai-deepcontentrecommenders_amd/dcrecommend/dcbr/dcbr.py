@@ -27,7 +27,11 @@ class DCBR:
     `target` [M, feature_dim] factors and returns the batch loss (a device scalar)."""
 
     def __init__(self, feature_dim=128, conv_hidden=128, model_type="truedcuemel1dbn", lr=1e-3,
-                 betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, device="cuda"):
+                 betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, device="cuda", comm=None):
+        """comm (distributed.NativeComm / HostComm): data parallelism -- each rank steps its own item
+        batches and the dense gradient is averaged over the ranks before Adam (DDP semantics,
+        per-replica BatchNorm), so every rank keeps the same ConvNet."""
+        self.comm = comm
         # the ConvNet is DCUENet's item tower; its user tower (one row) is carried but never used
         self.net = DCUENet({"feature_dim": feature_dim, "conv_hidden": conv_hidden, "user_embdim": 1,
                             "user_count": 1, "model_type": model_type}).to(device).train()
@@ -71,6 +75,8 @@ class DCBR:
 
     def step(self, tracks, item_track, target):
         loss = self.loss_and_grads(tracks, item_track, target)
+        if self.comm is not None and self.comm.world > 1:
+            self.comm.allreduce_mean_(self.net._flat["G"])  # the DDP mean of the dense gradient
         self.opt.step()
         return loss
 

@@ -33,9 +33,16 @@ class WRMF:
     or 1), preference 1 there and 0 elsewhere, L2 weight `regularization` on both factor sets.
 
     `fit(user_idx, item_idx, values=None)` runs `iterations` sweeps (users, then items) and leaves
-    `user_factors` [n_users, factors] and `item_factors` [n_items, factors] on the device."""
+    `user_factors` [n_users, factors] and `item_factors` [n_items, factors] on the device.
 
-    def __init__(self, factors=128, regularization=0.01, alpha=40.0, iterations=15, seed=0, device="cuda"):
+    Data parallelism (comm: a distributed.NativeComm / HostComm): every rank holds the whole
+    interaction set and both factor matrices; a half-step solves this rank's contiguous 1/world of
+    the rows (rows are independent, so each is solved exactly as on one GPU) and an in-place
+    all-gather (dcue_comm_allgather) hands every rank all of them before the next half-step. The
+    factor matrices are kept padded to a multiple of world rows (the pad rows have no pairs: 0)."""
+
+    def __init__(self, factors=128, regularization=0.01, alpha=40.0, iterations=15, seed=0, device="cuda",
+                 comm=None):
         if not 1 <= int(factors) <= 128:
             raise ValueError("factors must be in [1, 128] (the per-row solve holds a factors^2 matrix in LDS)")
         if not regularization > 0:
@@ -44,6 +51,10 @@ class WRMF:
         self.iterations, self.seed, self.device = int(iterations), int(seed), torch.device(device)
         self.user_factors = self.item_factors = None
         self._ws = None
+        self.comm = comm
+        self.world = comm.world if comm is not None else 1
+        self.rank = comm.rank if comm is not None else 0
+        self._uf = self._if = None  # the padded storage behind user_factors / item_factors
 
     def _workspace(self, n_fixed):
         nbytes = ctypes.c_size_t()
@@ -54,23 +65,44 @@ class WRMF:
         return self._ws
 
     def half_step(self, solve, fixed, csr):
-        """solve[r] <- the WRMF least-squares solution of row r with `fixed` held (in place)."""
+        """solve[r] <- the WRMF least-squares solution of row r with `fixed` held (in place). Under a
+        communicator, `solve` is a view of padded storage (user_factors / item_factors): this rank
+        solves its part of the rows, then every rank gathers the others'."""
         indptr, indices, values = csr
         if indptr.numel() != solve.shape[0] + 1:
             raise ValueError("the CSR has %d rows, the solved factors %d" % (indptr.numel() - 1, solve.shape[0]))
         if solve.shape[1] != self.factors or fixed.shape[1] != self.factors:
             raise ValueError("factor matrices must be [n, %d]" % self.factors)
         ws = self._workspace(fixed.shape[0])
-        nat.check(nat.lib().dcue_wrmf_half_step(
-            nat.ptr(solve), solve.shape[0], nat.ptr(fixed), fixed.shape[0], self.factors, nat.ptr(indptr),
-            nat.ptr(indices), nat.ptr(values), self.alpha, self.regularization, nat.ptr(ws), ws.numel(),
-            nat.stream_handle()), "dcue_wrmf_half_step")
+        n = solve.shape[0]
+        per = (n + self.world - 1) // self.world
+        r0, r1 = min(n, self.rank * per), min(n, (self.rank + 1) * per)
+        if r1 > r0:
+            nat.check(nat.lib().dcue_wrmf_half_step(
+                nat.ptr(solve[r0:r1]), r1 - r0, nat.ptr(fixed), fixed.shape[0], self.factors,
+                nat.ptr(indptr[r0:]), nat.ptr(indices), nat.ptr(values), self.alpha, self.regularization,
+                nat.ptr(ws), ws.numel(), nat.stream_handle()), "dcue_wrmf_half_step")
+        if self.world > 1:
+            full = self._storage(solve)
+            self.comm.allgather_(full[:per * self.world].view(-1))
         return solve
+
+    def _storage(self, view):
+        for buf in (self._uf, self._if):
+            if buf is not None and view.data_ptr() == buf.data_ptr():
+                return buf
+        raise ValueError("under a communicator, half_step solves user_factors or item_factors in place")
 
     def init_factors(self, n_users, n_items):
         g = torch.Generator(device="cpu").manual_seed(self.seed)
-        self.user_factors = (torch.randn(n_users, self.factors, generator=g) * 0.01).to(self.device)
-        self.item_factors = (torch.randn(n_items, self.factors, generator=g) * 0.01).to(self.device)
+        uf = (torch.randn(n_users, self.factors, generator=g) * 0.01).to(self.device)
+        itf = (torch.randn(n_items, self.factors, generator=g) * 0.01).to(self.device)
+        w = self.world
+        self._uf = torch.zeros(((n_users + w - 1) // w) * w, self.factors, device=self.device)
+        self._if = torch.zeros(((n_items + w - 1) // w) * w, self.factors, device=self.device)
+        self._uf[:n_users].copy_(uf)
+        self._if[:n_items].copy_(itf)
+        self.user_factors, self.item_factors = self._uf[:n_users], self._if[:n_items]
 
     def fit(self, user_idx, item_idx, values=None, n_users=None, n_items=None):
         u = torch.as_tensor(user_idx, device=self.device)

@@ -166,6 +166,16 @@ class NativeComm:
                   "dcue_comm_allreduce_mean")
         return t
 
+    def allgather_(self, t):
+        """In place: t holds world equal parts along dim 0, this rank's at index `rank`; afterwards
+        every rank holds all of them (dcue_comm_allgather)."""
+        from . import _native as nat
+        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous() or t.numel() % self.world:
+            raise ValueError("allgather_ needs a contiguous float32 GPU tensor of world equal parts")
+        nat.check(self._lib.dcue_comm_allgather(self.handle, nat.ptr(t), t.numel() // self.world,
+                                                nat.stream_handle()), "dcue_comm_allgather")
+        return t
+
     def close(self):
         if getattr(self, "handle", None) is not None:
             self._lib.dcue_comm_destroy(self.handle)

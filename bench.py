@@ -256,49 +256,60 @@ def row_flops(args, items_per_row):
 
 
 # --------------------------------------------------------------------------------- evaluation
-def dcbr_phase(args, tracks, pair_user, pair_track, n_users, dev, M):
+def dcbr_phase(args, tracks, pair_user, pair_track, n_users, dev, M, comm=None, world=1, rank=0):
     """BASELINE config 5 at this run's shape (no reference numbers exist: dcrecommend/dcbr is
     unpublished): WRMF (factors = d, alpha 40, lambda 0.1) on the interactions -- one untimed
     iteration, then two timed ALS iterations (users, then items) -- and the DCBR regression of the
-    item tower onto those factors, `warmup` + `steps` Adam steps over random M-item batches."""
+    item tower onto those factors, `warmup` + `steps` Adam steps over random M-item batches per
+    rank. N > 1 (comm: the library's communicator): every rank holds the same interactions, each
+    half-step solves 1/N of the rows and all-gathers them, and the regression averages its dense
+    gradient over the ranks before Adam (DDP) -- whole-job rates, the slowest rank's time."""
+    from dcrecommend import distributed as D
     from dcrecommend.dcbr import DCBR, WRMF
     d = args.feature_dim
-    w = WRMF(factors=d, regularization=0.1, alpha=40.0, iterations=1, seed=0, device=dev)
+    w = WRMF(factors=d, regularization=0.1, alpha=40.0, iterations=1, seed=0, device=dev, comm=comm)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     w.fit(pair_user, pair_track, None, n_users=n_users, n_items=args.tracks)
     torch.cuda.synchronize()
     t_fit1 = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(2):
         w.half_step(w.user_factors, w.item_factors, w.by_user)
         w.half_step(w.item_factors, w.user_factors, w.by_item)
     torch.cuda.synchronize()
-    t_iter = (time.perf_counter() - t0) / 2
-    gen = torch.Generator(device="cpu").manual_seed(17)
+    t_iter = D.max_over_ranks((time.perf_counter() - t0) / 2, dev)
+    gen = torch.Generator(device="cpu").manual_seed(17 + rank)
     n = args.warmup + args.steps
     items = torch.randint(0, args.tracks, (n, M), generator=gen, dtype=torch.int32).to(dev)
-    model = DCBR(feature_dim=d, conv_hidden=args.hidden, lr=1e-4, device=dev)
+    torch.manual_seed(3)  # the same ConvNet on every rank
+    model = DCBR(feature_dim=d, conv_hidden=args.hidden, lr=1e-4, device=dev, comm=comm)
     targets = w.item_factors
     losses = []
     for s in range(args.warmup):
         losses.append(model.step(tracks, items[s], targets[items[s].long()]))
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     for s in range(args.warmup, n):
         losses.append(model.step(tracks, items[s], targets[items[s].long()]))
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    dt = D.max_over_ranks(time.perf_counter() - t0, dev)
+    same, _, _ = D.replica_checksums(model.net._flat["P"])
     nnz = int(pair_user.shape[0])
     return {"workload": "WRMF d=%d over %d users x %d tracks, %d interactions; DCBR regression of the "
-                        "truedcuemel1dbn item tower (H=%d) onto the item factors, %d-item batches"
-                        % (d, n_users, args.tracks, nnz, args.hidden, M),
+                        "truedcuemel1dbn item tower (H=%d) onto the item factors, %d-item batches per GPU, %d GPU(s)"
+                        % (d, n_users, args.tracks, nnz, args.hidden, M, world),
             "wrmf_ms_per_iteration": t_iter * 1e3, "wrmf_rows_per_s": (n_users + args.tracks) / t_iter,
             "wrmf_first_iteration_ms_incl_csr_build": t_fit1 * 1e3,
-            "regression_ms_per_step": dt / args.steps * 1e3, "regression_items_per_s": M * args.steps / dt,
-            "loss_first": float(losses[0]), "loss_last": float(losses[-1]),
+            "regression_ms_per_step": dt / args.steps * 1e3, "regression_items_per_s": world * M * args.steps / dt,
+            "loss_first": float(losses[0]), "loss_last": float(losses[-1]), "replicas_identical": same,
             "parity": "unpinned against the reference (never published); pinned against oracle/wrmf_oracle.py "
-                      "and the fp64 oracle item tower (tests/test_gpu_dcbr.py)"}
+                      "and the fp64 oracle item tower (tests/test_gpu_dcbr.py); N>1 bit-exact with one rank "
+                      "(WRMF) and with an explicit all-reduce (regression), tests/test_gpu_dcbr_dp.py"}
 
 
 def evaluate_val(args, net, tracks, pair_user, pair_track, split, n_users, dev):
@@ -904,9 +915,17 @@ def main():
         del tplan, topt, tnet, tokens
     # ---- phase 5 (N = 1): the DCBR path (BASELINE config 5): WRMF target factors of
     # the same interactions, then the audio ConvNet regressing them (catalogue-sized item batches)
-    if "dcbr" in modes and world == 1 and args.feature_dim <= 128:
+    if "dcbr" in modes and (world == 1 or comm is not None) and args.feature_dim <= 128:
         mark("dcbr phase")
-        out["dcbr"] = dcbr_phase(args, tracks, pair_user, pair_track, n_users_local, dev, B * (1 + N))
+        if world == 1:
+            out["dcbr"] = dcbr_phase(args, tracks, pair_user, pair_track, n_users_local, dev, B * (1 + N))
+        else:  # every rank the same (global) interaction set, solved row-sharded
+            g_all = torch.Generator(device=dev).manual_seed(4242)
+            all_u = torch.randint(0, args.users, (args.interactions,), generator=g_all, device=dev)
+            all_t = torch.randint(0, args.tracks, (args.interactions,), generator=g_all, device=dev, dtype=torch.int64)
+            out["dcbr"] = dcbr_phase(args, tracks, all_u, all_t, args.users, dev, B * (1 + N), comm=comm,
+                                     world=world, rank=rank)
+            del all_u, all_t
     head = out.get("inbatch", out["inbatch_cold"])
     E = args.user_embdim
     result = {

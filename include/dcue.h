@@ -423,6 +423,11 @@ int dcue_comm_create_host(int32_t world, int32_t rank, dcue_host_allreduce_fn fn
 int dcue_comm_destroy(dcue_comm* comm);
 /* In-place mean over the ranks of n floats, ordered on `stream` (sum all-reduce, then / world). */
 int dcue_comm_allreduce_mean(dcue_comm* comm, float* buf, int64_t n, void* stream);
+/* In-place all-gather, ordered on `stream`: buf holds world * count floats, rank r's own part at
+ * buf[r * count, (r + 1) * count); afterwards every rank holds every part (RCCL: ncclAllGather; the
+ * host transport: the other parts zeroed, then the sum). The DCBR path's row-sharded WRMF half-steps
+ * (each rank solves its rows, every rank needs all of them as the next half-step's fixed side). */
+int dcue_comm_allgather(dcue_comm* comm, float* buf, int64_t count, void* stream);
 /* Bind (or, with NULL, unbind) a communicator to an eager plan. dcue_plan_step then exchanges the
  * dense gradient between the backward and Adam, in two buckets on the communicator's stream: the
  * gradients the side streams finish (everything after DCUE_SEG_LATE) as soon as they are in,
