@@ -69,17 +69,14 @@ SidePool* side_pool() {
 // now. The ring is long enough that no event is re-recorded before its waits are enqueued
 // (a step records fewer than 16 points).
 int fork_point(SidePool* p, hipStream_t from, hipEvent_t* ev) {
-  hipEvent_t e = p->ev[p->next];
-  p->next = (p->next + 1) % SidePool::kEvents;
+  hipEvent_t e = ring_event(p);
   DCUE_HIP_CHECK(hipEventRecord(e, from));
   *ev = e;
   return DCUE_OK;
 }
 
 hipEvent_t ring_event(SidePool* p) {
-  hipEvent_t e = p->ev[p->next];
-  p->next = (p->next + 1) % SidePool::kEvents;
-  return e;
+  return p->ev[p->next.fetch_add(1, std::memory_order_relaxed) % SidePool::kEvents];
 }
 
 LaunchTag& launch_tag() {
@@ -139,8 +136,7 @@ int wait_point(hipStream_t to, hipEvent_t ev) {
 // `to` waits for everything enqueued on `from` so far. An event is re-recorded only after the
 // wait on its previous record has been enqueued, so a small ring of events suffices.
 int stream_wait(SidePool* p, hipStream_t to, hipStream_t from) {
-  hipEvent_t e = p->ev[p->next];
-  p->next = (p->next + 1) % SidePool::kEvents;
+  hipEvent_t e = ring_event(p);
   DCUE_HIP_CHECK(hipEventRecord(e, from));
   DCUE_HIP_CHECK(hipStreamWaitEvent(to, e, 0));
   return DCUE_OK;
@@ -805,10 +801,15 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
     const char* e = getenv("DCUE_USER_EARLY");
     return e && e[0] == '1';
   }();
+  // with the side-issue thread (side.hip) the user tower is issued there, beside the item tower's issue
+  SideQueue side;
+  int ust = DCUE_OK;
+  const uint64_t useq = side.threaded() ? side.run(user_part, &ust) : 0;
   TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s,
                    o.prologue_done, o.input_stats_done && o.prologue_done, o.clear_bn0, o.wait_late,
-                   early ? &user_part : nullptr, o.sync_bn));
-  if (!early) TRY(user_part());
+                   early && !side.threaded() ? &user_part : nullptr, o.sync_bn));
+  if (!early && !side.threaded()) TRY(user_part());
+  TRY(side.wait(useq));
   TRY(wait_point(s, ev_uf));
   HPROF("capi:9");
   if (o.fuse_score) {
@@ -954,6 +955,193 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(fk.done());
   }
   if (c.text && !t->tokens) return DCUE_ERR_INVALID;
+  hipEvent_t tail[4] = {};  // caller's stream, user stream, wgrad streams 0 and 1
+  // user tower (userembedding.py:33-44 backward), the compact embedding rows, and -- when the step
+  // carries it -- the user table's Adam step (it needs nothing from the item tower)
+  auto user_bwd = [&]() -> int {
+    TRY(wait_point(su, ev_score));
+    HPROF("capi:26");
+    {
+      // two launches of two independent GEMMs each (launch_tgemm_pair; the same blocks as four
+      // launch_tgemm calls, so the same bits): (dW2, dh1) from du, then (dW1, de) from dh1
+      TGemmArgs g = {}, h = {};
+      // dW2[n][k] = sum_b du[b][n] relu(h1)[b][k]; db2[n] = sum_b du[b][n]
+      g.M = D; g.N = E; g.K = B;
+      g.A = w.du; g.sam = 1; g.sak = D;
+      g.B = w.h1; g.sbk = E; g.sbn = 1;
+      g.C = c.Gd(SEG_L2_W); g.scm = E; g.scn = 1;
+      g.rowsum = c.Gd(SEG_L2_B);
+      // dh1 = (du W2) * (h1 > 0)
+      h.M = B; h.N = E; h.K = D;
+      h.A = w.du; h.sam = D; h.sak = 1;
+      h.B = c.P(SEG_L2_W); h.sbk = E; h.sbn = 1;
+      h.C = w.dh1; h.scm = E; h.scn = 1;
+      h.cmask = w.h1; h.smm = E; h.smn = 1;
+      TRY(launch_tgemm_pair(g, h, su));
+      HPROF("capi:28");
+      // dW1[n][k] = sum_b dh1[b][n] relu(E[u_b])[k]; db1[n] = sum_b dh1[b][n]
+      g = TGemmArgs{};
+      g.M = E; g.N = E; g.K = B;
+      g.A = w.dh1; g.sam = 1; g.sak = E;
+      g.B = m->emb; g.sbk = E; g.sbn = 1; g.brow = b->users;
+      g.C = c.Gd(SEG_L1_W); g.scm = E; g.scn = 1;
+      g.rowsum = c.Gd(SEG_L1_B);
+      // de = (dh1 W1) * (E[u_b] > 0)
+      h = TGemmArgs{};
+      h.M = B; h.N = E; h.K = E;
+      h.A = w.dh1; h.sam = E; h.sak = 1;
+      h.B = c.P(SEG_L1_W); h.sbk = E; h.sbn = 1;
+      h.C = w.de; h.scm = E; h.scn = 1;
+      h.cmask = m->emb; h.smm = E; h.smn = 1; h.cmrow = b->users;
+      TRY(launch_tgemm_pair(g, h, su));
+      HPROF("capi:30");
+    }
+    // the step's end joins the user stream here: its Adam part (and the rolling flush slice) below
+    // needs nothing more from this step and runs on into the next one, ordered on this stream
+    // deferred user-table Adam with the step (plans): the compact rows and their Adam step in one
+    // launch (k_emb_grad_adam: each distinct user's workgroup sums its rows, then steps them)
+    const bool emb_fused = o.emb_adam && m->emb_step && o.defer_flush_slice;
+    {
+      ForkAfter fk(sp, su, &tail[1]);
+      if (emb_fused)
+        TRY(launch_emb_grad_adam(m, o.emb_adam, w.de, b->users, B, emb_grad_scale, su));
+      else
+        TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, m->emb_rows,
+                            m->emb_step ? m->emb_log : nullptr, su));
+      TRY(fk.done());
+      HPROF("capi:31");
+    }
+    if (o.emb_adam && !emb_fused) TRY(launch_adam(m, o.emb_adam, c.poff, su, !o.defer_flush_slice));
+    HPROF("capi:32");
+    return DCUE_OK;
+  };
+
+  // fc weight gradient of the res / text towers: dW[n][k] = sum_m df[m][n] xfc[m][k], db = sum df over the
+  // concatenated fc input (the other towers' fc rides in the layer 3-5 launch, below)
+  auto fc_text_wgrad = [&]() -> int {
+    TRY(wait_point(sw[1], ev_layer[5]));
+    HPROF("capi:23");
+    TGemmArgs g = {};
+    g.M = D; g.N = c.FI; g.K = M;
+    g.A = w.df; g.sam = 1; g.sak = D;
+    g.C = c.Gd(SEG_FC_W); g.scm = c.FI; g.scn = 1;
+    g.rowsum = c.Gd(SEG_FC_B);
+    g.B = w.xfc; g.sbk = c.FI; g.sbn = 1;
+    TRY(launch_tgemm(0, 0, g, sw[1]));
+    HPROF("capi:24");
+    // the text conv's weight and bias gradients (the max routes each gradient to one position)
+    if (c.text)
+      TRY(launch_text_wgrad(text_branch(c, t), b->item_track, M, w.dtp, w.tidx, w.twpart, c.Gd(SEG_TX_W),
+                            c.Gd(SEG_TX_B), sw[1]));
+    return DCUE_OK;
+  };
+
+  // (wgrad of layer l reads g_l, which dgrad l+1 produced: ev_layer[l]) layers 5..3 in one launch
+  // on wgrad stream 0 once dgrad 4 is done (beside dgrad 3-2); layer 2 on wgrad stream 1 (behind
+  // xhat0 and the fc weight gradient) once dgrad 3 is (beside dgrad 2 and the conv-1 tail); each
+  // + one reduce launch.
+  auto issue_multi = [&](int lo, int hi, bool with_fc, hipStream_t so, hipEvent_t after, hipEvent_t* tl) -> int {
+    TRY(wait_point(so, after));
+    WgradMulti mw = {};
+    if (with_fc) {  // fc: dW[n][k] = sum_m df[m][n] bn5(y5)[m][k], db = sum_m df (df final since item_grad)
+      const int j = mw.n++;
+      mw.layer[j] = 6;
+      WgradArgs& wa = mw.a[j];
+      wa.xsrc = w.y[5];
+      wa.x_mean = w.mean[5]; wa.x_a = w.a[5]; wa.x_beta = c.beta_bwd(w, 5);
+      wa.g_l = w.df;
+      wa.M = M; wa.cout = D; wa.cin = D;
+      wa.wpart = w.wpm[4]; wa.bpart = w.bpm[4];
+      if (f16w) {
+        wa.x_range = rng_at(w, 5); wa.g_range = grng_at(w, 6);
+      }
+      mw.nchunk[j] = wgrad_nchunk(6, M, D, D);
+      mw.dW[j] = c.Gd(SEG_FC_W);
+      mw.db[j] = c.Gd(SEG_FC_B);
+    }
+    for (int l = hi; l >= lo; --l) {
+      const LayerGeom gm = layer_geom(l);
+      const int j = mw.n++;
+      mw.layer[j] = l;
+      WgradArgs& wa = mw.a[j];
+      wa.xsrc = w.y[l - 1];
+      wa.item_track = b->item_track;
+      wa.x_mean = w.mean[l - 1]; wa.x_a = w.a[l - 1]; wa.x_beta = c.beta_bwd(w, l - 1);
+      wa.g_l = w.g[l]; wa.y_l = w.y[l]; wa.idx_l = w.idx[l];
+      wa.mean_l = w.mean[l]; wa.invstd_l = w.invstd[l]; wa.a_l = w.a[l];
+      wa.dz_acc = bn_acc(w.bnbacc, w.cmax, l); wa.dgamma = c.dgamma(w, l); wa.dbeta = c.dbeta(w, l);
+      wa.invN = c.bn ? (float)(1.0 / (copies * gm.lp)) : 0.f;
+      wa.bn_world = bn_world;
+      wa.counts = w.counts;
+      wa.M = M; wa.cout = l == 5 ? D : H; wa.cin = H;
+      wa.wpart = w.wpm[l - 2]; wa.bpart = w.bpm[l - 2];
+      if (f16w) {
+        wa.x_range = rng_at(w, l - 1); wa.y_range = rng_at(w, l); wa.g_range = grng_at(w, l);
+        wa.kd_max = (float)kd_max * wa.invN;
+      }
+      mw.nchunk[j] = wgrad_nchunk(l, M, wa.cout, wa.cin);
+      mw.dW[j] = c.Gd(seg_conv_w(l));
+      mw.db[j] = c.Gd(seg_conv_b(l));
+    }
+    ForkAfter fk(sp, so, tl);
+    TRY(launch_conv_wgrad_multi(mw, so));
+    return fk.done();
+  };
+
+  // the step's end. Split plans: the late segments' Adam (every gradient the side streams made) on the
+  // user stream once the two weight-gradient streams' tails are in -- the user stream's own tail is in
+  // stream order -- and bn0 / conv 1 / bn1 on this stream behind its conv-1 tail (unless it rode in
+  // the bn0-gradient launch); this stream does not wait for the late part (the next forward waits
+  // for *late_done before conv 2). Other steps: the join -- wgrad stream 0 collects the user
+  // stream's and wgrad stream 1's tails, and the caller's stream waits for it once (each
+  // cross-queue wait on a pending event costs the waiting queue ≈4 µs, measured; on the side
+  // stream that time is slack, on the caller's it is the step's). DCUE_LATE_JOIN=hop keeps the join
+  // in split plans too, for the A/B.
+  static const bool hop = [] {
+    const char* e = getenv("DCUE_LATE_JOIN");
+    return e && e[0] == 'h';
+  }();
+  hipEvent_t joined = nullptr;
+  dcue_adam_args dense = {};
+  if (o.dense_split) {
+    dense = *o.dense_split;
+    dense.parts = DCUE_ADAM_DENSE;
+  }
+  const long late = c.poff[DCUE_SEG_LATE];
+  auto late_part = [&]() -> int {
+    if (!o.dense_split || hop) {
+      if (tail[1]) TRY(wait_point(sw[0], tail[1]));
+      TRY(wait_point(sw[0], tail[3]));
+      TRY(fork_point(sp, sw[0], &joined));
+    }
+    if (o.dense_split) {
+      if (hop) {
+        TRY(wait_point(su, joined));
+      } else {
+        TRY(wait_point(su, tail[2]));
+        TRY(wait_point(su, tail[3]));
+      }
+      ForkAfter fk(sp, su, o.late_done);
+      TRY(launch_adam(m, &dense, c.poff, su, true, late, -1));
+      TRY(fk.done());
+    }
+    return DCUE_OK;
+  };
+
+  // Side-stream work on the side-issue thread (side.hip) when it runs: each part is posted as soon as
+  // the events it waits on are recorded on this thread, and runs beside the chain's issue below.
+  // Without it the parts are issued here after the chain, in critical-path order.
+  SideQueue side;
+  const bool thr = side.threaded();
+  int ist = DCUE_OK;
+  auto post = [&](std::function<int()> f) -> int {
+    side.run(std::move(f), &ist);
+    return ist;
+  };
+  auto multi_hi = [&]() { return issue_multi(3, 5, !c.res && !c.text, sw[0], ev_layer[3], &tail[2]); };
+  auto multi_2 = [&]() { return issue_multi(2, 2, false, sw[1], ev_layer[2], &tail[3]); };
+  // the user tower's backward needs only the score kernel's du
+  if (thr && !o.item_only) TRY(post(user_bwd));
   if (c.res || c.text) {  // df; then the fc input gradient split: g5 = df W[:, off5:] (+ BN5's sums) and
                           // the time-pooled blocks' dtp = df W[:, :4H] (text: the text features' df W[:, :C])
     TRY(launch_item_grad(w.dfcopy, b, D, w.df, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
@@ -974,6 +1162,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     ForkAfter fk(sp, s, &ev_layer[5]);
     TRY(launch_tgemm(0, 0, g, s));
     TRY(fk.done());
+    if (thr) TRY(post(fc_text_wgrad));
   } else {  // per-item feature gradients df, then (same kernel) the fc input gradient g5 = df W and BN5's sums
     // (no fork point here: the fc weight gradient waits with the layer 3-5 weight gradients, below)
     TRY(launch_item_grad(w.dfcopy, b, D, w.df, c.P(SEG_FC_W), w.g[5], bn_acc(w.bnbacc, w.cmax, 5),
@@ -1018,6 +1207,14 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
         launch_tag().missed = true;
       }
       TRY(fk.done());
+      if (thr && l - 1 == 3 && !fork_once()) TRY(post(multi_hi));
+      if (thr && l - 1 == 2) {
+        if (fork_once()) {
+          ev_layer[3] = ev_layer[2];
+          TRY(post(multi_hi));
+        }
+        TRY(post(multi_2));
+      }
     } else {
       TRY(launch_conv_dgrad(l, l == 5 ? D : H, ra, s));
       if (sync) TRY(comm_allreduce_u64(o.sync_bn, bn_acc(w.bnbacc, w.cmax, l - 1), 4L * w.cmax, s));
@@ -1086,166 +1283,34 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
                          c.Gd(seg_conv_b(1)), so));
     return fk.done();
   };
-  hipEvent_t tail[4] = {};  // caller's stream, user stream, wgrad streams 0 and 1
   // layer 1 (the step's tail) follows the chain on the caller's stream, issued right away
   if (ev_x0) TRY(wait_point(s, ev_x0));
-  if (o.wait_inputs) TRY(wait_point(s, o.wait_inputs));
+  if (o.wait_inputs) {
+    TRY(side.wait(o.wait_inputs_seq));
+    TRY(wait_point(s, o.wait_inputs));
+  }
   TRY(issue_wgrad(1, s, 2, &tail[0]));
   HPROF("capi:22");
 
-  if (c.res || c.text) {  // fc weight gradient of the res / text towers: dW[n][k] = sum_m df[m][n] xfc[m][k],
-    // db = sum df over the concatenated fc input (the other towers' fc rides in the layer 3-5 launch, below)
-    TRY(wait_point(sw[1], ev_layer[5]));
-    HPROF("capi:23");
-    TGemmArgs g = {};
-    g.M = D; g.N = c.FI; g.K = M;
-    g.A = w.df; g.sam = 1; g.sak = D;
-    g.C = c.Gd(SEG_FC_W); g.scm = c.FI; g.scn = 1;
-    g.rowsum = c.Gd(SEG_FC_B);
-    g.B = w.xfc; g.sbk = c.FI; g.sbn = 1;
-    TRY(launch_tgemm(0, 0, g, sw[1]));
-    HPROF("capi:24");
-    // the text conv's weight and bias gradients (the max routes each gradient to one position)
-    if (c.text)
-      TRY(launch_text_wgrad(text_branch(c, t), b->item_track, M, w.dtp, w.tidx, w.twpart, c.Gd(SEG_TX_W),
-                            c.Gd(SEG_TX_B), sw[1]));
+  if (!thr) {
+    if (c.res || c.text) TRY(fc_text_wgrad());
+    if (fork_once()) ev_layer[3] = ev_layer[2];
+    TRY(multi_hi());
+    TRY(multi_2());
+    HPROF("capi:25");
+    if (!o.item_only) TRY(user_bwd());
+    HPROF("capi:32");
   }
-  // (wgrad of layer l reads g_l, which dgrad l+1 produced: ev_layer[l]) layers 5..3 in one launch
-  // on wgrad stream 0 once dgrad 4 is done (beside dgrad 3-2); layer 2 on wgrad stream 1 (behind
-  // xhat0 and the fc weight gradient) once dgrad 3 is (beside dgrad 2 and the conv-1 tail); each
-  // + one reduce launch.
-  auto issue_multi = [&](int lo, int hi, bool with_fc, hipStream_t so, hipEvent_t after, hipEvent_t* tl) -> int {
-    TRY(wait_point(so, after));
-    WgradMulti mw = {};
-    if (with_fc) {  // fc: dW[n][k] = sum_m df[m][n] bn5(y5)[m][k], db = sum_m df (df final since item_grad)
-      const int j = mw.n++;
-      mw.layer[j] = 6;
-      WgradArgs& wa = mw.a[j];
-      wa.xsrc = w.y[5];
-      wa.x_mean = w.mean[5]; wa.x_a = w.a[5]; wa.x_beta = c.beta_bwd(w, 5);
-      wa.g_l = w.df;
-      wa.M = M; wa.cout = D; wa.cin = D;
-      wa.wpart = w.wpm[4]; wa.bpart = w.bpm[4];
-      if (f16w) {
-        wa.x_range = rng_at(w, 5); wa.g_range = grng_at(w, 6);
-      }
-      mw.nchunk[j] = wgrad_nchunk(6, M, D, D);
-      mw.dW[j] = c.Gd(SEG_FC_W);
-      mw.db[j] = c.Gd(SEG_FC_B);
-    }
-    for (int l = hi; l >= lo; --l) {
-      const LayerGeom gm = layer_geom(l);
-      const int j = mw.n++;
-      mw.layer[j] = l;
-      WgradArgs& wa = mw.a[j];
-      wa.xsrc = w.y[l - 1];
-      wa.item_track = b->item_track;
-      wa.x_mean = w.mean[l - 1]; wa.x_a = w.a[l - 1]; wa.x_beta = c.beta_bwd(w, l - 1);
-      wa.g_l = w.g[l]; wa.y_l = w.y[l]; wa.idx_l = w.idx[l];
-      wa.mean_l = w.mean[l]; wa.invstd_l = w.invstd[l]; wa.a_l = w.a[l];
-      wa.dz_acc = bn_acc(w.bnbacc, w.cmax, l); wa.dgamma = c.dgamma(w, l); wa.dbeta = c.dbeta(w, l);
-      wa.invN = c.bn ? (float)(1.0 / (copies * gm.lp)) : 0.f;
-      wa.bn_world = bn_world;
-      wa.counts = w.counts;
-      wa.M = M; wa.cout = l == 5 ? D : H; wa.cin = H;
-      wa.wpart = w.wpm[l - 2]; wa.bpart = w.bpm[l - 2];
-      if (f16w) {
-        wa.x_range = rng_at(w, l - 1); wa.y_range = rng_at(w, l); wa.g_range = grng_at(w, l);
-        wa.kd_max = (float)kd_max * wa.invN;
-      }
-      mw.nchunk[j] = wgrad_nchunk(l, M, wa.cout, wa.cin);
-      mw.dW[j] = c.Gd(seg_conv_w(l));
-      mw.db[j] = c.Gd(seg_conv_b(l));
-    }
-    ForkAfter fk(sp, so, tl);
-    TRY(launch_conv_wgrad_multi(mw, so));
-    return fk.done();
-  };
-  if (fork_once()) ev_layer[3] = ev_layer[2];
-  TRY(issue_multi(3, 5, !c.res && !c.text, sw[0], ev_layer[3], &tail[2]));
-  TRY(issue_multi(2, 2, false, sw[1], ev_layer[2], &tail[3]));
-  HPROF("capi:25");
-  // user tower (userembedding.py:33-44 backward), the compact embedding rows, and -- when the step
-  // carries it -- the user table's Adam step (it needs nothing from the item tower)
-  if (!o.item_only) {
-  TRY(wait_point(su, ev_score));
-  HPROF("capi:26");
-  {
-    // two launches of two independent GEMMs each (launch_tgemm_pair; the same blocks as four
-    // launch_tgemm calls, so the same bits): (dW2, dh1) from du, then (dW1, de) from dh1
-    TGemmArgs g = {}, h = {};
-    // dW2[n][k] = sum_b du[b][n] relu(h1)[b][k]; db2[n] = sum_b du[b][n]
-    g.M = D; g.N = E; g.K = B;
-    g.A = w.du; g.sam = 1; g.sak = D;
-    g.B = w.h1; g.sbk = E; g.sbn = 1;
-    g.C = c.Gd(SEG_L2_W); g.scm = E; g.scn = 1;
-    g.rowsum = c.Gd(SEG_L2_B);
-    // dh1 = (du W2) * (h1 > 0)
-    h.M = B; h.N = E; h.K = D;
-    h.A = w.du; h.sam = D; h.sak = 1;
-    h.B = c.P(SEG_L2_W); h.sbk = E; h.sbn = 1;
-    h.C = w.dh1; h.scm = E; h.scn = 1;
-    h.cmask = w.h1; h.smm = E; h.smn = 1;
-    TRY(launch_tgemm_pair(g, h, su));
-    HPROF("capi:28");
-    // dW1[n][k] = sum_b dh1[b][n] relu(E[u_b])[k]; db1[n] = sum_b dh1[b][n]
-    g = TGemmArgs{};
-    g.M = E; g.N = E; g.K = B;
-    g.A = w.dh1; g.sam = 1; g.sak = E;
-    g.B = m->emb; g.sbk = E; g.sbn = 1; g.brow = b->users;
-    g.C = c.Gd(SEG_L1_W); g.scm = E; g.scn = 1;
-    g.rowsum = c.Gd(SEG_L1_B);
-    // de = (dh1 W1) * (E[u_b] > 0)
-    h = TGemmArgs{};
-    h.M = B; h.N = E; h.K = E;
-    h.A = w.dh1; h.sam = E; h.sak = 1;
-    h.B = c.P(SEG_L1_W); h.sbk = E; h.sbn = 1;
-    h.C = w.de; h.scm = E; h.scn = 1;
-    h.cmask = m->emb; h.smm = E; h.smn = 1; h.cmrow = b->users;
-    TRY(launch_tgemm_pair(g, h, su));
-    HPROF("capi:30");
-  }
-  // the step's end joins the user stream here: its Adam part (and the rolling flush slice) below
-  // needs nothing more from this step and runs on into the next one, ordered on this stream
-  // deferred user-table Adam with the step (plans): the compact rows and their Adam step in one
-  // launch (k_emb_grad_adam: each distinct user's workgroup sums its rows, then steps them)
-  const bool emb_fused = o.emb_adam && m->emb_step && o.defer_flush_slice;
-  {
-    ForkAfter fk(sp, su, &tail[1]);
-    if (emb_fused)
-      TRY(launch_emb_grad_adam(m, o.emb_adam, w.de, b->users, B, emb_grad_scale, su));
-    else
-      TRY(launch_emb_grad(w.de, b->users, B, E, emb_grad_scale, m->emb_grad, m->emb_slot, m->emb_rows,
-                          m->emb_step ? m->emb_log : nullptr, su));
-    TRY(fk.done());
-    HPROF("capi:31");
-  }
-  if (o.emb_adam && !emb_fused) TRY(launch_adam(m, o.emb_adam, c.poff, su, !o.defer_flush_slice));
-  HPROF("capi:32");
-  }  // !item_only
-
-  // the join: wgrad stream 0 collects the user stream's and wgrad stream 1's tails, and the caller's
-  // stream waits for it once (each cross-queue wait on a pending event costs the waiting queue
-  // ≈4 µs, measured; on the side stream that time is slack, on the caller's it is the step's).
-  // Split plans need no join (their late Adam waits for the two weight-gradient tails itself, and
-  // nothing else reads `joined`): its two waits and one record are host time saved on every step
-  // (DCUE_LATE_JOIN=hop keeps it, for the A/B below).
-  static const bool hop = [] {
-    const char* e = getenv("DCUE_LATE_JOIN");
-    return e && e[0] == 'h';
-  }();
-  hipEvent_t joined = nullptr;
   if (o.dense_split && o.comm) {
     // data parallelism, split: each bucket's Adam waits only for its all-reduce (comm_exchange_split):
     // the late segments' (every side stream's gradient) on the comm stream, then bn0 / conv 1 / bn1 on
     // this stream after the early bucket; *late_done (the late Adam) is what the next forward's conv 2
     // waits for, as without an exchange
-    dcue_adam_args dense = *o.dense_split;
-    dense.parts = DCUE_ADAM_DENSE;
-    const long late = c.poff[DCUE_SEG_LATE], n = c.poff[kSeg];
-    const hipEvent_t side[3] = {tail[1], tail[2], tail[3]};
+    TRY(side.drain());
+    const long n = c.poff[kSeg];
+    const hipEvent_t sides[3] = {tail[1], tail[2], tail[3]};
     hipEvent_t ld = ring_event(sp);
-    TRY(comm_exchange_split(o.comm, m, &dense, c.poff, late, n, side, 3, ld, s));
+    TRY(comm_exchange_split(o.comm, m, &dense, c.poff, late, n, sides, 3, ld, s));
     if (o.late_done) *o.late_done = ld;
     TRY(launch_adam(m, &dense, c.poff, s, true, 0, late));
     if (o.tails) {
@@ -1254,39 +1319,14 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     }
     return DCUE_OK;
   }
-  if (!o.dense_split || hop) {
-    if (tail[1]) TRY(wait_point(sw[0], tail[1]));
-    HPROF("capi:33");
-    TRY(wait_point(sw[0], tail[3]));
-    HPROF("capi:34");
-    TRY(fork_point(sp, sw[0], &joined));
-    HPROF("capi:35");
-  }
+  TRY(post(late_part));
   if (o.dense_split) {
-    // split dense Adam: the late segments (every gradient the side streams made) on the user stream
-    // once they are in, bn0 / conv 1 / bn1 on this stream behind its conv-1 tail; this stream does
-    // not wait for the join (the next forward waits for *late_done before conv 2)
-    dcue_adam_args dense = *o.dense_split;
-    dense.parts = DCUE_ADAM_DENSE;
-    const long late = c.poff[DCUE_SEG_LATE];
-    // the user stream waits for the two weight-gradient streams' tails itself (its own tail is in
-    // stream order) instead of for `joined`, which is one cross-queue hop further (wgrad stream 1 ->
-    // wgrad stream 0 -> here); DCUE_LATE_JOIN=hop restores the hop (A/B)
-    if (hop) {
-      TRY(wait_point(su, joined));
-    } else {
-      TRY(wait_point(su, tail[2]));
-      TRY(wait_point(su, tail[3]));
-    }
-    {
-      ForkAfter fk(sp, su, o.late_done);
-      TRY(launch_adam(m, &dense, c.poff, su, true, late, -1));
-      TRY(fk.done());
-    }
     if (!fuse_late) TRY(launch_adam(m, &dense, c.poff, s, true, 0, late));
   } else {
+    TRY(side.drain());
     TRY(wait_point(s, joined));
   }
+  TRY(side.drain());
   HPROF("capi:36");
   if (o.tails) {
     o.tails[0] = tail[0];

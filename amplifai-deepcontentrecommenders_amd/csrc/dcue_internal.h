@@ -1,7 +1,10 @@
 // Internal launch interfaces shared by the libdcue_hip translation units.
 #pragma once
 
+#include <atomic>
 #include <vector>
+
+#include <functional>
 
 #include "dcue_common.h"
 #include "bnacc.h"
@@ -11,10 +14,11 @@
 namespace dcue {
 bool host_profile_on();
 void host_profile_mark(const char* label);
+bool on_side_worker();  // side.hip: this thread is the side-issue worker
 }  // namespace dcue
 #define HPROF(label)                                          \
   do {                                                        \
-    if (::dcue::host_profile_on()) ::dcue::host_profile_mark(label); \
+    if (::dcue::host_profile_on() && !::dcue::on_side_worker()) ::dcue::host_profile_mark(label); \
   } while (0)
 
 // propagate a non-zero dcue_status
@@ -422,7 +426,7 @@ struct SidePool {
   hipStream_t st[3] = {nullptr, nullptr, nullptr};
   static constexpr int kEvents = 512;
   hipEvent_t ev[kEvents] = {};
-  int next = 0;
+  std::atomic<unsigned> next{0};  // fork_point / ring_event: both host threads (side.hip) take events
 };
 SidePool* side_pool();
 int stream_wait(SidePool* p, hipStream_t to, hipStream_t from);
@@ -453,10 +457,33 @@ class ForkAfter {
 int wait_point(hipStream_t to, hipEvent_t ev);
 int join_user_stream(hipStream_t s);
 
+// Side-stream issue on a second host thread (side.hip). run(fn) posts fn to the device's worker
+// (FIFO) and returns its sequence number, or runs it here (returning 0, status in *inline_status)
+// when the worker is off (DCUE_SIDE_THREAD=0), under stream capture, or on the worker itself.
+// wait(seq): fn and everything posted before it have been issued; returns the first error a
+// closure reported. The destructor waits for everything this queue posted.
+class SideQueue {
+ public:
+  explicit SideQueue(bool enable = true);
+  ~SideQueue();
+  SideQueue(const SideQueue&) = delete;
+  SideQueue& operator=(const SideQueue&) = delete;
+  bool threaded() const { return impl_ != nullptr; }
+  uint64_t run(std::function<int()> fn, int* inline_status);
+  int wait(uint64_t seq);
+  int drain();
+
+ private:
+  void* impl_ = nullptr;
+  uint64_t last_ = 0;
+};
+bool on_side_worker();
+
 // ------------------------------------------------------------- step implementation (capi.hip)
 struct StepOpts {
   hipEvent_t wait_inputs = nullptr;  // plans: the next step's prepared inputs; the caller's stream
                                      // waits for it before the conv-1 weight gradient
+  uint64_t wait_inputs_seq = 0;      // ... once the side-issue thread has recorded it (SideQueue)
   dcue_comm* sync_bn = nullptr;  // SyncBN: BatchNorm sums all-reduced over this communicator's ranks
   bool prologue_done = false;  // counts written + accumulators cleared by the prologue
   bool fuse_score = false;     // train forward also runs the hinge backward (k_score_fused)

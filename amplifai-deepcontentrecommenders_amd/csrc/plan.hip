@@ -122,7 +122,10 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   // the caller's stream waited for everything on that stream before step t was issued)
   // the next step's inputs + what the caller sees of this one, once the last step is over (its
   // side-stream part is ordered before this point on wgrad stream 0 itself)
-  if (p->tails[0]) TRY(wait_point(sa, p->tails[0]));
+  // (with the side-issue thread, side.hip, the two wgrad-stream parts below -- this prologue and the
+  // lookahead after the forward -- are issued there)
+  SideQueue side;
+  int sst = DCUE_OK;
   {
     StepPrologue q = inputs(nxt);
     if (inbatch) {
@@ -134,7 +137,12 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
     }
     q.users_dst = const_cast<int64_t*>(b0.users); q.users_src = users_src;
     q.items_dst = const_cast<int32_t*>(b0.item_track); q.items_src = items_src;
-    TRY(launch_step_prologue(q, sa));
+    const hipEvent_t last = p->tails[0];
+    side.run([q, sa, last]() -> int {
+      if (last) TRY(wait_point(sa, last));
+      return launch_step_prologue(q, sa);
+    }, &sst);
+    TRY(sst);
     HPROF("plan:3");
   }
   dcue_batch b = b0;
@@ -189,16 +197,26 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   // caller's, written in the caller's stream order: wait for this step's score kernel (a fork point
   // the step records anyway), which comes after everything the caller enqueued before this launch.
   p->ahead_items[nxt] = nullptr;
-  if (p->next_items && p->xh[nxt] && score_done) {
-    TRY(wait_point(sa, score_done));
-    TRY(ahead_item_inputs(&p->model, &b0, &p->tracks, p->next_items, p->counts[nxt], p->acc[nxt], p->xh[nxt], sa));
-    p->ahead_items[nxt] = p->next_items;
-  }
+  const bool look = p->next_items && p->xh[nxt] && score_done;
+  if (look) p->ahead_items[nxt] = p->next_items;
+  p->inputs_ready = ring_event(sp);  // slot nxt's inputs, for the next launch (recorded below)
+  const uint64_t iseq = side.run([p, sa, nxt, look, score_done, ir = p->inputs_ready]() -> int {
+    if (look) {
+      TRY(wait_point(sa, score_done));
+      TRY(ahead_item_inputs(&p->model, &p->batch, &p->tracks, p->ahead_items[nxt], p->counts[nxt], p->acc[nxt],
+                            p->xh[nxt], sa));
+    }
+    DCUE_HIP_CHECK(hipEventRecord(ir, sa));
+    return DCUE_OK;
+  }, &sst);
+  TRY(sst);
   p->next_items = nullptr;
-  TRY(fork_point(sp, sa, &p->inputs_ready));  // slot nxt's inputs, for the next launch
   if (inputs_wait == 1) {
     o.wait_inputs = p->inputs_ready;
+    o.wait_inputs_seq = iseq;
     p->inputs_ready = nullptr;
+  } else {
+    TRY(side.wait(iseq));
   }
   TRY(backward_impl(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, nullptr, p->cfg.emb_grad_scale, o, s));
   HPROF("plan:5");

@@ -3,13 +3,14 @@
 // stride-th launch of the class. Under stream capture the
 // launch's graph node and its predecessors are noted instead; the plan adds event-record nodes
 // around the kernel node and re-points them at fresh events on every launch (plan.hip), so each
-// replay is timed. Single host thread per process (the
-// library's usage model: one process per GPU).
+// replay is timed. One lock guards the state: the side-issue worker (side.hip) times its launches
+// too.
 #include <stdio.h>
 #include <stdlib.h>
 
 #include <chrono>
 #include <map>
+#include <mutex>
 #include <string>
 
 #include <utility>
@@ -31,9 +32,15 @@ TimerState& ts() {
   static TimerState s;
   return s;
 }
+// the side-issue worker (side.hip) times its own launches: one lock around the shared state
+std::recursive_mutex& tmu() {
+  static std::recursive_mutex m;
+  return m;
+}
 }  // namespace
 
 hipEvent_t timer_event() {
+  std::lock_guard<std::recursive_mutex> lk(tmu());
   TimerState& t = ts();
   if (!t.pool.empty()) {
     hipEvent_t e = t.pool.back();
@@ -47,14 +54,16 @@ hipEvent_t timer_event() {
   return e;
 }
 
-void timer_add_recorded(int cls, hipEvent_t a, hipEvent_t b) { ts().recorded[cls].emplace_back(a, b); }
+void timer_add_recorded(int cls, hipEvent_t a, hipEvent_t b) { std::lock_guard<std::recursive_mutex> lk(tmu()); ts().recorded[cls].emplace_back(a, b); }
 
 bool timer_take_turn(int cls) {
+  std::lock_guard<std::recursive_mutex> lk(tmu());
   if (cls < 0 || cls >= DCUE_N_TIMED || !ts().stride[cls]) return false;
   return ts().seen[cls]++ % ts().stride[cls] == 0;
 }
 
 int timer_begin(TimerScope* sc, int cls, hipStream_t s) {
+  std::lock_guard<std::recursive_mutex> lk(tmu());
   sc->cls = cls;
   sc->s = s;
   sc->a = sc->b = nullptr;
@@ -81,6 +90,7 @@ int timer_begin(TimerScope* sc, int cls, hipStream_t s) {
 }
 
 int timer_end(TimerScope* sc) {
+  std::lock_guard<std::recursive_mutex> lk(tmu());
   if (sc->capturing) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     const hipGraphNode_t* deps = nullptr;
@@ -105,12 +115,14 @@ int timer_end(TimerScope* sc) {
 }
 
 std::vector<CapturedTimer> timer_take_captured() {
+  std::lock_guard<std::recursive_mutex> lk(tmu());
   std::vector<CapturedTimer> out;
   out.swap(ts().captured);
   return out;
 }
 
 void timer_release(hipEvent_t e) {
+  std::lock_guard<std::recursive_mutex> lk(tmu());
   if (e) ts().pool.push_back(e);
 }
 
@@ -173,6 +185,7 @@ extern "C" const char* dcue_last_error(void) { return dcue::g_last_error; }
 extern "C" int dcue_timer_enable(int32_t kernel, int32_t enable) {
   if (kernel < 0 || kernel >= DCUE_N_TIMED) return DCUE_ERR_INVALID;
   if (enable < 0) return DCUE_ERR_INVALID;
+  std::lock_guard<std::recursive_mutex> lk(dcue::tmu());
   dcue::ts().stride[kernel] = enable;
   dcue::ts().seen[kernel] = 0;
   return DCUE_OK;
@@ -180,6 +193,7 @@ extern "C" int dcue_timer_enable(int32_t kernel, int32_t enable) {
 
 extern "C" int dcue_timer_read(int32_t kernel, double* total_ms_host, int64_t* launches_host) {
   if (kernel < 0 || kernel >= DCUE_N_TIMED || !total_ms_host || !launches_host) return DCUE_ERR_INVALID;
+  std::lock_guard<std::recursive_mutex> lk(dcue::tmu());
   auto& rec = dcue::ts().recorded[kernel];
   double total = 0.0;
   int64_t n = 0;
