@@ -18,18 +18,14 @@
 //   k_wrmf_gram    G = F^T F over row chunks: a workgroup sums its chunk's rank-1 terms in
 //                  registers (thread t owns G[t & 127][(t >> 7) * 64 + 0..63]); partials [chunk][d][d]
 //   k_wrmf_gram_reduce  the chunk partials in a fixed order (deterministic)
-//   k_wrmf_solve   one workgroup per row (grid-stride): A = G + lambda I + the row's rank-1 terms
-//                  and b in LDS, then an in-LDS blocked Cholesky A = L L^T (16-column steps: a
-//                  register-resident diagonal factor, a panel solve, a rank-16 trailing update --
-//                  three barriers per 16 columns) and the two blocked triangular solves.
+//   k_wrmf_solve   one workgroup per row (grid-stride): A and b accumulated in register tiles, a
+//                  right-looking Cholesky of [[A, b], [b^T, *]] (16-column steps) whose last row
+//                  is L^{-1} b, then L^T x = y (see the kernel)
 // All of it in fp64: A's condition number is max eig(G + ...)/lambda, 1e4-1e6 for typical lambda,
-// which an fp32 Cholesky (or an fp32 Gram matrix) turns into 1e-3 relative errors. dim <= 128: A
-// is [128][129] doubles (132 KB, one workgroup per CU); the factors stay fp32 in HBM.
+// which an fp32 Cholesky (or an fp32 Gram matrix) turns into 1e-3 relative errors. dim <= 128; the
+// factors stay fp32 in HBM.
 #include "dcue_internal.h"
 
-#ifndef WRMF_EXP
-#define WRMF_EXP 31
-#endif
 
 namespace dcue {
 
@@ -110,21 +106,24 @@ __device__ inline int woff(int r) {
   return 32 * m * (m + 1) + 8 * (m + 1) * (r - 8 * m);
 }
 
-// One workgroup per row (grid-stride), two workgroups per CU (76 KB of LDS each). The row's system
-// is the augmented matrix [[A, b], [b^T, *]] of size D16 + 1 (D16 = dim rounded up to 16, padded
-// with the identity): its Cholesky factor's last row is y = L^{-1} b, so the forward solve comes
-// out of the factorisation and only L^T x = y remains.
+// One workgroup per row (grid-stride), two workgroups per CU (80 KB of LDS each, <= 256 VGPRs). The
+// row's system is the augmented matrix [[A, b], [b^T, *]] of size D16 + 1 (D16 = dim rounded up to
+// 16, padded with the identity): its Cholesky factor's last row is y = L^{-1} b, so the forward
+// solve comes out of the factorisation and only L^T x = y remains.
 //   * A lives in registers as 8 x 8 tiles of the lower triangle (thread t owns tile t; the
 //     augmented row b^T adds one tile per tile column, of which row 0 is real): the accumulation
 //     A = G + lambda I + sum (c - 1) f f^T, b = sum c f is 64 FMAs per staged factor per tile, and
 //     the right-looking Cholesky's trailing update is a register-tile rank-16 update.
-//   * Per 16-column step: the two panel tile columns are written to LDS (packed lower triangle,
-//     rows padded to whole tiles, woff); waves 0 and 1 each factor the 16 x 16 diagonal block in lanes 0-15
-//     (v_readlane broadcasts, no barrier) and solve one panel row per lane; the trailing tiles
-//     read the panel from LDS. Two barriers per step.
+//   * Per 16-column step: the diagonal block's three tiles go to LDS (packed lower triangle, rows
+//     padded to whole tiles, woff); wave 0 factors it in lanes 0-15 (v_readlane broadcasts);
+//     the panel tiles below solve against it in their owners' registers (first tile column, then
+//     the second after removing the first's part) and are stored; the trailing tiles read the panel
+//     from LDS. Four barriers per step.
 //   * L^T x = y: wave 0, lane l holding x[l] and x[l + 64], eight rows of L at a time.
 // Tiles are numbered by tile column descending, so the trailing tiles of every step are a prefix
-// of the thread range (the later steps keep fewer waves busy).
+// of the thread range (the later steps keep fewer waves busy). Loop-invariant per-thread values are
+// passed through empty asm at the row and step boundaries, so their address arithmetic is redone
+// there instead of being hoisted into live registers (which would spill at 256 VGPRs).
 __global__ __launch_bounds__(256, 2) void k_wrmf_solve(float* __restrict__ X, long n_rows, const float* __restrict__ F,
                                                     int dim, const wacc_t* __restrict__ G,
                                                     const int64_t* __restrict__ indptr,
@@ -240,7 +239,7 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve(float* __restrict__ X, lo
       const int kt = k0 >> 3;  // tile column of the step's first 8 columns
       asm volatile("" : "+v"(r0), "+v"(c0));
       __syncthreads();
-      if (WRMF_EXP & 1 && t < 64) {
+      if (t < 64) {
         // the 16 x 16 diagonal block, factored in wave 0's lanes 0-15 (lane i holds row i)
         int i = lane;
         asm volatile("" : "+v"(i));  // lane predicates are formed here, not hoisted out of the k0 loop
@@ -275,13 +274,13 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve(float* __restrict__ X, lo
       __syncthreads();
       // the panel below the block, in its owners' registers: first tile column (columns k0..k0+7)
       const bool below = has_tile && TI >= kt + 2;
-      if (WRMF_EXP & 2 && below && TJ == kt) {
+      if (below && TJ == kt) {
         solve_cols();
         store_tile();
       }
       __syncthreads();
       // second tile column: remove the first column's part, then solve against L[k0+8..][k0+8..]
-      if (WRMF_EXP & 4 && below && TJ == kt + 1) {
+      if (below && TJ == kt + 1) {
 #pragma unroll 1
         for (int q = 0; q < 8; ++q) {
           wacc_t xa[8];
@@ -300,7 +299,7 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve(float* __restrict__ X, lo
       }
       __syncthreads();
       // trailing tiles: acc -= L[rows][k0:k0+16] L[cols][k0:k0+16]^T; then the next diagonal block's tiles
-      if (WRMF_EXP & 8 && has_tile && c0 >= k0 + 16) {
+      if (has_tile && c0 >= k0 + 16) {
 #pragma unroll 1
         for (int q = 0; q < 16; ++q) {
           wacc_t fc[8];
@@ -319,7 +318,7 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve(float* __restrict__ X, lo
     }
     __syncthreads();
     // L^T x = y (y: the augmented row), wave 0; eight rows of L loaded ahead of each chain
-    if (WRMF_EXP & 16 && t < 64) {
+    if (t < 64) {
       const wacc_t* y = Ls + woff(RA);
       wacc_t xlo = lane < D16 ? y[lane] : 0.0, xhi = lane + 64 < D16 ? y[lane + 64] : 0.0;
       for (int kb = D16 - 8; kb >= 0; kb -= 8) {
