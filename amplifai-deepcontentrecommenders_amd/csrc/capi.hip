@@ -774,8 +774,8 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   if (!sp) return DCUE_ERR_HIP;
   hipStream_t su = sp->st[0];
   // the user tower runs beside the item tower; the item tower's chain is issued first
-  hipEvent_t ev_in = nullptr;
-  TRY(fork_point(sp, s, &ev_in));
+  hipEvent_t ev_in = o.ev_in;
+  if (!ev_in) TRY(fork_point(sp, s, &ev_in));
   HPROF("capi:3");
   if (!o.prologue_done) TRY(batch_counts(b, w, s));
   HPROF("capi:4");
@@ -805,21 +805,31 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   SideQueue side;
   int ust = DCUE_OK;
   const uint64_t useq = side.threaded() ? side.run(user_part, &ust) : 0;
+  // (under an exchange the late Adam follows the all-reduce: it keeps its wait before conv 2)
+  const bool late_first = o.wait_late && late_wait_at_conv1() && !o.comm;
+  if (late_first) TRY(wait_point(s, o.wait_late));
   TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s,
-                   o.prologue_done, o.input_stats_done && o.prologue_done, o.clear_bn0, o.wait_late,
+                   o.prologue_done, o.input_stats_done && o.prologue_done, o.clear_bn0,
+                   late_first ? nullptr : o.wait_late,
                    early && !side.threaded() ? &user_part : nullptr, o.sync_bn));
   if (!early && !side.threaded()) TRY(user_part());
   TRY(side.wait(useq));
   TRY(wait_point(s, ev_uf));
   HPROF("capi:9");
   if (o.fuse_score) {
+    // a fork point after the score kernel only for a caller that asks for one: a launch-bound event
+    // costs the chain a ≈6 µs gap before its next kernel (the backward's side work waits for the
+    // dgrad chain's first fork point instead)
+    if (!o.score_done)
+      return launch_score_fused(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.rowsum, w.du,
+                                w.dfcopy, s);
     hipEvent_t ev = nullptr;
     ForkAfter fk(sp, s, &ev);
     TRY(launch_score_fused(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.rowsum, w.du,
                            w.dfcopy, s));
     TRY(fk.done());
     HPROF("capi:10");
-    if (o.score_done) *o.score_done = ev;
+    *o.score_done = ev;
     return DCUE_OK;
   }
   return launch_score_fwd(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.hinge, w.loss,
@@ -867,6 +877,20 @@ int step_prologue(const dcue_model* m, const dcue_batch* b, void* ws, size_t ws_
     p.copy_idx = w.copy_idx;
   }
   return launch_step_prologue(p, s);
+}
+
+// Split plans: where the caller's stream waits for the previous step's late Adam (StepOpts::
+// wait_late). Default: before conv 2, and for the next step's prepared inputs (StepOpts::
+// wait_inputs) before the conv-1 weight gradient. DCUE_LATE_WAIT=conv1: one wait before conv 1, the
+// late Adam itself waiting for the inputs on the user stream first -- one barrier gap fewer on the
+// chain, but conv 1 then starts behind the previous step's late Adam: 4-5 µs slower per step
+// (GPU-only A/B, profiles/r04_ab_late_wait.txt).
+bool late_wait_at_conv1() {
+  static const bool on = [] {
+    const char* e = getenv("DCUE_LATE_WAIT");
+    return e && e[0] == 'c' && e[4] == '1';
+  }();
+  return on;
 }
 
 static bool fuse_late_adam_on() {
@@ -929,10 +953,12 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(launch_score_bwd(w.uf, w.f, b, D, dscores ? dscores : w.dhinge, w.cosv, w.norms, w.du,
                          w.dfcopy, s));
   // fork points on the chain are bound to its launches (ForkAfter): no record packets between them
+  // ev_score: after the score backward, for the xhat0 build of the f32 weight-gradient path only
+  // (the user tower's backward waits for the dgrad chain's first fork point, ev_layer[3])
   hipEvent_t ev_score = nullptr, ev_layer[6] = {};
   if (o.fuse_score && o.score_done && *o.score_done)
     ev_score = *o.score_done;
-  else
+  else if (!o.xhat0 && !wgrad_f16_on())
     TRY(fork_point(sp, s, &ev_score));
     HPROF("capi:14");
   // the conv-1 weight gradient's X operand, bn0(x) without gamma/beta, materialised once beside the
@@ -959,7 +985,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   // user tower (userembedding.py:33-44 backward), the compact embedding rows, and -- when the step
   // carries it -- the user table's Adam step (it needs nothing from the item tower)
   auto user_bwd = [&]() -> int {
-    TRY(wait_point(su, ev_score));
+    TRY(wait_point(su, ev_score ? ev_score : ev_layer[3]));
     HPROF("capi:26");
     {
       // two launches of two independent GEMMs each (launch_tgemm_pair; the same blocks as four
@@ -1101,6 +1127,9 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     const char* e = getenv("DCUE_LATE_JOIN");
     return e && e[0] == 'h';
   }();
+  // split plans without an exchange: the late Adam on the user stream waits for the prepared inputs
+  // and the next launch waits for it before conv 1 (late_wait_at_conv1)
+  const bool inputs_via_late = o.dense_split && !o.comm && o.late_done && late_wait_at_conv1();
   hipEvent_t joined = nullptr;
   dcue_adam_args dense = {};
   if (o.dense_split) {
@@ -1121,6 +1150,8 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
         TRY(wait_point(su, tail[2]));
         TRY(wait_point(su, tail[3]));
       }
+      // (recorded by the plan's prologue closure, posted before this one: FIFO on the side thread)
+      if (inputs_via_late && o.wait_inputs) TRY(wait_point(su, o.wait_inputs));
       ForkAfter fk(sp, su, o.late_done);
       TRY(launch_adam(m, &dense, c.poff, su, true, late, -1));
       TRY(fk.done());
@@ -1140,8 +1171,20 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   };
   auto multi_hi = [&]() { return issue_multi(3, 5, !c.res && !c.text, sw[0], ev_layer[3], &tail[2]); };
   auto multi_2 = [&]() { return issue_multi(2, 2, false, sw[1], ev_layer[2], &tail[3]); };
-  // the user tower's backward needs only the score kernel's du
-  if (thr && !o.item_only) TRY(post(user_bwd));
+  // the user tower's backward needs only the score kernel's du; it and a plan's lookahead are issued
+  // at the dgrad chain's first fork point (ev_layer[3]), which the layer 3-5 weight gradients wait
+  // for anyway: no extra fork event on the chain
+  uint64_t ahead_seq = 0;
+  auto after_fork3 = [&]() -> int {
+    if (thr && !o.item_only) TRY(post(user_bwd));
+    if (o.ahead) {
+      const std::function<int(hipEvent_t)>* ah = o.ahead;
+      const hipEvent_t e3 = ev_layer[3];
+      ahead_seq = side.run([ah, e3]() { return (*ah)(e3); }, &ist);
+      TRY(ist);
+    }
+    return DCUE_OK;
+  };
   if (c.res || c.text) {  // df; then the fc input gradient split: g5 = df W[:, off5:] (+ BN5's sums) and
                           // the time-pooled blocks' dtp = df W[:, :4H] (text: the text features' df W[:, :C])
     TRY(launch_item_grad(w.dfcopy, b, D, w.df, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
@@ -1207,13 +1250,17 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
         launch_tag().missed = true;
       }
       TRY(fk.done());
-      if (thr && l - 1 == 3 && !fork_once()) TRY(post(multi_hi));
-      if (thr && l - 1 == 2) {
+      if (l - 1 == 3 && !fork_once()) {
+        if (thr) TRY(post(multi_hi));
+        TRY(after_fork3());
+      }
+      if (l - 1 == 2) {
         if (fork_once()) {
           ev_layer[3] = ev_layer[2];
-          TRY(post(multi_hi));
+          if (thr) TRY(post(multi_hi));
+          TRY(after_fork3());
         }
-        TRY(post(multi_2));
+        if (thr) TRY(post(multi_2));
       }
     } else {
       TRY(launch_conv_dgrad(l, l == 5 ? D : H, ra, s));
@@ -1285,8 +1332,8 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   };
   // layer 1 (the step's tail) follows the chain on the caller's stream, issued right away
   if (ev_x0) TRY(wait_point(s, ev_x0));
-  if (o.wait_inputs) {
-    TRY(side.wait(o.wait_inputs_seq));
+  if (o.wait_inputs && !inputs_via_late) {
+    TRY(side.wait(o.ahead ? ahead_seq : o.wait_inputs_seq));
     TRY(wait_point(s, o.wait_inputs));
   }
   TRY(issue_wgrad(1, s, 2, &tail[0]));

@@ -478,12 +478,23 @@ class SideQueue {
   uint64_t last_ = 0;
 };
 bool on_side_worker();
+// split plans: one wait before conv 1 for the previous step's late Adam, which covers the prepared
+// inputs (capi.hip)
+bool late_wait_at_conv1();
 
 // ------------------------------------------------------------- step implementation (capi.hip)
 struct StepOpts {
   hipEvent_t wait_inputs = nullptr;  // plans: the next step's prepared inputs; the caller's stream
                                      // waits for it before the conv-1 weight gradient
   uint64_t wait_inputs_seq = 0;      // ... once the side-issue thread has recorded it (SideQueue)
+  // plans: the next step's input preparation (lookahead), issued by the backward on the side path
+  // once the dgrad chain's first fork point exists (its argument: that point, which orders it after
+  // everything the caller enqueued before the step); the conv-1 weight gradient's wait for
+  // wait_inputs then waits for it to be issued
+  const std::function<int(hipEvent_t)>* ahead = nullptr;
+  // plans: a point on the caller's stream at the launch's start (the user tower waits for it);
+  // null: the forward records one
+  hipEvent_t ev_in = nullptr;
   dcue_comm* sync_bn = nullptr;  // SyncBN: BatchNorm sums all-reduced over this communicator's ranks
   bool prologue_done = false;  // counts written + accumulators cleared by the prologue
   bool fuse_score = false;     // train forward also runs the hinge backward (k_score_fused)

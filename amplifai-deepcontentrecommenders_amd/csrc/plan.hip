@@ -118,33 +118,12 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
     TRY(fork_point(sp, s, &p->tails[0]));
     HPROF("plan:2");
   }
-  // (step t's inputs, prepared by launch t-1 on wgrad stream 0, are covered by that step's join:
-  // the caller's stream waited for everything on that stream before step t was issued)
-  // the next step's inputs + what the caller sees of this one, once the last step is over (its
-  // side-stream part is ordered before this point on wgrad stream 0 itself)
-  // (with the side-issue thread, side.hip, the two wgrad-stream parts below -- this prologue and the
-  // lookahead after the forward -- are issued there)
-  SideQueue side;
-  int sst = DCUE_OK;
-  {
-    StepPrologue q = inputs(nxt);
-    if (inbatch) {
-      q.mt = p->mt_ahead;
-      q.mt_commit = p->cfg.mt;
-      q.copy_src = p->neg[cur];
-      q.copy_dst = const_cast<int32_t*>(b0.neg_item);
-      q.ncopy = (long)b0.n_rows * b0.n_neg;
-    }
-    q.users_dst = const_cast<int64_t*>(b0.users); q.users_src = users_src;
-    q.items_dst = const_cast<int32_t*>(b0.item_track); q.items_src = items_src;
-    const hipEvent_t last = p->tails[0];
-    side.run([q, sa, last]() -> int {
-      if (last) TRY(wait_point(sa, last));
-      return launch_step_prologue(q, sa);
-    }, &sst);
-    TRY(sst);
-    HPROF("plan:3");
-  }
+  // A point on the caller's stream at this launch's start: the user tower, this launch's prologue
+  // for the next step and the lookahead wait for it (it orders them after everything the caller
+  // enqueued before the launch -- the batch indices, the announced next items -- and after the last
+  // step, which ended on this stream).
+  hipEvent_t ev_in = nullptr;
+  TRY(fork_point(sp, s, &ev_in));
   dcue_batch b = b0;
   if (users_src) b.users = users_src;
   if (items_src) b.item_track = items_src;
@@ -153,19 +132,44 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   const bool prepared = p->ahead_items[cur] != nullptr;
   const bool ahead = prepared && items_src == p->ahead_items[cur];
   p->ahead_items[cur] = nullptr;
-  // The next step's inputs (slot nxt: prologue at this launch's start, lookahead after its score
-  // kernel) are made on wgrad stream 0, which split plans never join back into the caller's stream.
-  // The caller's stream waits for them inside this step's backward, just before the conv-1 weight
-  // gradient -- a point that already idles behind the layer-2 dgrad's bound fork event and is long
-  // after the lookahead finished -- so the next launch's conv 1 is ordered after them.
+  // The next step's inputs (slot nxt) are made on wgrad stream 0, which split plans never join back
+  // into the caller's stream: the prologue (draws, copy counts, cleared accumulators, published
+  // batch) and the lookahead (the announced next batch's bn0 sums and, on the f32 path, its xhat0),
+  // issued on the side-issue thread (side.hip) when it runs. The caller's stream waits for them
+  // (inputs_ready) inside this step's backward, just before the conv-1 weight gradient -- long after
+  // they finished -- so the next launch's conv 1 is ordered after them.
   // DCUE_INPUTS_WAIT=start waits at the next launch's start instead, =0 not at all (A/B only).
+  // DCUE_AHEAD_AT=fork: the lookahead at the backward's first dgrad fork point instead of right
+  // behind the prologue (A/B).
   static const int inputs_wait = [] {
     const char* e = getenv("DCUE_INPUTS_WAIT");
     return !e ? 1 : e[0] == '0' ? 0 : e[0] == 's' ? 2 : 1;
   }();
+  static const bool ahead_at_fork = [] {
+    const char* e = getenv("DCUE_AHEAD_AT");
+    return e && e[0] == 'f';
+  }();
   if (p->inputs_ready && inputs_wait == 2) TRY(wait_point(s, p->inputs_ready));
-  p->inputs_ready = nullptr;
+  p->ahead_items[nxt] = nullptr;
+  const bool look = p->next_items && p->xh[nxt];
+  if (look) p->ahead_items[nxt] = p->next_items;
+  p->next_items = nullptr;
+  p->inputs_ready = ring_event(sp);  // slot nxt's inputs, for the next launch (recorded below)
+  // the lookahead, then the inputs_ready record, on wgrad stream 0 after `after`
+  const std::function<int(hipEvent_t)> lookahead = [p, sa, nxt, look, ir = p->inputs_ready](hipEvent_t after) -> int {
+    if (look) {
+      if (after) TRY(wait_point(sa, after));
+      TRY(ahead_item_inputs(&p->model, &p->batch, &p->tracks, p->ahead_items[nxt], p->counts[nxt], p->acc[nxt],
+                            p->xh[nxt], sa));
+    }
+    DCUE_HIP_CHECK(hipEventRecord(ir, sa));
+    return DCUE_OK;
+  };
+  SideQueue side;
+  int sst = DCUE_OK;
+  uint64_t iseq = 0;
   StepOpts o;
+  o.ev_in = ev_in;
   o.sync_bn = p->sync_bn ? p->comm : nullptr;
   o.prologue_done = true;
   o.fuse_score = true;
@@ -177,10 +181,8 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   o.input_stats_done = ahead;
   o.xhat0 = ahead ? p->xh[cur] : nullptr;
   o.clear_bn0 = prepared && !ahead;
-  hipEvent_t score_done = nullptr;
-  o.score_done = &score_done;
   o.tails = p->tails;
-  o.wait_late = p->late_done;  // the previous split step's late Adam, before conv 2
+  o.wait_late = p->late_done;  // the previous split step's late Adam (before conv 1 or 2, late_wait_at_conv1)
   o.dense_split = dense_split;
   if (dense_split) o.y1 = p->y1[cur];
   o.comm = dense_split ? p->comm : nullptr;  // the exchange inside the backward (comm_exchange_split)
@@ -190,32 +192,49 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   const bool deferred = p->model.emb_step != nullptr;
   o.flush_slice_step = deferred ? p->pending_flush : -1;
   o.defer_flush_slice = deferred && emb_adam != nullptr;
+  // DCUE_SCORE_FORK=1: the score kernel binds a fork point that the user tower's backward waits for
+  // (A/B; default: it waits for the dgrad chain's first fork point, one bound event fewer)
+  static const bool score_fork = [] {
+    const char* e = getenv("DCUE_SCORE_FORK");
+    return e && e[0] == '1';
+  }();
+  hipEvent_t score_done = nullptr;
+  if (score_fork) o.score_done = &score_done;
+  // DCUE_PROLOGUE_FIRST=1: the prologue closure is posted before the forward (A/B)
+  static const bool prologue_first = [] {
+    const char* e = getenv("DCUE_PROLOGUE_FIRST");
+    return e && e[0] == '1';
+  }();
+  auto post_prologue = [&]() -> int {
+    StepPrologue q = inputs(nxt);
+    if (inbatch) {
+      q.mt = p->mt_ahead;
+      q.mt_commit = p->cfg.mt;
+      q.copy_src = p->neg[cur];
+      q.copy_dst = const_cast<int32_t*>(b0.neg_item);
+      q.ncopy = (long)b0.n_rows * b0.n_neg;
+    }
+    q.users_dst = const_cast<int64_t*>(b0.users); q.users_src = users_src;
+    q.items_dst = const_cast<int32_t*>(b0.item_track); q.items_src = items_src;
+    iseq = side.run([q, sa, ev_in, &lookahead]() -> int {
+      TRY(wait_point(sa, ev_in));
+      TRY(launch_step_prologue(q, sa));
+      return ahead_at_fork ? DCUE_OK : lookahead(nullptr);  // (the prologue on sa orders it)
+    }, &sst);
+    return sst;
+  };
+  if (prologue_first) TRY(post_prologue());
   TRY(forward_impl(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, 1, p->cfg.margin, o, s));
   HPROF("plan:4");
-  // lookahead: the announced next batch's bn0 sums (into slot nxt's accumulator block, cleared and
-  // weighted by the counts drawn above on the same stream) and its xhat0. The items are the
-  // caller's, written in the caller's stream order: wait for this step's score kernel (a fork point
-  // the step records anyway), which comes after everything the caller enqueued before this launch.
-  p->ahead_items[nxt] = nullptr;
-  const bool look = p->next_items && p->xh[nxt] && score_done;
-  if (look) p->ahead_items[nxt] = p->next_items;
-  p->inputs_ready = ring_event(sp);  // slot nxt's inputs, for the next launch (recorded below)
-  const uint64_t iseq = side.run([p, sa, nxt, look, score_done, ir = p->inputs_ready]() -> int {
-    if (look) {
-      TRY(wait_point(sa, score_done));
-      TRY(ahead_item_inputs(&p->model, &p->batch, &p->tracks, p->ahead_items[nxt], p->counts[nxt], p->acc[nxt],
-                            p->xh[nxt], sa));
-    }
-    DCUE_HIP_CHECK(hipEventRecord(ir, sa));
-    return DCUE_OK;
-  }, &sst);
-  TRY(sst);
-  p->next_items = nullptr;
+  // posted after the forward, whose user tower (on the critical path's first fork) the side thread
+  // then issues first
+  if (!prologue_first) TRY(post_prologue());
+  if (ahead_at_fork) o.ahead = &lookahead;
   if (inputs_wait == 1) {
     o.wait_inputs = p->inputs_ready;
     o.wait_inputs_seq = iseq;
     p->inputs_ready = nullptr;
-  } else {
+  } else if (!ahead_at_fork) {
     TRY(side.wait(iseq));
   }
   TRY(backward_impl(&p->model, &b, &p->tracks, p->ws, p->ws_bytes, nullptr, p->cfg.emb_grad_scale, o, s));
