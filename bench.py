@@ -255,6 +255,19 @@ def row_flops(args, items_per_row):
     return 3 * item_flops(args.hidden, d) * items_per_row + 3 * 2 * (E * E + E * d)
 
 
+F64_PEAK_TFLOPS = 78.6  # MI355X fp64 vector (half the guide's 157.3 TF f32 vector rate; AMD spec)
+
+
+def wrmf_half_step_flops(indptr, d, n_fixed):
+    """Algorithmic fp64 FLOPs of one WRMF half-step: the Gram matrix F^T F (lower
+    triangle, n_fixed rows), and per row with pairs its rank-1 terms (nnz x (d(d+1)/2 + d) FMAs),
+    the Cholesky (d^3/6) and the two triangular solves (d^2)."""
+    nnz = (indptr[1:] - indptr[:-1]).double()
+    rows = float((nnz > 0).sum())
+    fma = float(nnz.sum()) * (d * (d + 1) / 2 + d) + rows * (d ** 3 / 6 + d * d) + n_fixed * d * (d + 1) / 2
+    return 2.0 * fma
+
+
 # --------------------------------------------------------------------------------- evaluation
 def dcbr_phase(args, tracks, pair_user, pair_track, n_users, dev, M, comm=None, world=1, rank=0):
     """BASELINE config 5 at this run's shape (no reference numbers exist: dcrecommend/dcbr is
@@ -300,12 +313,34 @@ def dcbr_phase(args, tracks, pair_user, pair_track, n_users, dev, M, comm=None, 
     dt = D.max_over_ranks(time.perf_counter() - t0, dev)
     same, _, _ = D.replica_checksums(model.net._flat["P"])
     nnz = int(pair_user.shape[0])
+    # rooflines: the ALS iteration against the fp64 vector peak (its solve is fp64 VALU work); the
+    # regression step against the ceiling of the arithmetic its kernels run (executed_work, per item,
+    # the user tower left out)
+    f_iter = (wrmf_half_step_flops(w.by_user[0], d, args.tracks) +
+              wrmf_half_step_flops(w.by_item[0], d, n_users))
+    ach = f_iter / t_iter / 1e12
+    wroof = {"kernel": "dcue_wrmf_half_step x 2 (k_wrmf_gram + k_wrmf_solve: fp64 register-tile Cholesky)",
+             "bound": "valu (fp64)", "achieved": ach, "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s (fp64)",
+             "frac": ach / F64_PEAK_TFLOPS, "algorithmic_flops": f_iter, "traffic": None}
+    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_wrmf_solve.json")
+    if os.path.exists(pmc):
+        with open(pmc) as fh:
+            wroof["traffic_per_solve_launch"] = json.load(fh).get("hbm_bytes")
+    ex_f, ex_t = executed_work(args, 1, M)
+    u = 3 * 2 * (args.user_embdim ** 2 + args.user_embdim * d)
+    ex_f, ex_t = ex_f - u, ex_t - u / (F32_PEAK_TFLOPS * 1e12)
+    r_ach = world * M * args.steps * ex_f / dt / 1e12
+    rroof = {"kernel": "DCBR regression step (item-tower train forward + MSE head + item-only backward)",
+             "bound": "mfma", "achieved": r_ach, "peak": ex_f / ex_t / 1e12,
+             "unit": "TFLOP/s (f32-equivalent, executed work; peak = the blended ceiling of its kernels)",
+             "frac": r_ach / (ex_f / ex_t / 1e12), "flops_per_item": ex_f}
     return {"workload": "WRMF d=%d over %d users x %d tracks, %d interactions; DCBR regression of the "
                         "truedcuemel1dbn item tower (H=%d) onto the item factors, %d-item batches per GPU, %d GPU(s)"
                         % (d, n_users, args.tracks, nnz, args.hidden, M, world),
             "wrmf_ms_per_iteration": t_iter * 1e3, "wrmf_rows_per_s": (n_users + args.tracks) / t_iter,
             "wrmf_first_iteration_ms_incl_csr_build": t_fit1 * 1e3,
             "regression_ms_per_step": dt / args.steps * 1e3, "regression_items_per_s": world * M * args.steps / dt,
+            "wrmf_roofline": wroof, "regression_roofline": rroof,
             "loss_first": float(losses[0]), "loss_last": float(losses[-1]), "replicas_identical": same,
             "parity": "unpinned against the reference (never published); pinned against oracle/wrmf_oracle.py "
                       "and the fp64 oracle item tower (tests/test_gpu_dcbr.py); N>1 bit-exact with one rank "
