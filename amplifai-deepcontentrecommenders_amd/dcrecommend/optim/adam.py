@@ -24,7 +24,7 @@ from dcrecommend import _native as nat
 class NativeAdam(torch.optim.Optimizer):
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0,
-                 defer_embedding=False, flush_every=64):
+                 defer_embedding=False, flush_every=16):
         params = list(params)
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         owners = {}
