@@ -784,10 +784,21 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   const std::function<int()> user_part = [&]() -> int {
     TRY(wait_point(su, ev_in));
     HPROF("capi:5");
+    // DCUE_USER_FWD=split: the rows' sync (k_emb_sync, one workgroup per row) and the two GEMMs
+    // (k_tgemm, 16 x 64 blocks) as three launches instead of k_user_fwd (A/B)
+    static const bool split_fwd = [] {
+      const char* e = getenv("DCUE_USER_FWD");
+      return e && e[0] == 's';
+    }();
     {
       // the deferred rows' sync and the two GEMMs in one launch (k_user_fwd)
       ForkAfter fk(sp, su, &ev_uf);
-      TRY(user_forward_fused(c, w, b->users, b->n_rows, su));
+      if (split_fwd) {
+        if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
+        TRY(user_forward(c, w, b->users, b->n_rows, nullptr, su));
+      } else {
+        TRY(user_forward_fused(c, w, b->users, b->n_rows, su));
+      }
       HPROF("capi:7");
       TRY(fk.done());
       HPROF("capi:8");
