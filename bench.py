@@ -85,7 +85,7 @@ def parse():
     ap.add_argument("--gpu-only", action="store_true",
                     help="diagnostic: hold the stream behind a sleep kernel while the warm in-batch "
                          "steps are enqueued, then report the GPU's own time for them")
-    ap.add_argument("--profile-phase", choices=["inbatch_cold", "inbatch", "catalogue"],
+    ap.add_argument("--profile-phase", choices=["inbatch_cold", "inbatch", "catalogue", "text"],
                     help="under `rocprofv3 --kernel-trace`: bracket this phase's timed steps with a "
                          "marker kernel (profiles/summarize_pmc.py keeps what lies between)")
     ap.add_argument("--sync-bn", action="store_true",
@@ -738,7 +738,7 @@ def main():
 
     def traffic_for(kernel_name, mode):
         tag = {"k_conv1_wgrad": "conv1_wgrad", "k_conv_wgrad16": "conv1_wgrad16", "k_emb_flush_rows": "emb_flush_rows",
-               "k_conv_rows<0,0>": "conv1_fwd"}.get(kernel_name.split(" ")[0])
+               "k_conv_rows<0,0>": "conv1_fwd", "k_text_fwd": "text_fwd"}.get(kernel_name.split(" ")[0])
         path = os.path.join(ROOT, "profiles", "pmc_%s_%s.json" % (tag, mode)) if tag else None
         if path and os.path.exists(path):
             try:
@@ -931,6 +931,8 @@ def main():
         ks = kernel_rooflines(kern, B, args.steps)
         tk = [k for k in ks if k["kernel"].startswith("k_text_fwd")]
         troof = dict(tk[0]) if tk else {}
+        if troof:
+            troof["traffic"] = traffic_for(troof["kernel"], "text")
         tflops_row = 3 * (item_flops(args.hidden, Dt) + 2.0 * args.text_dim * Dt
                           + text_conv_flops(args.text_len, args.word_dim, args.text_dim)) \
             + 3 * 2 * (args.user_embdim ** 2 + args.user_embdim * Dt)

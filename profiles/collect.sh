@@ -21,13 +21,13 @@ export TMPDIR=/tmp
 BENCH="$ROOT/bench.py --no-cpu-baseline --no-eval --steps $STEPS --warmup 20"
 (cd "$ROOT" && timeout -k 10 300 python3 $BENCH > "$OUT/plain.log" 2>&1)
 grep '^{' "$OUT/plain.log" | tail -n 1 > "$OUT/${TAG}_bench_plain.json"
-for PH in inbatch catalogue inbatch_cold; do
+for PH in inbatch catalogue inbatch_cold text; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/stats_$PH" -o run \
     -- python3 $BENCH --profile-phase $PH > "$OUT/stats_$PH.log" 2>&1
 done
-for PH in inbatch catalogue; do
+for PH in inbatch catalogue text; do
   for C in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 180 rocprofv3 --pmc $C --kernel-include-regex 'k_conv1_wgrad|k_conv_wgrad16|k_emb_flush_rows|k_conv_rows|spin_kernel' \
+    timeout -s KILL 180 rocprofv3 --pmc $C --kernel-include-regex 'k_conv1_wgrad|k_conv_wgrad16|k_emb_flush_rows|k_conv_rows|k_text_fwd|spin_kernel' \
       -f csv -d "$OUT/pmc_${PH}_$C" -o run -- python3 $ROOT/bench.py --no-cpu-baseline --no-eval --steps 40 \
       --warmup 5 --profile-phase $PH > "$OUT/pmc_${PH}_$C.log" 2>&1
   done
@@ -35,8 +35,8 @@ done
 python3 "$ROOT/profiles/summarize_pmc.py" "$OUT" "$TAG"
 # keep the summaries and rocprofv3's own --stats tables; drop the raw traces (gpurun copies back at
 # most 64 MiB of gpurun_out/)
-for PH in inbatch catalogue inbatch_cold; do
+for PH in inbatch catalogue inbatch_cold text; do
   f=$(find "$OUT/stats_$PH" -name '*kernel_stats.csv' | head -n 1)
   [ -n "$f" ] && cp "$f" "$OUT/${TAG}_${PH}_rocprof_kernel_stats.csv"
 done
-rm -rf "$OUT"/stats_inbatch "$OUT"/stats_catalogue "$OUT"/stats_inbatch_cold "$OUT"/pmc_*_FETCH_SIZE "$OUT"/pmc_*_WRITE_SIZE
+rm -rf "$OUT"/stats_inbatch "$OUT"/stats_catalogue "$OUT"/stats_inbatch_cold "$OUT"/stats_text "$OUT"/pmc_*_FETCH_SIZE "$OUT"/pmc_*_WRITE_SIZE

@@ -25,7 +25,7 @@ import sys
 # tap-fused weight gradient runs beside the dgrad chain on a side stream
 KERNELS = {"conv1_wgrad": "k_conv1_wgrad", "conv1_wgrad16": "k_conv_wgrad16t<0,",
            "wgrad16t_layer2": "k_conv_wgrad16t<2,", "wgrad16_multi": "k_conv_wgrad16_multi", "emb_flush_rows": "k_emb_flush_rows",
-           "conv1_fwd": "k_conv_rows<0, 0,"}
+           "conv1_fwd": "k_conv_rows<0, 0,", "text_fwd": "k_text_fwd"}
 MARK = "spin_kernel"
 
 
@@ -82,7 +82,7 @@ def per_dispatch(d, counter, kernel):
 def main():
     d, tag = sys.argv[1], sys.argv[2]
     out = {}
-    for mode in ("inbatch", "catalogue"):
+    for mode in ("inbatch", "catalogue", "text"):
         for short, kname in KERNELS.items():
             fetch_kb, n_f = per_dispatch(os.path.join(d, "pmc_%s_FETCH_SIZE" % mode), "FETCH_SIZE", kname)
             write_kb, n_w = per_dispatch(os.path.join(d, "pmc_%s_WRITE_SIZE" % mode), "WRITE_SIZE", kname)
@@ -102,7 +102,7 @@ def main():
     if os.path.exists(plain):
         steps = json.load(open(plain)).get("steps")
     per_step = {}
-    for ph in ("inbatch", "catalogue", "inbatch_cold"):
+    for ph in ("inbatch", "catalogue", "inbatch_cold", "text"):
         agg = phase_stats(os.path.join(d, "stats_%s" % ph))
         if not agg or not steps:
             continue
