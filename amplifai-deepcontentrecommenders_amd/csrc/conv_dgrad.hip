@@ -2,6 +2,8 @@
 // conv_rows.h.
 #include "conv_rows.h"
 
+DCUE_KTRACE_READER(dgrad)  // diagnostic builds only (dcue_common.h)
+
 namespace dcue {
 
 // dgrad of layer L: rows = (item, input position t' < Lin_L), slab = layer-L conv positions

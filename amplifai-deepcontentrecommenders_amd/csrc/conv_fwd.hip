@@ -2,6 +2,8 @@
 // input width. Kernel body: conv_rows.h.
 #include "conv_rows.h"
 
+DCUE_KTRACE_READER(fwd)  // diagnostic builds only (dcue_common.h)
+
 namespace dcue {
 
 template <int L, int KC, int SRC, int TW>

@@ -244,6 +244,10 @@ template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL,
           int POOLL, bool DEEP, bool F16>
 __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
   critical_path_priority();
+  // (DCUE_KTRACE: kernels 2-6 the forwards by input length (layers 1-5), 7-11 the dgrads)
+  [[maybe_unused]] constexpr int KID = 2 + MODE * 5 + (LIN >= 131 ? 0 : LIN >= 32 ? 1 : LIN >= 8 ? 2 : LIN >= 2 ? 3 : 4);
+  DCUE_KTW(KID, 6);
+  DCUE_KT(KID, 0);
   constexpr int RX = R + KS - 1;
   constexpr int ROWS = TW * 16;
   constexpr int MAXI = (ROWS + R - 1) / R + 1;
@@ -375,7 +379,9 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
       store_batch(base, kop);
     }
   }
+  DCUE_KT(KID, 1);
   __syncthreads();
+  DCUE_KT(KID, 2);
   if (!colok) return;  // no barrier follows
 
   int sbase[TW];
@@ -463,6 +469,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
       for (int ct = 0; ct < CT; ++ct) acc[r][ct] = mfma4(av[r].w, b[ct].w, acc[r][ct]);
   }
 
+  DCUE_KT(KID, 3);
   if constexpr (MODE == 1) {
     // g_{l-1} rows, plus this tile's share of BN_{l-1}'s backward sums (sum g, sum g*xhat)
     float sg[CT] = {}, sgx[CT] = {}, gmx[CT] = {};
@@ -572,6 +579,8 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
       }
     }
   }
+  DCUE_KT(KID, 4);
+  DCUE_KTW(KID, 7);
 }
 
 template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,

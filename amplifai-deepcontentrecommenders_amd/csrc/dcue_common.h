@@ -57,6 +57,36 @@ void count_launch();
     }                                                                                             \
   } while (0)
 
+// DCUE_KTRACE diagnostic builds (scratch/build_ktrace.sh): thread 0 of each workgroup stores phase
+// timestamps of selected kernels (slots 0-5 shader clock, 6-7 the 100 MHz wall clock) into
+// dcue_ktrace_buf[kernel][block] (tail.hip), read back with dcue_ktrace_read. Compiled out otherwise.
+constexpr int kKtraceKernels = 16, kKtraceBlocks = 512;
+#ifdef DCUE_KTRACE
+// one buffer per translation unit (no relocatable device code): each traced .hip file exports its
+// own reader, dcue_ktrace_read_<file> (DCUE_KTRACE_READER)
+static __device__ unsigned long long dcue_ktrace_buf[kKtraceKernels][kKtraceBlocks][8];
+#define DCUE_KTRACE_READER(name)                                                           \
+  extern "C" int dcue_ktrace_read_##name(void* host, size_t bytes) {                       \
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(dcue_ktrace_buf), bytes) == hipSuccess ? 0 : 3; \
+  }
+#define DCUE_KT(kid, slot)                                                                          \
+  do {                                                                                              \
+    if (threadIdx.x == 0 && blockIdx.x < kKtraceBlocks) dcue_ktrace_buf[kid][blockIdx.x][slot] = clock64(); \
+  } while (0)
+#define DCUE_KTW(kid, slot)                                                                              \
+  do {                                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < kKtraceBlocks) dcue_ktrace_buf[kid][blockIdx.x][slot] = wall_clock64(); \
+  } while (0)
+#else
+#define DCUE_KTRACE_READER(name)
+#define DCUE_KT(kid, slot) \
+  do {                     \
+  } while (0)
+#define DCUE_KTW(kid, slot) \
+  do {                      \
+  } while (0)
+#endif
+
 namespace dcue {
 
 constexpr int kMels = DCUE_N_MELS;     // 128, truedcuemel1dbn.py:24

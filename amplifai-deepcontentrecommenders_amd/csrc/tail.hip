@@ -13,6 +13,8 @@
 #include "dcue_internal.h"
 #include "tgemm.h"
 
+DCUE_KTRACE_READER(tail)  // diagnostic builds only (dcue_common.h)
+
 namespace dcue {
 
 // ------------------------------------------------------------------------ batch bookkeeping
@@ -206,6 +208,8 @@ __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ u
                                                      float* norms, float* rowsum, float* dU,
                                                      float* dfcopy) {
   critical_path_priority();
+  DCUE_KTW(0, 6);
+  DCUE_KT(0, 0);
   constexpr int CMAX = CPW > 0 ? 4 * CPW : 1025;
   __shared__ float cs[CMAX], dcs[CMAX], hs[CMAX];
   __shared__ float gus[4][256];
@@ -239,6 +243,7 @@ __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ u
     su += u[e] * u[e];
   }
   const float nu = sqrtf(wave_sum(su));
+  DCUE_KT(0, 2);
   const float du = fmaxf(nu, eps);
   if (wave == 0 && lane == 0) norms[(long)row * (N + 2)] = nu;
   auto score_copy = [&](int c, const float (&w)[4]) {
@@ -259,9 +264,48 @@ __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ u
     return nf;
   };
   if constexpr (CPW > 0) {
+    // score_copy's arithmetic for the wave's CPW copies at once: each cross-lane sum's six
+    // shuffle steps run for all copies together, so their latencies overlap instead of adding up
+    // (the same operations per value in the same order as score_copy: the same bits)
+    float sq[CPW], dq[CPW];
 #pragma unroll
-    for (int q = 0; q < CPW; ++q)
-      if (wave + 4 * q <= N) nfr[q] = score_copy(wave + 4 * q, v[q]);
+    for (int q = 0; q < CPW; ++q) {
+      float sf = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sf += v[q][e] * v[q][e];
+      sq[q] = sf;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+      for (int q = 0; q < CPW; ++q) sq[q] += __shfl_xor(sq[q], off, 64);
+    float un[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) un[e] = u[e] / du;
+#pragma unroll
+    for (int q = 0; q < CPW; ++q) {
+      nfr[q] = sqrtf(sq[q]);
+      const float dfn = fmaxf(nfr[q], eps);
+      float dot = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dot += un[e] * (v[q][e] / dfn);
+      dq[q] = dot;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+      for (int q = 0; q < CPW; ++q) dq[q] += __shfl_xor(dq[q], off, 64);
+    if (lane == 0) {
+#pragma unroll
+      for (int q = 0; q < CPW; ++q) {
+        const int c = wave + 4 * q;
+        if (c <= N) {
+          norms[(long)row * (N + 2) + 1 + c] = nfr[q];
+          cosv[(long)row * (N + 1) + c] = dq[q];
+          cs[c] = dq[q];
+        }
+      }
+    }
   } else {
     for (int c = wave; c <= N; c += 4) {
       const long item = copy_item(b, row, c);
@@ -274,6 +318,7 @@ __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ u
       score_copy(c, w);
     }
   }
+  DCUE_KT(0, 1);
   __syncthreads();
   const float invB = 1.f / (float)b.n_rows;
   for (int j = threadIdx.x; j < N; j += blockDim.x) {
@@ -296,6 +341,7 @@ __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ u
     rowsum[row] = s;
   }
   __syncthreads();
+  DCUE_KT(0, 3);
   // backward of the cosines: d cos/dx = (yhat - cos*xhat)/|x|
   const float nuc = fmaxf(nu, eps);
   float uh[4], gu[4];
@@ -304,17 +350,19 @@ __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ u
     uh[e] = u[e] / nuc;
     gu[e] = 0.f;
   }
+  const float rnuc = 1.f / nuc;
   auto back_copy = [&](int c, const float (&w)[4], float nf_raw) {
     const float dc = dcs[c];
     const float cv = cs[c];
     const float nf = fmaxf(nf_raw, eps);
+    const float rnf = 1.f / nf;  // divisions as products, as k_score_bwd (the same bits)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int k = lane + 64 * e;
       if (e < per && k < d) {
-        const float fh = w[e] / nf;
-        gu[e] += dc * (fh - cv * uh[e]) / nuc;
-        dfcopy[((long)row * (N + 1) + c) * d + k] = dc * (uh[e] - cv * fh) / nf;
+        const float fh = w[e] * rnf;
+        gu[e] += dc * (fh - cv * uh[e]) * rnuc;
+        dfcopy[((long)row * (N + 1) + c) * d + k] = dc * (uh[e] - cv * fh) * rnf;
       }
     }
   };
@@ -339,9 +387,12 @@ __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ u
     const int k = lane + 64 * e;
     if (e < per && k < d) gus[wave][k] = gu[e];
   }
+  DCUE_KT(0, 4);
   __syncthreads();
   for (int k = threadIdx.x; k < d; k += blockDim.x)
     dU[(long)row * d + k] = ((gus[0][k] + gus[1][k]) + gus[2][k]) + gus[3][k];
+  DCUE_KT(0, 5);
+  DCUE_KTW(0, 7);
 }
 
 int launch_score_fused(const float* uf, const float* f, const dcue_batch* b, int d, float margin,
@@ -372,6 +423,7 @@ __global__ __launch_bounds__(256) void k_score_bwd(const float* __restrict__ uf,
   const int N = b.n_neg, per = (d + 63) / 64;
   const float eps = 1e-8f;
   const float nu = fmaxf(norms[(long)row * (N + 2)], eps);
+  const float rnu = 1.f / nu;
   float u[4], gu[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -386,13 +438,14 @@ __global__ __launch_bounds__(256) void k_score_bwd(const float* __restrict__ uf,
     const float dc = c == 0 ? dpos : -dscores[(long)row * N + c - 1];
     const float cv = cosv[(long)row * (N + 1) + c];
     const float nf = fmaxf(norms[(long)row * (N + 2) + 1 + c], eps);
+    const float rnf = 1.f / nf;  // the backward's divisions as products (k_score_fused: the same)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int k = lane + 64 * e;
       if (e < per && k < d) {
-        const float fh = f[item * d + k] / nf;
-        gu[e] += dc * (fh - cv * u[e]) / nu;
-        dfcopy[((long)row * (N + 1) + c) * d + k] = dc * (u[e] - cv * fh) / nf;
+        const float fh = f[item * d + k] * rnf;
+        gu[e] += dc * (fh - cv * u[e]) * rnu;
+        dfcopy[((long)row * (N + 1) + c) * d + k] = dc * (u[e] - cv * fh) * rnf;
       }
     }
   }
@@ -438,7 +491,6 @@ struct ItemGradFc {
 };
 
 constexpr int kItemGradWLds = 128;  // W staged in LDS up to d = 128 (64 KB)
-
 template <bool WLDS>
 __global__ __launch_bounds__(256) void k_item_grad(const float* __restrict__ dfcopy, dcue_batch b, int d,
                                                    float* df, ItemGradFc fc) {
@@ -629,22 +681,83 @@ __global__ __launch_bounds__(256) void k_item_grad_multi(const float* __restrict
   __shared__ float dfs[IT][256];
   __shared__ float part[2][IT][128];
   __shared__ float rs[1024];
+  __shared__ float pw[IT == 1 ? 4 : 1][256];  // one item per workgroup: the four waves' copy sums
   extern __shared__ __attribute__((aligned(16))) float wl[];  // [d][d] when WLDS
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i0 = blockIdx.x * IT;
   const int N = b.n_neg, B = b.n_rows, M = b.n_items;
   const bool gather = b.layout != DCUE_LAYOUT_CATALOGUE;
   const int per = (d + 63) / 64;
+  DCUE_KTW(1, 6);
+  DCUE_KT(1, 0);
   if constexpr (WLDS) {
     if (fc.W) {
+      // four loads in flight before their LDS stores (a load-store loop waits one L2 round trip
+      // per float4)
       const int n4 = d * d / 4;
-      for (int q = threadIdx.x; q < n4; q += blockDim.x)
-        reinterpret_cast<float4*>(wl)[q] = reinterpret_cast<const float4*>(fc.W)[q];
+      const float4* W4 = reinterpret_cast<const float4*>(fc.W);
+      float4* L4 = reinterpret_cast<float4*>(wl);
+      int q = threadIdx.x;
+      for (; q + 768 < n4; q += 1024) {
+        const float4 a = W4[q], b1 = W4[q + 256], c = W4[q + 512], e = W4[q + 768];
+        L4[q] = a;
+        L4[q + 256] = b1;
+        L4[q + 512] = c;
+        L4[q + 768] = e;
+      }
+      for (; q < n4; q += 256) L4[q] = W4[q];
     }
   }
+  DCUE_KT(1, 1);
   if (fc.rowsum && blockIdx.x == 0)
     for (int r = threadIdx.x; r < B; r += blockDim.x) rs[r] = fc.rowsum[r];
-  for (int it = wave; it < IT; it += 4) {
+  if constexpr (IT == 1) {
+    // one item: its copies over the four waves (wave w: copies c0 + w, c0 + w + 4, ...), each
+    // wave's sum in copy order, then the four sums in wave order (deterministic)
+    const int i = i0;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (i < M) {
+      int c0 = 0, c1 = 1;
+      long cat_idx = 0;
+      if (gather) {
+        c0 = copy_ptr[i];
+        c1 = copy_ptr[i + 1];
+      } else {
+        cat_idx = i < B ? (long)i * (N + 1) : (long)((i - B) / N) * (N + 1) + 1 + (i - B) % N;
+      }
+      constexpr int kRows = 8;
+      for (int qb = c0 + wave; qb < c1; qb += 4 * kRows) {
+        long ci[kRows];
+#pragma unroll
+        for (int r = 0; r < kRows; ++r)
+          ci[r] = qb + 4 * r < c1 ? (gather ? (long)copy_idx[qb + 4 * r] : cat_idx) : -1;
+        float v[kRows][4];
+#pragma unroll
+        for (int r = 0; r < kRows; ++r)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int k = lane + 64 * e;
+            v[r][e] = (ci[r] >= 0 && e < per && k < d) ? dfcopy[ci[r] * d + k] : 0.f;
+          }
+#pragma unroll
+        for (int r = 0; r < kRows; ++r)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[e] += v[r][e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = lane + 64 * e;
+      if (e < per && k < d) pw[wave][k] = acc[e];
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < d; k += blockDim.x) {
+      const float v = ((pw[0][k] + pw[1][k]) + pw[2][k]) + pw[3][k];
+      dfs[0][k] = v;
+      if (i < M) df[(long)i * d + k] = v;
+    }
+  }
+  for (int it = wave; IT > 1 && it < IT; it += 4) {
     const int i = i0 + it;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     if (i < M) {
@@ -688,6 +801,7 @@ __global__ __launch_bounds__(256) void k_item_grad_multi(const float* __restrict
       if (e < per && k < d) dfs[it][k] = acc[e];
     }
   }
+  DCUE_KT(1, 2);
   if (fc.dfmax) {  // max |df| per column over the block's items
     __syncthreads();
     if (threadIdx.x < d) {
@@ -716,7 +830,9 @@ __global__ __launch_bounds__(256) void k_item_grad_multi(const float* __restrict
 #pragma unroll
       for (int it = 0; it < IT; ++it) part[h][it][n] = g[it];
     }
+    DCUE_KT(1, 3);
     __syncthreads();
+    DCUE_KT(1, 4);
     if (threadIdx.x < d) {
       const int n = threadIdx.x;
       const float mu5 = fc.mean5[n], is5 = fc.invstd5[n];
@@ -737,6 +853,7 @@ __global__ __launch_bounds__(256) void k_item_grad_multi(const float* __restrict
       if (fc.g5max) atomicMax(fc.g5max + n, ord_key(gm));
     }
   }
+  DCUE_KT(1, 5);
   if (fc.rowsum && blockIdx.x == 0) {  // loss = mean of the row sums in row order (k_loss_mean's sums)
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -745,6 +862,7 @@ __global__ __launch_bounds__(256) void k_item_grad_multi(const float* __restrict
       *fc.loss = s / (float)B;
     }
   }
+  DCUE_KTW(1, 7);
 }
 
 template <int IT, bool WLDS>
