@@ -370,6 +370,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
     if constexpr (F16) range_stage<SRC>(a, KC, chl);
     if constexpr (SRC != SRC_DZ)
       if (blockIdx.x == 0 && blockIdx.y == 0) bn_publish(a.in_bn, threadIdx.x);
+    DCUE_KT(KID, 5);
     __syncthreads();
     if constexpr (F16) sscale = split_scale(chl, KC);
     const ChanOps kop = chan_ops<SRC>(chl, c);

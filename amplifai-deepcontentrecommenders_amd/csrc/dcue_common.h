@@ -57,7 +57,7 @@ void count_launch();
     }                                                                                             \
   } while (0)
 
-// DCUE_KTRACE diagnostic builds (scratch/build_ktrace.sh): thread 0 of each workgroup stores phase
+// DCUE_KTRACE diagnostic builds (profiles/tools/build_ktrace.sh): thread 0 of each workgroup stores phase
 // timestamps of selected kernels (slots 0-5 shader clock, 6-7 the 100 MHz wall clock) into
 // dcue_ktrace_buf[kernel][block] (tail.hip), read back with dcue_ktrace_read. Compiled out otherwise.
 constexpr int kKtraceKernels = 16, kKtraceBlocks = 512;

@@ -2,7 +2,7 @@
 // launches, the late Adam, a plan's next-step inputs) while the calling thread issues the caller's
 // stream chain. Each HIP launch costs the issuing thread ~2.6 µs and each record/wait pair ~2.8 µs
 // on MI355X / ROCm 7.2; two threads issuing to different streams reach ~1.7 µs per launch of wall
-// time (scratch/mtlaunch.cpp, measured), so a step's host issue time becomes roughly the longer of
+// time (profiles/tools/mtlaunch.cpp, measured), so a step's host issue time becomes roughly the longer of
 // the two parts instead of their sum.
 //
 // Ordering is the same as with one thread: the caller posts a side closure only after it has
