@@ -2,8 +2,8 @@
 // launches, the late Adam, a plan's next-step inputs) while the calling thread issues the caller's
 // stream chain. Each HIP launch costs the issuing thread ~2.6 µs and each record/wait pair ~2.8 µs
 // on MI355X / ROCm 7.2; two threads issuing to different streams reach ~1.7 µs per launch of wall
-// time (profiles/tools/mtlaunch.cpp, measured), so a step's host issue time becomes roughly the longer of
-// the two parts instead of their sum.
+// time (profiles/tools/mtlaunch.cpp, measured), so a step's host issue time becomes roughly the
+// longer of the two parts instead of their sum.
 //
 // Ordering is the same as with one thread: the caller posts a side closure only after it has
 // recorded (or bound to a launch) every event the closure waits on, and waits for a closure's
@@ -109,16 +109,21 @@ bool side_thread_on() {
 }
 
 SideIssuer* issuer_for_device() {
-  static SideIssuer* per_dev[64] = {};
+  static std::atomic<SideIssuer*> per_dev[64] = {};
   static std::mutex mu;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!per_dev[dev]) {
+  SideIssuer* p = per_dev[dev].load(std::memory_order_acquire);
+  if (!p) {
     std::lock_guard<std::mutex> lk(mu);
     // never destroyed: the worker parks when idle and ends with the process
-    if (!per_dev[dev]) per_dev[dev] = new SideIssuer(dev);
+    p = per_dev[dev].load(std::memory_order_relaxed);
+    if (!p) {
+      p = new SideIssuer(dev);
+      per_dev[dev].store(p, std::memory_order_release);
+    }
   }
-  return per_dev[dev];
+  return p;
 }
 }  // namespace
 
