@@ -38,9 +38,10 @@ __device__ __forceinline__ void acc128_add(unsigned long long* a, float v) {
   if (hi) atomicAdd(a + 1, (unsigned long long)hi);
 }
 
-__device__ __forceinline__ double acc128_value(const unsigned long long* a) {
-  return (double)(long long)a[1] * 0x1p-24 + (double)a[0] * 0x1p-64;
+__device__ __forceinline__ double acc128_words(unsigned long long lo, unsigned long long hi) {
+  return (double)(long long)hi * 0x1p-24 + (double)lo * 0x1p-64;
 }
+__device__ __forceinline__ double acc128_value(const unsigned long long* a) { return acc128_words(a[0], a[1]); }
 
 // Accumulator block of one BN layer: [2 sums][C channels][2 words].
 __device__ __forceinline__ unsigned long long* acc_at(unsigned long long* acc, int C, int which, int c) {
@@ -55,9 +56,8 @@ struct BnChan {
   float mean, invstd, var;
   double var_unbiased;
 };
-__device__ __forceinline__ BnChan bn_chan_train(const unsigned long long* acc, int C, int c, double count,
-                                                double inv_count) {
-  const double s = acc_sum(acc, C, 0, c), ss = acc_sum(acc, C, 1, c);
+// ... from the channel's two sums (s = sum x, ss = sum x^2)
+__device__ __forceinline__ BnChan bn_chan_sums(double s, double ss, double count, double inv_count) {
   const double m = s * inv_count;
   double v = ss * inv_count - m * m;
   if (v < 0.0) v = 0.0;
@@ -67,6 +67,10 @@ __device__ __forceinline__ BnChan bn_chan_train(const unsigned long long* acc, i
   r.invstd = 1.f / sqrtf(r.var + 1e-5f);
   r.var_unbiased = count > 1.0 ? v * count / (count - 1.0) : v;
   return r;
+}
+__device__ __forceinline__ BnChan bn_chan_train(const unsigned long long* acc, int C, int c, double count,
+                                                double inv_count) {
+  return bn_chan_sums(acc_sum(acc, C, 0, c), acc_sum(acc, C, 1, c), count, inv_count);
 }
 
 // Where a forward consumer publishes a finalized BN layer (its block 0 does it once per step):

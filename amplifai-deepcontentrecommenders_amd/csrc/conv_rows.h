@@ -31,17 +31,67 @@ struct ChanOps {        // per-channel constants of the fused op for one channel
   float4 inv, sd, sdx;  // dgrad: BN_l backward (mu = mean_l, sc = a_l)
 };
 
-// BN_l backward sums of channel c from its accumulators: sum g (sD) and sum g*xhat (sDx)
-__device__ __forceinline__ float2 bwd_sums(const unsigned long long* acc, int C, int c) {
-  return make_float2((float)acc_sum(acc, C, 0, c), (float)acc_sum(acc, C, 1, c));
-}
-
 // Per-channel constants of the fused op, finalized once per channel per workgroup (thread t owns
 // channel t) into LDS, then read by quad: the fp64 finalize is one short chain per thread.
 struct ChanLds {
   float v[5][256];
   float wmax[4];  // split-f16 forward: the per-wave maxima of the channels' value bounds
 };
+
+// The global inputs of chan_stage / range_stage for thread t's channel, loaded at the kernel's
+// entry before the weight prefetch and the slab reads: loads return in issue order, so loaded after
+// those (as they were) the fp64 finalize and the split-scale bound waited for the whole first slab
+// batch and then added their own chain (kernel-phase traces).
+struct ChanPre {
+  unsigned long long w[4];  // forward train: the input BN's (sum, sum sq) words; dgrad: (sD, sDx)
+  float f[3];               // forward: gamma | (mean, a), beta; dgrad: mean_l, a_l, invstd_l
+  unsigned r[2];            // split-f16: range keys (forward hi / -lo; dgrad max|g|, y_l's max)
+  double count, inv_count;
+  bool train;
+};
+template <int SRC, bool F16>
+__device__ __forceinline__ ChanPre chan_preload(const RowsArgs& a, int KC) {
+  ChanPre q;
+  const int t = threadIdx.x;
+  q.w[0] = q.w[1] = q.w[2] = q.w[3] = 0;
+  q.f[0] = q.f[1] = q.f[2] = 0.f;
+  q.r[0] = q.r[1] = 0u;
+  q.count = a.in_bn.count;
+  q.inv_count = a.in_bn.inv_count;
+  q.train = SRC != SRC_DZ && a.in_bn.acc != nullptr;
+  if (t >= KC) return q;
+  const unsigned long long* acc = SRC == SRC_DZ ? a.dz_acc : a.in_bn.acc;
+  if (SRC == SRC_DZ || q.train) {
+    q.w[0] = acc[(size_t)t * 2];
+    q.w[1] = acc[(size_t)t * 2 + 1];
+    q.w[2] = acc[((size_t)KC + t) * 2];
+    q.w[3] = acc[((size_t)KC + t) * 2 + 1];
+  }
+  if constexpr (SRC != SRC_DZ) {
+    if (q.train) {
+      q.f[0] = a.in_bn.gamma[t];
+    } else {
+      q.f[0] = a.in_mean[t];
+      q.f[1] = a.in_a[t];
+    }
+    q.f[2] = a.in_beta ? a.in_beta[t] : 0.f;
+    if constexpr (F16)
+      if (a.in_range) {
+        q.r[0] = a.in_range[t];
+        q.r[1] = a.in_range[kRngC + t];
+      }
+  } else {
+    q.f[0] = a.mean_l[t];
+    q.f[1] = a.a_l[t];
+    q.f[2] = a.invstd_l[t];
+    if constexpr (F16)
+      if (a.in_range) {
+        q.r[0] = a.in_range[t];
+        q.r[1] = a.y_range ? a.y_range[t] : 0u;
+      }
+  }
+  return q;
+}
 
 // Split-f16 forward operand scale. Every slab value v is stored as v*S = hi + lo in
 // fp16, S a power of two, and the epilogue multiplies the accumulators by 1/S: exact, so the result
@@ -57,20 +107,20 @@ struct ChanLds {
 // kDmax (|sD| + max|xhat| |sDx|)), max|g| from the producer's epilogue (in_range), max|xhat| from
 // y_l's range -- the same bound as the split-f16 weight gradient's (conv_wgrad.hip).
 template <int SRC>
-__device__ __forceinline__ void range_stage(const RowsArgs& a, int KC, ChanLds& L) {
+__device__ __forceinline__ void range_stage(const RowsArgs& a, const ChanPre& q, int KC, ChanLds& L) {
   const int t = threadIdx.x;
   if (t >= 256) return;  // waves 0-3 (uniform per wave)
   float bnd = 0.f;
   if (SRC == SRC_DZ) {
     if (t < KC && a.in_range) {
-      const unsigned kg = a.in_range[t], ky = a.y_range ? a.y_range[t] : 0u;
+      const unsigned kg = q.r[0], ky = q.r[1];
       const float gmax = kg ? ord_value(kg) : 0.f, ym = ky ? fmaxf(ord_value(ky), 0.f) : 0.f;
       const float mu = L.v[0][t], av = L.v[1][t], iv = L.v[2][t];
       const float xhm = fmaxf(fabsf(mu), fabsf(ym - mu)) * iv;
       bnd = fabsf(av) * (gmax + a.kd_max * (fabsf(L.v[3][t]) + xhm * fabsf(L.v[4][t])));
     }
   } else if (t < KC && a.in_range) {
-    const unsigned khi = a.in_range[t], knlo = a.in_range[kRngC + t];
+    const unsigned khi = q.r[0], knlo = q.r[1];
     float hi = khi ? ord_value(khi) : 0.f;
     float lo = (SRC == SRC_ACT) ? 0.f : (knlo ? -ord_value(knlo) : 0.f);
     if (SRC == SRC_ACT) hi = fmaxf(hi, 0.f);
@@ -100,26 +150,26 @@ __device__ __forceinline__ SplitScale split_scale(const ChanLds& L, int KC) {
 }
 
 template <int SRC>
-__device__ __forceinline__ void chan_stage(const RowsArgs& a, int KC, ChanLds& L) {
+__device__ __forceinline__ void chan_stage(const ChanPre& q, int KC, ChanLds& L) {
   const int t = threadIdx.x;
   if (t >= KC) return;
   if constexpr (SRC != SRC_DZ) {
-    if (a.in_bn.acc) {  // train: the input BN's batch statistics, finalized here
-      const BnChan st = bn_chan_train(a.in_bn.acc, KC, t, a.in_bn.count, a.in_bn.inv_count);
+    if (q.train) {  // train: the input BN's batch statistics, finalized here
+      const BnChan st = bn_chan_sums(acc128_words(q.w[0], q.w[1]), acc128_words(q.w[2], q.w[3]), q.count,
+                                     q.inv_count);
       L.v[0][t] = st.mean;
-      L.v[1][t] = a.in_bn.gamma[t] * st.invstd;
+      L.v[1][t] = q.f[0] * st.invstd;
     } else {
-      L.v[0][t] = a.in_mean[t];
-      L.v[1][t] = a.in_a[t];
+      L.v[0][t] = q.f[0];
+      L.v[1][t] = q.f[1];
     }
-    L.v[2][t] = a.in_beta ? a.in_beta[t] : 0.f;
+    L.v[2][t] = q.f[2];
   } else {
-    L.v[0][t] = a.mean_l[t];
-    L.v[1][t] = a.a_l[t];
-    L.v[2][t] = a.invstd_l[t];
-    const float2 sd = bwd_sums(a.dz_acc, KC, t);
-    L.v[3][t] = sd.x;
-    L.v[4][t] = sd.y;
+    L.v[0][t] = q.f[0];
+    L.v[1][t] = q.f[1];
+    L.v[2][t] = q.f[2];
+    L.v[3][t] = (float)acc128_words(q.w[0], q.w[1]);
+    L.v[4][t] = (float)acc128_words(q.w[2], q.w[3]);
   }
 }
 
@@ -248,6 +298,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
   [[maybe_unused]] constexpr int KID = 2 + MODE * 5 + (LIN >= 131 ? 0 : LIN >= 32 ? 1 : LIN >= 8 ? 2 : LIN >= 2 ? 3 : 4);
   DCUE_KTW(KID, 6);
   DCUE_KT(KID, 0);
+  const ChanPre cpre = chan_preload<SRC, F16>(a, KC);
   constexpr int RX = R + KS - 1;
   constexpr int ROWS = TW * 16;
   constexpr int MAXI = (ROWS + R - 1) / R + 1;
@@ -366,8 +417,8 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
     };
     // the first batch's reads are in flight while the per-channel constants are finalized
     load_batch(threadIdx.x);
-    chan_stage<SRC>(a, KC, chl);
-    if constexpr (F16) range_stage<SRC>(a, KC, chl);
+    chan_stage<SRC>(cpre, KC, chl);
+    if constexpr (F16) range_stage<SRC>(a, cpre, KC, chl);
     if constexpr (SRC != SRC_DZ)
       if (blockIdx.x == 0 && blockIdx.y == 0) bn_publish(a.in_bn, threadIdx.x);
     DCUE_KT(KID, 5);
