@@ -357,7 +357,12 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
   SplitScale sscale = {1.f, 1.f};  // split-f16 operand scale (range_stage)
   {
     static_assert(kRowsThreads % C4 == 0, "a thread's slab slots share one channel quad");
-    constexpr int FB = SRC == SRC_DZ ? 4 : 8;  // slab slots (float4) in flight per thread
+    // slab slots (float4) in flight per thread: at most what the workgroup's slab can hold (its rows
+    // plus a KS-1 halo per item spanned) -- every slot of a batch is loaded, masked or not, so the
+    // one-tile launches of in-batch steps (<= 2 slots per thread) issued 6 of 8 loads for nothing
+    constexpr int FB0 = SRC == SRC_DZ ? 4 : 8;
+    constexpr int FB_NEED = ((ROWS + MAXI * (KS - 1)) * C4 + kRowsThreads - 1) / kRowsThreads;
+    constexpr int FB = FB_NEED < FB0 ? FB_NEED : FB0;
     const int nfill = nslab * C4;
     const int c = 4 * (threadIdx.x % C4);
     __shared__ ChanLds chl;
