@@ -784,14 +784,16 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   const std::function<int()> user_part = [&]() -> int {
     TRY(wait_point(su, ev_in));
     HPROF("capi:5");
-    // DCUE_USER_FWD=split: the rows' sync (k_emb_sync, one workgroup per row) and the two GEMMs
-    // (k_tgemm, 16 x 64 blocks) as three launches instead of k_user_fwd (A/B)
+    // The rows' sync (k_emb_sync, one workgroup per row) and the two GEMMs (k_tgemm, 16 x 64
+    // blocks) as three launches. DCUE_USER_FWD=fused issues them as one (k_user_fwd) instead: off by
+    // default -- in 7 of 32 runs of the schedule test (tests/test_gpu_schedule.py) a fused-path
+    // process went non-finite from its second step on (loss = N x margin), never the split path;
+    // the cause is not found yet
     static const bool split_fwd = [] {
       const char* e = getenv("DCUE_USER_FWD");
-      return e && e[0] == 's';
+      return !(e && e[0] == 'f');
     }();
     {
-      // the deferred rows' sync and the two GEMMs in one launch (k_user_fwd)
       ForkAfter fk(sp, su, &ev_uf);
       if (split_fwd) {
         if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));

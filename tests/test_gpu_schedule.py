@@ -22,8 +22,9 @@ VARIANTS = [
     {"DCUE_PROLOGUE_FIRST": "1"},
     {"DCUE_LATE_WAIT": "conv1"},
     {"DCUE_AHEAD_AT": "fork"},
-    {"DCUE_USER_FWD": "split"},
 ]
+# (DCUE_USER_FWD=fused, the one-launch user tower, is left out: it is off by default because this
+# test caught it going non-finite in some runs)
 
 
 def test_schedule_variants_bit_identical(tmp_path):
