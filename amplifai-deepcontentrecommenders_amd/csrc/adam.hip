@@ -513,7 +513,9 @@ __global__ __launch_bounds__(512) void k_user_fwd(UserFwdArgs a) {
     const AdamScalars* hist = log_hist(a.hdr);
     for (int j = lo + t; j <= T; j += blockDim.x) hs[j % cap] = hist[j % cap];
     __syncthreads();
+    // (lo > T: nothing to replay -- no row is claimed -- but sb is still read below: give it a value)
     if (lo <= T) window_bound(hs, lo, T, cap, 0.f, &sb);
+    else if (t == 0) sb = ReplayBound{};
     __syncthreads();
     const ReplayBound b = sb;
     for (int e = t; e < nr * a.E; e += blockDim.x) {
@@ -527,22 +529,25 @@ __global__ __launch_bounds__(512) void k_user_fwd(UserFwdArgs a) {
       a.p[off] = pp[0]; a.m[off] = mm[0]; a.v[off] = vv[0];
     }
     __syncthreads();
-    if (t < nr) {
+    // Every claimed clock is released before any lane waits: claimers and waiters are lanes of one
+    // wave, and a wave spinning with its claimer lanes masked off would never release them (two
+    // workgroups each waiting for a row the other holds would then both spin to the bound).
+    if (t < nr && claim_s[t]) {
+      __threadfence();  // the row's replayed values before its clock (other workgroups wait on it)
+      __hip_atomic_store(a.emb_step + a.users[r0 + t], T, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (t < nr && !claim_s[t]) {
       int32_t* clk = a.emb_step + a.users[r0 + t];
-      if (claim_s[t]) {
-        __threadfence();  // the row's replayed values before its clock (other workgroups wait on it)
-        __hip_atomic_store(clk, T, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        unsigned spins = 0;
-        while (__hip_atomic_load(clk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == INT_MIN) {
-          __builtin_amdgcn_s_sleep(2);
-          if (++spins > (1u << 22)) {
-            if (a.fail) atomicOr(a.fail, 1u);
-            break;
-          }
+      unsigned spins = 0;
+      while (__hip_atomic_load(clk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == INT_MIN) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 22)) {  // never expected: reported (dcue_debug_fail_flags), not silent
+          atomicOr(a.fail, 1u);
+          break;
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
   }
@@ -561,7 +566,9 @@ int launch_user_fwd(const dcue_model* md, const TGemmArgs& g1, const TGemmArgs& 
   a.p = md->emb; a.m = md->emb_exp_avg; a.v = md->emb_exp_avg_sq;
   a.hdr = md->emb_log; a.emb_step = md->emb_step;
   a.users = users; a.B = B; a.E = md->dims.user_embdim;
-  a.fail = nullptr;
+  static unsigned* const fail = user_fwd_fail_flag();
+  if (!fail) return DCUE_ERR_HIP;
+  a.fail = fail;
   DCUE_LAUNCH(k_user_fwd, dim3((unsigned)((B + 15) / 16)), dim3(512), 0, s, a);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;

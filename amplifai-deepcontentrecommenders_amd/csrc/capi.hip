@@ -494,6 +494,7 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     // the previous step's late-segment Adam (split plans, StepOpts::dense_split) ran on the user
     // stream: conv 2 is the first kernel on this stream to read those parameters
     if (l == 2 && before_l2) TRY(wait_point(s, before_l2));
+    if (l == 2 && train) TRY(debug_delay(DCUE_SITE_CONV2, s));
     RowsArgs a = {};
     a.src = l == 1 ? t->data : (const void*)w.y[l - 1];
     a.item_track = item_track;
@@ -516,6 +517,7 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     TRY(timer_begin(&tsc, l == 1 ? DCUE_TIMED_CONV1_FWD : -1, s));
     TRY(launch_conv_fwd(l, l == 1 ? kMels : c.H, l == 1 ? src : SRC_ACT, a, s));
     TRY(timer_end(&tsc));
+    TRY(probe(PR_Y1 + l - 1, w.y[l], (long)M * layer_geom(l).lp * a.nout, s));
     if (sync) TRY(comm_allreduce_u64(sync_bn, bn_acc(w.bnacc, w.cmax, l), 4L * w.cmax, s));
     if (l == 1 && after_l1) TRY((*after_l1)());
   }
@@ -536,7 +538,8 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     g.B = c.P(SEG_FC_W); g.sbk = 1; g.sbn = c.FI;
     g.bias = c.P(SEG_FC_B);
     g.C = f_out ? f_out : w.f; g.scm = c.D; g.scn = 1;
-    return launch_tgemm(0, 0, g, s);
+    TRY(launch_tgemm(0, 0, g, s));
+    return probe(PR_F, g.C, (long)M * c.D, s);
   }
   // fc on BN5(y5): f = bn5(y5) W^T + b   (truedcuemel1dbn.py:65,101)
   TGemmArgs g = {};
@@ -547,7 +550,8 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
   g.B = c.P(SEG_FC_W); g.sbk = 1; g.sbn = c.D;
   g.bias = c.P(SEG_FC_B);
   g.C = f_out ? f_out : w.f; g.scm = c.D; g.scn = 1;
-  return launch_tgemm(2, 0, g, s);
+  TRY(launch_tgemm(2, 0, g, s));
+  return probe(PR_F, g.C, (long)M * c.D, s);
 }
 
 // user tower (userembedding.py:33-44): h1 = relu(E[u]) W1^T + b1; uf = relu(h1) W2^T + b2
@@ -784,6 +788,7 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   const std::function<int()> user_part = [&]() -> int {
     TRY(wait_point(su, ev_in));
     HPROF("capi:5");
+    TRY(debug_delay(DCUE_SITE_USER_FWD, su));
     // The rows' sync (k_emb_sync, one workgroup per row) and the two GEMMs (k_tgemm, 16 x 64
     // blocks) as three launches. DCUE_USER_FWD=fused issues them as one (k_user_fwd) instead: off by
     // default -- in 7 of 32 runs of the schedule test (tests/test_gpu_schedule.py) a fused-path
@@ -805,6 +810,8 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
       TRY(fk.done());
       HPROF("capi:8");
     }
+    TRY(probe(PR_H1, w.h1, (long)b->n_rows * c.E, su));
+    TRY(probe(PR_UF, w.uf, (long)b->n_rows * c.D, su));
     if (o.flush_slice_step >= 0 && m->emb_step) TRY(launch_emb_flush_rows(m, o.flush_slice_step, su));
     return DCUE_OK;
   };
@@ -833,9 +840,17 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
     // a fork point after the score kernel only for a caller that asks for one: a launch-bound event
     // costs the chain a ≈6 µs gap before its next kernel (the backward's side work waits for the
     // dgrad chain's first fork point instead)
-    if (!o.score_done)
-      return launch_score_fused(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.rowsum, w.du,
-                                w.dfcopy, s);
+    const int B = b->n_rows, N = b->n_neg;
+    auto probes = [&]() -> int {
+      TRY(probe(PR_SCORES, w.scores, (long)B * N, s));
+      TRY(probe(PR_DU, w.du, (long)B * c.D, s));
+      return probe(PR_DFCOPY, w.dfcopy, (long)B * (N + 1) * c.D, s);
+    };
+    if (!o.score_done) {
+      TRY(launch_score_fused(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.rowsum, w.du,
+                             w.dfcopy, s));
+      return probes();
+    }
     hipEvent_t ev = nullptr;
     ForkAfter fk(sp, s, &ev);
     TRY(launch_score_fused(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.rowsum, w.du,
@@ -843,7 +858,7 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
     TRY(fk.done());
     HPROF("capi:10");
     *o.score_done = ev;
-    return DCUE_OK;
+    return probes();
   }
   return launch_score_fwd(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.hinge, w.loss,
                           w.dhinge, s);
@@ -1000,6 +1015,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   auto user_bwd = [&]() -> int {
     TRY(wait_point(su, ev_score ? ev_score : ev_layer[3]));
     HPROF("capi:26");
+    TRY(debug_delay(DCUE_SITE_USER_BWD, su));
     {
       // two launches of two independent GEMMs each (launch_tgemm_pair; the same blocks as four
       // launch_tgemm calls, so the same bits): (dW2, dh1) from du, then (dW1, de) from dh1
@@ -1050,6 +1066,10 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       TRY(fk.done());
       HPROF("capi:31");
     }
+    if (probes_on()) {
+      TRY(probe(PR_DE, w.de, (long)B * E, su));
+      TRY(probe(PR_G_USER, c.Gd(SEG_L1_W), c.poff[SEG_L2_B + 1] - c.poff[SEG_L1_W], su));
+    }
     if (o.emb_adam && !emb_fused) TRY(launch_adam(m, o.emb_adam, c.poff, su, !o.defer_flush_slice));
     HPROF("capi:32");
     return DCUE_OK;
@@ -1060,6 +1080,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   auto fc_text_wgrad = [&]() -> int {
     TRY(wait_point(sw[1], ev_layer[5]));
     HPROF("capi:23");
+    TRY(debug_delay(DCUE_SITE_FC_WGRAD, sw[1]));
     TGemmArgs g = {};
     g.M = D; g.N = c.FI; g.K = M;
     g.A = w.df; g.sam = 1; g.sak = D;
@@ -1072,6 +1093,10 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     if (c.text)
       TRY(launch_text_wgrad(text_branch(c, t), b->item_track, M, w.dtp, w.tidx, w.twpart, c.Gd(SEG_TX_W),
                             c.Gd(SEG_TX_B), sw[1]));
+    if (probes_on()) {
+      TRY(probe(PR_G_FC, c.Gd(SEG_FC_W), c.poff[SEG_FC_B + 1] - c.poff[SEG_FC_W], sw[1]));
+      if (c.text) TRY(probe(PR_G_FC, c.Gd(SEG_TX_W), c.poff[SEG_TX_B + 1] - c.poff[SEG_TX_W], sw[1]));
+    }
     return DCUE_OK;
   };
 
@@ -1081,6 +1106,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   // + one reduce launch.
   auto issue_multi = [&](int lo, int hi, bool with_fc, hipStream_t so, hipEvent_t after, hipEvent_t* tl) -> int {
     TRY(wait_point(so, after));
+    TRY(debug_delay(lo == 2 ? DCUE_SITE_WGRAD_2 : DCUE_SITE_WGRAD_HI, so));
     WgradMulti mw = {};
     if (with_fc) {  // fc: dW[n][k] = sum_m df[m][n] bn5(y5)[m][k], db = sum_m df (df final since item_grad)
       const int j = mw.n++;
@@ -1122,9 +1148,14 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       mw.dW[j] = c.Gd(seg_conv_w(l));
       mw.db[j] = c.Gd(seg_conv_b(l));
     }
-    ForkAfter fk(sp, so, tl);
-    TRY(launch_conv_wgrad_multi(mw, so));
-    return fk.done();
+    {
+      ForkAfter fk(sp, so, tl);
+      TRY(launch_conv_wgrad_multi(mw, so));
+      TRY(fk.done());
+    }
+    if (!probes_on()) return DCUE_OK;
+    const int s1 = with_fc ? SEG_FC_B : seg_bn_b(hi);
+    return probe(lo == 2 ? PR_G_2 : PR_G_HI, c.Gd(seg_conv_w(lo)), c.poff[s1 + 1] - c.poff[seg_conv_w(lo)], so);
   };
 
   // the step's end. Split plans: the late segments' Adam (every gradient the side streams made) on the
@@ -1163,11 +1194,18 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
         TRY(wait_point(su, tail[2]));
         TRY(wait_point(su, tail[3]));
       }
+      // and the caller's stream up to its conv-1 tail: the dgrad of conv 2 (after the chain's last
+      // fork point) reads conv 2's packed weights, which this Adam rewrites
+      if (!legacy_orders()) TRY(wait_point(su, tail[0]));
       // (recorded by the plan's prologue closure, posted before this one: FIFO on the side thread)
       if (inputs_via_late && o.wait_inputs) TRY(wait_point(su, o.wait_inputs));
-      ForkAfter fk(sp, su, o.late_done);
-      TRY(launch_adam(m, &dense, c.poff, su, true, late, -1));
-      TRY(fk.done());
+      TRY(debug_delay(DCUE_SITE_LATE_ADAM, su));
+      {
+        ForkAfter fk(sp, su, o.late_done);
+        TRY(launch_adam(m, &dense, c.poff, su, true, late, -1));
+        TRY(fk.done());
+      }
+      TRY(probe(PR_P_LATE, m->params + late, c.poff[kSeg] - late, su));
     }
     return DCUE_OK;
   };
@@ -1226,6 +1264,10 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
                          cptr, cidx, grng_at(w, 5), grng_at(w, 6), s));
     HPROF("capi:15");
   }
+  if (probes_on()) {
+    TRY(probe(PR_DF, w.df, (long)M * D, s));
+    TRY(probe(PR_G5, w.g[5], (long)M * D, s));
+  }
   if (sync) TRY(comm_allreduce_u64(o.sync_bn, bn_acc(w.bnbacc, w.cmax, 5), 4L * w.cmax, s));
   for (int l = 5; l >= 2; --l) {  // dgrad chain: g_l (+ BN_l sums) -> g_{l-1} (+ BN_{l-1} sums)
     const LayerGeom gm = layer_geom(l);
@@ -1276,9 +1318,11 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
         if (thr) TRY(post(multi_2));
       }
     } else {
+      if (l == 2) TRY(debug_delay(DCUE_SITE_DGRAD_2, s));
       TRY(launch_conv_dgrad(l, l == 5 ? D : H, ra, s));
       if (sync) TRY(comm_allreduce_u64(o.sync_bn, bn_acc(w.bnbacc, w.cmax, l - 1), 4L * w.cmax, s));
     }
+    TRY(probe(PR_G4 + (5 - l), w.g[l - 1], (long)M * layer_geom(l - 1).lp * H, s));
     HPROF("capi:16");
   }
   // conv weight gradient of layer l on stream `so` (its own split-K partial set `ps`); `tail`:
@@ -1335,13 +1379,17 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       ba.md = m; ba.poff = c.poff; ba.args = *o.dense_split; ba.bn = c.bn;
       TRY(launch_bn0_grads_adam(w.G, w.S, c.gamma(w, 0), c.beta(w, 0), graw ? w.mean[0] : nullptr,
                                 graw ? w.invstd[0] : nullptr, H, c.dgamma(w, 0), c.dbeta(w, 0), ba, so));
-      return fk.done();
+      TRY(fk.done());
+      if (!probes_on()) return DCUE_OK;
+      TRY(probe(PR_G_1, m->grads, late, so));
+      return probe(PR_P_EARLY, m->params, late, so);
     }
     TRY(launch_bn0_grads(w.G, w.S, c.P(seg_conv_w(1)), c.gamma(w, 0), c.beta(w, 0),
                          graw ? w.mean[0] : nullptr, graw ? w.invstd[0] : nullptr, H,
                          c.Gd(seg_conv_w(1)), c.dgamma(w, 0), c.dbeta(w, 0),
                          c.Gd(seg_conv_b(1)), so));
-    return fk.done();
+    TRY(fk.done());
+    return probe(PR_G_1, m->grads, late, so);
   };
   // layer 1 (the step's tail) follows the chain on the caller's stream, issued right away
   if (ev_x0) TRY(wait_point(s, ev_x0));
@@ -1349,6 +1397,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(side.wait(o.ahead ? ahead_seq : o.wait_inputs_seq));
     TRY(wait_point(s, o.wait_inputs));
   }
+  TRY(debug_delay(DCUE_SITE_WGRAD_1, s));
   TRY(issue_wgrad(1, s, 2, &tail[0]));
   HPROF("capi:22");
 
@@ -1373,24 +1422,28 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(comm_exchange_split(o.comm, m, &dense, c.poff, late, n, sides, 3, ld, s));
     if (o.late_done) *o.late_done = ld;
     TRY(launch_adam(m, &dense, c.poff, s, true, 0, late));
-    if (o.tails) {
+    TRY(probe(PR_P_EARLY, m->params, late, s));
+    if (o.tails) {  // [1]: the comm stream after the late Adam, which waited for every side stream
       o.tails[0] = tail[0];
-      o.tails[1] = nullptr;
+      o.tails[1] = ld;
     }
     return DCUE_OK;
   }
   TRY(post(late_part));
   if (o.dense_split) {
-    if (!fuse_late) TRY(launch_adam(m, &dense, c.poff, s, true, 0, late));
+    if (!fuse_late) {
+      TRY(launch_adam(m, &dense, c.poff, s, true, 0, late));
+      TRY(probe(PR_P_EARLY, m->params, late, s));
+    }
   } else {
     TRY(side.drain());
     TRY(wait_point(s, joined));
   }
   TRY(side.drain());
   HPROF("capi:36");
-  if (o.tails) {
+  if (o.tails) {  // [1], split steps: the user stream after the late Adam (it waited for the others)
     o.tails[0] = tail[0];
-    o.tails[1] = joined;
+    o.tails[1] = o.dense_split && o.late_done ? *o.late_done : joined;
   }
   return DCUE_OK;
 }

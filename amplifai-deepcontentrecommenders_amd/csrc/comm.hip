@@ -129,10 +129,21 @@ int comm_exchange_split(dcue_comm* c, const dcue_model* m, const dcue_adam_args*
   for (int i = 0; i < nside; ++i)
     if (side[i]) DCUE_HIP_CHECK(hipStreamWaitEvent(c->stream, side[i], 0));
   TRY(comm_allreduce_sum(c, m->grads + late, n - late));
+  // The late Adam rewrites conv 2's packed weights, which the caller's stream reads in its last
+  // input gradient (after the side streams forked off): it waits for the caller's stream first.
+  // The late bucket's all-reduce above still overlaps the conv-1 weight gradient.
+  const bool legacy = legacy_orders();
+  if (!legacy) {
+    DCUE_HIP_CHECK(hipEventRecord(c->ev_tail, s));
+    DCUE_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_tail, 0));
+  }
+  TRY(debug_delay(DCUE_SITE_LATE_ADAM, c->stream));
   TRY(launch_adam(m, dense, poff, c->stream, true, late, n));  // the late segments' Adam, divide fused
   DCUE_HIP_CHECK(hipEventRecord(late_done, c->stream));
-  DCUE_HIP_CHECK(hipEventRecord(c->ev_tail, s));
-  DCUE_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_tail, 0));
+  if (legacy) {
+    DCUE_HIP_CHECK(hipEventRecord(c->ev_tail, s));
+    DCUE_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_tail, 0));
+  }
   TRY(comm_allreduce_sum(c, m->grads, late));
   DCUE_HIP_CHECK(hipEventRecord(c->ev_done, c->stream));
   DCUE_HIP_CHECK(hipStreamWaitEvent(s, c->ev_done, 0));

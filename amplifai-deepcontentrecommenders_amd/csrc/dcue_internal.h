@@ -482,6 +482,29 @@ bool on_side_worker();
 // inputs (capi.hip)
 bool late_wait_at_conv1();
 
+// ---------------------------------------------------------------- diagnostics (debug.hip)
+// a spin kernel ahead of the work at `site` when a delay is set for it (dcue_debug_delay)
+int debug_delay(int site, hipStream_t s);
+// dcue_debug_probes: one record per probe id
+struct ProbeRec {
+  unsigned nonfinite, nonzero;
+  unsigned long long first_bad;
+};
+enum ProbeId {
+  PR_Y1 = 0,  // ... PR_Y1 + 4 = y5
+  PR_H1 = 5, PR_UF, PR_F, PR_SCORES, PR_DU, PR_DFCOPY, PR_DF, PR_G5,
+  PR_G4, PR_G3, PR_G2, PR_G1,  // dgrads 5..2
+  PR_DE, PR_G_USER, PR_G_HI, PR_G_2, PR_G_FC, PR_G_1, PR_P_EARLY, PR_P_LATE,
+  kNumProbes
+};
+bool probes_on();
+int probe(int id, const float* x, long n, hipStream_t s);
+bool poison_on();
+unsigned* user_fwd_fail_flag();
+// DCUE_LEGACY_ORDERS=1: the round-4 cross-stream orders, without the waits that closed its races
+//  -- only to show tests/test_gpu_races.py failing on them
+bool legacy_orders();
+
 // ------------------------------------------------------------- step implementation (capi.hip)
 struct StepOpts {
   hipEvent_t wait_inputs = nullptr;  // plans: the next step's prepared inputs; the caller's stream

@@ -159,6 +159,7 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   const std::function<int(hipEvent_t)> lookahead = [p, sa, nxt, look, ir = p->inputs_ready](hipEvent_t after) -> int {
     if (look) {
       if (after) TRY(wait_point(sa, after));
+      TRY(debug_delay(DCUE_SITE_LOOKAHEAD, sa));
       TRY(ahead_item_inputs(&p->model, &p->batch, &p->tracks, p->ahead_items[nxt], p->counts[nxt], p->acc[nxt],
                             p->xh[nxt], sa));
     }
@@ -216,8 +217,18 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
     }
     q.users_dst = const_cast<int64_t*>(b0.users); q.users_src = users_src;
     q.items_dst = const_cast<int32_t*>(b0.item_track); q.items_src = items_src;
-    iseq = side.run([q, sa, ev_in, &lookahead]() -> int {
+    // Slot nxt was last read by the previous step, partly on side streams that the caller's stream
+    // does not join (split plans): the layer-2 weight gradient on wgrad stream 1 reads its copy
+    // counts, BN sums and value ranges, which this prologue clears and rewrites. The previous step's
+    // late Adam waited for every side stream, so its point (late_done, also what this step's conv 2
+    // waits for) orders the prologue after all of them. Without this wait a delayed layer-2 weight
+    // gradient read a cleared range -- a NaN operand scale -- and the step's conv-2 gradient went
+    // non-finite (tests/test_gpu_races.py).
+    const hipEvent_t prev_late = legacy_orders() ? nullptr : p->late_done;
+    iseq = side.run([q, sa, ev_in, prev_late, &lookahead]() -> int {
       TRY(wait_point(sa, ev_in));
+      if (prev_late) TRY(wait_point(sa, prev_late));
+      TRY(debug_delay(DCUE_SITE_PROLOGUE, sa));
       TRY(launch_step_prologue(q, sa));
       return ahead_at_fork ? DCUE_OK : lookahead(nullptr);  // (the prologue on sa orders it)
     }, &sst);
@@ -307,7 +318,12 @@ extern "C" int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const 
     // conv 1's output per slot (StepOpts::y1): [M][33][H_s] floats
     const size_t by1 = al(sizeof(float) * (size_t)M * dcue::layer_geom(1).lp * dcue::st_hidden(&m->dims));
     void* mem = nullptr;
-    DCUE_HIP_CHECK(hipMalloc(&mem, 2 * (bneg + bcnt + bacc + bxh + bptr + bidx + by1) + bmt));
+    const size_t mem_bytes = 2 * (bneg + bcnt + bacc + bxh + bptr + bidx + by1) + bmt;
+    DCUE_HIP_CHECK(hipMalloc(&mem, mem_bytes));
+    if (dcue::poison_on()) {  // debug: a read of a word no kernel wrote shows as NaN
+      DCUE_HIP_CHECK(hipMemset(mem, 0xFF, mem_bytes));
+      DCUE_HIP_CHECK(hipDeviceSynchronize());
+    }
     dcue_plan* p = new dcue_plan;
     p->model = *m;
     p->batch = *b;

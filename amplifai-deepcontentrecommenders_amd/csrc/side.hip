@@ -34,12 +34,17 @@ class SideIssuer {
     wake();
     if (th_.joinable()) th_.join();
   }
+  // Any host thread of the process may post (one issuer per device): posts are serialised. The
+  // head store and the parked load are sequentially consistent, as are the worker's parked store
+  // and its head load: either this post sees the worker parked and wakes it, or the worker's check
+  // before sleeping sees the new head.
   uint64_t post(std::function<int()> fn) {
+    std::lock_guard<std::mutex> lk(post_mu_);
     const uint64_t h = head_.load(std::memory_order_relaxed);
     while (h - done_.load(std::memory_order_acquire) >= kQ) __builtin_ia32_pause();
     q_[h % kQ] = std::move(fn);
-    head_.store(h + 1, std::memory_order_release);
-    if (parked_.load(std::memory_order_acquire)) wake();
+    head_.store(h + 1, std::memory_order_seq_cst);
+    if (parked_.load(std::memory_order_seq_cst)) wake();
     return h + 1;
   }
   int wait(uint64_t seq) {
@@ -81,12 +86,12 @@ class SideIssuer {
         continue;
       }
       std::unique_lock<std::mutex> lk(mu_);
-      parked_.store(true, std::memory_order_release);
+      parked_.store(true, std::memory_order_seq_cst);
       cv_.wait_for(lk, std::chrono::milliseconds(100), [this] {
         return stop_.load(std::memory_order_acquire) ||
-               done_.load(std::memory_order_relaxed) < head_.load(std::memory_order_acquire);
+               done_.load(std::memory_order_relaxed) < head_.load(std::memory_order_seq_cst);
       });
-      parked_.store(false, std::memory_order_release);
+      parked_.store(false, std::memory_order_seq_cst);
       idle_since = std::chrono::steady_clock::now();
     }
   }
@@ -96,7 +101,7 @@ class SideIssuer {
   std::atomic<uint64_t> head_{0}, done_{0};
   std::atomic<int> err_{0};
   std::atomic<bool> stop_{false}, parked_{false};
-  std::mutex mu_;
+  std::mutex mu_, post_mu_;
   std::condition_variable cv_;
 };
 

@@ -103,10 +103,13 @@ class PlanConfig(ctypes.Structure):
 
 MT_STATE_BYTES = 624 * 4 + 16
 MAX_LOG_CAP = 256
-ABI_VERSION = 13
+ABI_VERSION = 14
 COMM_F32, COMM_U64 = 0, 1  # dcue_host_allreduce_fn dtypes
 HOST_ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32)
 RANK_SPLIT, RANK_SINGLE = 0, 1
+# dcue_debug_delay sites (include/dcue.h)
+DEBUG_SITES = ("user_fwd", "user_bwd", "wgrad_hi", "wgrad_2", "fc_wgrad", "late_adam", "prologue", "lookahead",
+               "conv2", "dgrad_2", "wgrad_1")
 
 _P = ctypes.c_void_p
 _SIGS = {
@@ -178,9 +181,21 @@ _SIGS = {
     "dcue_rank_metrics": ([_P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int32, _P, ctypes.c_int32, _P, _P,
                            _P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_size_t, _P, _P, _P, _P], ctypes.c_int),
     "dcue_factor_repeat_mean": ([_P, ctypes.c_int64, ctypes.c_int32, _P], ctypes.c_int),
+    "dcue_debug_delay": ([ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
+    "dcue_debug_probes": ([_P], ctypes.c_int),
+    "dcue_debug_probe_count": ([], ctypes.c_int),
+    "dcue_debug_probe_name": ([ctypes.c_int32], ctypes.c_char_p),
+    "dcue_debug_poison": ([ctypes.c_int32], ctypes.c_int),
+    "dcue_debug_fail_flags": ([_P], ctypes.c_int),
 }
 
 _lib = None
+
+
+def poison_on():
+    """DCUE_POISON=1 (debug): every workspace the library is handed, and the scratch plans allocate,
+    starts as 0xFF bytes (float NaN), so a read of a word no kernel wrote shows as a non-finite result."""
+    return os.environ.get("DCUE_POISON", "0") == "1"
 
 
 def lib():
@@ -197,6 +212,8 @@ def lib():
             fn.restype = res
         if handle.dcue_abi_version() != ABI_VERSION:
             raise RuntimeError("libdcue_hip ABI mismatch")
+        if poison_on():  # debug: plan scratch starts as NaN bytes (dcue_debug_poison)
+            handle.dcue_debug_poison(1)
         _lib = handle
     return _lib
 
@@ -339,3 +356,22 @@ def workspace_bytes(dims, max_rows, max_neg, max_items):
     check(lib().dcue_workspace_bytes(ctypes.byref(dims), max_rows, max_neg, max_items, ctypes.byref(n)),
           "dcue_workspace_bytes")
     return n.value
+
+
+def debug_delay(site, microseconds):
+    """Spin `microseconds` on the stream of the step's work at `site` (a DEBUG_SITES name or index)
+    before that work, in every later step (include/dcue.h dcue_debug_delay); 0 turns it off."""
+    i = DEBUG_SITES.index(site) if isinstance(site, str) else int(site)
+    check(lib().dcue_debug_delay(i, int(microseconds)), "dcue_debug_delay")
+
+
+def debug_clear_delays():
+    for i in range(len(DEBUG_SITES)):
+        check(lib().dcue_debug_delay(i, 0), "dcue_debug_delay")
+
+
+def debug_fail_flags():
+    """Read and clear the fused user-tower forward's gave-up flag (dcue_debug_fail_flags)."""
+    v = ctypes.c_uint32()
+    check(lib().dcue_debug_fail_flags(ctypes.byref(v)), "dcue_debug_fail_flags")
+    return v.value

@@ -12,7 +12,52 @@ from dcrecommend import _native as nat
 
 
 def enabled_by_env():
-    return os.environ.get("DCUE_CHECK", "0") not in ("", "0")
+    """DCUE_CHECK=1: per-step checks (they synchronise each step); DCUE_CHECK=probe: the in-stream
+    probes only (ProbeCheck), which keep the step's concurrency."""
+    v = os.environ.get("DCUE_CHECK", "0")
+    if v == "probe":
+        return "probe"
+    return v not in ("", "0")
+
+
+class ProbeCheck:
+    """In-stream output probes (include/dcue.h dcue_debug_probes). While bound, every step checks the
+    output of each probed launch on that launch's own stream -- no extra order between streams, so a
+    race still shows -- and report() names, by the device's wall clock, the first launch that wrote a
+    non-finite value. One binding per process."""
+
+    def __init__(self, device):
+        n = nat.lib().dcue_debug_probe_count()
+        self.names = [nat.lib().dcue_debug_probe_name(i).decode() for i in range(n)]
+        # records {u32 nonfinite, u32 nonzero, u64 first_bad}
+        self.buf = torch.zeros((n, 2), dtype=torch.int64, device=device)
+        self.reset()
+        nat.check(nat.lib().dcue_debug_probes(nat.ptr(self.buf)), "dcue_debug_probes")
+
+    def reset(self):
+        self.buf[:, 0] = 0
+        self.buf[:, 1] = -1  # UINT64_MAX
+
+    def report(self):
+        """[(name, first_bad_tick)] of the probes that saw a non-finite value, earliest first
+        (synchronises), and the names of the probes whose output was zero everywhere."""
+        torch.cuda.synchronize(self.buf.device)
+        rec = self.buf.cpu()
+        flags = rec[:, 0]
+        bad = [(self.names[i], int(rec[i, 1]) & (2 ** 64 - 1)) for i in range(len(self.names))
+               if int(flags[i]) & 0xFFFFFFFF]
+        bad.sort(key=lambda x: x[1])
+        return bad
+
+    def raise_if_any(self):
+        bad = self.report()
+        if bad:
+            self.reset()
+            raise RuntimeError("DCUE probes: first non-finite output from %s (then: %s)"
+                               % (bad[0][0], ", ".join(b[0] for b in bad[1:]) or "none"))
+
+    def close(self):
+        nat.check(nat.lib().dcue_debug_probes(None), "dcue_debug_probes")
 
 
 class StepCheck:

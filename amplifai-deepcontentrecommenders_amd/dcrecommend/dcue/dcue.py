@@ -298,6 +298,8 @@ class DCUENet(nn.Module):
             grow = tuple(max(a, b) for a, b in zip(self._ws_key or key, key))
             nbytes = nat.workspace_bytes(self._flat["dims"], *grow)
             self._ws = torch.empty(nbytes, dtype=torch.uint8, device=self._flat["P"].device)
+            if nat.poison_on():
+                self._ws.fill_(255)
             self._ws_key = grow
         if self._flat["emb_grad"].numel() < B * self.user_embdim:
             self._flat["emb_grad"] = torch.zeros(B * self.user_embdim, dtype=torch.float32,

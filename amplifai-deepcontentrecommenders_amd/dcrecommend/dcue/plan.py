@@ -16,7 +16,7 @@ import ctypes
 import torch
 
 from dcrecommend import _native as nat
-from dcrecommend.check import StepCheck, enabled_by_env
+from dcrecommend.check import ProbeCheck, StepCheck, enabled_by_env
 
 
 class TrainPlan:
@@ -76,7 +76,9 @@ class TrainPlan:
         # check mode (dcrecommend.check): ids validated before each step, loss/params/grads after
         if check is None:
             check = enabled_by_env()
-        self._check = StepCheck(dev) if check else None
+        # check="probe": in-stream output probes only, read at close() / probe_report()
+        self._probes = ProbeCheck(dev) if check == "probe" else None
+        self._check = StepCheck(dev) if check and check != "probe" else None
         self._n_users = int(fl["dims"].n_users)
 
     def _check_before(self, users, item_track):
@@ -205,6 +207,11 @@ class TrainPlan:
         h = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
         nat.check(self._lib.dcue_plan_wait_side(self._handle, h), "dcue_plan_wait_side")
 
+    def probe_report(self):
+        """check="probe" plans: the probes that saw a non-finite output so far, earliest first
+        (dcrecommend.check.ProbeCheck.report); [] otherwise."""
+        return self._probes.report() if getattr(self, "_probes", None) is not None else []
+
     def close(self):
         if getattr(self, "_handle", None) is not None:
             self.sync()
@@ -213,6 +220,10 @@ class TrainPlan:
                 self.net._pending_plan = None
             self._lib.dcue_plan_destroy(self._handle)
             self._handle = None
+            if getattr(self, "_probes", None) is not None:
+                probes, self._probes = self._probes, None
+                probes.close()
+                probes.raise_if_any()
 
     def __del__(self):
         try:

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DCUE_ABI_VERSION 13
+#define DCUE_ABI_VERSION 14
 #define DCUE_N_MELS 128
 #define DCUE_N_FRAMES 131
 #define DCUE_N_BN 6
@@ -398,6 +398,39 @@ int dcue_check_finite(const float* buf, int64_t n, int32_t* flags, int32_t bit, 
 int dcue_check_ids(const void* ids, int32_t id_bytes, int64_t n, int64_t limit, int32_t* flags, int32_t bit,
                    void* stream);
 int dcue_plan_destroy(dcue_plan* plan);
+
+/* ---- debug: schedule perturbation, probes, poison (no reference counterpart) ----
+ * dcue_debug_delay: every later step launches, ahead of the work at `site`, a spin kernel of
+ * `microseconds` (0: none, at most 1e6) on that work's stream. A step's results are bit-identical
+ * under any delays -- every buffer is ordered by the streams' events, not by timing -- so a
+ * difference names a missing cross-stream wait (tests/test_gpu_races.py). */
+#define DCUE_SITE_USER_FWD 0   /* user stream: the user tower's forward (deferred-row sync + GEMMs) */
+#define DCUE_SITE_USER_BWD 1   /* user stream: the user tower's backward + user-table Adam */
+#define DCUE_SITE_WGRAD_HI 2   /* wgrad stream 0: weight gradients of conv layers 3-5 (+ fc) */
+#define DCUE_SITE_WGRAD_2 3    /* wgrad stream 1: weight gradient of conv layer 2 */
+#define DCUE_SITE_FC_WGRAD 4   /* wgrad stream 1: res / text towers' fc (+ text conv) weight gradients */
+#define DCUE_SITE_LATE_ADAM 5  /* split plans: the late segments' Adam (user or comm stream) */
+#define DCUE_SITE_PROLOGUE 6   /* plans: the next step's prologue (wgrad stream 0) */
+#define DCUE_SITE_LOOKAHEAD 7  /* plans: the announced next batch's input statistics (wgrad stream 0) */
+#define DCUE_SITE_CONV2 8      /* caller's stream: conv 2 forward */
+#define DCUE_SITE_DGRAD_2 9    /* caller's stream: conv-2 input gradient (g1) */
+#define DCUE_SITE_WGRAD_1 10   /* caller's stream: conv-1 weight gradient */
+#define DCUE_N_DEBUG_SITES 11
+int dcue_debug_delay(int32_t site, int32_t microseconds);
+/* Probes: buf = NULL (off) or a device array of dcue_debug_probe_count() records
+ * { uint32 nonfinite; uint32 nonzero; uint64 first_bad } (the caller sets first_bad to UINT64_MAX
+ * and the rest to 0). While bound, steps check the output of each probed launch on its own stream
+ * (no added cross-stream order): a non-finite element sets `nonfinite` and takes the minimum of the
+ * device's 100 MHz wall clock into `first_bad`; any non-zero element sets `nonzero`. The record with
+ * the smallest first_bad names the first launch that wrote a non-finite value. */
+int dcue_debug_probes(void* buf);
+int dcue_debug_probe_count(void);
+const char* dcue_debug_probe_name(int32_t i);
+/* on != 0: plans created afterwards fill the scratch they allocate with 0xFF bytes (float NaN). */
+int dcue_debug_poison(int32_t on);
+/* Reads and clears the device word the fused user-tower forward (DCUE_USER_FWD=fused) sets when a
+ * bounded wait for another workgroup's row gave up (bit 0; never expected). */
+int dcue_debug_fail_flags(uint32_t* flags_host);
 
 /* ------------------------------------------------- data-parallel gradient exchange (RCCL) */
 /* One process per GPU; users are sharded over the ranks, so the only exchange of a step is the

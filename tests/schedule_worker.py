@@ -40,7 +40,8 @@ def main():
     opt.flush()
     sd = net.state_dict()
     torch.save({"loss": torch.stack(losses).cpu(), "P": net._flat["P"].detach().cpu(),
-                "emb": sd["user_embd.embeddings.weight"].cpu()}, os.environ["OUT"])
+                "emb": sd["user_embd.embeddings.weight"].cpu(), "fail_flags": nat.debug_fail_flags()},
+               os.environ["OUT"])
     plan.close()
     print("schedule worker ok", os.environ.get("DCUE_SIDE_THREAD"), os.environ.get("DCUE_SCORE_FORK"),
           [float(x) for x in losses])

@@ -22,9 +22,11 @@ VARIANTS = [
     {"DCUE_PROLOGUE_FIRST": "1"},
     {"DCUE_LATE_WAIT": "conv1"},
     {"DCUE_AHEAD_AT": "fork"},
+    {"DCUE_USER_FWD": "fused"},
+    {"DCUE_USER_FWD": "fused", "DCUE_SIDE_THREAD": "0"},
 ]
-# (DCUE_USER_FWD=fused, the one-launch user tower, is left out: it is off by default because this
-# test caught it going non-finite in some runs)
+# (the fused user tower's round-4 non-finite runs were the plan's cross-stream races, not the kernel:
+# DESIGN.md §4.7 round 5, tests/test_gpu_races.py)
 
 
 def test_schedule_variants_bit_identical(tmp_path):
@@ -41,7 +43,9 @@ def test_schedule_variants_bit_identical(tmp_path):
         assert p.returncode == 0, "variant %s failed:\n%s" % (extra, p.stdout[-3000:])
         res.append(torch.load(out, weights_only=True))
     base = res[0]
-    assert torch.isfinite(base["loss"]).all()
+    for extra, r in zip(VARIANTS, res):
+        assert torch.isfinite(r["loss"]).all(), "non-finite loss under %s" % extra
+        assert r["fail_flags"] == 0, "fused user forward gave up a wait under %s" % extra
     for extra, r in zip(VARIANTS[1:], res[1:]):
         for k in ("loss", "P", "emb"):
             assert torch.equal(r[k], base[k]), "%s differs under %s" % (k, extra)
