@@ -110,6 +110,7 @@ struct RankWs {
   int32_t* n_thr;    // [QB]
   int32_t* hist;     // [QB][4][cap+1]: lt list0, lt list1, eq list0, eq list1
   int32_t* status;   // [1] first query index over the cap, else -1
+  int32_t* nonfin;   // [QB] a score the reference's sklearn call would see is NaN / inf
 };
 
 // one workgroup per query of the batch
@@ -120,22 +121,24 @@ __global__ __launch_bounds__(256) void k_rank_thresholds(const float* __restrict
                                                          const uint8_t* __restrict__ cls, int64_t nc,
                                                          int pos_mask, RankWs w) {
   __shared__ uint64_t key[kRankCap];
-  __shared__ int cnt;
+  __shared__ int cnt, bad;
   const int i = blockIdx.x, tid = threadIdx.x;
   const int q = queries[i];
   const int64_t b = pos_ptr[q], e = pos_ptr[q + 1];
-  if (tid == 0) cnt = 0;
+  if (tid == 0) cnt = bad = 0;
   __syncthreads();
   for (int64_t p = b + tid; p < e; p += 256) {
     const int c = pos_idx[p];
     const uint8_t k = (c >= 0 && c < nc) ? cls[c] : 0;
     if (k & pos_mask) {
+      const float sc = S[(int64_t)i * ldS + c];
+      if (!isfinite(sc)) bad = 1;
       const int slot = atomicAdd(&cnt, 1);
-      if (slot < kRankCap)
-        key[slot] = ((uint64_t)float_order(S[(int64_t)i * ldS + c]) << 8) | k;
+      if (slot < kRankCap) key[slot] = ((uint64_t)float_order(sc) << 8) | k;
     }
   }
   __syncthreads();
+  if (tid == 0) w.nonfin[i] = bad;  // (k_rank_hist adds the list items' scores)
   const int n = cnt;
   int32_t* h = w.hist + (int64_t)i * 4 * (kRankCap + 1);
   for (int k = tid; k < 4 * (n + 1) && n <= kRankCap; k += 256) h[(k / (n + 1)) * (kRankCap + 1) + k % (n + 1)] = 0;
@@ -191,8 +194,12 @@ __device__ __forceinline__ int lower_bound_f(const float* t, int n, float s) {
 }
 
 // grid (candidate chunks, queries of the batch)
+// score_mask: the list bits whose items' scores the reference hands to sklearn (which raises on a
+// non-finite one): both lists for DCUE.score, the label-0 list (plus the positives, checked in
+// k_rank_thresholds) for score_song
 __global__ __launch_bounds__(256) void k_rank_hist(const float* __restrict__ S, int64_t ldS,
-                                                   const uint8_t* __restrict__ cls, int64_t nc, RankWs w) {
+                                                   const uint8_t* __restrict__ cls, int64_t nc, int score_mask,
+                                                   RankWs w) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int i = blockIdx.y, tid = threadIdx.x;
   const int n = w.n_thr[i];
@@ -205,10 +212,12 @@ __global__ __launch_bounds__(256) void k_rank_hist(const float* __restrict__ S, 
   const int64_t c_begin = (int64_t)blockIdx.x * kRankChunk;
   const int64_t c_end = min(c_begin + kRankChunk, nc);
   const float* Sr = S + (int64_t)i * ldS;
+  bool bad = false;
   for (int64_t c = c_begin + tid; c < c_end; c += 256) {
     const uint8_t k = cls[c];
     if (!k) continue;
     const float s = Sr[c];
+    bad |= (k & score_mask) && !isfinite(s);
     const int ub = upper_bound_f(t, n, s);
     const int lb = (ub > 0 && t[ub - 1] == s) ? lower_bound_f(t, ub, s) : ub;
     if (k & 1) {
@@ -220,6 +229,7 @@ __global__ __launch_bounds__(256) void k_rank_hist(const float* __restrict__ S, 
       if (lb < ub) atomicAdd(&hl[3 * nb + lb], 1);
     }
   }
+  if (__any(bad) && (tid & 63) == 0) atomicOr(&w.nonfin[i], 1);
   __syncthreads();
   int32_t* h = w.hist + (int64_t)i * 4 * (kRankCap + 1);
   for (int k = tid; k < 4 * nb; k += 256) {
@@ -326,7 +336,8 @@ __global__ __launch_bounds__(256) void k_rank_finalize(RankWs w, int mode, int q
       const long sz_pos = p0 + nn1, sz_neg = nn0 + p1, total = sz_pos + sz_neg;
       r_auc = total ? ((double)sz_pos / (double)total) * a_pos + ((double)sz_neg / (double)total) * a_neg : 0.0;
       r_ap = mtot ? c / (double)mtot : 0.0;
-      flag[q_offset + i] = p0 > 0;
+      // bit 1: average_precision_score sees every list item's score (nn/dcue.py:447)
+      flag[q_offset + i] = (p0 > 0) | (w.nonfin[i] ? 2 : 0);
     } else {
       // targets = [1] * n positives + [0] * n0 list items (nn/dcue.py:463-474)
       if (n0 == 0) {
@@ -339,7 +350,8 @@ __global__ __launch_bounds__(256) void k_rank_finalize(RankWs w, int mode, int q
         r_auc = a / ((double)n * (double)n0);
         r_ap = c / (double)n;
       }
-      flag[q_offset + i] = n > 0;
+      // bit 1: roc_auc_score / average_precision_score run only with both labels (:467-474)
+      flag[q_offset + i] = (n > 0) | (w.nonfin[i] && n > 0 && n0 > 0 ? 2 : 0);
     }
     auc[q_offset + i] = r_auc;
     ap[q_offset + i] = r_ap;
@@ -367,6 +379,7 @@ static size_t rank_carve(int64_t n_cand, int32_t d, int32_t qb, void* base, floa
   w->n_thr = ar.take<int32_t>(qb);
   w->hist = ar.take<int32_t>((size_t)qb * 4 * (kRankCap + 1));
   w->status = ar.take<int32_t>(1);
+  w->nonfin = ar.take<int32_t>(qb);
   return ar.used;
 }
 
@@ -428,7 +441,7 @@ int dcue_rank_metrics(const float* query_feat, int64_t n_query_rows, const float
                 pos_idx, cand_class, n_cand, mode == DCUE_RANK_SPLIT ? 3 : 2, w);
     DCUE_LAUNCH_CHECK();
     DCUE_LAUNCH(k_rank_hist, dim3((unsigned)((n_cand + kRankChunk - 1) / kRankChunk), (unsigned)nq), dim3(256),
-                lds_hist, s, S, n_cand, cand_class, n_cand, w);
+                lds_hist, s, S, n_cand, cand_class, n_cand, mode == DCUE_RANK_SPLIT ? 3 : 1, w);
     DCUE_LAUNCH_CHECK();
     DCUE_LAUNCH(k_rank_finalize, dim3((unsigned)nq), dim3(256), 0, s, w, mode, q0, auc, ap, has_pos);
     DCUE_LAUNCH_CHECK();

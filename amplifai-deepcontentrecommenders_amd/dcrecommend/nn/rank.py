@@ -85,7 +85,12 @@ class RankEvaluator:
         return self._ws
 
     def metrics(self, query_feat, cand_feat, queries, mode):
-        """(auc, ap, has_pos) numpy arrays, one entry per query (fp64)."""
+        """(auc, ap, has_pos) numpy arrays, one entry per query (fp64).
+
+        Raises ValueError where the reference's sklearn calls would (roc_auc_score /
+        average_precision_score on NaN or infinite scores, nn/dcue.py:440,447,473-474): DCUE.score
+        for a query before the first one without pred positives (its loop breaks there, :396-397),
+        DCUE.score_song for any query with both labels."""
         nat.require_gpu(query_feat, "query_feat")
         nat.require_gpu(cand_feat, "cand_feat")
         query_feat = query_feat.contiguous().float()
@@ -112,4 +117,15 @@ class RankEvaluator:
                 nat.ptr(self.pos_ptr), nat.ptr(self.pos_idx), nat.ptr(self.cand_class), int(mode), qb,
                 nat.ptr(ws), ws.numel(), nat.ptr(auc), nat.ptr(ap), nat.ptr(flag), nat.stream_handle(self.device)),
                 "dcue_rank_metrics")
-        return auc[:nq].cpu().numpy(), ap[:nq].cpu().numpy(), flag[:nq].cpu().numpy().astype(bool)
+        auc, ap, flag = auc[:nq].cpu().numpy(), ap[:nq].cpu().numpy(), flag[:nq].cpu().numpy()
+        ok = (flag & 1).astype(bool)
+        nonfinite = (flag & 2).astype(bool)
+        checked = nonfinite[:int(np.argmin(ok))] if (mode == nat.RANK_SPLIT and not ok.all()) else nonfinite
+        if checked.any():
+            # (a cosine of finite factors is finite: non-finite factors make NaN scores)
+            raise ValueError("Input contains NaN. (DCUE scores of query %d: the model's factors are not "
+                             "finite)" % int(np.asarray(queries)[int(np.argmax(checked))]))
+        sane = ~nonfinite
+        if not (np.all((auc[sane] >= 0.0) & (auc[sane] <= 1.0)) and np.all((ap[sane] >= 0.0) & (ap[sane] <= 1.0))):
+            raise RuntimeError("dcue_rank_metrics: AUC / AP outside [0, 1]")
+        return auc, ap, ok

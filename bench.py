@@ -316,6 +316,9 @@ def dcbr_phase(args, tracks, pair_user, pair_track, n_users, dev, M, comm=None, 
     torch.cuda.synchronize()
     dt = D.max_over_ranks(time.perf_counter() - t0, dev)
     same, _, _ = D.replica_checksums(model.net._flat["P"])
+    finite = bool(torch.isfinite(model.net._flat["P"]).all()) and all(
+        bool(torch.isfinite(torch.as_tensor(l)).all()) for l in losses) and bool(
+        torch.isfinite(w.user_factors).all()) and bool(torch.isfinite(w.item_factors).all())
     nnz = int(pair_user.shape[0])
     # rooflines: the ALS iteration against the fp64 vector peak (its solve is fp64 VALU work); the
     # regression step against the ceiling of the arithmetic its kernels run (executed_work, per item,
@@ -346,6 +349,7 @@ def dcbr_phase(args, tracks, pair_user, pair_track, n_users, dev, M, comm=None, 
             "regression_ms_per_step": dt / args.steps * 1e3, "regression_items_per_s": world * M * args.steps / dt,
             "wrmf_roofline": wroof, "regression_roofline": rroof,
             "loss_first": float(losses[0]), "loss_last": float(losses[-1]), "replicas_identical": same,
+            "finite": finite,
             "parity": "unpinned against the reference (never published); pinned against oracle/wrmf_oracle.py "
                       "and the fp64 oracle item tower (tests/test_gpu_dcbr.py); N>1 bit-exact with one rank "
                       "(WRMF) and with an explicit all-reduce (regression), tests/test_gpu_dcbr_dp.py"}
@@ -952,6 +956,8 @@ def main():
             "data": "synthetic: random word vectors (N(0, 0.09)) stand in for the LM-pretrained ones",
             "parity": "unpinned against the reference (its text encoder was never published, "
                       "datasets/dcuelmitemset.py:8); pinned against oracle/text_oracle.py (tests/test_gpu_text.py)"}
+        if not out["text"]["finite"]:
+            checks["failed"].append("text: non-finite dense parameters or loss")
         tplan.close()
         del tplan, topt, tnet, tokens
     # ---- phase 5 (N = 1): the DCBR path (BASELINE config 5): WRMF target factors of
@@ -967,6 +973,8 @@ def main():
             out["dcbr"] = dcbr_phase(args, tracks, all_u, all_t, args.users, dev, B * (1 + N), comm=comm,
                                      world=world, rank=rank)
             del all_u, all_t
+        if not out["dcbr"]["finite"]:
+            checks["failed"].append("dcbr: non-finite WRMF factors, regression parameters or loss")
     head = out.get("inbatch", out["inbatch_cold"])
     E = args.user_embdim
     result = {
@@ -1043,6 +1051,9 @@ def main():
         comm.close()
     if world > 1:
         dist.destroy_process_group()
+    if checks["failed"]:  # a diverged phase is a failed run, whatever its throughput
+        print("bench: checks failed: %s" % "; ".join(checks["failed"]), file=sys.stderr, flush=True)
+        sys.exit(1)
 
 
 if __name__ == "__main__":

@@ -519,6 +519,9 @@ int dcue_timer_read(int32_t kernel, double* total_ms_host, int64_t* launches_hos
  *     so it only drops user index 0 and keeps the song's own users as negatives too; callers set
  *     bit 0 on the split's users except user 0 and bit 1 on the split's users. AUC / AP over that
  *     list, 1/1 if every target is 1, 0/0 if none; has_pos = 0 marks a query the reference skips.
+ *   has_pos bit 1: a score the reference would hand to sklearn is NaN or infinite -- there
+ *     roc_auc_score / average_precision_score raise ValueError (:440, :447, :473-474), and the
+ *     query's auc / ap here are meaningless (the binding raises ValueError instead of using them).
  * Exact tie-aware AUC (Mann-Whitney, ties 1/2) and step-wise AP from integer rank counts, fp64.
  * At most 4096 positives per query inside the lists (else DCUE_ERR_UNSUPPORTED). query_batch
  * queries are scored per pass; the workspace holds their [query_batch][n_cand] score rows.

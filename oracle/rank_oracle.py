@@ -33,10 +33,19 @@ import numpy as np
 import torch
 
 
+def _assert_all_finite(s):
+    """sklearn's input validation (utils.validation._assert_all_finite, run by roc_auc_score and
+    average_precision_score on y_score): NaN or infinity raises ValueError."""
+    if not np.isfinite(s).all():
+        raise ValueError("Input contains NaN." if np.isnan(s).any() else
+                         "Input contains infinity or a value too large for dtype('float64').")
+
+
 def roc_auc(targets, scores):
     """sklearn roc_auc_score for binary targets with both classes present (tie-aware)."""
     y = np.asarray(targets).astype(bool)
     s = np.asarray(scores, dtype=np.float64)
+    _assert_all_finite(s)
     sp, sn = s[y], s[~y]
     if len(sp) == 0 or len(sn) == 0:
         raise ValueError("roc_auc needs both classes")
@@ -51,6 +60,7 @@ def average_precision(targets, scores):
     (every item with a score >= it counted), 0 when there is no positive."""
     y = np.asarray(targets).astype(bool)
     s = np.asarray(scores, dtype=np.float64)
+    _assert_all_finite(s)
     if not y.any():
         return 0.0
     srt = np.sort(s)
@@ -105,13 +115,16 @@ def rank_metrics(query_feat, cand_feat, queries, pos_ptr, pos_idx, cand_class, m
     above. mode 0 (DCUE.score): candidates with class bit 0 form the pred list, bit 1 the truth
     list; a candidate is a positive of query row q iff it is in q's CSR row. mode 1
     (DCUE.score_song): positives = CSR row & bit 1, label-0 list = every bit-0 candidate.
-    Returns (auc, ap, has_pos) arrays."""
+    Returns (auc, ap, has_pos) arrays. Raises ValueError where the reference's sklearn calls would
+    on non-finite scores: mode 0 for a query before the first one without pred positives (the
+    reference's user loop breaks there, nn/dcue.py:396-397), mode 1 for any query."""
     cand_class = np.asarray(cand_class)
     inP = (cand_class & 1) != 0
     inT = (cand_class & 2) != 0
     auc = np.zeros(len(queries))
     ap = np.zeros(len(queries))
     flag = np.zeros(len(queries), dtype=np.int32)
+    stopped = False
     for k, q in enumerate(queries):
         pos = np.zeros(len(cand_class), dtype=bool)
         pos[pos_idx[pos_ptr[q]:pos_ptr[q + 1]]] = True
@@ -119,7 +132,13 @@ def rank_metrics(query_feat, cand_feat, queries, pos_ptr, pos_idx, cand_class, m
         s = cosine_rows(qv, np.asarray(cand_feat, np.float32)).astype(np.float64)
         if mode == 0:
             flag[k] = int((pos & inP).any())
-            auc[k], ap[k] = user_metrics(s[inP], pos[inP].astype(int), s[inT], pos[inT].astype(int))
+            stopped |= not flag[k]
+            try:
+                auc[k], ap[k] = user_metrics(s[inP], pos[inP].astype(int), s[inT], pos[inT].astype(int))
+            except ValueError:
+                if not stopped:
+                    raise
+                auc[k] = ap[k] = np.nan
         else:
             # score_song's list: the song's users (1) + every list-0 user (0), its own users included
             # (dcuepredset.py:53-62 keeps them: getrow(i).nonzero()[0] are row indices, all 0)

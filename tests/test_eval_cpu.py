@@ -94,3 +94,36 @@ def test_item_factor_average(ev):
     f = np.random.RandomState(0).randn(48, 16).astype(np.float32)
     out = R.item_factors_avg(f).numpy()
     assert np.abs(out - f).max() < 1e-6
+
+
+def test_nonfinite_factors_raise_like_sklearn(ev):
+    """The reference's sklearn calls raise ValueError on NaN / inf scores (nn/dcue.py:440,447,473-474):
+    the restatement raises where they would -- a user before the score() loop's break, any song with
+    both labels -- and not for a user after the break."""
+    from sklearn.metrics import average_precision_score, roc_auc_score
+    for f in (roc_auc_score, average_precision_score, R.roc_auc, R.average_precision):
+        with pytest.raises(ValueError, match="Input contains NaN"):
+            f([0, 1, 1], [0.1, np.nan, 0.3])
+    g, train, val, items = ev
+    (u_in, s_in, uf, cand) = eval_structures(g, train, val, items)
+    q = _users(train, g["val_users"])
+    bad = np.array(uf, dtype=np.float32, copy=True)
+    bad[q[0]] = np.nan
+    with pytest.raises(ValueError, match="Input contains NaN"):
+        R.rank_metrics(bad, cand, q, u_in["pos_ptr"], u_in["pos_idx"], u_in["cand_class"], 0)
+    # a user with no pred-split songs stops the loop: a NaN factor after it is never scored
+    ptr = np.asarray(u_in["pos_ptr"])
+    cls = np.asarray(u_in["cand_class"])
+    no_pred = [u for u in range(len(ptr) - 1)
+               if not (cls[np.asarray(u_in["pos_idx"])[ptr[u]:ptr[u + 1]]] & 1).any()]
+    if no_pred:
+        after = np.array([q[0], no_pred[0], q[1]], dtype=np.int64)
+        bad2 = np.array(uf, dtype=np.float32, copy=True)
+        bad2[q[1]] = np.nan
+        _, _, flag = R.rank_metrics(bad2, cand, after, u_in["pos_ptr"], u_in["pos_idx"], u_in["cand_class"], 0)
+        assert list(flag[:2]) == [1, 0]
+    songs = np.array([val.item_index[s] for s in g["val_songs"]], dtype=np.int64)
+    badc = np.array(cand, dtype=np.float32, copy=True)
+    badc[songs[0]] = np.inf
+    with pytest.raises(ValueError):
+        R.rank_metrics(badc, uf, songs, s_in["pos_ptr"], s_in["pos_idx"], s_in["cand_class"], 1)

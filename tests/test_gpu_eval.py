@@ -122,6 +122,57 @@ def test_rank_metrics_random_vs_oracle(mode, d):
     np.testing.assert_allclose(ap, want_ap, rtol=0, atol=5e-5)
 
 
+def test_rank_metrics_nonfinite_raise():
+    """NaN factors raise ValueError where the reference's sklearn calls would (nn/dcue.py:440,447,
+    473-474) -- the oracle (pinned to sklearn in test_eval_cpu.py) and the GPU evaluator agree -- and
+    never yield an AUC outside [0, 1]: a NaN user factor before score()'s loop break, a NaN candidate
+    in a list; not a NaN candidate outside both lists, nor a NaN user after the break."""
+    from dcrecommend.nn import rank
+    qf, cand, inp = _random_case(11, 60, 1500, 64, 80)
+    ptr, cls = inp["pos_ptr"], inp["cand_class"]
+    has_pred = np.array([(cls[inp["pos_idx"][ptr[r]:ptr[r + 1]]] & 1).any() for r in range(60)])
+    good = np.flatnonzero(has_pred)
+    queries = good[:20]
+    ev = rank.RankEvaluator(inp, DEV)
+    args = (inp["pos_ptr"], inp["pos_idx"], inp["cand_class"])
+
+    def both(q, c, qs, mode):
+        err = []
+        for fn in (lambda: ev.metrics(torch.from_numpy(q).to(DEV), torch.from_numpy(c).to(DEV), qs, mode),
+                   lambda: R.rank_metrics(q, c, qs, *args, mode)):
+            try:
+                fn()
+                err.append(None)
+            except ValueError as e:
+                err.append(str(e))
+        return err
+
+    clean = ev.metrics(torch.from_numpy(qf).to(DEV), torch.from_numpy(cand).to(DEV), queries, 0)
+    bad_q = qf.copy()
+    bad_q[queries[3]] = np.nan
+    e = both(bad_q, cand, queries, 0)
+    assert e[0] and e[1] and "Input contains NaN" in e[0], e
+    bad_c = cand.copy()
+    bad_c[np.flatnonzero(cls == 2)[0]] = np.nan  # truth list only: in average_precision's input
+    assert all(both(qf, bad_c, queries, 0)), "a NaN truth-list candidate must raise"
+    outside = cand.copy()
+    outside[np.flatnonzero(cls == 0)[:5]] = np.nan  # in no list: never scored by the reference
+    assert both(qf, outside, queries, 0) == [None, None]
+    auc, ap, ok = ev.metrics(torch.from_numpy(qf).to(DEV), torch.from_numpy(outside).to(DEV), queries, 0)
+    assert np.array_equal(auc, clean[0]) and np.array_equal(ap, clean[1])
+    no_pred = np.flatnonzero(~has_pred)
+    if len(no_pred):
+        qs = np.array([good[0], no_pred[0], good[1]])
+        late = qf.copy()
+        late[good[1]] = np.nan  # after the break
+        assert both(late, cand, qs, 0) == [None, None]
+    # score_song: a NaN candidate of the label-0 list raises for every song with both labels
+    bad_s = cand.copy()
+    bad_s[np.flatnonzero(cls & 1)[0]] = np.nan
+    e = both(qf, bad_s, queries, 1)
+    assert e[0] and e[1], e
+
+
 def test_rank_metrics_cap():
     from dcrecommend.nn import rank
     rs = np.random.RandomState(0)
