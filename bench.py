@@ -670,12 +670,28 @@ def main():
             nat.timer_enable(k, False)
         return dt, t_enq, (ev0.elapsed_time(ev1) / args.steps if gpu_only else None), kern
 
-    def kernel_rooflines(kern, M, steps):
+    def replay_bytes(optim):
+        """Bytes the user-table replay moves over the whole table (k_emb_flush; adam.hip): m and v
+        read for every element, p read and m, v written for the float4 groups whose moments are not
+        the idle (+0, +0) fixed point (the replay skips those), the row clocks read. p's store
+        (only where the replay changed it) is left out: a lower bound, so the fraction stays
+        physical. Counted after the phase's final flush (an idle group stays idle)."""
+        st = optim._adam_state()
+        em, ev = st["em"], st["ev"]
+        n = em.numel()
+        if n % 4:
+            act = int(((em.view(torch.int32) | ev.view(torch.int32)) != 0).sum())
+        else:
+            act = 4 * int((((em.view(torch.int32) | ev.view(torch.int32)) != 0).view(-1, 4).any(1)).sum())
+        return 8.0 * n + 12.0 * act + 4.0 * em.shape[0], act / max(n, 1)
+
+    def kernel_rooflines(kern, M, steps, optim=None):
         """Live HIP-event timing of the candidate kernels: per launch and per step, with each
         one's algorithmic work against its roofline."""
         H, E = args.hidden, args.user_embdim
         conv1 = 2.0 * H * 128 * 4 * (M * 132)
         rows_slice = n_users_local / args.flush_every
+        table_bytes, active = replay_bytes(opt if optim is None else optim)
         spec = {
             nat.TIMED_CONV1_WGRAD: (("k_conv_wgrad16 layer 1 (conv-1 weight gradient, split-f16 MFMA 16x16x32 on "
                                      "the raw fp16 table: two f16 products per f32 product, dz hi+lo x exact x; "
@@ -688,10 +704,11 @@ def main():
                                   "mfma", conv1),
             nat.TIMED_EMB_SLICE: ("k_emb_flush_rows (deferred user-table Adam, one rolling slice; user "
                                   "stream, beside the item tower: its duration includes waiting behind the "
-                                  "priority-2 critical-path kernels)", "valu", 24.0 * rows_slice * E),
+                                  "priority-2 critical-path kernels; bytes: the table's at its active fraction)",
+                                  "valu", table_bytes * rows_slice / max(n_users_local, 1)),
             nat.TIMED_EMB_FLUSH: ("k_emb_flush (deferred user-table Adam, full-table flush at the phase end, "
                                   "alone on its stream: the replay's uncontended per-element rate)", "valu",
-                                  24.0 * n_users_local * E),
+                                  table_bytes),
             nat.TIMED_ALLREDUCE: ("RCCL all-reduce of the dense gradient (per bucket)", "xgmi", None),
             nat.TIMED_TEXT_FWD: ("k_text_fwd (config 4 text conv: word-vector gather + Conv1d(%d -> %d, k 3) "
                                  "over %d positions + masked max, split-f16 MFMA 16x16x32: three f16 products "
@@ -726,6 +743,8 @@ def main():
                 # per replayed element-step; its HBM fraction is informational
                 ent.update(achieved=work / (avg * 1e-3) / 1e9, peak=HBM_PEAK_GBS, unit="GB/s",
                            algorithmic_bytes=work)
+                if k in (nat.TIMED_EMB_SLICE, nat.TIMED_EMB_FLUSH):
+                    ent["active_fraction"] = active  # of the table's elements with live moments
                 ent["frac" if bound == "hbm" else "hbm_frac"] = ent["achieved"] / HBM_PEAK_GBS
             out.append(ent)
         byk = {e["kernel"]: e for e in out}
@@ -932,7 +951,7 @@ def main():
         ub, ib = batches(args.warmup + args.steps)
         dt, t_enq, _, kern = timed_phase("text", tplan, text_step(ub, ib), optim=topt)
         rows = world * B * args.steps / dt
-        ks = kernel_rooflines(kern, B, args.steps)
+        ks = kernel_rooflines(kern, B, args.steps, optim=topt)
         tk = [k for k in ks if k["kernel"].startswith("k_text_fwd")]
         troof = dict(tk[0]) if tk else {}
         if troof:
@@ -1023,7 +1042,22 @@ def main():
         result["text"] = out["text"]
     if "dcbr" in out:
         result["dcbr"] = out["dcbr"]
-    checks["finite"] = not checks["failed"]
+    # every roofline fraction in the line must be physically possible: a fraction above 1 is an
+    # algorithmic-work count that overstates what the kernel did
+    def over_one(o, path):
+        if isinstance(o, dict):
+            for k, v in o.items():
+                if k in ("frac", "hbm_frac", "step_frac") and isinstance(v, (int, float)) and v > 1.0:
+                    yield "%s.%s = %.3f" % (path, k, v)
+                else:
+                    yield from over_one(v, path + "." + k if path else k)
+        elif isinstance(o, list):
+            for i, v in enumerate(o):
+                yield from over_one(v, "%s[%d]" % (path, i))
+    bad_frac = list(over_one(result, ""))
+    if bad_frac:
+        checks["failed"].append("roofline fractions above 1: " + "; ".join(bad_frac))
+    checks["finite"] = not any(not f.startswith("roofline") for f in checks["failed"])
     result["checks"] = checks
     # data parallelism's invariant: every rank steps the same dense replica (the exchange averaged
     # the same gradient into every rank's Adam); a broken exchange shows up here as differing replicas

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round profile collection, run on the GPU box from the repo root:
-#   gpurun -- 'bash profiles/collect.sh r02_a'
+#   gpurun -- 'bash profiles/collect.sh r02_a [steps] [warmup]'
+# (round 5 on: the driver's shape, --steps 20 --warmup 5, unless given)
 # 1. the bench command without the profiler (its live HIP-event kernel timings are what the bench
 #    line reports; compared against 2.)
 # 2. per timed phase (cold in-batch, steady-state in-batch, catalogue): rocprofv3 --kernel-trace
@@ -12,13 +13,14 @@
 #    summarize_pmc.py (gfx950 FETCH_SIZE x2 correction, KB -> B) into pmc_<kernel>_<mode>.json
 set -euo pipefail
 TAG=${1:-rNN}
-STEPS=${2:-200}
+STEPS=${2:-20}
+WARMUP=${3:-5}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
-BENCH="$ROOT/bench.py --no-cpu-baseline --no-eval --steps $STEPS --warmup 20"
+BENCH="$ROOT/bench.py --no-cpu-baseline --no-eval --no-f32-probe --steps $STEPS --warmup $WARMUP"
 (cd "$ROOT" && timeout -k 10 300 python3 $BENCH > "$OUT/plain.log" 2>&1)
 grep '^{' "$OUT/plain.log" | tail -n 1 > "$OUT/${TAG}_bench_plain.json"
 for PH in inbatch catalogue inbatch_cold text; do
