@@ -2,24 +2,8 @@
 // Reference: optim.Adam as built at nn/dcue.py:143-147 and stepped at :209 (CPU single-tensor path).
 #include "dcue_internal.h"
 #include "tgemm.h"
+#include "bn0adam.h"
 
-namespace dcue {
-
-// Every operation rounded on its own unless written as an fma (fp contraction off for this file)
-// so that the dense sweep, the deferred replay and the touched-row step produce identical bits.
-// sqrt must be __builtin_sqrtf: hipcc lowers it to v_sqrt_f32 plus the two-fma correction, while
-// __fsqrt_rn compiles to the bare 1-ulp v_sqrt_f32.
-#define DCUE_RHD __device__ __forceinline__
-DCUE_RHD float rn_fma(float a, float b, float c) { return __fmaf_rn(a, b, c); }
-DCUE_RHD float rn_mul(float a, float b) { return __fmul_rn(a, b); }
-DCUE_RHD float rn_add(float a, float b) { return __fadd_rn(a, b); }
-DCUE_RHD float rn_sub(float a, float b) { return __fsub_rn(a, b); }
-DCUE_RHD float rn_div(float a, float b) { return __fdiv_rn(a, b); }
-DCUE_RHD float rn_sqrt(float a) { return __builtin_sqrtf(a); }
-
-}  // namespace dcue
-
-#include "adam_replay.h"
 
 namespace dcue {
 
@@ -67,12 +51,6 @@ __device__ __forceinline__ void window_bound(const AdamScalars* hs, int j0, int 
   }
 }
 
-struct PackSeg {
-  long src, fwd, bwd, f16, f16b;  // floats: W in params; f32 forward pack (-1: none); dgrad pack (-1:
-                                 // none); split-f16 forward and dgrad packs
-  int cout, cin, ks;
-  int cinp;  // the split-f16 forward pack's K per tap: cin rounded up to 32 (the text conv's word width)
-};
 struct PackArgs;
 PackArgs pack_args(const dcue_model* md, const int64_t* poff);
 // conv layers 1..5, then the text conv (text tower; an empty segment otherwise)
@@ -83,32 +61,6 @@ struct PackArgs {
 
 // Packed position of element e of conv segment sg (W[o][c][k], k fastest): the forward B operand
 // [k][cin/4][cout][4] and (layers >= 2) the dgrad one [ks-1-k][cout/4][cin][4].
-__device__ __forceinline__ void pack_store(const PackSeg& sg, long e, float w, float* wpack) {
-  const long ks = sg.ks;
-  const long o = e / ((long)sg.cin * ks);
-  const long rem = e - o * sg.cin * ks;
-  const long cc = rem / ks, k = rem - cc * ks;
-  if (sg.fwd >= 0) wpack[sg.fwd + (((k * (sg.cin / 4) + cc / 4) * sg.cout + o) * 4 + (cc & 3))] = w;
-  if (sg.bwd >= 0) {
-    const long kr = sg.ks - 1 - k;
-    wpack[sg.bwd + (((kr * (sg.cout / 4) + o / 4) * sg.cin + cc) * 4 + (o & 3))] = w;
-  }
-  // split-f16 forward operand: hi = fp16(w), lo = fp16(w - hi) (w - hi is exact in f32)
-  const _Float16 hi = (_Float16)w;
-  const _Float16 lo = (_Float16)(w - (float)hi);
-  _Float16* h16 = reinterpret_cast<_Float16*>(wpack + sg.f16);
-  const long q = k * (sg.cinp / 32) + cc / 32;
-  const long base = ((q * sg.cout + o) * 4 + (cc & 31) / 8) * 16 + (cc & 7);
-  h16[base] = hi;
-  h16[base + 8] = lo;
-  if (sg.f16b >= 0) {  // split-f16 dgrad operand: K = (reversed tap, o), columns cc
-    _Float16* b16 = reinterpret_cast<_Float16*>(wpack + sg.f16b);
-    const long qb = (sg.ks - 1 - k) * (sg.cout / 32) + o / 32;
-    const long bb = ((qb * sg.cin + cc) * 4 + (o & 31) / 8) * 16 + (o & 7);
-    b16[bb] = hi;
-    b16[bb + 8] = lo;
-  }
-}
 
 // Adam over the flat dense buffer with the conv-weight repack fused in: a float4 that lies in a
 // conv weight segment (segments are 4-float aligned) also writes its four packed copies.
@@ -640,21 +592,6 @@ static AdamScalars form_scalars(const dcue_adam_args* a) {
 // and workgroups 0 / 1 conv 1's bias and bn1's gamma/beta (whose gradients the conv-1 weight
 // gradient already wrote). Gradient arithmetic: bn0_elem, as k_bn0_grads; Adam: adam_elem, as the
 // dense sweep -- the plan's fused step and an eager backward + dcue_adam_step agree bit for bit.
-struct Bn0AdamDev {
-  float *p, *m, *v, *g;
-  long o_w1, o_cb1, o_g0, o_b0, o_g1, o_b1;  // -1: no such segment (towers without BatchNorm)
-  AdamScalars sc;
-  PackSeg seg1;
-  float* wpack;
-};
-
-__device__ __forceinline__ void adam_at(const Bn0AdamDev& a, long idx, float gr) {
-  float pp = a.p[idx], mm = a.m[idx], vv = a.v[idx];
-  adam_elem(pp, gr, mm, vv, a.sc);
-  a.p[idx] = pp;
-  a.m[idx] = mm;
-  a.v[idx] = vv;
-}
 
 __global__ __launch_bounds__(256) void k_bn0_grads_adam(const float* __restrict__ G, const float* __restrict__ E,
                                                         const float* gamma0, const float* beta0, const float* mean0,
@@ -662,79 +599,12 @@ __global__ __launch_bounds__(256) void k_bn0_grads_adam(const float* __restrict_
                                                         Bn0AdamDev a) {
   critical_path_priority();
   __shared__ float rg[256], rb[256];
-  const int c = blockIdx.x, t = threadIdx.x;
-  // the parameter, gradient and moment buffers never alias G / E (workspace): restrict lets every
-  // element's loads issue before the first element's stores (one memory round instead of one per
-  // element); the per-element arithmetic and the order of the dg / db sums are unchanged
-  float* __restrict__ P = a.p;
-  float* __restrict__ Mo = a.m;
-  float* __restrict__ V = a.v;
-  float* __restrict__ Gd = a.g;
-  // bn0's gamma / beta state of this channel, loaded up front (thread 0 steps them last)
-  float pg = 0.f, mg = 0.f, vg = 0.f, pb = 0.f, mb = 0.f, vb = 0.f;
-  if (t == 0 && a.o_g0 >= 0) {
-    pg = P[a.o_g0 + c]; mg = Mo[a.o_g0 + c]; vg = V[a.o_g0 + c];
-    pb = P[a.o_b0 + c]; mb = Mo[a.o_b0 + c]; vb = V[a.o_b0 + c];
-  }
-  const Bn0Chan ch = bn0_chan(gamma0, beta0, mean0, invstd0, c);
-  float dg = 0.f, db = 0.f;
-  constexpr int kMaxIt = 4;  // 4H <= 1024 = 4 x 256 threads (H <= 256)
-#pragma unroll
-  for (int it = 0; it < kMaxIt; ++it) {
-    const int e = t + 256 * it;
-    if (e < 4 * H) {
-      const int o = e >> 2, k = e & 3;
-      const long wi = ((long)o * kMels + c) * 4 + k;
-      const long idx = a.o_w1 + wi;
-      float pp = P[idx];
-      const float gw = bn0_elem(G, E, H, ch, o, k, c, pp, dg, db);  // reads the pre-step weight
-      Gd[idx] = gw;
-      float mm = Mo[idx], vv = V[idx];
-      adam_elem(pp, gw, mm, vv, a.sc);
-      P[idx] = pp;
-      Mo[idx] = mm;
-      V[idx] = vv;
-      pack_store(a.seg1, wi, pp, a.wpack);
-    }
-  }
-  if (c == 0)
-    for (int o = t; o < H; o += blockDim.x) {
-      a.g[a.o_cb1 + o] = E[o];
-      adam_at(a, a.o_cb1 + o, E[o]);
-    }
-  if (c == 1 && a.o_g1 >= 0)
-    for (int o = t; o < H; o += blockDim.x) {
-      adam_at(a, a.o_g1 + o, a.g[a.o_g1 + o]);
-      adam_at(a, a.o_b1 + o, a.g[a.o_b1 + o]);
-    }
-  rg[t] = dg;
-  rb[t] = db;
-  __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (t < off) {
-      rg[t] += rg[t + off];
-      rb[t] += rb[t + off];
-    }
-    __syncthreads();
-  }
-  if (t == 0) {
-    dgamma0[c] = rg[0];
-    dbeta0[c] = rb[0];
-    if (a.o_g0 >= 0) {
-      adam_elem(pg, rg[0], mg, vg, a.sc);
-      adam_elem(pb, rb[0], mb, vb, a.sc);
-      P[a.o_g0 + c] = pg; Mo[a.o_g0 + c] = mg; V[a.o_g0 + c] = vg;
-      P[a.o_b0 + c] = pb; Mo[a.o_b0 + c] = mb; V[a.o_b0 + c] = vb;
-    }
-  }
+  bn0_channel<true>(G, E, gamma0, beta0, mean0, invstd0, H, dgamma0, dbeta0, a, nullptr, nullptr, nullptr,
+                    blockIdx.x, threadIdx.x, rg, rb, true);
 }
 
-int launch_bn0_grads_adam(const float* G, const float* E, const float* gamma0, const float* beta0,
-                          const float* mean0, const float* invstd0, int H, float* dgamma0, float* dbeta0,
-                          const Bn0Adam& a, hipStream_t s) {
+Bn0AdamDev bn0adam_dev(const Bn0Adam& a) {
   const dcue_model* md = a.md;
-  if (H > 256) return DCUE_ERR_UNSUPPORTED;  // k_bn0_grads_adam: 4H elements over 4 x 256 threads
-  if (!md->params || !md->grads || !md->exp_avg || !md->exp_avg_sq || a.args.grad_div > 1.0) return DCUE_ERR_INVALID;
   Bn0AdamDev d;
   d.p = md->params; d.m = md->exp_avg; d.v = md->exp_avg_sq; d.g = md->grads;
   d.o_w1 = a.poff[2]; d.o_cb1 = a.poff[3];
@@ -743,6 +613,16 @@ int launch_bn0_grads_adam(const float* G, const float* E, const float* gamma0, c
   d.sc = form_scalars(&a.args);
   d.seg1 = pack_args(md, a.poff).seg[0];
   d.wpack = md->wpack;
+  return d;
+}
+
+int launch_bn0_grads_adam(const float* G, const float* E, const float* gamma0, const float* beta0,
+                          const float* mean0, const float* invstd0, int H, float* dgamma0, float* dbeta0,
+                          const Bn0Adam& a, hipStream_t s) {
+  const dcue_model* md = a.md;
+  if (H > 256) return DCUE_ERR_UNSUPPORTED;  // k_bn0_grads_adam: 4H elements over 4 x 256 threads
+  if (!md->params || !md->grads || !md->exp_avg || !md->exp_avg_sq || a.args.grad_div > 1.0) return DCUE_ERR_INVALID;
+  const Bn0AdamDev d = bn0adam_dev(a);
   DCUE_LAUNCH(k_bn0_grads_adam, dim3(kMels), dim3(256), 0, s, G, E, gamma0, beta0, mean0, invstd0, H, dgamma0,
               dbeta0, d);
   DCUE_LAUNCH_CHECK();

@@ -1353,6 +1353,34 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       wa.kd_max = kd_max * wa.invN;
     }
     const int nch = wgrad_nchunk(l, M, C, cin);
+    if (l == 1 && f16w) {  // the weight gradient, its reduce and bn0's gradients (+ Adam) in one launch
+      const bool graw = src == SRC_TRACK_F16;
+      Bn0Adam ba;
+      Bn0Tail bt = {};
+      bt.G = w.G; bt.S = w.S;
+      bt.gamma0 = c.gamma(w, 0); bt.beta0 = c.beta(w, 0);
+      bt.mean0 = graw ? w.mean[0] : nullptr; bt.invstd0 = graw ? w.invstd[0] : nullptr;
+      bt.dgamma0 = c.dgamma(w, 0); bt.dbeta0 = c.dbeta(w, 0);
+      bt.W1 = c.P(seg_conv_w(1)); bt.dW1 = c.Gd(seg_conv_w(1)); bt.db1 = c.Gd(seg_conv_b(1));
+      if (fuse_late) {
+        ba.md = m; ba.poff = c.poff; ba.args = *o.dense_split; ba.bn = c.bn;
+        bt.adam = &ba;
+      }
+      bt.ctr = w.grng + 7 * kRngC;  // (the gradient maxima's padding: cleared with the accumulators)
+      if (conv1_wgrad_tail_fits(wa, nch)) {
+        TimerScope tsc;
+        TRY(timer_begin(&tsc, DCUE_TIMED_CONV1_WGRAD, so));
+        {
+          ForkAfter fk(sp, so, tail);
+          TRY(launch_conv1_wgrad_tail(src, wa, nch, bt, so));
+          TRY(fk.done());
+        }
+        TRY(timer_end(&tsc));
+        if (!probes_on()) return DCUE_OK;
+        TRY(probe(PR_G_1, m->grads, late, so));
+        return fuse_late ? probe(PR_P_EARLY, m->params, late, so) : DCUE_OK;
+      }
+    }
     if (l == 1 && !f16w) {  // the GEMM reads the pooled BN1 backward, expanded to rows at MFMA time
       TRY(launch_conv1_dx(wa, w.dx1, so));
       wa.g_l = w.dx1;

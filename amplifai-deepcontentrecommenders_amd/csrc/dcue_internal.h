@@ -189,6 +189,21 @@ int launch_bn0_grads_adam(const float* G, const float* E, const float* gamma0, c
                           const float* mean0, const float* invstd0, int H, float* dgamma0, float* dbeta0,
                           const Bn0Adam& a, hipStream_t s);
 
+// The conv-1 weight gradient, its split-K reduce and bn0's gradients (+ Adam, adam != null) as one
+// launch with grid barriers (conv_wgrad.hip k_conv1_wgrad_tail): DCUE_ERR_UNSUPPORTED where its
+// workgroups cannot all be resident (the caller then issues the three launches)
+struct Bn0Tail {
+  float *G, *S;                            // reduce outputs (the workspace's G / S)
+  const float *gamma0, *beta0, *mean0, *invstd0;
+  float *dgamma0, *dbeta0;
+  const float* W1;                         // !adam: dW1 = f(W1), db1
+  float *dW1, *db1;
+  const Bn0Adam* adam;                     // split plans: Adam over [0, DCUE_SEG_LATE) in the same launch
+  unsigned* ctr;                           // a zeroed word (the step's accumulator block)
+};
+bool conv1_wgrad_tail_fits(const WgradArgs& a, int nchunk);
+int launch_conv1_wgrad_tail(int src, const WgradArgs& a, int nchunk, const Bn0Tail& b, hipStream_t s);
+
 // mean0 / invstd0 (nullable): G is the contraction with the raw input (split-f16 path, fp16 table)
 int launch_bn0_grads(const float* G, const float* E, const float* W1, const float* gamma0,
                      const float* beta0, const float* mean0, const float* invstd0, int H, float* dW1,

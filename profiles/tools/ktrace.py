@@ -31,7 +31,7 @@ items = torch.randint(0, n_tracks, (40, B), generator=gen, device=dev).to(torch.
 lib = nat.lib()
 KK, KB = 16, 512
 readers = {}
-for n in ("tail", "fwd", "dgrad"):
+for n in ("tail", "fwd", "dgrad", "wgrad"):
     fn = getattr(lib, "dcue_ktrace_read_" + n)
     fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     readers[n] = fn
@@ -42,6 +42,8 @@ for kid, nm in zip(range(2, 7), ["fwd L1", "fwd L2", "fwd L3", "fwd L4", "fwd L5
     KERNELS.append(("fwd", kid, "k_conv_rows " + nm, ["chan+range setup", "slab stores", "barrier", "MFMA", "epilogue"], [0, 5, 1, 2, 3, 4]))
 for kid, nm in zip(range(7, 12), ["dgrad in L1?", "dgrad l=2 (in 32)", "dgrad l=3 (in 8)", "dgrad l=4 (in 2)", "dgrad l=5 (in 1)"]):
     KERNELS.append(("dgrad", kid, "k_conv_rows " + nm, ["chan+range setup", "slab stores", "barrier", "MFMA", "epilogue"], [0, 5, 1, 2, 3, 4]))
+KERNELS.append(("wgrad", 0, "k_conv_wgrad16t conv 1", ["prologue consts", "first stage fill", "stages (MFMA)", "partial stores"], [0, 1, 2, 3, 4]))
+KERNELS.append(("wgrad", 1, "k_conv_wgrad16t layer 2", ["prologue consts", "first stage fill", "stages (MFMA)", "partial stores"], [0, 1, 2, 3, 4]))
 for s_ in range(40):
     plan.set_next(items[(s_ + 1) % 40])
     plan.step(users[s_], items[s_])
