@@ -35,6 +35,7 @@
 namespace dcue {
 
 typedef _Float16 t16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 t16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTextKC = 32;        // word channels per K chunk (one MFMA k-step)
 constexpr int kTextRowH = 72;      // LDS row: [hi x 32][lo x 32][pad x 8] halves = 144 B (conflict-free)
@@ -189,6 +190,141 @@ __global__ __launch_bounds__(256) void k_text_fwd(TextFwdArgs a) {
   }
 }
 
+// The same conv with each workgroup's word vectors gathered once: a workgroup owns ONE item and 16*WV
+// output channels (WV waves of 16), and stages the item's whole sentence -- every position's full
+// word vector, all EP channels, split into hi/lo fp16 halves -- in LDS with one burst of loads
+// before the MFMAs (k_text_fwd above refills one 32-channel chunk at a time, a dependent global
+// round trip per chunk, and its four 64-channel column blocks each re-gather the same vectors). The
+// column blocks of an item sit next to each other in XCD order, so the second reads the vectors from
+// the first's L2. The B operand is prefetched kTextBPD (chunk, tap) steps ahead. Per accumulator the
+// MFMA sequence (chunk-major, then tap, then lo*hi, hi*lo, hi*hi) and the epilogue are k_text_fwd's:
+// bit-identical output (DCUE_TEXT_FWD=chunked runs the old kernel: A/B and tests/test_gpu_text.py).
+constexpr int kTextBPD = 6;
+__host__ __device__ constexpr int text_full_pitch(int EP) {  // halves per staged row: [chunk][hi 32, lo 32] + pad
+  return 2 * EP + 2 * (((36 - EP % 64) % 64 + 64) % 64);  // row pitch = 36 (mod 64) dwords: conflict-free
+}
+
+template <int TB, int WV>
+__global__ __launch_bounds__(64 * WV) void k_text_fwd_full(TextFwdArgs a) {
+  constexpr int TP = TB * 16;  // conv positions computed (T rounded up)
+  constexpr int RS = TP + 2;   // staged rows: token positions -1 .. TP
+  constexpr int NT = 64 * WV;
+  extern __shared__ __attribute__((aligned(16))) _Float16 xf[];  // [RS][pitch]
+  __shared__ int32_t tok[RS];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int cb = a.C / (16 * WV);  // column blocks per item
+  const int L = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int i = L / cb;
+  const int o0 = (L - i * cb) * 16 * WV + wv * 16;
+  const int pitch = text_full_pitch(a.EP);
+  const int nchunk = a.EP / kTextKC;
+  const long trk = a.item_track[i];
+  for (int r = tid; r < RS; r += NT) {
+    const int t = r - 1;
+    tok[r] = (t >= 0 && t < a.T) ? a.tokens[trk * a.T + t] : -1;
+  }
+  __syncthreads();
+  // B operand of (chunk ch, tap k) for this lane's column: step q = ch * 3 + k, pack index k * nchunk + ch
+  const int col = o0 + (lane & 15), g = lane >> 4;
+  const int nq = 3 * nchunk;
+  auto bload = [&](int q, uint4& h, uint4& l) {
+    const int ch = q / 3, k = q - 3 * ch;
+    const uint4* wp = a.wpack + (((long)(k * nchunk + ch) * a.C + col) * 4 + g) * 2;
+    h = wp[0];
+    l = wp[1];
+  };
+  uint4 bh[kTextBPD], bl[kTextBPD];
+#pragma unroll
+  for (int q = 0; q < kTextBPD; ++q)
+    if (q < nq) bload(q, bh[q], bl[q]);
+  // the sentence: every row's EP channels, float4 slots gathered in batches of kB per thread
+  const int c4n = a.EP / 4, nslot = RS * c4n;
+  constexpr int kB = 8;
+  for (int base = tid; base < nslot; base += NT * kB) {
+    float4 v[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      const int e = base + NT * j;
+      v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < nslot) {
+        const int r = e / c4n, c = 4 * (e - r * c4n);
+        const int tk = tok[r];
+        if (tk >= 0 && c < a.E) v[j] = *reinterpret_cast<const float4*>(a.words + (long)tk * a.E + c);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      const int e = base + NT * j;
+      if (e < nslot) {
+        const int r = e / c4n, c = 4 * (e - r * c4n);
+        float4 x = v[j];
+        x.x *= a.xscale; x.y *= a.xscale; x.z *= a.xscale; x.w *= a.xscale;  // exact (power of two)
+        _Float16 hi[4], lo[4];
+        split4(x, hi, lo);
+        _Float16* row = xf + (long)r * pitch + (c / kTextKC) * 2 * kTextKC + (c % kTextKC);
+        *reinterpret_cast<t16x4*>(row) = t16x4{hi[0], hi[1], hi[2], hi[3]};
+        *reinterpret_cast<t16x4*>(row + kTextKC) = t16x4{lo[0], lo[1], lo[2], lo[3]};
+      }
+    }
+  }
+  __syncthreads();
+  f32x4 acc[TB];
+#pragma unroll
+  for (int b = 0; b < TB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int q0 = 0; q0 < nq; q0 += kTextBPD) {
+#pragma unroll
+    for (int j = 0; j < kTextBPD; ++j) {
+      const int q = q0 + j;
+      if (q < nq) {
+        const t16x8 wh = *reinterpret_cast<const t16x8*>(&bh[j]);
+        const t16x8 wl = *reinterpret_cast<const t16x8*>(&bl[j]);
+        if (q + kTextBPD < nq) bload(q + kTextBPD, bh[j], bl[j]);
+        const int ch = q / 3, k = q - 3 * ch;
+#pragma unroll
+        for (int b = 0; b < TB; ++b) {
+          // conv row t = 16b + (lane & 15) reads token t + k - 1 = staged row t + k
+          const _Float16* rp = xf + (long)(16 * b + (lane & 15) + k) * pitch + ch * 2 * kTextKC + 8 * g;
+          const t16x8 ah = *reinterpret_cast<const t16x8*>(rp);
+          const t16x8 al = *reinterpret_cast<const t16x8*>(rp + kTextKC);
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wh, acc[b], 0, 0, 0);
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wl, acc[b], 0, 0, 0);
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wh, acc[b], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // epilogue (k_text_fwd's): bias, masked first-max over the positions, ReLU
+  const float bo = a.bias[col];
+  float best = -INFINITY;
+  int bi = kTextNoGrad;
+#pragma unroll
+  for (int b = 0; b < TB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = 16 * b + 4 * g + j;
+      const int tk = tok[t + 1];
+      const float v = acc[b][j] * a.inv_xscale + bo;
+      if (t < a.T && tk >= 0 && tk != a.pad && v > best) {
+        best = v;
+        bi = t;
+      }
+    }
+#pragma unroll
+  for (int off = 16; off <= 32; off <<= 1) {
+    const float ob = __shfl_xor(best, off, 64);
+    const int oi = __shfl_xor(bi, off, 64);
+    if (ob > best || (ob == best && oi < bi)) {
+      best = ob;
+      bi = oi;
+    }
+  }
+  if (g == 0) {
+    const bool on = best > 0.f;
+    if (col < a.Creal) a.out[(long)i * a.ld + col] = on ? best : 0.f;
+    a.tidx[(long)i * a.C + col] = (uint8_t)(on ? bi : kTextNoGrad);
+  }
+}
+
 // ------------------------------------------------------------------------------- weight gradient
 struct TextWgradArgs {
   const int32_t* tokens;
@@ -303,6 +439,37 @@ int launch_text_fwd(const TextBranch& tb, const int32_t* item_track, int M, floa
   a.M = M; a.T = tb.T; a.E = tb.E; a.EP = tb.EP; a.C = tb.C; a.Creal = tb.Creal; a.pad = tb.pad;
   a.out = out; a.ld = ld; a.tidx = tidx;
   if (tb.C % 64 || tb.T < 1 || tb.T > 128 || tb.E % 4 || tb.EP % kTextKC || tb.EP < tb.E) return DCUE_ERR_INVALID;
+  // one item's staged sentence must fit the LDS (config 4: 66 rows x 1,424 B = 94 KB)
+  static const bool chunked = [] {
+    const char* e = getenv("DCUE_TEXT_FWD");
+    return e && e[0] == 'c';
+  }();
+  const int tb_ = tb.T <= 16 ? 1 : tb.T <= 32 ? 2 : tb.T <= 64 ? 4 : 8;
+  const size_t lds = (size_t)(16 * tb_ + 2) * text_full_pitch(tb.EP) * sizeof(_Float16);
+  if (!chunked && lds <= 150 * 1024) {
+    const int wv = tb.C % 128 == 0 ? 8 : 4;
+    const unsigned grid = (unsigned)((long)M * (tb.C / (16 * wv)));
+    auto pick = [&](auto kern) -> int {
+      static bool attr = false;  // (one per instantiation)
+      if (!attr) {
+        DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+        attr = true;
+      }
+      DCUE_LAUNCH(kern, dim3(grid), dim3(64 * wv), lds, s, a);
+      DCUE_LAUNCH_CHECK();
+      return DCUE_OK;
+    };
+    switch (tb_ * 16 + wv) {
+      case 16 + 4: return pick(k_text_fwd_full<1, 4>);
+      case 16 + 8: return pick(k_text_fwd_full<1, 8>);
+      case 32 + 4: return pick(k_text_fwd_full<2, 4>);
+      case 32 + 8: return pick(k_text_fwd_full<2, 8>);
+      case 64 + 4: return pick(k_text_fwd_full<4, 4>);
+      case 64 + 8: return pick(k_text_fwd_full<4, 8>);
+      case 128 + 4: return pick(k_text_fwd_full<8, 4>);
+      default: return pick(k_text_fwd_full<8, 8>);
+    }
+  }
   if (tb.T <= 16) return launch_text_fwd_t<1, 8>(a, s);
   if (tb.T <= 32) return launch_text_fwd_t<2, 4>(a, s);
   if (tb.T <= 64) return launch_text_fwd_t<4, 2>(a, s);

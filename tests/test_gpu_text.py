@@ -187,3 +187,27 @@ def test_text_plan_inbatch_bench_shape():
             adam.step(trainable, g32, lr)
             _close(plan.loss, leaves_loss, 1e-4, 1e-4, "step %d loss" % step)
     plan.close()
+
+
+def test_text_fwd_kernels_bit_identical(tmp_path):
+    """The gather-once text forward (k_text_fwd_full, the default) and the chunked one
+    (DCUE_TEXT_FWD=chunked) run the same MFMA sequence per accumulator: five plan steps of the text
+    tower (tests/race_worker.py) give bit-identical losses, dense parameters and user table."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, torch; sys.path.insert(0, %r); import race_worker as W; r = W.run('text'); "
+            "torch.save({k: r[k] for k in ('loss', 'P', 'emb')}, sys.argv[1])" % os.path.join(root, "tests"))
+    res = []
+    for i, extra in enumerate(({}, {"DCUE_TEXT_FWD": "chunked"})):
+        out = str(tmp_path / ("t%d.pt" % i))
+        env = dict(os.environ, **extra)
+        if not extra:
+            env.pop("DCUE_TEXT_FWD", None)
+        p = subprocess.run([sys.executable, "-c", code, out], env=env, stdout=subprocess.PIPE,
+                           stderr=subprocess.STDOUT, text=True, timeout=100)
+        assert p.returncode == 0, p.stdout[-3000:]
+        res.append(torch.load(out, weights_only=True))
+    for k in ("loss", "P", "emb"):
+        assert torch.equal(res[0][k], res[1][k]), k
