@@ -490,11 +490,7 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
   // this stream finalizes them); the counts are already the global ones (forward_impl)
   const bool sync = train && c.bn && sync_bn;
   if (sync) TRY(comm_allreduce_u64(sync_bn, bn_acc(w.bnacc, w.cmax, 0), 4L * w.cmax, s));
-  for (int l = 1; l <= 5; ++l) {
-    // the previous step's late-segment Adam (split plans, StepOpts::dense_split) ran on the user
-    // stream: conv 2 is the first kernel on this stream to read those parameters
-    if (l == 2 && before_l2) TRY(wait_point(s, before_l2));
-    if (l == 2 && train) TRY(debug_delay(DCUE_SITE_CONV2, s));
+  auto rows_args = [&](int l) {
     RowsArgs a = {};
     a.src = l == 1 ? t->data : (const void*)w.y[l - 1];
     a.item_track = item_track;
@@ -513,6 +509,37 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     a.out_range = rng_at(w, l);
     a.M = M;
     a.nout = l == 5 ? c.D : c.H;
+    return a;
+  };
+  // the fc of the BN tower: f = bn5(y5) W^T + b   (truedcuemel1dbn.py:65,101)
+  auto fc_args = [&]() {
+    TGemmArgs g = {};
+    g.M = M; g.N = c.D; g.K = c.D;
+    g.A = w.y[5]; g.sam = c.D; g.sak = 1;
+    g.amean = w.mean[5]; g.aa = w.a[5]; g.abeta = c.beta(w, 5);
+    g.abn = bn_of(5);
+    g.B = c.P(SEG_FC_W); g.sbk = 1; g.sbn = c.D;
+    g.bias = c.P(SEG_FC_B);
+    g.C = f_out ? f_out : w.f; g.scm = c.D; g.scn = 1;
+    return g;
+  };
+  // in-batch steps of the BN tower: conv 4, conv 5 and the fc in one launch (conv_fwd.hip k_fwd_tail)
+  const bool fuse_tail = train && c.bn && !c.res && !c.text && !sync && fwd_tail_fits(M, c.H, c.D, c.H);
+  for (int l = 1; l <= 5; ++l) {
+    // the previous step's late-segment Adam (split plans, StepOpts::dense_split) ran on the user
+    // stream: conv 2 is the first kernel on this stream to read those parameters
+    if (l == 2 && before_l2) TRY(wait_point(s, before_l2));
+    if (l == 2 && train) TRY(debug_delay(DCUE_SITE_CONV2, s));
+    if (l == 4 && fuse_tail) {
+      const TGemmArgs g = fc_args();
+      TRY(launch_fwd_tail(rows_args(4), rows_args(5), g, c.H, s));
+      if (probes_on()) {
+        TRY(probe(PR_Y1 + 3, w.y[4], (long)M * layer_geom(4).lp * c.H, s));
+        TRY(probe(PR_Y1 + 4, w.y[5], (long)M * layer_geom(5).lp * c.D, s));
+      }
+      return probe(PR_F, g.C, (long)M * c.D, s);
+    }
+    const RowsArgs a = rows_args(l);
     TimerScope tsc;
     TRY(timer_begin(&tsc, l == 1 ? DCUE_TIMED_CONV1_FWD : -1, s));
     TRY(launch_conv_fwd(l, l == 1 ? kMels : c.H, l == 1 ? src : SRC_ACT, a, s));
@@ -542,14 +569,7 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     return probe(PR_F, g.C, (long)M * c.D, s);
   }
   // fc on BN5(y5): f = bn5(y5) W^T + b   (truedcuemel1dbn.py:65,101)
-  TGemmArgs g = {};
-  g.M = M; g.N = c.D; g.K = c.D;
-  g.A = w.y[5]; g.sam = c.D; g.sak = 1;
-  g.amean = w.mean[5]; g.aa = w.a[5]; g.abeta = c.beta(w, 5);
-  g.abn = bn_of(5);
-  g.B = c.P(SEG_FC_W); g.sbk = 1; g.sbn = c.D;
-  g.bias = c.P(SEG_FC_B);
-  g.C = f_out ? f_out : w.f; g.scm = c.D; g.scn = 1;
+  const TGemmArgs g = fc_args();
   TRY(launch_tgemm(2, 0, g, s));
   return probe(PR_F, g.C, (long)M * c.D, s);
 }
@@ -1269,7 +1289,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(probe(PR_G5, w.g[5], (long)M * D, s));
   }
   if (sync) TRY(comm_allreduce_u64(o.sync_bn, bn_acc(w.bnbacc, w.cmax, 5), 4L * w.cmax, s));
-  for (int l = 5; l >= 2; --l) {  // dgrad chain: g_l (+ BN_l sums) -> g_{l-1} (+ BN_{l-1} sums)
+  auto dgrad_args = [&](int l) {
     const LayerGeom gm = layer_geom(l);
     RowsArgs ra = {};
     ra.src = w.g[l]; ra.y_l = w.y[l]; ra.idx_l = w.idx[l];
@@ -1294,6 +1314,30 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     ra.out_grange = grng_at(w, l - 1);  // max |g_{l-1}|: the split-f16 weight gradient's dz bound
     ra.M = M;
     ra.nout = H;
+    return ra;
+  };
+  // in-batch steps: conv 5's and conv 4's input gradients in one launch (conv_dgrad.hip k_dgrad_tail)
+  const bool fuse_dg = !sync && dgrad_tail_fits(M, H, D);
+  for (int l = 5; l >= 2; --l) {  // dgrad chain: g_l (+ BN_l sums) -> g_{l-1} (+ BN_{l-1} sums)
+    if (l == 5 && fuse_dg) {
+      const RowsArgs r5 = dgrad_args(5), r4 = dgrad_args(4);
+      if (!fork_once()) {  // the layer 3-5 weight gradients' fork point, bound to the launch
+        ForkAfter fk(sp, s, &ev_layer[3]);
+        TRY(launch_dgrad_tail(r5, r4, H, D, s));
+        TRY(fk.done());
+        if (thr) TRY(post(multi_hi));
+        TRY(after_fork3());
+      } else {
+        TRY(launch_dgrad_tail(r5, r4, H, D, s));
+      }
+      if (probes_on()) {
+        TRY(probe(PR_G4, w.g[4], (long)M * layer_geom(4).lp * H, s));
+        TRY(probe(PR_G3, w.g[3], (long)M * layer_geom(3).lp * H, s));
+      }
+      l = 4;  // (continues at conv 3's input gradient)
+      continue;
+    }
+    const RowsArgs ra = dgrad_args(l);
     // a fork point only where a side stream waits (wgrads of layers 3-5 after g_3, of layer 2
     // after g_2): every event bound to a launch costs the chain a gap before its next kernel
     if ((l - 1 == 3 && !fork_once()) || l - 1 == 2) {

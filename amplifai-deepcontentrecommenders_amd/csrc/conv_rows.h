@@ -290,9 +290,12 @@ __device__ __forceinline__ void st_split(float* row, int c, float4 v) {
 #endif
 constexpr int kRowsPD = DCUE_ROWS_PD;
 
+// The workgroup (bx, by) of a k_conv_rows launch, as a device function: k_conv_rows runs it on its
+// grid; the fused in-batch forward tail (conv_fwd.hip k_fwd_tail) runs layers 4 and 5 as one
+// workgroup each, back to back in one launch
 template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,
           int POOLL, bool DEEP, bool F16>
-__global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
+__device__ __forceinline__ void conv_rows_body(const RowsArgs& a, const int bx, const int by) {
   critical_path_priority();
   // (DCUE_KTRACE: kernels 2-6 the forwards by input length (layers 1-5), 7-11 the dgrads)
   [[maybe_unused]] constexpr int KID = 2 + MODE * 5 + (LIN >= 131 ? 0 : LIN >= 32 ? 1 : LIN >= 8 ? 2 : LIN >= 2 ? 3 : 4);
@@ -309,7 +312,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
 
   const int M = a.M;
   const long total = (long)M * R;
-  const long gr0 = (long)blockIdx.x * ROWS;
+  const long gr0 = (long)bx * ROWS;
   const long gr1 = min(gr0 + ROWS, total);
   const long i0 = gr0 / R, i1 = (gr1 - 1) / R;
   const long elo = i0 * RX + (gr0 - i0 * R);
@@ -319,7 +322,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
   const int g = lane >> 4, l16 = lane & 15;
   const int nout = a.nout;
   constexpr int CT = kRowsCT;  // 16-column MFMA tiles per wave
-  const int ocol0 = blockIdx.y * 128 + wave * 16 * CT;
+  const int ocol0 = by * 128 + wave * 16 * CT;
   const bool colok = ocol0 < nout;
 
   // B operand (packed weights, L2-resident): the first PD k-steps are requested before anything
@@ -425,7 +428,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
     chan_stage<SRC>(cpre, KC, chl);
     if constexpr (F16) range_stage<SRC>(a, cpre, KC, chl);
     if constexpr (SRC != SRC_DZ)
-      if (blockIdx.x == 0 && blockIdx.y == 0) bn_publish(a.in_bn, threadIdx.x);
+      if (bx == 0 && by == 0) bn_publish(a.in_bn, threadIdx.x);
     DCUE_KT(KID, 5);
     __syncthreads();
     if constexpr (F16) sscale = split_scale(chl, KC);
@@ -638,6 +641,12 @@ __global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
   }
   DCUE_KT(KID, 4);
   DCUE_KTW(KID, 7);
+}
+
+template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,
+          int POOLL, bool DEEP, bool F16>
+__global__ __launch_bounds__(kRowsThreads) void k_conv_rows(RowsArgs a) {
+  conv_rows_body<MODE, SRC, KC, KS, PADL, LIN, R, POOL, TW, LPL, POOLL, DEEP, F16>(a, blockIdx.x, blockIdx.y);
 }
 
 template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,

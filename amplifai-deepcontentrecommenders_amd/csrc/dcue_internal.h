@@ -134,7 +134,16 @@ int launch_conv_wgrad_multi(WgradMulti w, hipStream_t s);
 bool wgrad_f16_on();
 
 int launch_conv_fwd(int layer, int kc, int src, const RowsArgs& a, hipStream_t s);
+// in-batch forward tail (conv_fwd.hip k_fwd_tail): conv 4, conv 5 and the fc on BN5 in one workgroup
+// (M <= 64 items, H in {32, 64, 128}, d <= 128; DCUE_FWD_TAIL=0 turns it off)
+struct TGemmArgs;
+bool fwd_tail_fits(int M, int H, int D, int nout4);
+int launch_fwd_tail(const RowsArgs& a4, const RowsArgs& a5, const TGemmArgs& fc, int H, hipStream_t s);
 int launch_conv_dgrad(int layer, int kc, const RowsArgs& a, hipStream_t s);
+// in-batch input-gradient tail (conv_dgrad.hip k_dgrad_tail): conv 5's and conv 4's dgrads in one
+// workgroup (M <= 64, H and d in {32, 64, 128}; DCUE_DGRAD_TAIL=0 turns it off)
+bool dgrad_tail_fits(int M, int H, int D);
+int launch_dgrad_tail(const RowsArgs& a5, const RowsArgs& a4, int H, int D, hipStream_t s);
 int launch_conv_wgrad(int layer, int src, const WgradArgs& a, int nchunk, hipStream_t s);
 // xhat0[i][t + 2][c] = (x[track_i][t][c] - mean0[c]) * invstd0[c] in a [M][kXp][128] zero-padded
 // layout, bn0's batch statistics finalized from its accumulators (layer 1's wgrad reads it from `xsrc`)
