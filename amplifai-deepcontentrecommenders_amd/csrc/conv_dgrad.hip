@@ -82,10 +82,10 @@ template <int KC5, int KC4>
 __global__ __launch_bounds__(kRowsThreads) void k_dgrad_tail(RowsArgs a5, RowsArgs a4) {
   constexpr LayerGeom g5 = layer_geom(5), g4 = layer_geom(4);
   conv_rows_body<1, SRC_DZ, KC5, g5.ks, g5.ks - 1 - g5.pad, g5.lp * g5.pool, g5.lin, 1, 4, g5.lp, g5.pool, true,
-                 false>(a5, 0, 0);
+                 false, true>(a5, 0, 0);
   __syncthreads();  // g4, BN4's backward sums and max |g4| complete (this workgroup's own writes)
   conv_rows_body<1, SRC_DZ, KC4, g4.ks, g4.ks - 1 - g4.pad, g4.lp * g4.pool, g4.lin, 1, 8, g4.lp, g4.pool, true,
-                 false>(a4, 0, 0);
+                 false, true>(a4, 0, 0);
 }
 
 bool dgrad_tail_fits(int M, int H, int D) {

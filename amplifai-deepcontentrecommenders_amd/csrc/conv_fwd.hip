@@ -76,9 +76,9 @@ template <int KC, bool F16>
 __global__ __launch_bounds__(kRowsThreads) void k_fwd_tail(RowsArgs a4, RowsArgs a5, TGemmArgs fc) {
   extern __shared__ __attribute__((aligned(16))) float slab[];
   constexpr LayerGeom g4 = layer_geom(4), g5 = layer_geom(5);
-  conv_rows_body<0, SRC_ACT, KC, g4.ks, g4.pad, g4.lin, g4.lp * g4.pool, g4.pool, 8, 1, 1, true, F16>(a4, 0, 0);
+  conv_rows_body<0, SRC_ACT, KC, g4.ks, g4.pad, g4.lin, g4.lp * g4.pool, g4.pool, 8, 1, 1, true, F16, true>(a4, 0, 0);
   __syncthreads();  // y4, its BN sums and range complete (this workgroup's own stores and atomics)
-  conv_rows_body<0, SRC_ACT, KC, g5.ks, g5.pad, g5.lin, g5.lp * g5.pool, g5.pool, 4, 1, 1, true, F16>(a5, 0, 0);
+  conv_rows_body<0, SRC_ACT, KC, g5.ks, g5.pad, g5.lin, g5.lp * g5.pool, g5.pool, 4, 1, 1, true, F16, true>(a5, 0, 0);
   __syncthreads();
   TgLds* L = reinterpret_cast<TgLds*>(slab);
   const int half = threadIdx.x >> 8, t = threadIdx.x & 255;

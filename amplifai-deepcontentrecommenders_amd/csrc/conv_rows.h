@@ -293,8 +293,12 @@ constexpr int kRowsPD = DCUE_ROWS_PD;
 // The workgroup (bx, by) of a k_conv_rows launch, as a device function: k_conv_rows runs it on its
 // grid; the fused in-batch forward tail (conv_fwd.hip k_fwd_tail) runs layers 4 and 5 as one
 // workgroup each, back to back in one launch
+// TILESUM: the BatchNorm partial sums go to the exact accumulators once per 16-row tile (each tile's
+// fp32 partial formed exactly as a one-tile workgroup forms it), so a TW-tile workgroup adds what TW
+// one-tile workgroups would -- the accumulators are exact, so the totals are bit-identical to the
+// TW = 1 launches (the fused in-batch tails use it to stay bit-identical with the separate launches)
 template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,
-          int POOLL, bool DEEP, bool F16>
+          int POOLL, bool DEEP, bool F16, bool TILESUM = false>
 __device__ __forceinline__ void conv_rows_body(const RowsArgs& a, const int bx, const int by) {
   critical_path_priority();
   // (DCUE_KTRACE: kernels 2-6 the forwards by input length (layers 1-5), 7-11 the dgrads)
@@ -533,6 +537,19 @@ __device__ __forceinline__ void conv_rows_body(const RowsArgs& a, const int bx, 
   if constexpr (MODE == 1) {
     // g_{l-1} rows, plus this tile's share of BN_{l-1}'s backward sums (sum g, sum g*xhat)
     float sg[CT] = {}, sgx[CT] = {}, gmx[CT] = {};
+    // one tile's (or, !TILESUM, the workgroup's) partial sums into the exact accumulators
+    auto flush_g = [&](int ct) {
+      float s = sg[ct], q = sgx[ct];
+      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+      if (g == 0) {
+        const int o = ocol0 + 16 * ct + l16;
+        acc128_add(acc_at(a.out_acc, nout, 0, o), s);
+        acc128_add(acc_at(a.out_acc, nout, 1, o), q);
+      }
+      sg[ct] = 0.f;
+      sgx[ct] = 0.f;
+    };
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int o = ocol0 + 16 * ct + l16;
@@ -556,20 +573,12 @@ __device__ __forceinline__ void conv_rows_body(const RowsArgs& a, const int bx, 
             sg[ct] += gv;
             sgx[ct] += gv * ((yv[j] - mu) * is);
           }
+        if (TILESUM && a.out_acc) flush_g(ct);
       }
     }
-    if (a.out_acc) {
+    if (!TILESUM && a.out_acc) {
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        float s = sg[ct], q = sgx[ct];
-        s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
-        q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
-        if (g == 0) {
-          const int o = ocol0 + 16 * ct + l16;
-          acc128_add(acc_at(a.out_acc, nout, 0, o), s);
-          acc128_add(acc_at(a.out_acc, nout, 1, o), q);
-        }
-      }
+      for (int ct = 0; ct < CT; ++ct) flush_g(ct);
     }
     if (a.out_grange) {  // max |g_{l-1}| per channel: the split-f16 weight gradient's dz bound
 #pragma unroll
@@ -584,6 +593,18 @@ __device__ __forceinline__ void conv_rows_body(const RowsArgs& a, const int bx, 
     constexpr int LP = R / POOL;
     float ssum[CT] = {}, ssq[CT] = {}, ymax[CT] = {};
     const float inv_s = sscale.inv;  // 1 on the f32 path; exact power of two on the split path
+    auto flush_y = [&](int ct) {  // (as flush_g)
+      float s = ssum[ct], q = ssq[ct];
+      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+      if (g == 0) {
+        const int o = ocol0 + 16 * ct + l16;
+        acc128_add(acc_at(a.out_acc, nout, 0, o), s);
+        acc128_add(acc_at(a.out_acc, nout, 1, o), q);
+      }
+      ssum[ct] = 0.f;
+      ssq[ct] = 0.f;
+    };
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int o = ocol0 + 16 * ct + l16;
@@ -614,20 +635,12 @@ __device__ __forceinline__ void conv_rows_body(const RowsArgs& a, const int bx, 
             ssq[ct] += cnt * y * y;
           }
         }
+        if (TILESUM && a.out_acc) flush_y(ct);
       }
     }
-    if (a.out_acc) {
+    if (!TILESUM && a.out_acc) {
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        float s = ssum[ct], q = ssq[ct];
-        s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
-        q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
-        if (g == 0) {
-          const int o = ocol0 + 16 * ct + l16;
-          acc128_add(acc_at(a.out_acc, nout, 0, o), s);
-          acc128_add(acc_at(a.out_acc, nout, 1, o), q);
-        }
-      }
+      for (int ct = 0; ct < CT; ++ct) flush_y(ct);
     }
     if (a.out_range) {  // the output's per-channel maximum: the next layer's split scale
 #pragma unroll
