@@ -1414,12 +1414,16 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       if (conv1_wgrad_tail_fits(wa, nch)) {
         TimerScope tsc;
         TRY(timer_begin(&tsc, DCUE_TIMED_CONV1_WGRAD, so));
-        {
+        if (tsc.a || tsc.capturing) {  // a timed launch binds the timer's pair; the fork point is recorded
+          TRY(launch_conv1_wgrad_tail(src, wa, nch, bt, so));
+          TRY(timer_end(&tsc));
+          ForkAfter fk(sp, so, tail);
+          TRY(fk.done());
+        } else {
           ForkAfter fk(sp, so, tail);
           TRY(launch_conv1_wgrad_tail(src, wa, nch, bt, so));
           TRY(fk.done());
         }
-        TRY(timer_end(&tsc));
         if (!probes_on()) return DCUE_OK;
         TRY(probe(PR_G_1, m->grads, late, so));
         return fuse_late ? probe(PR_P_EARLY, m->params, late, so) : DCUE_OK;
