@@ -523,22 +523,11 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     g.C = f_out ? f_out : w.f; g.scm = c.D; g.scn = 1;
     return g;
   };
-  // in-batch steps of the BN tower: conv 4, conv 5 and the fc in one launch (conv_fwd.hip k_fwd_tail)
-  const bool fuse_tail = train && c.bn && !c.res && !c.text && !sync && fwd_tail_fits(M, c.H, c.D, c.H);
   for (int l = 1; l <= 5; ++l) {
     // the previous step's late-segment Adam (split plans, StepOpts::dense_split) ran on the user
     // stream: conv 2 is the first kernel on this stream to read those parameters
     if (l == 2 && before_l2) TRY(wait_point(s, before_l2));
     if (l == 2 && train) TRY(debug_delay(DCUE_SITE_CONV2, s));
-    if (l == 4 && fuse_tail) {
-      const TGemmArgs g = fc_args();
-      TRY(launch_fwd_tail(rows_args(4), rows_args(5), g, c.H, s));
-      if (probes_on()) {
-        TRY(probe(PR_Y1 + 3, w.y[4], (long)M * layer_geom(4).lp * c.H, s));
-        TRY(probe(PR_Y1 + 4, w.y[5], (long)M * layer_geom(5).lp * c.D, s));
-      }
-      return probe(PR_F, g.C, (long)M * c.D, s);
-    }
     const RowsArgs a = rows_args(l);
     TimerScope tsc;
     TRY(timer_begin(&tsc, l == 1 ? DCUE_TIMED_CONV1_FWD : -1, s));
@@ -1316,27 +1305,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     ra.nout = H;
     return ra;
   };
-  // in-batch steps: conv 5's and conv 4's input gradients in one launch (conv_dgrad.hip k_dgrad_tail)
-  const bool fuse_dg = !sync && dgrad_tail_fits(M, H, D);
   for (int l = 5; l >= 2; --l) {  // dgrad chain: g_l (+ BN_l sums) -> g_{l-1} (+ BN_{l-1} sums)
-    if (l == 5 && fuse_dg) {
-      const RowsArgs r5 = dgrad_args(5), r4 = dgrad_args(4);
-      if (!fork_once()) {  // the layer 3-5 weight gradients' fork point, bound to the launch
-        ForkAfter fk(sp, s, &ev_layer[3]);
-        TRY(launch_dgrad_tail(r5, r4, H, D, s));
-        TRY(fk.done());
-        if (thr) TRY(post(multi_hi));
-        TRY(after_fork3());
-      } else {
-        TRY(launch_dgrad_tail(r5, r4, H, D, s));
-      }
-      if (probes_on()) {
-        TRY(probe(PR_G4, w.g[4], (long)M * layer_geom(4).lp * H, s));
-        TRY(probe(PR_G3, w.g[3], (long)M * layer_geom(3).lp * H, s));
-      }
-      l = 4;  // (continues at conv 3's input gradient)
-      continue;
-    }
     const RowsArgs ra = dgrad_args(l);
     // a fork point only where a side stream waits (wgrads of layers 3-5 after g_3, of layer 2
     // after g_2): every event bound to a launch costs the chain a gap before its next kernel
@@ -1397,38 +1366,6 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       wa.kd_max = kd_max * wa.invN;
     }
     const int nch = wgrad_nchunk(l, M, C, cin);
-    if (l == 1 && f16w) {  // the weight gradient, its reduce and bn0's gradients (+ Adam) in one launch
-      const bool graw = src == SRC_TRACK_F16;
-      Bn0Adam ba;
-      Bn0Tail bt = {};
-      bt.G = w.G; bt.S = w.S;
-      bt.gamma0 = c.gamma(w, 0); bt.beta0 = c.beta(w, 0);
-      bt.mean0 = graw ? w.mean[0] : nullptr; bt.invstd0 = graw ? w.invstd[0] : nullptr;
-      bt.dgamma0 = c.dgamma(w, 0); bt.dbeta0 = c.dbeta(w, 0);
-      bt.W1 = c.P(seg_conv_w(1)); bt.dW1 = c.Gd(seg_conv_w(1)); bt.db1 = c.Gd(seg_conv_b(1));
-      if (fuse_late) {
-        ba.md = m; ba.poff = c.poff; ba.args = *o.dense_split; ba.bn = c.bn;
-        bt.adam = &ba;
-      }
-      bt.ctr = w.grng + 7 * kRngC;  // (the gradient maxima's padding: cleared with the accumulators)
-      if (conv1_wgrad_tail_fits(wa, nch)) {
-        TimerScope tsc;
-        TRY(timer_begin(&tsc, DCUE_TIMED_CONV1_WGRAD, so));
-        if (tsc.a || tsc.capturing) {  // a timed launch binds the timer's pair; the fork point is recorded
-          TRY(launch_conv1_wgrad_tail(src, wa, nch, bt, so));
-          TRY(timer_end(&tsc));
-          ForkAfter fk(sp, so, tail);
-          TRY(fk.done());
-        } else {
-          ForkAfter fk(sp, so, tail);
-          TRY(launch_conv1_wgrad_tail(src, wa, nch, bt, so));
-          TRY(fk.done());
-        }
-        if (!probes_on()) return DCUE_OK;
-        TRY(probe(PR_G_1, m->grads, late, so));
-        return fuse_late ? probe(PR_P_EARLY, m->params, late, so) : DCUE_OK;
-      }
-    }
     if (l == 1 && !f16w) {  // the GEMM reads the pooled BN1 backward, expanded to rows at MFMA time
       TRY(launch_conv1_dx(wa, w.dx1, so));
       wa.g_l = w.dx1;

@@ -1,7 +1,5 @@
 // Input gradients of conv layers 2..5 (k_conv_rows MODE 1): the launch dispatch. Kernel body:
 // conv_rows.h.
-#include <algorithm>
-
 #include "conv_rows.h"
 
 DCUE_KTRACE_READER(dgrad)  // diagnostic builds only (dcue_common.h)
@@ -70,59 +68,3 @@ int launch_conv_dgrad(int layer, int kc, const RowsArgs& a, hipStream_t s) {
 
 }  // namespace dcue
 
-namespace dcue {
-
-// ------------------------------------------------------------- in-batch input-gradient tail, fused
-// The input gradients of conv 5 (g4 + BN4's backward sums) and conv 4 (g3 + BN3's) in ONE workgroup:
-// at in-batch M <= 64 their M and 2M output rows fit four and eight 16-row tiles, and conv 4's
-// BN-backward operand (BN4's sums) is complete inside the workgroup once conv 5's part is done -- one
-// kernel boundary fewer on the backward chain. conv_rows_body with the separate launches' tile maps
-// (the f32 path they take at these sizes): bit-identical (DCUE_DGRAD_TAIL=0 runs the two launches).
-template <int KC5, int KC4>
-__global__ __launch_bounds__(kRowsThreads) void k_dgrad_tail(RowsArgs a5, RowsArgs a4) {
-  constexpr LayerGeom g5 = layer_geom(5), g4 = layer_geom(4);
-  conv_rows_body<1, SRC_DZ, KC5, g5.ks, g5.ks - 1 - g5.pad, g5.lp * g5.pool, g5.lin, 1, 4, g5.lp, g5.pool, true,
-                 false, true>(a5, 0, 0);
-  __syncthreads();  // g4, BN4's backward sums and max |g4| complete (this workgroup's own writes)
-  conv_rows_body<1, SRC_DZ, KC4, g4.ks, g4.ks - 1 - g4.pad, g4.lp * g4.pool, g4.lin, 1, 8, g4.lp, g4.pool, true,
-                 false, true>(a4, 0, 0);
-}
-
-bool dgrad_tail_fits(int M, int H, int D) {
-  static const bool on = [] {
-    const char* e = getenv("DCUE_DGRAD_TAIL");
-    return !(e && e[0] == '0');
-  }();
-  return on && M >= 1 && M <= 64 && (H == 32 || H == 64 || H == 128) && (D == 32 || D == 64 || D == 128) &&
-         (long)M * layer_geom(4).lin < kDgradF16MinRows;
-}
-
-int launch_dgrad_tail(const RowsArgs& a5, const RowsArgs& a4, int H, int D, hipStream_t s) {
-  const size_t lds = std::max(slab_bytes(layer_geom(5).lin, layer_geom(5).ks, D, 4),
-                              slab_bytes(layer_geom(4).lin, layer_geom(4).ks, H, 8));
-  auto launch = [&](auto kern) -> int {
-    static bool attr = false;
-    if (!attr) {
-      DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)std::max(slab_bytes(1, 1, 128, 4), slab_bytes(2, 2, 128, 8))));
-      attr = true;
-    }
-    DCUE_LAUNCH(kern, dim3(1), dim3(kRowsThreads), lds, s, a5, a4);
-    DCUE_LAUNCH_CHECK();
-    return DCUE_OK;
-  };
-  switch (D * 1000 + H) {
-    case 32032: return launch(k_dgrad_tail<32, 32>);
-    case 32064: return launch(k_dgrad_tail<32, 64>);
-    case 32128: return launch(k_dgrad_tail<32, 128>);
-    case 64032: return launch(k_dgrad_tail<64, 32>);
-    case 64064: return launch(k_dgrad_tail<64, 64>);
-    case 64128: return launch(k_dgrad_tail<64, 128>);
-    case 128032: return launch(k_dgrad_tail<128, 32>);
-    case 128064: return launch(k_dgrad_tail<128, 64>);
-    case 128128: return launch(k_dgrad_tail<128, 128>);
-    default: return DCUE_ERR_UNSUPPORTED;
-  }
-}
-
-}  // namespace dcue

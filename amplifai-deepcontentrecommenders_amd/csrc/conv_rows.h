@@ -290,15 +290,9 @@ __device__ __forceinline__ void st_split(float* row, int c, float4 v) {
 #endif
 constexpr int kRowsPD = DCUE_ROWS_PD;
 
-// The workgroup (bx, by) of a k_conv_rows launch, as a device function: k_conv_rows runs it on its
-// grid; the fused in-batch forward tail (conv_fwd.hip k_fwd_tail) runs layers 4 and 5 as one
-// workgroup each, back to back in one launch
-// TILESUM: the BatchNorm partial sums go to the exact accumulators once per 16-row tile (each tile's
-// fp32 partial formed exactly as a one-tile workgroup forms it), so a TW-tile workgroup adds what TW
-// one-tile workgroups would -- the accumulators are exact, so the totals are bit-identical to the
-// TW = 1 launches (the fused in-batch tails use it to stay bit-identical with the separate launches)
+// The workgroup (bx, by) of a k_conv_rows launch, as a device function (k_conv_rows runs it on its grid)
 template <int MODE, int SRC, int KC, int KS, int PADL, int LIN, int R, int POOL, int TW, int LPL,
-          int POOLL, bool DEEP, bool F16, bool TILESUM = false>
+          int POOLL, bool DEEP, bool F16>
 __device__ __forceinline__ void conv_rows_body(const RowsArgs& a, const int bx, const int by) {
   critical_path_priority();
   // (DCUE_KTRACE: kernels 2-6 the forwards by input length (layers 1-5), 7-11 the dgrads)
@@ -537,7 +531,7 @@ __device__ __forceinline__ void conv_rows_body(const RowsArgs& a, const int bx, 
   if constexpr (MODE == 1) {
     // g_{l-1} rows, plus this tile's share of BN_{l-1}'s backward sums (sum g, sum g*xhat)
     float sg[CT] = {}, sgx[CT] = {}, gmx[CT] = {};
-    // one tile's (or, !TILESUM, the workgroup's) partial sums into the exact accumulators
+    // the workgroup's partial sums into the exact accumulators
     auto flush_g = [&](int ct) {
       float s = sg[ct], q = sgx[ct];
       s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
@@ -573,10 +567,9 @@ __device__ __forceinline__ void conv_rows_body(const RowsArgs& a, const int bx, 
             sg[ct] += gv;
             sgx[ct] += gv * ((yv[j] - mu) * is);
           }
-        if (TILESUM && a.out_acc) flush_g(ct);
       }
     }
-    if (!TILESUM && a.out_acc) {
+    if (a.out_acc) {
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) flush_g(ct);
     }
@@ -635,10 +628,9 @@ __device__ __forceinline__ void conv_rows_body(const RowsArgs& a, const int bx, 
             ssq[ct] += cnt * y * y;
           }
         }
-        if (TILESUM && a.out_acc) flush_y(ct);
       }
     }
-    if (!TILESUM && a.out_acc) {
+    if (a.out_acc) {
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) flush_y(ct);
     }

@@ -1786,144 +1786,3 @@ int launch_bn0_grads(const float* G, const float* E, const float* W1, const floa
 
 }  // namespace dcue
 
-namespace dcue {
-
-// ------------------------------------------------------------- conv-1 weight-gradient tail, fused
-// The step's last three launches on the caller's stream -- the tap-fused conv-1 weight gradient
-// (k_conv_wgrad16t, split-K partials), their chunk reduce (k_wgrad_reduce) and bn0's gradients (+ the
-// split plans' Adam over bn0 / conv 1 / bn1, k_bn0_grads(_adam)) -- as one launch whose workgroups
-// pass two grid barriers: partials -> barrier -> every workgroup reduces a share of the blocks ->
-// barrier -> every workgroup takes two of bn0's input channels. The same device functions with the
-// same thread-to-element maps and summation orders as the three kernels: bit-identical results,
-// two kernel boundaries fewer on the critical path. Used when every
-// workgroup can be resident at once (in-batch steps: 66 workgroups at H = 128); the barrier waits
-// are bounded and report a gave-up wait (dcue_debug_fail_flags bit 1) instead of hanging.
-struct W1Tail {
-  float *G, *S;               // the reduce's outputs: G [cout][4 x 128], S (= E) [5][cout]
-  const float *gamma0, *beta0, *mean0, *invstd0;
-  float *dgamma0, *dbeta0;
-  const float* W1;            // !ADAM: W1, and where dW1 / db1 go
-  float *dW1, *db1;
-  Bn0AdamDev ad;              // ADAM: the dense Adam over [0, DCUE_SEG_LATE)
-  unsigned* ctr;              // barrier counter, zeroed with the step's accumulator block
-  unsigned* fail;
-  int nchunk;
-};
-
-__device__ __forceinline__ void tail_grid_barrier(unsigned* ctr, unsigned target, unsigned* fail) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();  // the workgroup's stores (ordered before by the barrier) before the arrival
-    atomicAdd(ctr, 1u);
-    unsigned spins = 0;
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 24)) {  // never expected (every workgroup is resident): report, do not hang
-        atomicOr(fail, 2u);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-}
-
-template <int SRCX, bool ADAM>
-__global__ __launch_bounds__(kW16tThreads, 1) void k_conv1_wgrad_tail(WgradArgs a, W1Tail t) {
-  critical_path_priority();
-  extern __shared__ __attribute__((aligned(16))) char lds1t[];
-  constexpr LayerGeom gm = layer_geom(1);
-  const int ot = (a.cout + kW16tO - 1) / kW16tO;
-  const int L = xcd_swizzle(blockIdx.x, gridDim.x);
-  wgrad16t_body<SRCX, gm.ks, gm.pad, gm.lin, gm.lp * gm.pool, gm.pool, gm.lp>(a, L % ot, L / ot, lds1t);
-  tail_grid_barrier(t.ctr, gridDim.x, t.fail);
-
-  // the chunk reduce (wgrad_reduce_body's blocks: 256 threads, 8 chunk groups x 32 float4 columns),
-  // two blocks per workgroup at a time
-  const int half = threadIdx.x >> 8, lt = threadIdx.x & 255, col = lt & 31, grp = lt >> 5;
-  float4 (*red)[kRedGroups][32] = reinterpret_cast<float4 (*)[kRedGroups][32]>(lds1t);
-  const long kcn = (long)gm.ks * a.cin, nw = (long)a.cout * kcn, nwblk = (nw + 127) / 128;
-  const long nbo = 5L * a.cout, nblk = nwblk + (nbo + 127) / 128;
-  for (long pb = 2L * blockIdx.x; pb < nblk; pb += 2L * gridDim.x) {  // (uniform per workgroup)
-    const long blk = pb + half;
-    const bool isw = blk < nwblk;
-    const long e4 = isw ? blk * 128 + 4 * col : (blk - nwblk) * 128 + 4 * col;
-    const bool ok = blk < nblk && e4 < (isw ? nw : nbo);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ok) v = sum_chunks((isw ? a.wpart : a.bpart) + e4, (size_t)(isw ? nw : nbo), t.nchunk, grp);
-    red[half][grp][col] = v;
-    __syncthreads();
-    if (grp == 0 && ok) st4((isw ? t.G : t.S) + e4, combine_groups(red[half], col));
-    __syncthreads();
-  }
-  tail_grid_barrier(t.ctr, 2 * gridDim.x, t.fail);
-
-  // bn0's input channels, two per workgroup (k_bn0_grads(_adam)'s 256-thread channel groups)
-  float* rg = reinterpret_cast<float*>(lds1t) + half * 512;
-  for (int cb = 2 * blockIdx.x; cb < kMels; cb += 2 * gridDim.x) {
-    const int c = cb + half;
-    bn0_channel<ADAM>(t.G, t.S, t.gamma0, t.beta0, t.mean0, t.invstd0, a.cout, t.dgamma0, t.dbeta0, t.ad, t.W1,
-                      t.dW1, t.db1, c, lt, rg, rg + 256, c < kMels);
-  }
-}
-
-static bool w1_tail_on() {  // DCUE_W1_TAIL=0: the three launches (A/B, and the bit-identity test)
-  static const bool on = [] {
-    const char* e = getenv("DCUE_W1_TAIL");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-static int device_cus() {
-  static int cus[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    cus[dev] = 0;
-  return cus[dev];
-}
-
-bool conv1_wgrad_tail_fits(const WgradArgs& a, int nchunk) {
-  if (!w1_tail_on() || !wgrad_f16_on() || !w16t_layer(1, a.cin)) return false;
-  if (a.cin != kMels || a.cout % 4 || a.cout > 256) return false;
-  if ((long)a.M * layer_geom(1).lp * layer_geom(1).pool >= (1L << 30)) return false;
-  // the barriers need every workgroup resident at once: one per CU (LDS-bound), at most the CU count
-  const long grid = (long)((a.cout + kW16tO - 1) / kW16tO) * nchunk;
-  const int cus = device_cus();
-  return cus > 0 && grid <= cus;
-}
-
-int launch_conv1_wgrad_tail(int src, const WgradArgs& a0, int nchunk, const Bn0Tail& b, hipStream_t s) {
-  if (!conv1_wgrad_tail_fits(a0, nchunk) || !b.ctr) return DCUE_ERR_UNSUPPORTED;
-  constexpr LayerGeom gm = layer_geom(1);
-  constexpr int R = gm.lp * gm.pool;
-  WgradArgs a = a0;
-  a.rows_per_chunk = (int)w16_rows_per_chunk((long)a.M * R, nchunk);
-  const unsigned grid = (unsigned)((a.cout + kW16tO - 1) / kW16tO) * (unsigned)nchunk;
-  W1Tail t = {};
-  t.G = b.G; t.S = b.S;
-  t.gamma0 = b.gamma0; t.beta0 = b.beta0; t.mean0 = b.mean0; t.invstd0 = b.invstd0;
-  t.dgamma0 = b.dgamma0; t.dbeta0 = b.dbeta0;
-  t.W1 = b.W1; t.dW1 = b.dW1; t.db1 = b.db1;
-  if (b.adam) t.ad = bn0adam_dev(*b.adam);
-  t.ctr = b.ctr;
-  t.fail = user_fwd_fail_flag();
-  t.nchunk = nchunk;
-  if (!t.fail) return DCUE_ERR_HIP;
-  const bool f16 = src == SRC_TRACK_F16;
-  const size_t LDS = f16 ? w16t_lds_bytes<R, gm.ks>(true) : w16t_lds_bytes<R, gm.ks>(false);
-  auto kern = f16 ? (b.adam ? k_conv1_wgrad_tail<SRC_TRACK_F16, true> : k_conv1_wgrad_tail<SRC_TRACK_F16, false>)
-                  : (b.adam ? k_conv1_wgrad_tail<SRC_TRACK_F32, true> : k_conv1_wgrad_tail<SRC_TRACK_F32, false>);
-  static bool attr[4] = {};
-  const int ai = (f16 ? 2 : 0) + (b.adam ? 1 : 0);
-  if (!attr[ai]) {
-    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS));
-    attr[ai] = true;
-  }
-  DCUE_LAUNCH(kern, dim3(grid), dim3(kW16tThreads), LDS, s, a, t);
-  DCUE_LAUNCH_CHECK();
-  return DCUE_OK;
-}
-
-}  // namespace dcue

@@ -134,16 +134,7 @@ int launch_conv_wgrad_multi(WgradMulti w, hipStream_t s);
 bool wgrad_f16_on();
 
 int launch_conv_fwd(int layer, int kc, int src, const RowsArgs& a, hipStream_t s);
-// in-batch forward tail (conv_fwd.hip k_fwd_tail): conv 4, conv 5 and the fc on BN5 in one workgroup
-// (M <= 64 items, H in {32, 64, 128}, d <= 128; DCUE_FWD_TAIL=0 turns it off)
-struct TGemmArgs;
-bool fwd_tail_fits(int M, int H, int D, int nout4);
-int launch_fwd_tail(const RowsArgs& a4, const RowsArgs& a5, const TGemmArgs& fc, int H, hipStream_t s);
 int launch_conv_dgrad(int layer, int kc, const RowsArgs& a, hipStream_t s);
-// in-batch input-gradient tail (conv_dgrad.hip k_dgrad_tail): conv 5's and conv 4's dgrads in one
-// workgroup (M <= 64, H and d in {32, 64, 128}; DCUE_DGRAD_TAIL=0 turns it off)
-bool dgrad_tail_fits(int M, int H, int D);
-int launch_dgrad_tail(const RowsArgs& a5, const RowsArgs& a4, int H, int D, hipStream_t s);
 int launch_conv_wgrad(int layer, int src, const WgradArgs& a, int nchunk, hipStream_t s);
 // xhat0[i][t + 2][c] = (x[track_i][t][c] - mean0[c]) * invstd0[c] in a [M][kXp][128] zero-padded
 // layout, bn0's batch statistics finalized from its accumulators (layer 1's wgrad reads it from `xsrc`)
@@ -197,21 +188,6 @@ struct Bn0Adam {
 int launch_bn0_grads_adam(const float* G, const float* E, const float* gamma0, const float* beta0,
                           const float* mean0, const float* invstd0, int H, float* dgamma0, float* dbeta0,
                           const Bn0Adam& a, hipStream_t s);
-
-// The conv-1 weight gradient, its split-K reduce and bn0's gradients (+ Adam, adam != null) as one
-// launch with grid barriers (conv_wgrad.hip k_conv1_wgrad_tail): DCUE_ERR_UNSUPPORTED where its
-// workgroups cannot all be resident (the caller then issues the three launches)
-struct Bn0Tail {
-  float *G, *S;                            // reduce outputs (the workspace's G / S)
-  const float *gamma0, *beta0, *mean0, *invstd0;
-  float *dgamma0, *dbeta0;
-  const float* W1;                         // !adam: dW1 = f(W1), db1
-  float *dW1, *db1;
-  const Bn0Adam* adam;                     // split plans: Adam over [0, DCUE_SEG_LATE) in the same launch
-  unsigned* ctr;                           // a zeroed word (the step's accumulator block)
-};
-bool conv1_wgrad_tail_fits(const WgradArgs& a, int nchunk);
-int launch_conv1_wgrad_tail(int src, const WgradArgs& a, int nchunk, const Bn0Tail& b, hipStream_t s);
 
 // mean0 / invstd0 (nullable): G is the contraction with the raw input (split-f16 path, fp16 table)
 int launch_bn0_grads(const float* G, const float* E, const float* W1, const float* gamma0,

@@ -3,10 +3,7 @@ schedule_worker.py, one process per variant, run one after another) give bit-ide
 dense parameters and user table with the side-issue thread on and off (DCUE_SIDE_THREAD, csrc/side.hip)
 and under each scheduling A/B knob of DESIGN.md §4.7 round 4 (a fork event after the score kernel,
 the prologue before the forward, one late wait before conv 1, the lookahead at the dgrad fork, the
-user tower's forward as three launches), the fused user-tower forward, and the conv-1 weight-gradient
-tail as three launches instead of one (DCUE_W1_TAIL=0), conv 4 + conv 5 + fc as three launches
-instead of one (DCUE_FWD_TAIL=0), the conv-5 and conv-4 input gradients as two launches
-(DCUE_DGRAD_TAIL=0) -- the same device functions, the same bits.
+user tower's forward as three launches) and the fused user-tower forward.
 Every variant orders the same kernels by the same data
 dependencies, so any difference would be a missing order."""
 import os
@@ -28,9 +25,6 @@ VARIANTS = [
     {"DCUE_AHEAD_AT": "fork"},
     {"DCUE_USER_FWD": "fused"},
     {"DCUE_USER_FWD": "fused", "DCUE_SIDE_THREAD": "0"},
-    {"DCUE_W1_TAIL": "0"},
-    {"DCUE_FWD_TAIL": "0"},
-    {"DCUE_DGRAD_TAIL": "0"},
 ]
 # (the fused user tower's round-4 non-finite runs were the plan's cross-stream races, not the kernel:
 # DESIGN.md §4.7 round 5, tests/test_gpu_races.py)
@@ -42,7 +36,7 @@ def test_schedule_variants_bit_identical(tmp_path):
         out = os.path.join(tmp_path, "v%d.pt" % i)
         env = dict(os.environ, OUT=out, **extra)
         for k in ("DCUE_SIDE_THREAD", "DCUE_SCORE_FORK", "DCUE_PROLOGUE_FIRST", "DCUE_LATE_WAIT",
-                  "DCUE_AHEAD_AT", "DCUE_USER_FWD", "DCUE_W1_TAIL", "DCUE_FWD_TAIL", "DCUE_DGRAD_TAIL"):
+                  "DCUE_AHEAD_AT", "DCUE_USER_FWD"):
             if k not in extra:
                 env.pop(k, None)
         p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "schedule_worker.py")], env=env,
