@@ -630,7 +630,7 @@ int launch_bn0_grads_adam(const float* G, const float* E, const float* gamma0, c
 }
 
 int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* poff, hipStream_t s,
-                bool flush_slice, long dense_lo, long dense_hi) {
+                bool flush_slice, long dense_lo, long dense_hi, bool defer_dgrad2) {
   const AdamScalars sc = form_scalars(a);
   const float gdiv = a->grad_div > 1.0 ? (float)a->grad_div : 0.f;
   const int parts = a->parts ? a->parts : (DCUE_ADAM_DENSE | DCUE_ADAM_EMBEDDING);
@@ -638,8 +638,10 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
   if (parts & DCUE_ADAM_DENSE) {  // Adam + the conv-weight repack in one sweep
     const long len = n - dense_lo;
     const long blocks = len >= 512L * 1024 ? 512 : (len / 4 + 255) / 256 + 1;
+    PackArgs pa = pack_args(md, poff);
+    if (defer_dgrad2) pa.seg[1].bwd = pa.seg[1].f16b = -1;  // (the next forward of conv 2 writes them)
     DCUE_LAUNCH(k_adam_dense_pack, dim3((unsigned)blocks), dim3(256), 0, s, md->params, md->grads, md->exp_avg,
-                       md->exp_avg_sq, dense_lo, n, sc, pack_args(md, poff), md->wpack, gdiv);
+                       md->exp_avg_sq, dense_lo, n, sc, pa, md->wpack, gdiv);
     DCUE_LAUNCH_CHECK();
   }
   if ((parts & DCUE_ADAM_EMBEDDING) && md->emb_step) {
@@ -701,6 +703,8 @@ PackArgs pack_args(const dcue_model* md, const int64_t* poff) {
   if (!tower_text(&md->dims)) tx.cout = tx.cin = 0;  // empty: no element lies in it
   return pa;
 }
+
+PackSeg pack_seg(const dcue_model* md, const int64_t* poff, int l) { return pack_args(md, poff).seg[l - 1]; }
 
 int launch_pack(const dcue_model* md, const int64_t* poff, hipStream_t s) {
   const PackArgs pa = pack_args(md, poff);

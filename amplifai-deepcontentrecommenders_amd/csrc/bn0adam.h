@@ -26,40 +26,6 @@ DCUE_RHD float rn_sqrt(float a) { return __builtin_sqrtf(a); }
 
 namespace dcue {
 
-struct PackSeg {
-  long src, fwd, bwd, f16, f16b;  // floats: W in params; f32 forward pack (-1: none); dgrad pack (-1:
-                                 // none); split-f16 forward and dgrad packs
-  int cout, cin, ks;
-  int cinp;  // the split-f16 forward pack's K per tap: cin rounded up to 32 (the text conv's word width)
-};
-
-__device__ __forceinline__ void pack_store(const PackSeg& sg, long e, float w, float* wpack) {
-  const long ks = sg.ks;
-  const long o = e / ((long)sg.cin * ks);
-  const long rem = e - o * sg.cin * ks;
-  const long cc = rem / ks, k = rem - cc * ks;
-  if (sg.fwd >= 0) wpack[sg.fwd + (((k * (sg.cin / 4) + cc / 4) * sg.cout + o) * 4 + (cc & 3))] = w;
-  if (sg.bwd >= 0) {
-    const long kr = sg.ks - 1 - k;
-    wpack[sg.bwd + (((kr * (sg.cout / 4) + o / 4) * sg.cin + cc) * 4 + (o & 3))] = w;
-  }
-  // split-f16 forward operand: hi = fp16(w), lo = fp16(w - hi) (w - hi is exact in f32)
-  const _Float16 hi = (_Float16)w;
-  const _Float16 lo = (_Float16)(w - (float)hi);
-  _Float16* h16 = reinterpret_cast<_Float16*>(wpack + sg.f16);
-  const long q = k * (sg.cinp / 32) + cc / 32;
-  const long base = ((q * sg.cout + o) * 4 + (cc & 31) / 8) * 16 + (cc & 7);
-  h16[base] = hi;
-  h16[base + 8] = lo;
-  if (sg.f16b >= 0) {  // split-f16 dgrad operand: K = (reversed tap, o), columns cc
-    _Float16* b16 = reinterpret_cast<_Float16*>(wpack + sg.f16b);
-    const long qb = (sg.ks - 1 - k) * (sg.cout / 32) + o / 32;
-    const long bb = ((qb * sg.cin + cc) * 4 + (o & 31) / 8) * 16 + (o & 7);
-    b16[bb] = hi;
-    b16[bb + 8] = lo;
-  }
-}
-
 // bn0's gradients + Adam over segments [0, DCUE_SEG_LATE) in one launch (dcue_internal.h Bn0Adam):
 // the channel owning input channel c -- W1[:, c, :] (gradient, Adam, repack), bn0's gamma/beta[c] --
 // and channels 0 / 1 conv 1's bias and bn1's gamma/beta (whose gradients the conv-1 weight gradient

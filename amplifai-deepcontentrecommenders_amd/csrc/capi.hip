@@ -256,6 +256,11 @@ struct Ws {
   // features, then block 5) and the text features' gradient [M][C_s]
   float *xfc, *dtp;
   uint8_t* tidx;  // text tower: [M][C_s] the max-over-positions argmax (255: no gradient)
+  // text tower: the forward's position-part merge (TextBranch::ticket / part): tickets in the
+  // accumulator block's forward part (ntick 64-bit words, cleared with it), maxima [M][2][C_s]
+  unsigned* tticket;
+  unsigned long long* tpart;
+  long ntick;
   float* twpart;  // text tower: the text conv's weight-gradient chunk partials
 };
 
@@ -266,7 +271,8 @@ constexpr long kGrngWords = 7L * kRngC / 2 + 64;  // the gradient maxima's (+ pa
 void rebase_acc(Ws* w, unsigned long long* acc) {
   w->bnacc = acc;
   w->rng = reinterpret_cast<unsigned*>(acc + 6L * 2 * w->cmax * 2);
-  w->bnbacc = acc + 6L * 2 * w->cmax * 2 + kRngWords;
+  w->tticket = w->ntick ? reinterpret_cast<unsigned*>(acc + 6L * 2 * w->cmax * 2 + kRngWords) : nullptr;
+  w->bnbacc = acc + 6L * 2 * w->cmax * 2 + kRngWords + w->ntick;
   w->grng = reinterpret_cast<unsigned*>(w->bnbacc + 6L * 2 * w->cmax * 2);
 }
 
@@ -290,7 +296,9 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
     w->bcp[l] = ar.take<float>(C);
   }
   w->cmax = Cmax > D ? Cmax : D;
-  w->nfwd = 6L * 2 * w->cmax * 2 + kRngWords;
+  // text tower: one 32-bit ticket per (item, column block of >= 64 columns), in 16-B units
+  w->ntick = tower_text(d) ? ((long)M * (st_text(d) / 64) + 3) / 4 * 2 : 0;
+  w->nfwd = 6L * 2 * w->cmax * 2 + kRngWords + w->ntick;
   w->nzero = w->nfwd + 6L * 2 * w->cmax * 2 + kGrngWords;
   w->bnacc = ar.take<unsigned long long>(w->nzero);
   rebase_acc(w, w->bnacc);
@@ -342,6 +350,7 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
   w->dx1 = ar.take<float>((long)M * layer_geom(1).lp * H);
   w->ones = w->zeros = w->sink = w->xfc = w->dtp = w->twpart = nullptr;
   w->tidx = nullptr;
+  w->tpart = nullptr;
   if (!tower_has_bn(d)) {
     w->ones = ar.take<float>(w->cmax);
     w->zeros = ar.take<float>(w->cmax);
@@ -356,6 +365,7 @@ size_t carve(const dcue_dims* d, int B, int N, int M, void* base, Ws* w) {
     w->xfc = ar.take<float>((long)M * fc_in(d));
     w->dtp = ar.take<float>((long)M * CT);
     w->tidx = ar.take<uint8_t>((long)M * CT);
+    w->tpart = ar.take<unsigned long long>((long)M * 2 * CT);
     w->twpart = ar.take<float>((long)text_wgrad_nchunk(M) * (CT * d->word_dim * 3 + CT));
   }
   return ar.used + 256;
@@ -509,6 +519,12 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     a.out_range = rng_at(w, l);
     a.M = M;
     a.nout = l == 5 ? c.D : c.H;
+    if (l == 2 && train) {  // conv 2's input-gradient operands, left by the split plans' late Adam
+      a.rp = pack_seg(m, c.poff, 2);
+      a.rp.fwd = a.rp.f16 = -1;
+      a.rp_src = c.P(seg_conv_w(2));
+      a.rp_wpack = m->wpack;
+    }
     return a;
   };
   // the fc of the BN tower: f = bn5(y5) W^T + b   (truedcuemel1dbn.py:65,101)
@@ -545,7 +561,10 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     if (c.text) {
       TimerScope tsc;
       TRY(timer_begin(&tsc, DCUE_TIMED_TEXT_FWD, s));
-      TRY(launch_text_fwd(text_branch(c, t), item_track, M, w.xfc, c.FI, w.tidx, s));
+      TextBranch tb = text_branch(c, t);
+      tb.ticket = w.tticket;
+      tb.part = w.tpart;
+      TRY(launch_text_fwd(tb, item_track, M, w.xfc, c.FI, w.tidx, s));
       TRY(timer_end(&tsc));
     }
     TGemmArgs g = {};
@@ -1203,15 +1222,15 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
         TRY(wait_point(su, tail[2]));
         TRY(wait_point(su, tail[3]));
       }
-      // and the caller's stream up to its conv-1 tail: the dgrad of conv 2 (after the chain's last
-      // fork point) reads conv 2's packed weights, which this Adam rewrites
-      if (!legacy_orders()) TRY(wait_point(su, tail[0]));
+      // (the dgrad of conv 2 on the caller's stream may still run: this Adam leaves its packed
+      // operands to the next forward of conv 2 -- launch_adam defer_dgrad2; DCUE_LEGACY_ORDERS=1
+      // restores the round-4 order, the repack here and no wait: the race tests/test_gpu_races.py shows)
       // (recorded by the plan's prologue closure, posted before this one: FIFO on the side thread)
       if (inputs_via_late && o.wait_inputs) TRY(wait_point(su, o.wait_inputs));
       TRY(debug_delay(DCUE_SITE_LATE_ADAM, su));
       {
         ForkAfter fk(sp, su, o.late_done);
-        TRY(launch_adam(m, &dense, c.poff, su, true, late, -1));
+        TRY(launch_adam(m, &dense, c.poff, su, true, late, -1, !legacy_orders()));
         TRY(fk.done());
       }
       TRY(probe(PR_P_LATE, m->params + late, c.poff[kSeg] - late, su));

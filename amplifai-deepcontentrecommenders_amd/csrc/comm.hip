@@ -129,21 +129,15 @@ int comm_exchange_split(dcue_comm* c, const dcue_model* m, const dcue_adam_args*
   for (int i = 0; i < nside; ++i)
     if (side[i]) DCUE_HIP_CHECK(hipStreamWaitEvent(c->stream, side[i], 0));
   TRY(comm_allreduce_sum(c, m->grads + late, n - late));
-  // The late Adam rewrites conv 2's packed weights, which the caller's stream reads in its last
-  // input gradient (after the side streams forked off): it waits for the caller's stream first.
-  // The late bucket's all-reduce above still overlaps the conv-1 weight gradient.
-  const bool legacy = legacy_orders();
-  if (!legacy) {
-    DCUE_HIP_CHECK(hipEventRecord(c->ev_tail, s));
-    DCUE_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_tail, 0));
-  }
+  // The caller's stream may still run its last input gradient, the dgrad of conv 2, which reads conv
+  // 2's packed weights: the late Adam leaves those to the next forward of conv 2 (launch_adam
+  // defer_dgrad2), so it waits for nothing on `s` and overlaps the conv-1 weight gradient
+  // (DCUE_LEGACY_ORDERS=1: the round-4 order, the repack here)
   TRY(debug_delay(DCUE_SITE_LATE_ADAM, c->stream));
-  TRY(launch_adam(m, dense, poff, c->stream, true, late, n));  // the late segments' Adam, divide fused
+  TRY(launch_adam(m, dense, poff, c->stream, true, late, n, !legacy_orders()));  // the late segments' Adam, divide fused
   DCUE_HIP_CHECK(hipEventRecord(late_done, c->stream));
-  if (legacy) {
-    DCUE_HIP_CHECK(hipEventRecord(c->ev_tail, s));
-    DCUE_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_tail, 0));
-  }
+  DCUE_HIP_CHECK(hipEventRecord(c->ev_tail, s));
+  DCUE_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_tail, 0));
   TRY(comm_allreduce_sum(c, m->grads, late));
   DCUE_HIP_CHECK(hipEventRecord(c->ev_done, c->stream));
   DCUE_HIP_CHECK(hipStreamWaitEvent(s, c->ev_done, 0));

@@ -300,6 +300,12 @@ __device__ __forceinline__ void conv_rows_body(const RowsArgs& a, const int bx, 
   DCUE_KTW(KID, 6);
   DCUE_KT(KID, 0);
   const ChanPre cpre = chan_preload<SRC, F16>(a, KC);
+  if (MODE == 0 && a.rp_src) {  // conv 2's deferred input-gradient operands (RowsArgs::rp)
+    const long n = (long)a.rp.cout * a.rp.cin * a.rp.ks;
+    const long nt = (long)gridDim.x * gridDim.y * blockDim.x;
+    for (long e = ((long)by * gridDim.x + bx) * blockDim.x + threadIdx.x; e < n; e += nt)
+      pack_store(a.rp, e, a.rp_src[e], a.rp_wpack);
+  }
   constexpr int RX = R + KS - 1;
   constexpr int ROWS = TW * 16;
   constexpr int MAXI = (ROWS + R - 1) / R + 1;

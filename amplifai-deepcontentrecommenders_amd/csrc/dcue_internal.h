@@ -38,6 +38,43 @@ namespace dcue {
 // backward + ReLU mask + max-pool routing in dgrad).
 enum SlabSrc { SRC_TRACK_F16 = 0, SRC_TRACK_F32 = 1, SRC_ACT = 2, SRC_DZ = 3 };
 
+// One conv weight segment's packed copies (WpackLayout): W[o][c][k] at params + src; -1 = no such copy
+struct PackSeg {
+  long src, fwd, bwd, f16, f16b;  // floats: W in params; f32 forward pack (-1: none); dgrad pack (-1:
+                                 // none); split-f16 forward and dgrad packs
+  int cout, cin, ks;
+  int cinp;  // the split-f16 forward pack's K per tap: cin rounded up to 32 (the text conv's word width)
+};
+
+__device__ __forceinline__ void pack_store(const PackSeg& sg, long e, float w, float* wpack) {
+  const long ks = sg.ks;
+  const long o = e / ((long)sg.cin * ks);
+  const long rem = e - o * sg.cin * ks;
+  const long cc = rem / ks, k = rem - cc * ks;
+  if (sg.fwd >= 0) wpack[sg.fwd + (((k * (sg.cin / 4) + cc / 4) * sg.cout + o) * 4 + (cc & 3))] = w;
+  if (sg.bwd >= 0) {
+    const long kr = sg.ks - 1 - k;
+    wpack[sg.bwd + (((kr * (sg.cout / 4) + o / 4) * sg.cin + cc) * 4 + (o & 3))] = w;
+  }
+  // split-f16 forward operand: hi = fp16(w), lo = fp16(w - hi) (w - hi is exact in f32)
+  const _Float16 hi = (_Float16)w;
+  const _Float16 lo = (_Float16)(w - (float)hi);
+  if (sg.f16 >= 0) {
+    _Float16* h16 = reinterpret_cast<_Float16*>(wpack + sg.f16);
+    const long q = k * (sg.cinp / 32) + cc / 32;
+    const long base = ((q * sg.cout + o) * 4 + (cc & 31) / 8) * 16 + (cc & 7);
+    h16[base] = hi;
+    h16[base + 8] = lo;
+  }
+  if (sg.f16b >= 0) {  // split-f16 dgrad operand: K = (reversed tap, o), columns cc
+    _Float16* b16 = reinterpret_cast<_Float16*>(wpack + sg.f16b);
+    const long qb = (sg.ks - 1 - k) * (sg.cout / 32) + o / 32;
+    const long bb = ((qb * sg.cin + cc) * 4 + (o & 31) / 8) * 16 + (o & 7);
+    b16[bb] = hi;
+    b16[bb + 8] = lo;
+  }
+}
+
 struct RowsArgs {
   const void* src;            // tracks [n_tracks][131][128] | y_{l-1} [M][Lin][KC] | g_l [M][Lp_l][KC]
   const int32_t* item_track;  // tracks only
@@ -81,6 +118,13 @@ struct RowsArgs {
   unsigned* out_grange;  // dgrad: max |g_{l-1}| per channel (ordered keys), for the split-f16 wgrad
   const unsigned* y_range;  // dgrad: y_l's range (its maximum), for the dz bound
   float kd_max;             // dgrad: the largest copies(item) * invN of the batch
+  // forward, train, layer 2: conv 2's input-gradient operands (rp: bwd / f16b only) repacked from its
+  // weights rp_src, spread over the grid -- the split plans' late Adam leaves them to this launch, the
+  // first on the caller's stream after that Adam and before the next input gradient of conv 2
+  // (launch_adam defer_dgrad2); rp_src null: none
+  const float* rp_src;
+  float* rp_wpack;  // the model's wpack
+  PackSeg rp;
 };
 
 struct WgradArgs {
@@ -327,8 +371,13 @@ int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float s
 // flush_slice = false: the user-table part leaves this step's rolling-flush slice to the caller
 // (plans issue it during the next step, after that step's user tower: launch_emb_flush_rows)
 // dense_lo / dense_hi: the dense part over [dense_lo, dense_hi) of the flat buffer only (-1: to the end)
+// defer_dgrad2: leave conv 2's input-gradient operands (WpackLayout conv_bwd[2] / conv_f16b[2]) to
+// the next training forward of conv 2 (RowsArgs::rp): the split plans' late Adam, which may run
+// beside the caller stream's dgrad of conv 2 that reads them
 int launch_adam(const dcue_model* m, const dcue_adam_args* a, const int64_t* poff, hipStream_t s,
-                bool flush_slice = true, long dense_lo = 0, long dense_hi = -1);
+                bool flush_slice = true, long dense_lo = 0, long dense_hi = -1, bool defer_dgrad2 = false);
+// conv layer l's packed copies (adam.hip pack_args)
+PackSeg pack_seg(const dcue_model* m, const int64_t* poff, int l);
 int launch_emb_flush_rows(const dcue_model* m, int step, hipStream_t s);
 // deferred mode: launch_emb_grad + the user-table part of launch_adam (k_adam_touched) in one launch
 // (k_emb_grad_adam, adam.hip): the same compact rows and the same per-element Adam arithmetic; the
@@ -355,6 +404,11 @@ struct TextBranch {
   const float* wpack16;   // WpackLayout::text_f16
   const float* bias;      // [C]
   int T, E, EP, C, Creal, pad;
+  // the forward's position parts (text.hip k_text_fwd_full): per (item, column block) arrival
+  // tickets, zero before the launch (the workspace's accumulator block), and the parts' maxima
+  // [M][2][C]; null: one workgroup over all positions
+  unsigned* ticket = nullptr;
+  unsigned long long* part = nullptr;
 };
 // s[i][o] (o < Creal) -> out[i * ld + o] (the fc input's text columns), argmax -> tidx [M][C]
 int launch_text_fwd(const TextBranch& tb, const int32_t* item_track, int M, float* out, long ld, uint8_t* tidx,
@@ -397,8 +451,9 @@ void timer_add_recorded(int cls, hipEvent_t a, hipEvent_t b);
 // after the caller's stream `s`; `s` then waits for both
 int comm_exchange_step(dcue_comm* c, float* grad, long late, long n, hipEvent_t side_done, hipStream_t s);
 // the split plans' exchange (StepOpts::comm): the comm stream waits for the side streams' points
-// side[0..nside), all-reduces grad[late:n), runs Adam over it (dense, grad_div = world) and records
-// *late_done; then, after the caller's stream `s`, all-reduces grad[0:late), and `s` waits for it.
+// side[0..nside), all-reduces grad[late:n), runs Adam over it (dense, grad_div = world, conv 2's
+// input-gradient operands deferred) and records *late_done; then, after the caller's stream `s`,
+// all-reduces grad[0:late), and `s` waits for it.
 // The caller then runs Adam over [0, late) on `s`.
 int comm_exchange_split(dcue_comm* c, const dcue_model* m, const dcue_adam_args* dense, const int64_t* poff,
                         long late, long n, const hipEvent_t* side, int nside, hipEvent_t late_done, hipStream_t s);

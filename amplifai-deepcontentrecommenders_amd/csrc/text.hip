@@ -30,7 +30,11 @@
 //                  chunk's word-vector slices staged in LDS once, 3 x C/8 fp32 accumulators per thread,
 //                  exact fp32 FMAs in item order (deterministic).
 //   k_text_wreduce the chunk partials in chunk order, and db[o] = sum_i g[i][o] in item order.
+#include <cstring>
+
 #include "dcue_internal.h"
+
+DCUE_KTRACE_READER(text)  // diagnostic builds only (dcue_common.h): kernel 0 = k_text_fwd_full
 
 namespace dcue {
 
@@ -52,6 +56,9 @@ struct TextFwdArgs {
   float* out;                 // s[i][o] at out[i * ld + o], o < Creal
   long ld;
   uint8_t* tidx;              // [M][C]
+  int nxcd;                   // k_text_fwd_full: XCDs its work units run on (8 or 4)
+  unsigned* ticket;           // k_text_fwd_full with position parts: [M][column blocks], zero
+  unsigned long long* part;   // [M][parts][C]
 };
 
 // Split f32 -> (hi, lo) fp16 halves: hi = fp16(v), lo = fp16(v - hi) (v - hi is exact in f32).
@@ -196,68 +203,116 @@ __global__ __launch_bounds__(256) void k_text_fwd(TextFwdArgs a) {
 // before the MFMAs (k_text_fwd above refills one 32-channel chunk at a time, a dependent global
 // round trip per chunk, and its four 64-channel column blocks each re-gather the same vectors). The
 // column blocks of an item sit next to each other in XCD order, so the second reads the vectors from
-// the first's L2. The B operand is prefetched kTextBPD (chunk, tap) steps ahead. Per accumulator the
+// the first's L2. The B operand is prefetched 3 or 6 (chunk, tap) steps ahead, the A fragments one. Per accumulator the
 // MFMA sequence (chunk-major, then tap, then lo*hi, hi*lo, hi*hi) and the epilogue are k_text_fwd's:
 // bit-identical output (DCUE_TEXT_FWD=chunked runs the old kernel: A/B and tests/test_gpu_text.py).
-constexpr int kTextBPD = 6;
 __host__ __device__ constexpr int text_full_pitch(int EP) {  // halves per staged row: [chunk][hi 32, lo 32] + pad
   return 2 * EP + 2 * (((36 - EP % 64) % 64 + 64) % 64);  // row pitch = 36 (mod 64) dwords: conflict-free
 }
 
-template <int TB, int WV>
+template <int TB, int WV, int NCT, int BPD, int NCH, int SPL>
 __global__ __launch_bounds__(64 * WV) void k_text_fwd_full(TextFwdArgs a) {
-  constexpr int TP = TB * 16;  // conv positions computed (T rounded up)
-  constexpr int RS = TP + 2;   // staged rows: token positions -1 .. TP
+  constexpr int TP = TB * 16;  // conv positions computed by this workgroup (its part of T)
+  constexpr int RS = TP + 2;   // staged rows: token positions p0 - 1 .. p0 + TP
   constexpr int NT = 64 * WV;
   extern __shared__ __attribute__((aligned(16))) _Float16 xf[];  // [RS][pitch]
-  __shared__ int32_t tok[RS];
+  __shared__ int32_t tok[RS], tneed[RS];
+  __shared__ unsigned s_arrived;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int cb = a.C / (16 * WV);  // column blocks per item
-  const int L = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int i = L / cb;
-  const int o0 = (L - i * cb) * 16 * WV + wv * 16;
+  const int cb = a.C / (16 * WV * NCT);  // column blocks per item
+  // work unit L: item i, position part h (SPL parts of TP positions), column block cbk. The units run
+  // on a.nxcd of the 8 XCDs (blocks are dealt to XCDs round-robin: block b on XCD b % 8), each XCD a
+  // contiguous range of units, so the column blocks and parts of an item share an L2; blocks of the
+  // other XCDs exit at once. Every XCD that runs units reads the whole weight operand into its own
+  // L2 (not coherent across XCDs): 4 XCDs halve those fills for the same 128 CUs of work.
+  const int xb = blockIdx.x & 7;
+  if (xb >= a.nxcd) return;
+  const int nunit = a.M * cb * SPL, per = (nunit + a.nxcd - 1) / a.nxcd;
+  const int L = xb * per + (int)(blockIdx.x >> 3);
+  if (L >= nunit) return;
+  const int i = L / (cb * SPL);
+  const int h = (L - i * cb * SPL) / cb;
+  const int cbk = L - i * cb * SPL - h * cb;
+  const int p0 = h * TP;
+  const int o0 = cbk * 16 * WV * NCT + wv * 16 * NCT;  // the wave's NCT column tiles
   const int pitch = text_full_pitch(a.EP);
-  const int nchunk = a.EP / kTextKC;
+  // NCH > 0: the chunk count at compile time (the step loop unrolls whole: loop-carried prefetch
+  // registers would be waited for at the loop's latch)
+  const int nchunk = NCH > 0 ? NCH : a.EP / kTextKC;
+  DCUE_KTW(0, 6);
+  DCUE_KT(0, 0);
   const long trk = a.item_track[i];
   for (int r = tid; r < RS; r += NT) {
-    const int t = r - 1;
+    const int t = p0 + r - 1;
     tok[r] = (t >= 0 && t < a.T) ? a.tokens[trk * a.T + t] : -1;
   }
   __syncthreads();
-  // B operand of (chunk ch, tap k) for this lane's column: step q = ch * 3 + k, pack index k * nchunk + ch
-  const int col = o0 + (lane & 15), g = lane >> 4;
-  const int nq = 3 * nchunk;
-  auto bload = [&](int q, uint4& h, uint4& l) {
-    const int ch = q / 3, k = q - 3 * ch;
-    const uint4* wp = a.wpack + (((long)(k * nchunk + ch) * a.C + col) * 4 + g) * 2;
-    h = wp[0];
-    l = wp[1];
-  };
-  uint4 bh[kTextBPD], bl[kTextBPD];
+  // the rows the unmasked positions read: staged row r feeds the positions of rows r - 1 .. r + 1;
+  // a row no unmasked position reads (PAD beyond the sentence's end) stays zero and is never loaded
+  // -- masked positions' values are never used, and every PAD row is one hot line of the table
+  for (int r = tid; r < RS; r += NT) {
+    bool need = false;
 #pragma unroll
-  for (int q = 0; q < kTextBPD; ++q)
-    if (q < nq) bload(q, bh[q], bl[q]);
-  // the sentence: every row's EP channels, float4 slots gathered in batches of kB per thread
-  const int c4n = a.EP / 4, nslot = RS * c4n;
-  constexpr int kB = 8;
-  for (int base = tid; base < nslot; base += NT * kB) {
-    float4 v[kB];
-#pragma unroll
-    for (int j = 0; j < kB; ++j) {
-      const int e = base + NT * j;
-      v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (e < nslot) {
-        const int r = e / c4n, c = 4 * (e - r * c4n);
-        const int tk = tok[r];
-        if (tk >= 0 && c < a.E) v[j] = *reinterpret_cast<const float4*>(a.words + (long)tk * a.E + c);
-      }
+    for (int d = -1; d <= 1; ++d) {
+      const int x = r + d;
+      need |= x >= 1 && x <= TP && tok[x] >= 0 && tok[x] != a.pad;
     }
+    tneed[r] = need ? tok[r] : -1;
+  }
+  __syncthreads();
+  // B operand of (chunk ch, tap k) for this lane's columns: step q = ch * 3 + k, pack index k * nchunk + ch.
+  // Every load below is unconditional (indices clamped in range, unused results dropped): a load
+  // under a branch makes the compiler wait for every load in flight at the join.
+  const int col = o0 + (lane & 15), g = lane >> 4;
+  const int nq = 3 * nchunk;  // a multiple of BPD (launcher)
+  auto bload = [&](int q, uint4* h, uint4* l) {
+    const int ch = q / 3, k = q - 3 * ch;
+#pragma unroll
+    for (int n = 0; n < NCT; ++n) {
+      const uint4* wp = a.wpack + (((long)(k * nchunk + ch) * a.C + col + 16 * n) * 4 + g) * 2;
+      h[n] = wp[0];
+      l[n] = wp[1];
+    }
+  };
+  uint4 bh[BPD][NCT], bl[BPD][NCT];
+#pragma unroll
+  for (int q = 0; q < BPD; ++q) bload(q, bh[q], bl[q]);
+  DCUE_KT(0, 1);
+  float bo[NCT];  // (the epilogue's bias, loaded now: off its dependency chain)
+#pragma unroll
+  for (int n = 0; n < NCT; ++n) bo[n] = a.bias[col + 16 * n];
+  // The sentence: every row's word channels [32 c0, 32 c1), float4 slots gathered kB per thread per
+  // pass into v (loads unconditional: clamped addresses, invalid slots zeroed at the store), then split
+  // into the hi/lo halves in LDS.
+  constexpr int kB = 8;
+  struct Gather {
+    float4 v[kB];
+    unsigned ok;
+  };
+  auto gather_issue = [&](int c0, int c1, int base, Gather& G) {
+    const int qn = (c1 - c0) * (kTextKC / 4), n = RS * qn;
+    int tkj[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) tkj[j] = tneed[min((base + NT * j) / qn, RS - 1)];
+    __builtin_amdgcn_sched_barrier(0);  // (the token reads back to back, then the loads)
+    G.ok = 0;
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       const int e = base + NT * j;
-      if (e < nslot) {
-        const int r = e / c4n, c = 4 * (e - r * c4n);
-        float4 x = v[j];
+      const int c = 4 * (c0 * (kTextKC / 4) + e - (e / qn) * qn);
+      const bool valid = e < n && tkj[j] >= 0 && c < a.E;
+      G.ok |= (unsigned)valid << j;
+      G.v[j] = *reinterpret_cast<const float4*>(a.words + (valid ? (long)tkj[j] * a.E + c : 0L));
+    }
+  };
+  auto gather_store = [&](int c0, int c1, int base, const Gather& G) {
+    const int qn = (c1 - c0) * (kTextKC / 4), n = RS * qn;
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      const int e = base + NT * j;
+      if (e < n) {
+        const int r = e / qn, c = 4 * (c0 * (kTextKC / 4) + e - r * qn);
+        float4 x = (G.ok >> j) & 1u ? G.v[j] : make_float4(0.f, 0.f, 0.f, 0.f);
         x.x *= a.xscale; x.y *= a.xscale; x.z *= a.xscale; x.w *= a.xscale;  // exact (power of two)
         _Float16 hi[4], lo[4];
         split4(x, hi, lo);
@@ -266,63 +321,145 @@ __global__ __launch_bounds__(64 * WV) void k_text_fwd_full(TextFwdArgs a) {
         *reinterpret_cast<t16x4*>(row + kTextKC) = t16x4{lo[0], lo[1], lo[2], lo[3]};
       }
     }
+  };
+  f32x4 acc[NCT][TB];
+#pragma unroll
+  for (int n = 0; n < NCT; ++n)
+#pragma unroll
+    for (int b = 0; b < TB; ++b) acc[n][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // A fragments of step q (conv row t = 16b + (lane & 15) reads token t + k - 1 = staged row t + k),
+  // read one step ahead of their MFMAs
+  auto aload = [&](int q, t16x8* ah, t16x8* al) {
+    const int ch = q / 3, k = q - 3 * ch;
+#pragma unroll
+    for (int b = 0; b < TB; ++b) {
+      const _Float16* rp = xf + (long)(16 * b + (lane & 15) + k) * pitch + ch * 2 * kTextKC + 8 * g;
+      ah[b] = *reinterpret_cast<const t16x8*>(rp);
+      al[b] = *reinterpret_cast<const t16x8*>(rp + kTextKC);
+    }
+  };
+  t16x8 ah[TB], al[TB];
+  // step q: B from ring slot j (refilled for step q + BPD), A of step q + 1 read ahead unless `last`
+  auto step = [&](int q, int j, bool last) {
+    t16x8 wh[NCT], wl[NCT];
+#pragma unroll
+    for (int n = 0; n < NCT; ++n) {
+      wh[n] = *reinterpret_cast<const t16x8*>(&bh[j][n]);
+      wl[n] = *reinterpret_cast<const t16x8*>(&bl[j][n]);
+    }
+    bload(min(q + BPD, nq - 1), bh[j], bl[j]);
+    t16x8 nh[TB], nl[TB];
+    if (!last) aload(q + 1, nh, nl);
+    __builtin_amdgcn_sched_barrier(0);  // (the loads stay ahead of this step's MFMAs)
+#pragma unroll
+    for (int b = 0; b < TB; ++b)
+#pragma unroll
+      for (int n = 0; n < NCT; ++n) {
+        acc[n][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[b], wh[n], acc[n][b], 0, 0, 0);
+        acc[n][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], wl[n], acc[n][b], 0, 0, 0);
+        acc[n][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], wh[n], acc[n][b], 0, 0, 0);
+      }
+    if (!last) {
+#pragma unroll
+      for (int b = 0; b < TB; ++b) {
+        ah[b] = nh[b];
+        al[b] = nl[b];
+      }
+    }
+  };
+  for (int base = tid; base < RS * (a.EP / 4); base += NT * kB) {
+    Gather g0;
+    gather_issue(0, nchunk, base, g0);
+    gather_store(0, nchunk, base, g0);
   }
   __syncthreads();
-  f32x4 acc[TB];
+  DCUE_KT(0, 2);
+  aload(0, ah, al);
+  constexpr int kUnroll = NCH > 0 ? 3 * NCH / BPD : 1;
+#pragma unroll kUnroll
+  for (int q0 = 0; q0 < nq; q0 += BPD) {
 #pragma unroll
-  for (int b = 0; b < TB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int q0 = 0; q0 < nq; q0 += kTextBPD) {
+    for (int j = 0; j < BPD; ++j) step(q0 + j, j, q0 + j + 1 == nq);
+  }
+  DCUE_KT(0, 3);
+  // epilogue (k_text_fwd's): bias, masked first-max over the positions, ReLU
+  float best[NCT];
+  int bi[NCT];
 #pragma unroll
-    for (int j = 0; j < kTextBPD; ++j) {
-      const int q = q0 + j;
-      if (q < nq) {
-        const t16x8 wh = *reinterpret_cast<const t16x8*>(&bh[j]);
-        const t16x8 wl = *reinterpret_cast<const t16x8*>(&bl[j]);
-        if (q + kTextBPD < nq) bload(q + kTextBPD, bh[j], bl[j]);
-        const int ch = q / 3, k = q - 3 * ch;
+  for (int n = 0; n < NCT; ++n) {
+    best[n] = -INFINITY;
+    bi[n] = kTextNoGrad;
 #pragma unroll
-        for (int b = 0; b < TB; ++b) {
-          // conv row t = 16b + (lane & 15) reads token t + k - 1 = staged row t + k
-          const _Float16* rp = xf + (long)(16 * b + (lane & 15) + k) * pitch + ch * 2 * kTextKC + 8 * g;
-          const t16x8 ah = *reinterpret_cast<const t16x8*>(rp);
-          const t16x8 al = *reinterpret_cast<const t16x8*>(rp + kTextKC);
-          acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wh, acc[b], 0, 0, 0);
-          acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wl, acc[b], 0, 0, 0);
-          acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wh, acc[b], 0, 0, 0);
+    for (int b = 0; b < TB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 16 * b + 4 * g + j, t = p0 + r;
+        const int tk = tok[r + 1];
+        const float v = acc[n][b][j] * a.inv_xscale + bo[n];
+        if (t < a.T && tk >= 0 && tk != a.pad && v > best[n]) {
+          best[n] = v;
+          bi[n] = t;
+        }
+      }
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {  // the four row groups: larger value, earlier position on a tie
+      const float ob = __shfl_xor(best[n], off, 64);
+      const int oi = __shfl_xor(bi[n], off, 64);
+      if (ob > best[n] || (ob == best[n] && oi < bi[n])) {
+        best[n] = ob;
+        bi[n] = oi;
+      }
+    }
+  }
+  if constexpr (SPL > 1) {
+    // The parts' maxima meet in a.part [M][SPL][C] ((value bits << 32) | position); the last part of
+    // the (item, column block) to arrive (a.ticket, zero before the launch and left zero) merges them
+    // in position order -- the same first maximum as one pass over all positions. Every access is a
+    // device-coherent (agent-scope) atomic, performed past the XCD's L2, and the ticket is taken only
+    // once the stores are acknowledged: no L2 write-back or invalidate fence is needed.
+    if (g == 0) {
+#pragma unroll
+      for (int n = 0; n < NCT; ++n)
+        __hip_atomic_store(a.part + ((long)i * SPL + h) * a.C + col + 16 * n,
+                           ((unsigned long long)__float_as_uint(best[n]) << 32) | (unsigned)bi[n],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // (vmcnt 0: on gfx9 it counts the stores too)
+    __syncthreads();
+    if (tid == 0)
+      s_arrived = __hip_atomic_fetch_add(a.ticket + (long)i * cb + cbk, 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_arrived != SPL - 1) return;
+    if (tid == 0) __hip_atomic_store(a.ticket + (long)i * cb + cbk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int n = 0; n < NCT; ++n) {
+      best[n] = -INFINITY;
+      bi[n] = kTextNoGrad;
+#pragma unroll
+      for (int hh = 0; hh < SPL; ++hh) {
+        const unsigned long long pv = __hip_atomic_load(a.part + ((long)i * SPL + hh) * a.C + col + 16 * n,
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float v = __uint_as_float((unsigned)(pv >> 32));
+        const int t = (int)(unsigned)(pv & 0xffffffffu);
+        if (v > best[n]) {  // (parts in position order: a tie keeps the earlier)
+          best[n] = v;
+          bi[n] = t;
         }
       }
     }
   }
-  // epilogue (k_text_fwd's): bias, masked first-max over the positions, ReLU
-  const float bo = a.bias[col];
-  float best = -INFINITY;
-  int bi = kTextNoGrad;
-#pragma unroll
-  for (int b = 0; b < TB; ++b)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int t = 16 * b + 4 * g + j;
-      const int tk = tok[t + 1];
-      const float v = acc[b][j] * a.inv_xscale + bo;
-      if (t < a.T && tk >= 0 && tk != a.pad && v > best) {
-        best = v;
-        bi = t;
-      }
-    }
-#pragma unroll
-  for (int off = 16; off <= 32; off <<= 1) {
-    const float ob = __shfl_xor(best, off, 64);
-    const int oi = __shfl_xor(bi, off, 64);
-    if (ob > best || (ob == best && oi < bi)) {
-      best = ob;
-      bi = oi;
-    }
-  }
   if (g == 0) {
-    const bool on = best > 0.f;
-    if (col < a.Creal) a.out[(long)i * a.ld + col] = on ? best : 0.f;
-    a.tidx[(long)i * a.C + col] = (uint8_t)(on ? bi : kTextNoGrad);
+#pragma unroll
+    for (int n = 0; n < NCT; ++n) {
+      const int cn = col + 16 * n;
+      const bool on = best[n] > 0.f;
+      if (cn < a.Creal) a.out[(long)i * a.ld + cn] = on ? best[n] : 0.f;
+      a.tidx[(long)i * a.C + cn] = (uint8_t)(on ? bi[n] : kTextNoGrad);
+    }
   }
+  DCUE_KT(0, 4);
+  DCUE_KTW(0, 7);
 }
 
 // ------------------------------------------------------------------------------- weight gradient
@@ -438,17 +575,45 @@ int launch_text_fwd(const TextBranch& tb, const int32_t* item_track, int M, floa
   a.bias = tb.bias;
   a.M = M; a.T = tb.T; a.E = tb.E; a.EP = tb.EP; a.C = tb.C; a.Creal = tb.Creal; a.pad = tb.pad;
   a.out = out; a.ld = ld; a.tidx = tidx;
+  a.ticket = tb.ticket; a.part = tb.part;
   if (tb.C % 64 || tb.T < 1 || tb.T > 128 || tb.E % 4 || tb.EP % kTextKC || tb.EP < tb.E) return DCUE_ERR_INVALID;
-  // one item's staged sentence must fit the LDS (config 4: 66 rows x 1,424 B = 94 KB)
   static const bool chunked = [] {
     const char* e = getenv("DCUE_TEXT_FWD");
     return e && e[0] == 'c';
   }();
+  // A/B: DCUE_TEXT_FWD=<waves>x<column tiles per wave> (default 8x1), DCUE_TEXT_PARTS=2 (two
+  // workgroups per item and column block over halves of the positions, merged through tickets:
+  // measured no faster -- the merge's three device-coherent round trips cost what the halves save)
+  static const int shape = [] {
+    const char* e = getenv("DCUE_TEXT_FWD");
+    return e && e[0] >= '1' && e[0] <= '9' ? atoi(e) * 10 + (strchr(e, 'x') ? atoi(strchr(e, 'x') + 1) : 1) : 81;
+  }();
+  static const int parts_env = [] {
+    const char* e = getenv("DCUE_TEXT_PARTS");
+    return e ? atoi(e) : 1;
+  }();
+  static const int xcds_env = [] {
+    const char* e = getenv("DCUE_TEXT_XCDS");
+    return e ? atoi(e) : 4;
+  }();
+  static const int bpd_env = [] {  // (A/B: the config-4 kernel's weight-prefetch depth, 6 / 10 / 15 steps)
+    const char* e = getenv("DCUE_TEXT_BPD");
+    return e ? atoi(e) : 6;
+  }();
   const int tb_ = tb.T <= 16 ? 1 : tb.T <= 32 ? 2 : tb.T <= 64 ? 4 : 8;
-  const size_t lds = (size_t)(16 * tb_ + 2) * text_full_pitch(tb.EP) * sizeof(_Float16);
+  // position parts (DCUE_TEXT_PARTS=2): two workgroups per (item, column block), given the merge buffers
+  const int spl = parts_env == 2 && tb_ >= 2 && tb.ticket && tb.part ? 2 : 1;
+  const int tbw = tb_ / spl;  // 16-position tiles per workgroup
+  // the workgroup's staged rows must fit the LDS (config 4, two parts: 34 rows x 1,424 B = 48 KB)
+  const size_t lds = (size_t)(16 * tbw + 2) * text_full_pitch(tb.EP) * sizeof(_Float16);
   if (!chunked && lds <= 150 * 1024) {
-    const int wv = tb.C % 128 == 0 ? 8 : 4;
-    const unsigned grid = (unsigned)((long)M * (tb.C / (16 * wv)));
+    int wv = shape / 10, nct = shape % 10;
+    if (tb.C % (16 * wv * nct) || wv > 8) wv = tb.C % 128 == 0 ? 8 : 4, nct = 1;
+    // work units on 4 XCDs while they fill at most 4 x 32 CUs at one workgroup per CU (the weight
+    // operand's per-XCD L2 fills halve); DCUE_TEXT_XCDS=8 spreads them over all eight
+    const long nunit = (long)M * (tb.C / (16 * wv * nct)) * spl;
+    a.nxcd = xcds_env == 8 || nunit > 4 * 32 ? 8 : 4;
+    const unsigned grid = (unsigned)((nunit + a.nxcd - 1) / a.nxcd * 8);
     auto pick = [&](auto kern) -> int {
       static bool attr = false;  // (one per instantiation)
       if (!attr) {
@@ -459,16 +624,42 @@ int launch_text_fwd(const TextBranch& tb, const int32_t* item_track, int M, floa
       DCUE_LAUNCH_CHECK();
       return DCUE_OK;
     };
-    switch (tb_ * 16 + wv) {
-      case 16 + 4: return pick(k_text_fwd_full<1, 4>);
-      case 16 + 8: return pick(k_text_fwd_full<1, 8>);
-      case 32 + 4: return pick(k_text_fwd_full<2, 4>);
-      case 32 + 8: return pick(k_text_fwd_full<2, 8>);
-      case 64 + 4: return pick(k_text_fwd_full<4, 4>);
-      case 64 + 8: return pick(k_text_fwd_full<4, 8>);
-      case 128 + 4: return pick(k_text_fwd_full<8, 4>);
-      default: return pick(k_text_fwd_full<8, 8>);
-    }
+    // B steps in flight: a divisor of the 3 * nchunk steps (registers: 8 * NCT per step); the config-4
+    // word width (EP = 320: 10 chunks) at compile time
+    const bool b6 = nct == 1 && tbw <= 4 && (tb.EP / kTextKC) % 2 == 0;
+#define DCUE_TEXT_PICK_S(TBW, W, N, P, S)                                             \
+  if (tbw == TBW && spl == S) {                                                       \
+    if (P == 6 && tb.EP == 320) {                                                     \
+      if constexpr (TBW == 4 && W == 8 && N == 1 && S == 1) {                         \
+        if (bpd_env == 10) return pick(k_text_fwd_full<TBW, W, N, 10, 10, S>);        \
+        if (bpd_env == 15) return pick(k_text_fwd_full<TBW, W, N, 15, 10, S>);        \
+      }                                                                               \
+      return pick(k_text_fwd_full<TBW, W, N, P, 10, S>);                              \
+    }                                                                                 \
+    return pick(k_text_fwd_full<TBW, W, N, P, 0, S>);                                 \
+  }
+#define DCUE_TEXT_PICK_B(W, N, P)        \
+  DCUE_TEXT_PICK_S(1, W, N, P, 2)        \
+  DCUE_TEXT_PICK_S(2, W, N, P, 2)        \
+  DCUE_TEXT_PICK_S(4, W, N, P, 2)        \
+  DCUE_TEXT_PICK_S(1, W, N, P, 1)        \
+  DCUE_TEXT_PICK_S(2, W, N, P, 1)        \
+  DCUE_TEXT_PICK_S(4, W, N, P, 1)        \
+  DCUE_TEXT_PICK_S(8, W, N, P, 1)
+#define DCUE_TEXT_PICK(W, N)              \
+  if (wv == W && nct == N) {              \
+    if constexpr (N == 1)                 \
+      if (b6) { DCUE_TEXT_PICK_B(W, N, 6) } \
+    DCUE_TEXT_PICK_B(W, N, 3)             \
+  }
+    DCUE_TEXT_PICK(4, 1)
+    DCUE_TEXT_PICK(8, 1)
+    DCUE_TEXT_PICK(8, 2)
+    DCUE_TEXT_PICK(4, 2)
+#undef DCUE_TEXT_PICK
+#undef DCUE_TEXT_PICK_B
+#undef DCUE_TEXT_PICK_S
+    return DCUE_ERR_INVALID;
   }
   if (tb.T <= 16) return launch_text_fwd_t<1, 8>(a, s);
   if (tb.T <= 32) return launch_text_fwd_t<2, 4>(a, s);

@@ -190,9 +190,12 @@ def test_text_plan_inbatch_bench_shape():
 
 
 def test_text_fwd_kernels_bit_identical(tmp_path):
-    """The gather-once text forward (k_text_fwd_full, the default) and the chunked one
-    (DCUE_TEXT_FWD=chunked) run the same MFMA sequence per accumulator: five plan steps of the text
-    tower (tests/race_worker.py) give bit-identical losses, dense parameters and user table."""
+    """The gather-once text forward (k_text_fwd_full, the default), its two-position-part form
+    (DCUE_TEXT_PARTS=2: halves of the positions merged through tickets), a two-column-tile shape
+    (DCUE_TEXT_FWD=4x2), a deeper weight prefetch (DCUE_TEXT_BPD=15) and the chunked kernel
+    (DCUE_TEXT_FWD=chunked) run the same MFMA sequence per accumulator and the same first-maximum
+    rule: five plan steps of the text tower (tests/race_worker.py) give bit-identical losses, dense
+    parameters and user table."""
     import os
     import subprocess
     import sys
@@ -200,14 +203,17 @@ def test_text_fwd_kernels_bit_identical(tmp_path):
     code = ("import sys, torch; sys.path.insert(0, %r); import race_worker as W; r = W.run('text'); "
             "torch.save({k: r[k] for k in ('loss', 'P', 'emb')}, sys.argv[1])" % os.path.join(root, "tests"))
     res = []
-    for i, extra in enumerate(({}, {"DCUE_TEXT_FWD": "chunked"})):
+    for i, extra in enumerate(({}, {"DCUE_TEXT_FWD": "chunked"}, {"DCUE_TEXT_PARTS": "2"},
+                               {"DCUE_TEXT_FWD": "4x2"}, {"DCUE_TEXT_BPD": "15"})):
         out = str(tmp_path / ("t%d.pt" % i))
         env = dict(os.environ, **extra)
-        if not extra:
-            env.pop("DCUE_TEXT_FWD", None)
+        for k in ("DCUE_TEXT_FWD", "DCUE_TEXT_PARTS", "DCUE_TEXT_BPD"):
+            if k not in extra:
+                env.pop(k, None)
         p = subprocess.run([sys.executable, "-c", code, out], env=env, stdout=subprocess.PIPE,
                            stderr=subprocess.STDOUT, text=True, timeout=100)
         assert p.returncode == 0, p.stdout[-3000:]
         res.append(torch.load(out, weights_only=True))
-    for k in ("loss", "P", "emb"):
-        assert torch.equal(res[0][k], res[1][k]), k
+    for r in res[1:]:
+        for k in ("loss", "P", "emb"):
+            assert torch.equal(res[0][k], r[k]), k
