@@ -451,13 +451,31 @@ TextBranch text_branch(const Ctx& c, const dcue_tracks* t) {
   return tb;
 }
 
+// ... with the workspace's position-part merge buffers (k_text_fwd_full, DCUE_TEXT_PARTS=2)
+TextBranch text_branch_ws(const Ctx& c, const dcue_tracks* t, const Ws& w) {
+  TextBranch tb = text_branch(c, t);
+  tb.ticket = w.tticket;
+  tb.part = w.tpart;
+  return tb;
+}
+
+// DCUE_TEXT_SIDE=0: the training forward's text branch on the caller's stream after conv 5 instead
+// of on the user stream beside the audio convs (A/B)
+bool text_side_on() {
+  static const bool on = [] {
+    const char* e = getenv("DCUE_TEXT_SIDE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // Item tower forward. train: batch statistics (weighted by counts, accumulated exactly by the
 // producing kernels) + running-stat update by each BN's first consumer; eval: running statistics.
 int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t* item_track, int M,
                  double copies, bool train, const float* counts, float* f_out, hipStream_t s,
                  bool acc_cleared = false, bool stats_done = false, bool clear_bn0 = false,
                  hipEvent_t before_l2 = nullptr, const std::function<int()>* after_l1 = nullptr,
-                 dcue_comm* sync_bn = nullptr) {
+                 dcue_comm* sync_bn = nullptr, const std::function<int()>* text_join = nullptr) {
   const dcue_model* m = c.m;
   if (c.text && !t->tokens) return DCUE_ERR_INVALID;
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
@@ -558,13 +576,12 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
                         c.bn ? c.P(seg_bn_b(3)) : nullptr, c.bn ? c.P(seg_bn_b(4)) : nullptr,
                         c.bn ? c.P(seg_bn_b(5)) : nullptr, bn_of(5), M, c.H, c.res ? c.HL : 0, c.D, c.off5,
                         c.FI, w.xfc, s));
-    if (c.text) {
+    if (c.text && text_join) {  // the text branch ran on a side stream (forward_impl): join it
+      TRY((*text_join)());
+    } else if (c.text) {
       TimerScope tsc;
       TRY(timer_begin(&tsc, DCUE_TIMED_TEXT_FWD, s));
-      TextBranch tb = text_branch(c, t);
-      tb.ticket = w.tticket;
-      tb.part = w.tpart;
-      TRY(launch_text_fwd(tb, item_track, M, w.xfc, c.FI, w.tidx, s));
+      TRY(launch_text_fwd(text_branch_ws(c, t, w), item_track, M, w.xfc, c.FI, w.tidx, s));
       TRY(timer_end(&tsc));
     }
     TGemmArgs g = {};
@@ -811,20 +828,21 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   HPROF("capi:3");
   if (!o.prologue_done) TRY(batch_counts(b, w, s));
   HPROF("capi:4");
-  hipEvent_t ev_uf = nullptr;
-  // the user tower on su: emb rows brought up to date, then the two GEMMs (+ the rolling flush slice)
+  hipEvent_t ev_uf = nullptr, ev_tx = nullptr;
+  const bool text_side = c.text && text_side_on();
+  // the user tower on su: emb rows brought up to date, then the two GEMMs (+ the text branch, the
+  // rolling flush slice)
   const std::function<int()> user_part = [&]() -> int {
     TRY(wait_point(su, ev_in));
     HPROF("capi:5");
     TRY(debug_delay(DCUE_SITE_USER_FWD, su));
-    // The rows' sync (k_emb_sync, one workgroup per row) and the two GEMMs (k_tgemm, 16 x 64
-    // blocks) as three launches. DCUE_USER_FWD=fused issues them as one (k_user_fwd) instead: off by
-    // default -- in 7 of 32 runs of the schedule test (tests/test_gpu_schedule.py) a fused-path
-    // process went non-finite from its second step on (loss = N x margin), never the split path;
-    // the cause is not found yet
+    // The rows' sync and the two GEMMs in one launch (k_user_fwd); DCUE_USER_FWD=split issues them
+    // as three (k_emb_sync, one workgroup per row, then two k_tgemm) -- A/B and the schedule test.
+    // (Round 4 made the fused form opt-in after non-finite runs; their cause was the plan's
+    // cross-stream races, DESIGN.md §4.7 round 5, tests/test_gpu_races.py.)
     static const bool split_fwd = [] {
       const char* e = getenv("DCUE_USER_FWD");
-      return !(e && e[0] == 'f');
+      return e && e[0] == 's';
     }();
     {
       ForkAfter fk(sp, su, &ev_uf);
@@ -840,6 +858,21 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
     }
     TRY(probe(PR_H1, w.h1, (long)b->n_rows * c.E, su));
     TRY(probe(PR_UF, w.uf, (long)b->n_rows * c.D, su));
+    if (text_side) {  // the text branch: the item tower's fc input columns [0, C_s), beside its convs
+      // (its weights: the previous step's late Adam -- on this stream, or on the exchange's)
+      if (o.comm && o.wait_late) TRY(wait_point(su, o.wait_late));
+      TimerScope tsc;
+      TRY(timer_begin(&tsc, DCUE_TIMED_TEXT_FWD, su));
+      if (tsc.b && !tsc.capturing) {  // a timed launch: the timer's stop event is its end
+        TRY(launch_text_fwd(text_branch_ws(c, t, w), b->item_track, b->n_items, w.xfc, c.FI, w.tidx, su));
+        ev_tx = tsc.b;
+      } else {
+        ForkAfter fk(sp, su, &ev_tx);
+        TRY(launch_text_fwd(text_branch_ws(c, t, w), b->item_track, b->n_items, w.xfc, c.FI, w.tidx, su));
+        TRY(fk.done());
+      }
+      TRY(timer_end(&tsc));
+    }
     if (o.flush_slice_step >= 0 && m->emb_step) TRY(launch_emb_flush_rows(m, o.flush_slice_step, su));
     return DCUE_OK;
   };
@@ -856,11 +889,20 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   // (under an exchange the late Adam follows the all-reduce: it keeps its wait before conv 2)
   const bool late_first = o.wait_late && late_wait_at_conv1() && !o.comm;
   if (late_first) TRY(wait_point(s, o.wait_late));
+  // the fc waits for the text branch: its launch issued (the side thread's part done), then its end
+  const std::function<int()> text_join = [&]() -> int {
+    if (!early && !side.threaded()) TRY(user_part());
+    TRY(side.wait(useq));
+    return wait_point(s, ev_tx);
+  };
+  bool user_done = false;
+  if (text_side) user_done = !early || side.threaded();  // (text_join issues the user part)
   TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s,
                    o.prologue_done, o.input_stats_done && o.prologue_done, o.clear_bn0,
                    late_first ? nullptr : o.wait_late,
-                   early && !side.threaded() ? &user_part : nullptr, o.sync_bn));
-  if (!early && !side.threaded()) TRY(user_part());
+                   early && !side.threaded() ? &user_part : nullptr, o.sync_bn,
+                   text_side ? &text_join : nullptr));
+  if (!early && !side.threaded() && !user_done) TRY(user_part());
   TRY(side.wait(useq));
   TRY(wait_point(s, ev_uf));
   HPROF("capi:9");

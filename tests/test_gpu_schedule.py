@@ -23,11 +23,11 @@ VARIANTS = [
     {"DCUE_PROLOGUE_FIRST": "1"},
     {"DCUE_LATE_WAIT": "conv1"},
     {"DCUE_AHEAD_AT": "fork"},
-    {"DCUE_USER_FWD": "fused"},
-    {"DCUE_USER_FWD": "fused", "DCUE_SIDE_THREAD": "0"},
+    {"DCUE_USER_FWD": "split"},
+    {"DCUE_USER_FWD": "split", "DCUE_SIDE_THREAD": "0"},
 ]
-# (the fused user tower's round-4 non-finite runs were the plan's cross-stream races, not the kernel:
-# DESIGN.md §4.7 round 5, tests/test_gpu_races.py)
+# (the fused user tower, the default since round 5: its round-4 non-finite runs were the plan's
+# cross-stream races, not the kernel -- DESIGN.md §4.7 round 5, tests/test_gpu_races.py)
 
 
 def test_schedule_variants_bit_identical(tmp_path):
