@@ -128,7 +128,8 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve(float* __restrict__ X, lo
                                                     int dim, const wacc_t* __restrict__ G,
                                                     const int64_t* __restrict__ indptr,
                                                     const int32_t* __restrict__ indices,
-                                                    const float* __restrict__ values, float alpha, float lambda) {
+                                                    const float* __restrict__ values, float alpha, float lambda,
+                                                    int phases) {
   extern __shared__ __attribute__((aligned(16))) wacc_t wl[];
   wacc_t* Ls = wl;                                          // packed lower triangle, rows 0..D16
   wacc_t* dg = Ls + kWrmfTri;                               // 1 / L[k][k]
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve(float* __restrict__ X, lo
       for (int i = 0; i < 8; ++i) acc[i][i] += r0 + i < dim ? (wacc_t)lambda : 1.0;
     }
     // the row's observed factors: A += (c - 1) f f^T, b += c f, kWrmfStage at a time
-    for (long pb = p0; pb < p1; pb += kWrmfStage) {
+    for (long pb = p0; pb < ((phases & 1) ? p1 : p0); pb += kWrmfStage) {
       const int ns = (int)min((long)kWrmfStage, p1 - pb);
       for (int e = t; e < ns * D16; e += blockDim.x) {
         const int s = e / D16, c = e - s * D16;
@@ -235,11 +236,11 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve(float* __restrict__ X, lo
     };
     const bool diag_tile = !aug && (TI >> 1) == (TJ >> 1);  // inside a 16 x 16 diagonal block
     if (has_tile && TJ < 2 && diag_tile) store_tile();
-    for (int k0 = 0; k0 < D16; k0 += 16) {
+    for (int k0 = 0; k0 < ((phases & 2) ? D16 : 0); k0 += 16) {
       const int kt = k0 >> 3;  // tile column of the step's first 8 columns
       asm volatile("" : "+v"(r0), "+v"(c0));
       __syncthreads();
-      if (t < 64) {
+      if (t < 64 && (phases & 8)) {
         // the 16 x 16 diagonal block, factored in wave 0's lanes 0-15 (lane i holds row i)
         int i = lane;
         asm volatile("" : "+v"(i));  // lane predicates are formed here, not hoisted out of the k0 loop
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve(float* __restrict__ X, lo
       }
       __syncthreads();
       // the panel below the block, in its owners' registers: first tile column (columns k0..k0+7)
-      const bool below = has_tile && TI >= kt + 2;
+      const bool below = has_tile && TI >= kt + 2 && (phases & 16);
       if (below && TJ == kt) {
         solve_cols();
         store_tile();
@@ -299,7 +300,7 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve(float* __restrict__ X, lo
       }
       __syncthreads();
       // trailing tiles: acc -= L[rows][k0:k0+16] L[cols][k0:k0+16]^T; then the next diagonal block's tiles
-      if (has_tile && c0 >= k0 + 16) {
+      if (has_tile && c0 >= k0 + 16 && (phases & 32)) {
 #pragma unroll 1
         for (int q = 0; q < 16; ++q) {
           wacc_t fc[8];
@@ -318,7 +319,7 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve(float* __restrict__ X, lo
     }
     __syncthreads();
     // L^T x = y (y: the augmented row), wave 0; eight rows of L loaded ahead of each chain
-    if (t < 64) {
+    if (t < 64 && (phases & 4)) {
       const wacc_t* y = Ls + woff(RA);
       wacc_t xlo = lane < D16 ? y[lane] : 0.0, xhi = lane + 64 < D16 ? y[lane + 64] : 0.0;
       for (int kb = D16 - 8; kb >= 0; kb -= 8) {
@@ -348,6 +349,312 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve(float* __restrict__ X, lo
     }
     __syncthreads();  // Ls and dg are rewritten by the next row
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_wrmf_solve_mfma: the same per-row system on fp64 MFMA (v_mfma_f64_16x16x4_f64), D16 = 16 NB.
+// One workgroup per row (grid-stride), 4 waves, two workgroups per CU. The augmented matrix
+// [[A, b], [b^T, *]] is held as 16 x 16 tiles (I, J), J <= I, of the lower block triangle plus the
+// augmented block row I = NB (only its row 0, b^T, is real): tile number
+// tau(I, J) = J (NB + 1) - J (J - 1) / 2 + (I - J), owned by wave tau % 4 in its register slot tau / 4
+// (C/D layout of the f64 MFMA: lane l holds column l & 15, rows (l >> 4) + 4 r, r = 0..3).
+//   * accumulation: A_IJ += sum_s (c_s - 1) f_s[16 I + i] f_s[16 J + j], b += c_s f_s, as MFMAs of
+//     K = 4 staged factors (A operand lane l: row l & 15, factor l >> 4);
+//   * right-looking block Cholesky, per block column kb: wave 0 factors the diagonal tile (lanes
+//     hold rows, v_readlane broadcasts) and inverts the factor (lane j: column j of L_kk^{-1}); the
+//     panel L_Ikb = A_Ikb L_kk^{-T} and the trailing updates A_IJ -= L_Ikb L_Jkb^T are MFMAs with
+//     operands read from LDS (the off-diagonal factor tiles stay there for the back substitution);
+//     the augmented row's panel is y_kb = (L^{-1} b)_kb;
+//   * L^T x = y block by block in wave 0 (four lanes per row, a shuffle reduction).
+// LDS: off-diagonal factor tiles (I > J, I < NB) 16 x 16 each, column-major (an MFMA operand's
+// 16 rows are 16 consecutive doubles: conflict-free), the inverses of the diagonal factors packed
+// lower column-major (136 doubles each; the diagonal tile itself is factored there packed
+// row-major first), y, x, the 1 / L[k][k] of the current block, and the staged factors (fp32) with
+// their weights.
+typedef double wf64x4 __attribute__((ext_vector_type(4)));
+template <int NB>
+constexpr int wm_ntiles() { return NB * (NB + 1) / 2 + NB; }
+__host__ __device__ constexpr int wm_lt_doubles(int NB) { return (NB * (NB - 1) / 2) * 256; }
+template <int NB>
+__device__ __forceinline__ int wm_lt(int I, int J) { return (I * (I - 1) / 2 + J) * 256; }  // I > J, I < NB
+__device__ __forceinline__ int wm_pk(int i, int j) { return i * (i + 1) / 2 + j; }          // j <= i < 16
+// packed lower triangle, column-major: column k holds rows k..15 contiguously (lane-contiguous reads)
+__device__ __forceinline__ int wm_ck(int i, int k) { return 16 * k - k * (k - 1) / 2 + (i - k); }  // k <= i
+
+template <int NB>
+size_t wm_lds_bytes() {
+  return sizeof(double) * ((size_t)wm_lt_doubles(NB) + 136 * NB + 16 * NB + 16 * NB + 16 + 16) +
+         sizeof(float) * ((size_t)kWrmfStage * 16 * NB + 2 * kWrmfStage);
+}
+
+template <int NB>
+__global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ X, long n_rows,
+                                                         const float* __restrict__ F, int dim,
+                                                         const wacc_t* __restrict__ G,
+                                                         const int64_t* __restrict__ indptr,
+                                                         const int32_t* __restrict__ indices,
+                                                         const float* __restrict__ values, float alpha,
+                                                         float lambda, int phases) {
+  constexpr int D16 = 16 * NB, NT = wm_ntiles<NB>(), NS = (NT + 3) / 4;
+  extern __shared__ __attribute__((aligned(16))) double wsm[];
+  double* Lt = wsm;                               // off-diagonal factor tiles [i][j]
+  double* Li = Lt + wm_lt_doubles(NB);            // diagonal factor inverses, packed lower
+  double* ys = Li + 136 * NB;                     // y = L^{-1} b
+  double* xs = ys + 16 * NB;                      // x
+  double* rs = xs + 16 * NB;                      // back substitution: the block's right-hand side
+  double* dgs = rs + 16;                          // 1 / L[k][k] of the block being inverted
+  float* st = reinterpret_cast<float*>(dgs + 16);  // [kWrmfStage][D16] staged factors
+  float* ws = st + kWrmfStage * D16;               // c_s - 1
+  float* cs = ws + kWrmfStage;                     // c_s
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);  // (uniform: tile coordinates in SGPRs)
+  const int li = lane & 15, lk = lane >> 4;
+  // this wave's tiles
+  int TI[NS], TJ[NS];
+#pragma unroll
+  for (int sl = 0; sl < NS; ++sl) {
+    const int tau = 4 * sl + wave;
+    int I = -1, J = -1, base = 0;
+    for (int j = 0; j < NB; ++j) {
+      const int cnt = NB - j + 1;
+      if (tau >= base && tau < base + cnt) {
+        J = j;
+        I = j + (tau - base);
+      }
+      base += cnt;
+    }
+    TI[sl] = tau < NT ? I : -1;
+    TJ[sl] = tau < NT ? J : -1;
+  }
+  for (long r = blockIdx.x; r < n_rows; r += gridDim.x) {
+    const long p0 = indptr[r], p1 = indptr[r + 1];
+    if (p1 <= p0) {  // no observed pair: b = 0, so x = 0
+      for (int c = t; c < dim; c += blockDim.x) X[r * dim + c] = 0.f;
+      continue;
+    }
+    // A = G + lambda I (identity on the padding); the augmented row b = 0
+    wf64x4 acc[NS];
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl) {
+      const int I = TI[sl], J = TJ[sl];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = lk + 4 * q;
+        double v = 0.0;
+        if (I >= 0 && I < NB) {
+          v = G[(size_t)(16 * I + i) * D16 + 16 * J + li];
+          if (I == J && i == li) v += 16 * I + i < dim ? (double)lambda : 1.0;
+        }
+        acc[sl][q] = v;
+      }
+    }
+    // the row's observed factors, kWrmfStage at a time: K = 4 factors per MFMA
+#pragma unroll 1
+    for (long pb = p0; pb < ((phases & 1) ? p1 : p0); pb += kWrmfStage) {
+      const int ns = (int)min((long)kWrmfStage, p1 - pb);
+      __syncthreads();  // (the previous pass's reads)
+      for (int e = t; e < kWrmfStage * D16; e += blockDim.x) {
+        const int sf = e / D16, c = e - sf * D16;
+        st[e] = sf < ns && c < dim ? F[(long)indices[pb + sf] * dim + c] : 0.f;
+      }
+      if (t < kWrmfStage) {
+        const float w = t < ns ? alpha * (values ? values[pb + t] : 1.f) : 0.f;
+        ws[t] = w;
+        cs[t] = t < ns ? 1.f + w : 0.f;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < kWrmfStage / 4; ++kk) {
+        const int sf = 4 * kk + lk;
+        const double w = (double)ws[sf], c = (double)cs[sf];
+#pragma unroll
+        for (int sl = 0; sl < NS; ++sl) {
+          const int I = TI[sl], J = TJ[sl];
+          if (I < 0) continue;
+          const double a = I == NB ? (li == 0 ? c : 0.0) : w * (double)st[sf * D16 + 16 * I + li];
+          const double b = (double)st[sf * D16 + 16 * J + li];
+          acc[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[sl], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);  // (operand loads stay next to their MFMA: register budget)
+        }
+      }
+    }
+    // block Cholesky
+#pragma unroll 1
+    for (int kb = 0; kb < NB; ++kb) {
+      // tile coordinates opaque per step: their address arithmetic is redone here instead of being
+      // hoisted out of the step loop into live registers
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl) asm volatile("" : "+s"(TI[sl]), "+s"(TJ[sl]));
+      __syncthreads();  // (the previous block's trailing reads of Lt; the first: the staging reads)
+      // (a) the diagonal tile to Li[kb] (packed lower)
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl)
+        if (TI[sl] == kb && TJ[sl] == kb) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int i = lk + 4 * q;
+            if (li <= i) Li[136 * kb + wm_pk(i, li)] = acc[sl][q];
+          }
+        }
+      __syncthreads();
+      // (b) wave 0: factor it (lane i holds row i), then invert the factor (lane j: column j)
+      if (wave == 0 && (phases & 8)) {
+        double* Lk = Li + 136 * kb;
+        // 64 lanes: lane (i, g) = (lane & 15, lane >> 4) holds row i, columns 4g .. 4g + 3; column k
+        // of L goes through LDS (rs) to every lane after its scaling
+        const int i = lane & 15, g = lane >> 4;
+        double a4[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a4[c] = 4 * g + c <= i ? Lk[wm_pk(i, 4 * g + c)] : 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int gk = k >> 2, ck = k & 3;
+          const double pk = readlane_d(a4[ck], k + 16 * gk);
+          const double inv = rsqrt_d(pk);
+          if (g == gk) {
+            if (i == k) a4[ck] = pk * inv;
+            else if (i > k) a4[ck] *= inv;
+            if (i >= k) rs[i] = a4[ck];
+          }
+          if (lane == 0) dgs[k] = inv;
+          const double lik = rs[i];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int j = 4 * g + c;
+            if (j > k && i >= j) a4[c] = fma(-lik, rs[j], a4[c]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (4 * g + c <= i) Lk[wm_pk(i, 4 * g + c)] = a4[c];
+        // (LDS accesses of one wave are in order: the reads below see the stores above)
+        const int jc = (phases & 64) ? lane : 99;  // column of L^{-1}
+        double xv[16];
+#pragma unroll
+        for (int ii = 0; ii < 16; ++ii) {
+          double sum = 0.0;
+#pragma unroll
+          for (int m = 0; m < ii; ++m)
+            if (m >= jc) sum = fma(Lk[wm_pk(ii, m)], xv[m], sum);
+          const double d = dgs[ii];
+          xv[ii] = ii < jc ? 0.0 : ii == jc ? d : -sum * d;
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (jc < 16) {  // (over the factor: packed column-major, L^{-1}[ii][jc] at wm_ck(ii, jc))
+#pragma unroll
+          for (int ii = 0; ii < 16; ++ii)
+            if (ii >= jc) Lk[wm_ck(ii, jc)] = xv[ii];
+        }
+      }
+      __syncthreads();
+      // (c) panel: L_Ikb = A_Ikb L_kk^{-T}; A_Ikb through LDS (its tile slot / ys) into the A layout
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl) {
+        const int I = TI[sl];
+        if (TJ[sl] != kb || I <= kb) continue;
+        if (I < NB) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) Lt[wm_lt<NB>(I, kb) + li * 16 + lk + 4 * q] = acc[sl][q];
+        } else if (lk == 0) {
+          ys[16 * kb + li] = acc[sl][0];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl) {
+        const int I = TI[sl];
+        if (TJ[sl] != kb || I <= kb || !(phases & 16)) continue;
+        wf64x4 d = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int k = 4 * kk + lk;
+          const double a = I < NB ? Lt[wm_lt<NB>(I, kb) + k * 16 + li] : (li == 0 ? ys[16 * kb + k] : 0.0);
+          const double b = k <= li ? Li[136 * kb + wm_ck(li, k)] : 0.0;  // L^{-T}[k][j] = L^{-1}[j][k]
+          d = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, d, 0, 0, 0);
+        }
+        acc[sl] = d;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __syncthreads();  // (every panel operand read before it is overwritten)
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl) {
+        const int I = TI[sl];
+        if (TJ[sl] != kb || I <= kb) continue;
+        if (I < NB) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) Lt[wm_lt<NB>(I, kb) + li * 16 + lk + 4 * q] = acc[sl][q];
+        } else if (lk == 0) {
+          ys[16 * kb + li] = acc[sl][0];
+        }
+      }
+      __syncthreads();
+      // (d) trailing: A_IJ -= L_Ikb L_Jkb^T for kb < J <= I
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl) {
+        const int I = TI[sl], J = TJ[sl];
+        if (J <= kb || I < 0 || !(phases & 32)) continue;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int k = 4 * kk + lk;
+          const double a = I < NB ? Lt[wm_lt<NB>(I, kb) + k * 16 + li] : (li == 0 ? ys[16 * kb + k] : 0.0);
+          const double b = Lt[wm_lt<NB>(J, kb) + k * 16 + li];  // L_Jkb^T[k][j] = L_Jkb[j][k]
+          acc[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(-a, b, acc[sl], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __syncthreads();
+    // L^T x = y, block rows NB-1 .. 0, wave 0: lane (m, q) = (lane & 15, lane >> 4) sums a quarter
+    // of each dot product, the quarters meet by shuffles
+    if (wave == 0 && (phases & 4)) {
+#pragma unroll 1
+      for (int I = NB - 1; I >= 0; --I) {
+        // r_I[m] = y_I[m] - sum_{J > I} sum_n L_JI[n][m] x_J[n]
+        double part = 0.0;
+#pragma unroll 1
+        for (int J = I + 1; J < NB; ++J) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int n = 4 * lk + u;
+            part = fma(Lt[wm_lt<NB>(J, I) + li * 16 + n], xs[16 * J + n], part);
+          }
+        }
+        part += __shfl_xor(part, 16, 64);
+        part += __shfl_xor(part, 32, 64);
+        if (lane < 16) rs[li] = ys[16 * I + li] - part;
+        // x_I[i] = sum_{m >= i} L_II^{-1}[m][i] r[m]
+        double xp = 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int m = 4 * lk + u;
+          if (m >= li) xp = fma(Li[136 * I + wm_ck(m, li)], rs[m], xp);
+        }
+        xp += __shfl_xor(xp, 16, 64);
+        xp += __shfl_xor(xp, 32, 64);
+        if (lane < 16) xs[16 * I + li] = xp;
+      }
+      for (int c = lane; c < dim; c += 64) X[r * dim + c] = (float)xs[c];
+    }
+  }
+}
+
+template <int NB>
+static int launch_wrmf_mfma(float* solve, long n_rows, const float* fixed, int dim, const wacc_t* G,
+                            const int64_t* indptr, const int32_t* indices, const float* values, float alpha,
+                            float lambda, hipStream_t s) {
+  static const int phases = [] {  // (DCUE_WRMF_PHASES: see dcue_wrmf_half_step; + 64: the inverse)
+    const char* e = getenv("DCUE_WRMF_PHASES");
+    return e ? atoi(e) : 127;
+  }();
+  const size_t lds = wm_lds_bytes<NB>();
+  DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_wrmf_solve_mfma<NB>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const long grid = n_rows < 4096 ? n_rows : 4096;
+  DCUE_LAUNCH(k_wrmf_solve_mfma<NB>, dim3((unsigned)grid), dim3(256), lds, s, solve, n_rows, fixed, dim, G, indptr,
+              indices, values, alpha, lambda, phases);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
 }
 
 size_t wrmf_solve_lds_bytes() {
@@ -396,8 +703,34 @@ int dcue_wrmf_half_step(float* solve, int64_t n_rows, const float* fixed, int64_
   DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_wrmf_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds));
   const long grid = n_rows < 4096 ? n_rows : 4096;  // grid-stride over rows
+  // the register-tile solve (k_wrmf_solve) by default; DCUE_WRMF_SOLVE=mfma: the fp64-MFMA block
+  // Cholesky (k_wrmf_solve_mfma), measured 96-98 ms per ALS iteration against 90 at the bench's
+  // shape -- both are bound by the diagonal blocks' serial factorization
+  static const bool tile_solve = [] {
+    const char* e = getenv("DCUE_WRMF_SOLVE");
+    return !(e && e[0] == 'm');
+  }();
+  if (!tile_solve) {
+    switch ((dim + 15) / 16) {
+      case 1: return launch_wrmf_mfma<1>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
+      case 2: return launch_wrmf_mfma<2>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
+      case 3: return launch_wrmf_mfma<3>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
+      case 4: return launch_wrmf_mfma<4>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
+      case 5: return launch_wrmf_mfma<5>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
+      case 6: return launch_wrmf_mfma<6>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
+      case 7: return launch_wrmf_mfma<7>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
+      default: return launch_wrmf_mfma<8>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
+    }
+  }
+  // DCUE_WRMF_PHASES (timing diagnostic, wrong results): bit 1 the accumulation, 2 the Cholesky,
+  // 4 the back substitution, 8 / 16 / 32 the Cholesky's diagonal blocks / panels / trailing
+  // updates (default 63: all)
+  static const int phases = [] {
+    const char* e = getenv("DCUE_WRMF_PHASES");
+    return e ? atoi(e) : 63;
+  }();
   DCUE_LAUNCH(k_wrmf_solve, dim3((unsigned)grid), dim3(256), lds, s, solve, (long)n_rows, fixed, (int)dim, G,
-              indptr, indices, values, alpha, lambda);
+              indptr, indices, values, alpha, lambda, phases);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
