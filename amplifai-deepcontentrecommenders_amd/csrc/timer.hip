@@ -211,3 +211,24 @@ extern "C" int dcue_timer_read(int32_t kernel, double* total_ms_host, int64_t* l
   *launches_host = n;
   return DCUE_OK;
 }
+
+// each recorded launch's duration (the first `cap`; *launches_host counts all of them), then reset
+extern "C" int dcue_timer_samples(int32_t kernel, float* ms_host, int64_t cap, int64_t* launches_host) {
+  if (kernel < 0 || kernel >= DCUE_N_TIMED || !launches_host || cap < 0 || (cap > 0 && !ms_host))
+    return DCUE_ERR_INVALID;
+  std::lock_guard<std::recursive_mutex> lk(dcue::tmu());
+  auto& rec = dcue::ts().recorded[kernel];
+  int64_t n = 0;
+  for (auto& pr : rec) {
+    DCUE_HIP_CHECK(hipEventSynchronize(pr.second));
+    float ms = 0.f;
+    DCUE_HIP_CHECK(hipEventElapsedTime(&ms, pr.first, pr.second));
+    if (n < cap) ms_host[n] = ms;
+    ++n;
+    dcue::timer_release(pr.first);
+    dcue::timer_release(pr.second);
+  }
+  rec.clear();
+  *launches_host = n;
+  return DCUE_OK;
+}

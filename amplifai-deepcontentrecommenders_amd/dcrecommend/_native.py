@@ -103,7 +103,7 @@ class PlanConfig(ctypes.Structure):
 
 MT_STATE_BYTES = 624 * 4 + 16
 MAX_LOG_CAP = 256
-ABI_VERSION = 14
+ABI_VERSION = 15
 COMM_F32, COMM_U64 = 0, 1  # dcue_host_allreduce_fn dtypes
 HOST_ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32)
 RANK_SPLIT, RANK_SINGLE = 0, 1
@@ -176,6 +176,8 @@ _SIGS = {
     "dcue_timer_enable": ([ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
     "dcue_timer_read": ([ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)],
                         ctypes.c_int),
+    "dcue_timer_samples": ([ctypes.c_int32, ctypes.POINTER(ctypes.c_float), ctypes.c_int64,
+                            ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
     "dcue_rank_workspace_bytes": ([ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                    ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "dcue_rank_metrics": ([_P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int32, _P, ctypes.c_int32, _P, _P,
@@ -336,6 +338,14 @@ def workspace_activations(dims, B, N, M):
 def timer_enable(kernel, enable=True):
     """enable: True / 1 times every launch of the class, n > 1 every n-th, False / 0 none."""
     check(lib().dcue_timer_enable(kernel, int(enable)), "dcue_timer_enable")
+
+
+def timer_samples(kernel, cap=4096):
+    """Each recorded launch's duration in ms (the first `cap`) since the last read (waits; resets)."""
+    buf = (ctypes.c_float * cap)()
+    n = ctypes.c_int64()
+    check(lib().dcue_timer_samples(kernel, buf, cap, ctypes.byref(n)), "dcue_timer_samples")
+    return [float(buf[i]) for i in range(min(n.value, cap))]
 
 
 def timer_read(kernel):

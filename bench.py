@@ -665,7 +665,7 @@ def main():
         if world > 1:
             dist.barrier()
         dt = D.max_over_ranks(time.perf_counter() - t0, dev)
-        kern = {k: nat.timer_read(k) for k in timed}
+        kern = {k: nat.timer_samples(k) for k in timed}
         for k in timed:
             nat.timer_enable(k, False)
         return dt, t_enq, (ev0.elapsed_time(ev1) / args.steps if gpu_only else None), kern
@@ -717,15 +717,20 @@ def main():
                                  M * text_conv_flops(args.text_len, args.word_dim, args.text_dim)),
         }
         out = []
-        for k, (ms, n) in kern.items():
+        for k, samples in kern.items():
+            n = len(samples)
             if n == 0:
                 continue
             name, bound, work = spec[k]
-            avg = ms / n
+            avg = sum(samples) / n
             # launches per step from the timer stride (every stride-th launch is timed); the full flush
             # runs once per phase (opt.flush() after the timed steps)
             per_step = 1.0 / steps if k == nat.TIMED_EMB_FLUSH else n * stride / steps
+            srt = sorted(samples)
+            # the live samples' spread: a launch that shares the CUs with side-stream work (or waits for
+            # them) runs long; the average is what the roofline uses, the median is the typical launch
             ent = {"kernel": name, "bound": bound, "avg_ms": avg, "launches_timed": n,
+                   "median_ms": (srt[(n - 1) // 2] + srt[n // 2]) / 2, "min_ms": srt[0], "max_ms": srt[-1],
                    "ms_per_step": avg * per_step,
                    "critical_path": k not in (nat.TIMED_EMB_SLICE, nat.TIMED_EMB_FLUSH)}
             if bound == "mfma":

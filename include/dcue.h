@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DCUE_ABI_VERSION 14
+#define DCUE_ABI_VERSION 15
 #define DCUE_N_MELS 128
 #define DCUE_N_FRAMES 131
 #define DCUE_N_BN 6
@@ -498,6 +498,9 @@ int dcue_plan_set_sync_bn(dcue_plan* plan, int32_t on);
 #define DCUE_N_TIMED 7
 int dcue_timer_enable(int32_t kernel, int32_t enable);
 int dcue_timer_read(int32_t kernel, double* total_ms_host, int64_t* launches_host);
+/* The same recorded launches one by one: each duration in ms into ms_host[0 .. min(n, cap)), the
+ * count into *launches_host; resets (ABI 15). */
+int dcue_timer_samples(int32_t kernel, float* ms_host, int64_t cap, int64_t* launches_host);
 
 /* ------------------------------------------------------------------------ evaluation metrics */
 /* Ranking metrics of DCUE's evaluation for a batch of queries (users for DCUE.score, songs for

@@ -117,6 +117,13 @@ def test_timer_counts_eager_and_plan_launches():
             ms, n = nat.timer_read(nat.TIMED_CONV1_WGRAD)
             assert n == 3 and ms > 0.0
             plan.close()
+        # the per-launch read (dcue_timer_samples): one positive duration per timed launch, then reset
+        for _ in range(2):
+            net.native_forward(users, tracks, items, N, nat.LAYOUT_CATALOGUE, None, train=True)
+            net.native_backward(None)
+        samples = nat.timer_samples(nat.TIMED_CONV1_WGRAD)
+        assert len(samples) == 2 and all(v > 0.0 for v in samples)
+        assert nat.timer_samples(nat.TIMED_CONV1_WGRAD) == []
     finally:
         nat.timer_enable(nat.TIMED_CONV1_WGRAD, False)
 
