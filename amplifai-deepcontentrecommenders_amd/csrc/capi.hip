@@ -859,16 +859,20 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
     TRY(probe(PR_H1, w.h1, (long)b->n_rows * c.E, su));
     TRY(probe(PR_UF, w.uf, (long)b->n_rows * c.D, su));
     if (text_side) {  // the text branch: the item tower's fc input columns [0, C_s), beside its convs
-      // (its weights: the previous step's late Adam -- on this stream, or on the exchange's)
-      if (o.comm && o.wait_late) TRY(wait_point(su, o.wait_late));
+      // on wgrad stream 1 (the user stream holds the user tower's ≈65 µs): after the launch's start
+      // point (the items) and the previous step's late Adam (its weights); the previous step's text
+      // weight gradient, which read xfc / tidx, ran on this same stream
+      hipStream_t stx = sp->st[2];
+      TRY(wait_point(stx, ev_in));
+      if (o.wait_late) TRY(wait_point(stx, o.wait_late));
       TimerScope tsc;
-      TRY(timer_begin(&tsc, DCUE_TIMED_TEXT_FWD, su));
+      TRY(timer_begin(&tsc, DCUE_TIMED_TEXT_FWD, stx));
       if (tsc.b && !tsc.capturing) {  // a timed launch: the timer's stop event is its end
-        TRY(launch_text_fwd(text_branch_ws(c, t, w), b->item_track, b->n_items, w.xfc, c.FI, w.tidx, su));
+        TRY(launch_text_fwd(text_branch_ws(c, t, w), b->item_track, b->n_items, w.xfc, c.FI, w.tidx, stx));
         ev_tx = tsc.b;
       } else {
-        ForkAfter fk(sp, su, &ev_tx);
-        TRY(launch_text_fwd(text_branch_ws(c, t, w), b->item_track, b->n_items, w.xfc, c.FI, w.tidx, su));
+        ForkAfter fk(sp, stx, &ev_tx);
+        TRY(launch_text_fwd(text_branch_ws(c, t, w), b->item_track, b->n_items, w.xfc, c.FI, w.tidx, stx));
         TRY(fk.done());
       }
       TRY(timer_end(&tsc));

@@ -13,13 +13,15 @@ for r in $(seq 1 $ROUNDS); do
     i=$((i + 1))
     EV=$([ "$E" = "-" ] && echo "DCUE_AB_VARIANT=$i" || echo "$E")
     env $EV timeout -k 10 200 python3 $ROOT/bench.py --no-cpu-baseline --no-eval --no-f32-probe --steps 20 --warmup 5 \
-      --modes inbatch > "$OUT/v${i}_$r.log" 2>&1 || exit 1
+      --modes ${MODES:-inbatch} > "$OUT/v${i}_$r.log" 2>&1 || exit 1
     python3 - "$OUT/v${i}_$r.log" "$EV" <<'PY' >> "$OUT/summary.txt"
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
-ks = " ".join("%s %.1f" % (k["kernel"].split()[0], k["avg_ms"] * 1e3) for k in d.get("kernels", []))
-print("%-26s warm %.4f host %.4f cold %.4f | %s" % (sys.argv[2], d["ms_per_step"], d.get("host_enqueue_ms_per_step", 0),
-      d.get("inbatch_cold", {}).get("ms_per_step", -1), ks))
+ph = d.get("text", d)  # (MODES=text: the text phase's block)
+ks = " ".join("%s %.1f/%.1f" % (k["kernel"].split()[0], k["avg_ms"] * 1e3, k.get("median_ms", 0) * 1e3)
+              for k in ph.get("kernels", []))
+print("%-26s step %.4f host %.4f cold %.4f | avg/median us: %s" % (sys.argv[2], ph["ms_per_step"],
+      ph.get("host_enqueue_ms_per_step", 0), d.get("inbatch_cold", {}).get("ms_per_step", -1), ks))
 PY
   done
 done
