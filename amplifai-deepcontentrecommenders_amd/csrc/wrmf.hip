@@ -497,15 +497,20 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
           }
         }
       __syncthreads();
-      // (b) wave 0: factor it (lane i holds row i), then invert the factor (lane j: column j)
+      // (b) wave 0: factor it and invert the factor in one pass. Lane (i, g) = (lane & 15, lane >> 4)
+      // holds row i, columns 4g .. 4g + 3, of A and of X (= I at the start); step k scales column k
+      // of L and row k of X by 1 / L[k][k] (the pivot's rsqrt) and sends both through LDS (rs, xs) to
+      // every lane, which updates A's trailing part and X's rows below k: X ends as L_kk^{-1}
+      // (forward substitution on all columns of I at once, off the pivot's dependency chain)
       if (wave == 0 && (phases & 8)) {
         double* Lk = Li + 136 * kb;
-        // 64 lanes: lane (i, g) = (lane & 15, lane >> 4) holds row i, columns 4g .. 4g + 3; column k
-        // of L goes through LDS (rs) to every lane after its scaling
         const int i = lane & 15, g = lane >> 4;
-        double a4[4];
+        double a4[4], x4[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) a4[c] = 4 * g + c <= i ? Lk[wm_pk(i, 4 * g + c)] : 0.0;
+        for (int c = 0; c < 4; ++c) {
+          a4[c] = 4 * g + c <= i ? Lk[wm_pk(i, 4 * g + c)] : 0.0;
+          x4[c] = 4 * g + c == i ? 1.0 : 0.0;
+        }
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
           const int gk = k >> 2, ck = k & 3;
@@ -516,39 +521,31 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
             else if (i > k) a4[ck] *= inv;
             if (i >= k) rs[i] = a4[ck];
           }
-          if (lane == 0) dgs[k] = inv;
+          if (i == k) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              x4[c] *= inv;
+              xs[4 * g + c] = x4[c];
+            }
+          }
           const double lik = rs[i];
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const int j = 4 * g + c;
             if (j > k && i >= j) a4[c] = fma(-lik, rs[j], a4[c]);
+            if (i > k) x4[c] = fma(-lik, xs[j], x4[c]);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
+        // L_kk^{-1} over the block's slot, packed column-major (its A_kk input was read above)
 #pragma unroll
         for (int c = 0; c < 4; ++c)
-          if (4 * g + c <= i) Lk[wm_pk(i, 4 * g + c)] = a4[c];
-        // (LDS accesses of one wave are in order: the reads below see the stores above)
-        const int jc = (phases & 64) ? lane : 99;  // column of L^{-1}
-        double xv[16];
-#pragma unroll
-        for (int ii = 0; ii < 16; ++ii) {
-          double sum = 0.0;
-#pragma unroll
-          for (int m = 0; m < ii; ++m)
-            if (m >= jc) sum = fma(Lk[wm_pk(ii, m)], xv[m], sum);
-          const double d = dgs[ii];
-          xv[ii] = ii < jc ? 0.0 : ii == jc ? d : -sum * d;
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if (jc < 16) {  // (over the factor: packed column-major, L^{-1}[ii][jc] at wm_ck(ii, jc))
-#pragma unroll
-          for (int ii = 0; ii < 16; ++ii)
-            if (ii >= jc) Lk[wm_ck(ii, jc)] = xv[ii];
-        }
+          if (4 * g + c <= i) Lk[wm_ck(i, 4 * g + c)] = x4[c];
       }
       __syncthreads();
-      // (c) panel: L_Ikb = A_Ikb L_kk^{-T}; A_Ikb through LDS (its tile slot / ys) into the A layout
+      // (c) panel: L_Ikb = A_Ikb L_kk^{-T}. A_Ikb goes through its own LDS slot (ys for the augmented
+      // row) into the MFMA A layout and L_Ikb comes back over it -- all within the owning wave, whose
+      // LDS accesses run in order: no barrier until the trailing update reads other waves' tiles
 #pragma unroll
       for (int sl = 0; sl < NS; ++sl) {
         const int I = TI[sl];
@@ -559,34 +556,24 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
         } else if (lk == 0) {
           ys[16 * kb + li] = acc[sl][0];
         }
-      }
-      __syncthreads();
+        if (phases & 16) {
+          wf64x4 d = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int sl = 0; sl < NS; ++sl) {
-        const int I = TI[sl];
-        if (TJ[sl] != kb || I <= kb || !(phases & 16)) continue;
-        wf64x4 d = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const int k = 4 * kk + lk;
-          const double a = I < NB ? Lt[wm_lt<NB>(I, kb) + k * 16 + li] : (li == 0 ? ys[16 * kb + k] : 0.0);
-          const double b = k <= li ? Li[136 * kb + wm_ck(li, k)] : 0.0;  // L^{-T}[k][j] = L^{-1}[j][k]
-          d = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, d, 0, 0, 0);
+          for (int kk = 0; kk < 4; ++kk) {
+            const int k = 4 * kk + lk;
+            const double a = I < NB ? Lt[wm_lt<NB>(I, kb) + k * 16 + li] : (li == 0 ? ys[16 * kb + k] : 0.0);
+            const double b = k <= li ? Li[136 * kb + wm_ck(li, k)] : 0.0;  // L^{-T}[k][j] = L^{-1}[j][k]
+            d = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, d, 0, 0, 0);
+          }
+          acc[sl] = d;
         }
-        acc[sl] = d;
+        if (I < NB) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) Lt[wm_lt<NB>(I, kb) + li * 16 + lk + 4 * q] = acc[sl][q];
+        } else if (lk == 0) {
+          ys[16 * kb + li] = acc[sl][0];
+        }
         __builtin_amdgcn_sched_barrier(0);
-      }
-      __syncthreads();  // (every panel operand read before it is overwritten)
-#pragma unroll
-      for (int sl = 0; sl < NS; ++sl) {
-        const int I = TI[sl];
-        if (TJ[sl] != kb || I <= kb) continue;
-        if (I < NB) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) Lt[wm_lt<NB>(I, kb) + li * 16 + lk + 4 * q] = acc[sl][q];
-        } else if (lk == 0) {
-          ys[16 * kb + li] = acc[sl][0];
-        }
       }
       __syncthreads();
       // (d) trailing: A_IJ -= L_Ikb L_Jkb^T for kb < J <= I
@@ -703,12 +690,12 @@ int dcue_wrmf_half_step(float* solve, int64_t n_rows, const float* fixed, int64_
   DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_wrmf_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds));
   const long grid = n_rows < 4096 ? n_rows : 4096;  // grid-stride over rows
-  // the register-tile solve (k_wrmf_solve) by default; DCUE_WRMF_SOLVE=mfma: the fp64-MFMA block
-  // Cholesky (k_wrmf_solve_mfma), measured 96-98 ms per ALS iteration against 90 at the bench's
-  // shape -- both are bound by the diagonal blocks' serial factorization
+  // the fp64-MFMA block Cholesky (k_wrmf_solve_mfma) by default: 79-82 ms per ALS iteration
+  // against 90 for the register-tile solve (DCUE_WRMF_SOLVE=tile) at the bench's shape; both are
+  // bound by the diagonal blocks' serial factorization
   static const bool tile_solve = [] {
     const char* e = getenv("DCUE_WRMF_SOLVE");
-    return !(e && e[0] == 'm');
+    return e && e[0] == 't';
   }();
   if (!tile_solve) {
     switch ((dim + 15) / 16) {
