@@ -326,8 +326,12 @@ def dcbr_phase(args, tracks, pair_user, pair_track, n_users, dev, M, comm=None, 
     f_iter = (wrmf_half_step_flops(w.by_user[0], d, args.tracks) +
               wrmf_half_step_flops(w.by_item[0], d, n_users))
     ach = f_iter / t_iter / 1e12
-    wroof = {"kernel": "dcue_wrmf_half_step x 2 (k_wrmf_gram + k_wrmf_solve: fp64 register-tile Cholesky)",
-             "bound": "valu (fp64)", "achieved": ach, "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s (fp64)",
+    tile = os.environ.get("DCUE_WRMF_SOLVE", "")[:1] == "t"
+    wroof = {"kernel": "dcue_wrmf_half_step x 2 (k_wrmf_gram + %s)" % (
+                 "k_wrmf_solve: fp64 register-tile Cholesky" if tile else
+                 "k_wrmf_solve_mfma: fp64-MFMA block Cholesky, v_mfma_f64_16x16x4_f64"),
+             "bound": "valu (fp64)" if tile else "mfma (fp64; MI355X's fp64 matrix and vector peaks are equal)",
+             "achieved": ach, "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s (fp64)",
              "frac": ach / F64_PEAK_TFLOPS, "algorithmic_flops": f_iter, "traffic": None}
     pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_wrmf_solve.json")
     if os.path.exists(pmc):
