@@ -371,6 +371,19 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve(float* __restrict__ X, lo
 // lower column-major (136 doubles each; the diagonal tile itself is factored there packed
 // row-major first), y, x, the 1 / L[k][k] of the current block, and the staged factors (fp32) with
 // their weights.
+DCUE_KTRACE_READER(wrmf)  // diagnostic builds only (dcue_common.h): k_wrmf_solve_mfma, wave 0 / wave 1 cycles
+#ifdef DCUE_KTRACE
+#define WM_T(slot)                          \
+  do {                                      \
+    const unsigned long long n_ = clock64(); \
+    kt[slot] += n_ - kt0;                   \
+    kt0 = n_;                               \
+  } while (0)
+#else
+#define WM_T(slot) \
+  do {             \
+  } while (0)
+#endif
 typedef double wf64x4 __attribute__((ext_vector_type(4)));
 template <int NB>
 constexpr int wm_ntiles() { return NB * (NB + 1) / 2 + NB; }
@@ -381,10 +394,15 @@ __device__ __forceinline__ int wm_pk(int i, int j) { return i * (i + 1) / 2 + j;
 // packed lower triangle, column-major: column k holds rows k..15 contiguously (lane-contiguous reads)
 __device__ __forceinline__ int wm_ck(int i, int k) { return 16 * k - k * (k - 1) / 2 + (i - k); }  // k <= i
 
+// the staged factors (two buffers of kWrmfStage rows, fp32, with their weights) share the region of
+// the off-diagonal factor tiles: accumulation and factorization never overlap within a row
+__host__ __device__ constexpr int wm_stage_floats(int NB) { return kWrmfStage * 16 * NB + 2 * kWrmfStage; }
+__host__ __device__ constexpr int wm_region_doubles(int NB) {
+  return wm_lt_doubles(NB) > wm_stage_floats(NB) ? wm_lt_doubles(NB) : wm_stage_floats(NB);  // >= 2 buffers
+}
 template <int NB>
 size_t wm_lds_bytes() {
-  return sizeof(double) * ((size_t)wm_lt_doubles(NB) + 136 * NB + 16 * NB + 16 * NB + 16 + 16) +
-         sizeof(float) * ((size_t)kWrmfStage * 16 * NB + 2 * kWrmfStage);
+  return sizeof(double) * ((size_t)wm_region_doubles(NB) + 136 * NB + 16 * NB + 16 * NB + 16 + 16);
 }
 
 template <int NB>
@@ -398,14 +416,12 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
   constexpr int D16 = 16 * NB, NT = wm_ntiles<NB>(), NS = (NT + 3) / 4;
   extern __shared__ __attribute__((aligned(16))) double wsm[];
   double* Lt = wsm;                               // off-diagonal factor tiles [i][j]
-  double* Li = Lt + wm_lt_doubles(NB);            // diagonal factor inverses, packed lower
+  double* Li = Lt + wm_region_doubles(NB);        // diagonal factor inverses, packed lower
   double* ys = Li + 136 * NB;                     // y = L^{-1} b
   double* xs = ys + 16 * NB;                      // x
   double* rs = xs + 16 * NB;                      // back substitution: the block's right-hand side
-  double* dgs = rs + 16;                          // 1 / L[k][k] of the block being inverted
-  float* st = reinterpret_cast<float*>(dgs + 16);  // [kWrmfStage][D16] staged factors
-  float* ws = st + kWrmfStage * D16;               // c_s - 1
-  float* cs = ws + kWrmfStage;                     // c_s
+  // staging buffer b: [kWrmfStage][D16] factors, then c_s - 1 and c_s (over Lt: see wm_stage_floats)
+  float* const stb = reinterpret_cast<float*>(wsm);
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);  // (uniform: tile coordinates in SGPRs)
   const int li = lane & 15, lk = lane >> 4;
@@ -426,12 +442,21 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
     TI[sl] = tau < NT ? I : -1;
     TJ[sl] = tau < NT ? J : -1;
   }
+#ifdef DCUE_KTRACE
+  // per-phase cycles of one thread of wave 0 and of wave 1: 0 G, 1 accumulation, 2 diagonal blocks,
+  // 3 barriers, 4 panels, 5 trailing, 6 back substitution + store, 7 rows
+  unsigned long long kt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, kt0 = clock64();
+#endif
   for (long r = blockIdx.x; r < n_rows; r += gridDim.x) {
     const long p0 = indptr[r], p1 = indptr[r + 1];
     if (p1 <= p0) {  // no observed pair: b = 0, so x = 0
       for (int c = t; c < dim; c += blockDim.x) X[r * dim + c] = 0.f;
       continue;
     }
+#ifdef DCUE_KTRACE
+    ++kt[7];
+#endif
+    WM_T(6);
     // A = G + lambda I (identity on the padding); the augmented row b = 0
     wf64x4 acc[NS];
 #pragma unroll
@@ -439,30 +464,56 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
       const int I = TI[sl], J = TJ[sl];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        // (the load is unconditional, its use selected: a load under a branch would be waited for
+        // at the branch's join, one tile at a time, instead of all of them in flight together)
         const int i = lk + 4 * q;
-        double v = 0.0;
-        if (I >= 0 && I < NB) {
-          v = G[(size_t)(16 * I + i) * D16 + 16 * J + li];
-          if (I == J && i == li) v += 16 * I + i < dim ? (double)lambda : 1.0;
-        }
-        acc[sl][q] = v;
+        const bool in = I >= 0 && I < NB;
+        double v = G[(size_t)(16 * (in ? I : 0) + i) * D16 + 16 * (in ? J : 0) + li];
+        if (I == J && i == li) v += 16 * I + i < dim ? (double)lambda : 1.0;
+        acc[sl][q] = in ? v : 0.0;
       }
     }
-    // the row's observed factors, kWrmfStage at a time: K = 4 factors per MFMA
-#pragma unroll 1
-    for (long pb = p0; pb < ((phases & 1) ? p1 : p0); pb += kWrmfStage) {
+    WM_T(0);
+    // the row's observed factors, kWrmfStage at a time: K = 4 factors per MFMA. The next pass's
+    // gather is in flight (registers) during this pass's MFMAs and lands in the other buffer after them
+    constexpr int SD = kWrmfStage * D16, PER = (SD + 255) / 256;
+    float pre[PER], wpre = 0.f;
+    auto gather = [&](const long pb) {
       const int ns = (int)min((long)kWrmfStage, p1 - pb);
-      __syncthreads();  // (the previous pass's reads)
-      for (int e = t; e < kWrmfStage * D16; e += blockDim.x) {
-        const int sf = e / D16, c = e - sf * D16;
-        st[e] = sf < ns && c < dim ? F[(long)indices[pb + sf] * dim + c] : 0.f;
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = t + 256 * u, sf = e / D16, c = e - sf * D16;
+        pre[u] = e < SD && sf < ns && c < dim ? F[(long)indices[pb + sf] * dim + c] : 0.f;
       }
+      if (t < kWrmfStage) wpre = t < ns ? alpha * (values ? values[pb + t] : 1.f) : 0.f;
+      return ns;
+    };
+    auto put = [&](const int buf, const int ns) {
+      float* st = stb + buf * wm_stage_floats(NB);
+#pragma unroll
+      for (int u = 0; u < PER; ++u)
+        if (t + 256 * u < SD) st[t + 256 * u] = pre[u];
       if (t < kWrmfStage) {
-        const float w = t < ns ? alpha * (values ? values[pb + t] : 1.f) : 0.f;
-        ws[t] = w;
-        cs[t] = t < ns ? 1.f + w : 0.f;
+        st[SD + t] = wpre;
+        st[SD + kWrmfStage + t] = t < ns ? 1.f + wpre : 0.f;
       }
-      __syncthreads();
+    };
+    if ((phases & 1) && p1 > p0) {
+      const int ns0 = gather(p0);
+      __syncthreads();  // (the previous row's factorization and back substitution over this region)
+      put(0, ns0);
+    }
+#pragma unroll 1
+    for (long pb = p0, buf = 0; pb < ((phases & 1) ? p1 : p0); pb += kWrmfStage, buf ^= 1) {
+      __syncthreads();  // (buffer buf written; every wave done with the other one)
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl) asm volatile("" : "+s"(TI[sl]), "+s"(TJ[sl]));  // (as below)
+      const bool more = pb + kWrmfStage < p1;
+      int ns1 = 0;
+      if (more) ns1 = gather(pb + kWrmfStage);
+      const float* st = stb + buf * wm_stage_floats(NB);
+      const float* ws = st + SD;
+      const float* cs = ws + kWrmfStage;
 #pragma unroll
       for (int kk = 0; kk < kWrmfStage / 4; ++kk) {
         const int sf = 4 * kk + lk;
@@ -477,15 +528,12 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
           __builtin_amdgcn_sched_barrier(0);  // (operand loads stay next to their MFMA: register budget)
         }
       }
+      if (more) put(buf ^ 1, ns1);
     }
+    WM_T(1);
     // block Cholesky
-#pragma unroll 1
-    for (int kb = 0; kb < NB; ++kb) {
-      // tile coordinates opaque per step: their address arithmetic is redone here instead of being
-      // hoisted out of the step loop into live registers
-#pragma unroll
-      for (int sl = 0; sl < NS; ++sl) asm volatile("" : "+s"(TI[sl]), "+s"(TJ[sl]));
-      __syncthreads();  // (the previous block's trailing reads of Lt; the first: the staging reads)
+    // (a) + (b) for diagonal block kb
+    auto factor_diag = [&](const int kb) {
       // (a) the diagonal tile to Li[kb] (packed lower)
 #pragma unroll
       for (int sl = 0; sl < NS; ++sl)
@@ -497,52 +545,64 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
           }
         }
       __syncthreads();
-      // (b) wave 0: factor it and invert the factor in one pass. Lane (i, g) = (lane & 15, lane >> 4)
-      // holds row i, columns 4g .. 4g + 3, of A and of X (= I at the start); step k scales column k
-      // of L and row k of X by 1 / L[k][k] (the pivot's rsqrt) and sends both through LDS (rs, xs) to
-      // every lane, which updates A's trailing part and X's rows below k: X ends as L_kk^{-1}
-      // (forward substitution on all columns of I at once, off the pivot's dependency chain)
+      // (b) wave 0: factor it and invert the factor in one pass, in registers. Lane j < 16 holds row j
+      // of A, lane 16 + j column j of X (= I at the start; lanes 32-63 repeat them, unused). Step k
+      // scales every lane's element k by 1 / L[k][k] -- row k's pivot becomes L[k][k], rows below
+      // their L[j][k], and X's row k is divided by L[k][k] -- then broadcasts L[c][k] (c > k) through
+      // SGPRs and each lane applies R[c] -= L[c][k] R[k]: A's trailing update (lanes j < 16, whose
+      // upper-triangle elements take harmless garbage) and X's forward substitution (X ends as
+      // L_kk^{-1}) in the same instructions, without LDS round trips or divergence
       if (wave == 0 && (phases & 8)) {
         double* Lk = Li + 136 * kb;
-        const int i = lane & 15, g = lane >> 4;
-        double a4[4], x4[4];
+        const int j = lane & 15;
+        const bool xl = lane >= 16;
+        double R[16];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          a4[c] = 4 * g + c <= i ? Lk[wm_pk(i, 4 * g + c)] : 0.0;
-          x4[c] = 4 * g + c == i ? 1.0 : 0.0;
-        }
+        for (int c = 0; c < 16; ++c) R[c] = xl ? (c == j ? 1.0 : 0.0) : (c <= j ? Lk[wm_pk(j, c)] : 0.0);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-          const int gk = k >> 2, ck = k & 3;
-          const double pk = readlane_d(a4[ck], k + 16 * gk);
-          const double inv = rsqrt_d(pk);
-          if (g == gk) {
-            if (i == k) a4[ck] = pk * inv;
-            else if (i > k) a4[ck] *= inv;
-            if (i >= k) rs[i] = a4[ck];
-          }
-          if (i == k) {
+          const double inv = rsqrt_d(readlane_d(R[k], k));
+          R[k] *= inv;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-              x4[c] *= inv;
-              xs[4 * g + c] = x4[c];
-            }
-          }
-          const double lik = rs[i];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int j = 4 * g + c;
-            if (j > k && i >= j) a4[c] = fma(-lik, rs[j], a4[c]);
-            if (i > k) x4[c] = fma(-lik, xs[j], x4[c]);
-          }
-          __builtin_amdgcn_sched_barrier(0);
+          for (int c = k + 1; c < 16; ++c) R[c] = fma(-readlane_d(R[k], c), R[k], R[c]);
         }
         // L_kk^{-1} over the block's slot, packed column-major (its A_kk input was read above)
+        if (xl && lane < 32) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (4 * g + c <= i) Lk[wm_ck(i, 4 * g + c)] = x4[c];
+          for (int i = 0; i < 16; ++i)
+            if (i >= j) Lk[wm_ck(i, j)] = R[i];
+        }
       }
-      __syncthreads();
+      WM_T(2);
+    };
+    auto trailing = [&](const int kb) {
+      // (d) trailing: A_IJ -= L_Ikb L_Jkb^T for kb < J <= I
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl) {
+        const int I = TI[sl], J = TJ[sl];
+        if (J <= kb || I < 0 || !(phases & 32)) continue;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int k = 4 * kk + lk;
+          const double a = I < NB ? Lt[wm_lt<NB>(I, kb) + k * 16 + li] : (li == 0 ? ys[16 * kb + k] : 0.0);
+          const double b = Lt[wm_lt<NB>(J, kb) + k * 16 + li];  // L_Jkb^T[k][j] = L_Jkb[j][k]
+          acc[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(-a, b, acc[sl], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      WM_T(5);
+    };
+#pragma unroll 1
+    for (int kb = 0; kb < NB; ++kb) {
+      // tile coordinates opaque per step: their address arithmetic is redone here instead of being
+      // hoisted out of the step loop into live registers
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl) asm volatile("" : "+s"(TI[sl]), "+s"(TJ[sl]));
+      __syncthreads();  // (the previous block's trailing reads of Lt; the first: the staging reads)
+      WM_T(3);
+      factor_diag(kb);
+      __syncthreads();  // (L_kk^{-1} in Li[kb])
+      WM_T(3);
       // (c) panel: L_Ikb = A_Ikb L_kk^{-T}. A_Ikb goes through its own LDS slot (ys for the augmented
       // row) into the MFMA A layout and L_Ikb comes back over it -- all within the owning wave, whose
       // LDS accesses run in order: no barrier until the trailing update reads other waves' tiles
@@ -575,23 +635,13 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+      WM_T(4);
       __syncthreads();
-      // (d) trailing: A_IJ -= L_Ikb L_Jkb^T for kb < J <= I
-#pragma unroll
-      for (int sl = 0; sl < NS; ++sl) {
-        const int I = TI[sl], J = TJ[sl];
-        if (J <= kb || I < 0 || !(phases & 32)) continue;
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const int k = 4 * kk + lk;
-          const double a = I < NB ? Lt[wm_lt<NB>(I, kb) + k * 16 + li] : (li == 0 ? ys[16 * kb + k] : 0.0);
-          const double b = Lt[wm_lt<NB>(J, kb) + k * 16 + li];  // L_Jkb^T[k][j] = L_Jkb[j][k]
-          acc[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(-a, b, acc[sl], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      WM_T(3);
+      trailing(kb);
     }
     __syncthreads();
+    WM_T(3);
     // L^T x = y, block rows NB-1 .. 0, wave 0: lane (m, q) = (lane & 15, lane >> 4) sums a quarter
     // of each dot product, the quarters meet by shuffles
     if (wave == 0 && (phases & 4)) {
@@ -624,6 +674,11 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
       for (int c = lane; c < dim; c += 64) X[r * dim + c] = (float)xs[c];
     }
   }
+#ifdef DCUE_KTRACE
+  WM_T(6);
+  if ((t == 0 || t == 64) && blockIdx.x < kKtraceBlocks)
+    for (int k = 0; k < 8; ++k) dcue_ktrace_buf[t >> 6][blockIdx.x][k] = kt[k];
+#endif
 }
 
 template <int NB>
@@ -635,11 +690,11 @@ static int launch_wrmf_mfma(float* solve, long n_rows, const float* fixed, int d
     return e ? atoi(e) : 127;
   }();
   const size_t lds = wm_lds_bytes<NB>();
-  DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_wrmf_solve_mfma<NB>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  auto kern = k_wrmf_solve_mfma<NB>;
+  DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const long grid = n_rows < 4096 ? n_rows : 4096;
-  DCUE_LAUNCH(k_wrmf_solve_mfma<NB>, dim3((unsigned)grid), dim3(256), lds, s, solve, n_rows, fixed, dim, G, indptr,
-              indices, values, alpha, lambda, phases);
+  DCUE_LAUNCH(kern, dim3((unsigned)grid), dim3(256), lds, s, solve, n_rows, fixed, dim, G, indptr, indices, values,
+              alpha, lambda, phases);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }

@@ -150,7 +150,7 @@ for dim in (7, 40, 100, 128):
 torch.save(out, sys.argv[1])
 ''' % (os.path.join(root, "amplifai-deepcontentrecommenders_amd"), os.path.join(root, "tests"))
     res = []
-    for i, extra in enumerate(({}, {"DCUE_WRMF_SOLVE": "tile"})):
+    for i, extra in enumerate(({"DCUE_WRMF_SOLVE": "tile"}, {})):
         out = str(tmp_path / ("w%d.pt" % i))
         env = dict(os.environ, **extra)
         if not extra:
@@ -160,7 +160,9 @@ torch.save(out, sys.argv[1])
         assert p.returncode == 0, p.stdout[-3000:]
         res.append(torch.load(out, weights_only=True))
     for k in res[0]:
-        a, b = res[0][k].double(), res[1][k].double()
+        b = res[0][k].double()
         scale = float(b.abs().max())
-        assert float((a - b).abs().max()) <= 1e-6 * scale, (k, float((a - b).abs().max()) / scale)
-        assert bool(torch.isfinite(a).all())
+        for v, r in enumerate(res[1:]):
+            a = r[k].double()
+            assert float((a - b).abs().max()) <= 1e-6 * scale, (k, v, float((a - b).abs().max()) / scale)
+            assert bool(torch.isfinite(a).all())
