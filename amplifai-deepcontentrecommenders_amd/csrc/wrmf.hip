@@ -514,18 +514,29 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
       const float* st = stb + buf * wm_stage_floats(NB);
       const float* ws = st + SD;
       const float* cs = ws + kWrmfStage;
+      // operands one MFMA ahead: (kk, sl)'s loads are issued before the MFMA of the step before it
+      float na, nb;
+      auto ld = [&](const int kk, const int sl) {
+        const int sf = 4 * kk + lk, I = TI[sl], J = TJ[sl];
+        na = st[sf * D16 + 16 * (I < NB && I >= 0 ? I : 0) + li];
+        nb = st[sf * D16 + 16 * (J >= 0 ? J : 0) + li];
+      };
+      ld(0, 0);
 #pragma unroll
       for (int kk = 0; kk < kWrmfStage / 4; ++kk) {
         const int sf = 4 * kk + lk;
         const double w = (double)ws[sf], c = (double)cs[sf];
 #pragma unroll
         for (int sl = 0; sl < NS; ++sl) {
-          const int I = TI[sl], J = TJ[sl];
-          if (I < 0) continue;
-          const double a = I == NB ? (li == 0 ? c : 0.0) : w * (double)st[sf * D16 + 16 * I + li];
-          const double b = (double)st[sf * D16 + 16 * J + li];
-          acc[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[sl], 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);  // (operand loads stay next to their MFMA: register budget)
+          const int I = TI[sl];
+          const float ca = na, cb = nb;
+          if (sl + 1 < NS) ld(kk, sl + 1);
+          else if (kk + 1 < kWrmfStage / 4) ld(kk + 1, 0);
+          if (I >= 0) {
+            const double a = I == NB ? (li == 0 ? c : 0.0) : w * (double)ca;
+            acc[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, (double)cb, acc[sl], 0, 0, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);  // (one step of loads in flight: register budget)
         }
       }
       if (more) put(buf ^ 1, ns1);
@@ -584,7 +595,9 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
           const int k = 4 * kk + lk;
-          const double a = I < NB ? Lt[wm_lt<NB>(I, kb) + k * 16 + li] : (li == 0 ? ys[16 * kb + k] : 0.0);
+          // (operand addresses selected, the loads themselves unconditional: see the G loads)
+          const double ra = *(I < NB ? Lt + wm_lt<NB>(I, kb) + k * 16 + li : ys + 16 * kb + k);
+          const double a = I < NB || li == 0 ? ra : 0.0;
           const double b = Lt[wm_lt<NB>(J, kb) + k * 16 + li];  // L_Jkb^T[k][j] = L_Jkb[j][k]
           acc[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(-a, b, acc[sl], 0, 0, 0);
         }
@@ -621,8 +634,10 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) {
             const int k = 4 * kk + lk;
-            const double a = I < NB ? Lt[wm_lt<NB>(I, kb) + k * 16 + li] : (li == 0 ? ys[16 * kb + k] : 0.0);
-            const double b = k <= li ? Li[136 * kb + wm_ck(li, k)] : 0.0;  // L^{-T}[k][j] = L^{-1}[j][k]
+            const double ra = *(I < NB ? Lt + wm_lt<NB>(I, kb) + k * 16 + li : ys + 16 * kb + k);
+            const double a = I < NB || li == 0 ? ra : 0.0;
+            const double rb = Li[136 * kb + wm_ck(k <= li ? li : k, k)];
+            const double b = k <= li ? rb : 0.0;  // L^{-T}[k][j] = L^{-1}[j][k]
             d = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, d, 0, 0, 0);
           }
           acc[sl] = d;
