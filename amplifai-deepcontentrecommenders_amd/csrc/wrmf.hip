@@ -15,8 +15,9 @@
 // CSR (indptr int64 [n_rows + 1], indices int32 [nnz] into the fixed side, values fp32 or NULL).
 //
 // Kernels:
-//   k_wrmf_gram    G = F^T F over row chunks: a workgroup sums its chunk's rank-1 terms in
-//                  registers (thread t owns G[t & 127][(t >> 7) * 64 + 0..63]); partials [chunk][d][d]
+//   k_wrmf_gram_mfma  G = F^T F over 512-row chunks on fp64 MFMA (lower block triangle, stored with
+//                  its transpose); partials [chunk][d][d]. k_wrmf_gram (DCUE_WRMF_GRAM=scalar): the
+//                  same with fp64 FMAs (thread t owns G[t & 127][(t >> 7) * 64 + 0..63])
 //   k_wrmf_gram_reduce  the chunk partials in a fixed order (deterministic)
 //   k_wrmf_solve   one workgroup per row (grid-stride): A and b accumulated in register tiles, a
 //                  right-looking Cholesky of [[A, b], [b^T, *]] (16-column steps) whose last row
@@ -34,7 +35,7 @@ typedef double wacc_t;
 // rows 0..128 (128: the augmented row) of the tile-padded triangle, then an 8-double dummy row
 constexpr int kWrmfDummy = 32 * (kWrmfMaxDim / 8) * (kWrmfMaxDim / 8 + 1) + 8 * (kWrmfMaxDim / 8 + 1);
 constexpr int kWrmfTri = kWrmfDummy + 8;
-constexpr int kWrmfGramChunk = 2048;         // fixed-side rows per gram workgroup
+constexpr int kWrmfGramChunk = 512;          // fixed-side rows per gram workgroup (a multiple of 4)
 constexpr int kWrmfStage = 16;               // observed factors staged in LDS per pass
 
 __global__ __launch_bounds__(256) void k_wrmf_gram(const float* __restrict__ F, long n, int dim,
@@ -66,6 +67,89 @@ __global__ __launch_bounds__(256) void k_wrmf_gram(const float* __restrict__ F, 
 #pragma unroll
     for (int q = 0; q < 64; ++q)
       if (j0 + q < dim) out[j0 + q] = acc[q];
+  }
+}
+
+// The same partials on fp64 MFMA (v_mfma_f64_16x16x4_f64, the default): G_IJ += F_chunk[:, I]^T
+// F_chunk[:, J] four rows per MFMA, both operands straight from global memory in the MFMA operand
+// layout (lane l: row l >> 4 of the step, column 16 X + (l & 15)). Only the lower block triangle is
+// computed -- wave w owns block rows w and NB8 - 1 - w (NB8 = 8 tile rows at dim <= 128: 9 tiles
+// per wave) -- and each tile is stored with its transpose, so the partials keep k_wrmf_gram's
+// full [chunk][d][d] layout and k_wrmf_gram_reduce is shared.
+typedef double wgf64x4 __attribute__((ext_vector_type(4)));
+template <int W>  // the wave: block rows IA = W and IB = 7 - W, compile-time so every index is
+__device__ __forceinline__ void wrmf_gram_wave(const float* __restrict__ F, long r0, long r1, int dim,
+                                               wacc_t* __restrict__ out) {
+  constexpr int IA = W, IB = 7 - W;
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  const int NB = (dim + 15) >> 4;
+  // slots: (IA, J) for J <= IA, then (IB, J) for J <= IB -- 9 in all
+  wgf64x4 acc[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) acc[q] = wgf64x4{0.0, 0.0, 0.0, 0.0};
+  // the step's operands: v[X] = F[r + lk][16 X + li] (0 past the chunk or past dim); the loads are
+  // unconditional (clamped), their values selected
+  auto load = [&](const long r, float (&v)[8]) {
+    const long row = r + lk;
+    const float* src = F + (row < r1 ? row : r1 - 1) * dim;
+#pragma unroll
+    for (int X = 0; X < 8; ++X) {
+      const int c = 16 * X + li;
+      const float x = src[c < dim ? c : dim - 1];
+      v[X] = row < r1 && c < dim ? x : 0.f;
+    }
+  };
+  float cur[8], nxt[8];
+  load(r0, cur);
+#pragma unroll 1
+  for (long r = r0; r < r1; r += 4) {
+    if (r + 4 < r1) load(r + 4, nxt);  // (the next step's loads in flight during these MFMAs)
+    if (IA < NB) {
+#pragma unroll
+      for (int J = 0; J <= IA; ++J)
+        acc[J] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)cur[IA], (double)cur[J], acc[J], 0, 0, 0);
+    }
+    if (IB < NB) {
+#pragma unroll
+      for (int J = 0; J <= IB; ++J)
+        acc[IA + 1 + J] =
+            __builtin_amdgcn_mfma_f64_16x16x4f64((double)cur[IB], (double)cur[J], acc[IA + 1 + J], 0, 0, 0);
+    }
+#pragma unroll
+    for (int X = 0; X < 8; ++X) cur[X] = nxt[X];
+  }
+  // tile (I, J) and, off the diagonal, its transpose (C layout: lane l holds column l & 15, rows
+  // (l >> 4) + 4 q)
+  auto store = [&](const int I, const int J, const wgf64x4& t) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = 16 * I + lk + 4 * q, j = 16 * J + li;
+      if (i < dim && j < dim) {
+        out[(size_t)i * dim + j] = t[q];
+        if (I != J) out[(size_t)j * dim + i] = t[q];
+      }
+    }
+  };
+  if (IA < NB) {
+#pragma unroll
+    for (int J = 0; J <= IA; ++J) store(IA, J, acc[J]);
+  }
+  if (IB < NB) {
+#pragma unroll
+    for (int J = 0; J <= IB; ++J) store(IB, J, acc[IA + 1 + J]);
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void k_wrmf_gram_mfma(const float* __restrict__ F, long n, int dim,
+                                                          wacc_t* __restrict__ part) {
+  const long r0 = (long)blockIdx.x * kWrmfGramChunk;
+  const long r1 = min(r0 + kWrmfGramChunk, n);
+  wacc_t* out = part + (size_t)blockIdx.x * dim * dim;
+  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+    case 0: wrmf_gram_wave<0>(F, r0, r1, dim, out); break;
+    case 1: wrmf_gram_wave<1>(F, r0, r1, dim, out); break;
+    case 2: wrmf_gram_wave<2>(F, r0, r1, dim, out); break;
+    default: wrmf_gram_wave<3>(F, r0, r1, dim, out); break;
   }
 }
 
@@ -748,7 +832,14 @@ int dcue_wrmf_half_step(float* solve, int64_t n_rows, const float* fixed, int64_
   const long nch = wrmf_gram_chunks(n_fixed);
   wacc_t* part = reinterpret_cast<wacc_t*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
   wacc_t* G = part + (size_t)nch * dim * dim;
-  DCUE_LAUNCH(k_wrmf_gram, dim3((unsigned)nch), dim3(256), 0, s, fixed, (long)n_fixed, (int)dim, part);
+  static const bool scalar_gram = [] {  // DCUE_WRMF_GRAM=scalar: k_wrmf_gram (fp64 FMAs), A/B and check
+    const char* e = getenv("DCUE_WRMF_GRAM");
+    return e && e[0] == 's';
+  }();
+  if (scalar_gram)
+    DCUE_LAUNCH(k_wrmf_gram, dim3((unsigned)nch), dim3(256), 0, s, fixed, (long)n_fixed, (int)dim, part);
+  else
+    DCUE_LAUNCH(k_wrmf_gram_mfma, dim3((unsigned)nch), dim3(256), 0, s, fixed, (long)n_fixed, (int)dim, part);
   DCUE_LAUNCH_CHECK();
   const long dd = (long)((dim + 15) & ~15) * ((dim + 15) & ~15);
   DCUE_LAUNCH(k_wrmf_gram_reduce, dim3((unsigned)((dd + 255) / 256)), dim3(256), 0, s, part, (int)nch, (int)dim, G);
@@ -760,9 +851,8 @@ int dcue_wrmf_half_step(float* solve, int64_t n_rows, const float* fixed, int64_
   DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_wrmf_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds));
   const long grid = n_rows < 4096 ? n_rows : 4096;  // grid-stride over rows
-  // the fp64-MFMA block Cholesky (k_wrmf_solve_mfma) by default: 79-82 ms per ALS iteration
-  // against 90 for the register-tile solve (DCUE_WRMF_SOLVE=tile) at the bench's shape; both are
-  // bound by the diagonal blocks' serial factorization
+  // the fp64-MFMA block Cholesky (k_wrmf_solve_mfma) by default: 45 ms per ALS iteration against
+  // 90 for the register-tile solve (DCUE_WRMF_SOLVE=tile) at the bench's shape
   static const bool tile_solve = [] {
     const char* e = getenv("DCUE_WRMF_SOLVE");
     return e && e[0] == 't';
