@@ -496,7 +496,7 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
                                                          const int64_t* __restrict__ indptr,
                                                          const int32_t* __restrict__ indices,
                                                          const float* __restrict__ values, float alpha,
-                                                         float lambda, int phases) {
+                                                         float lambda, int phases, int min_pairs) {
   constexpr int D16 = 16 * NB, NT = wm_ntiles<NB>(), NS = (NT + 3) / 4;
   extern __shared__ __attribute__((aligned(16))) double wsm[];
   double* Lt = wsm;                               // off-diagonal factor tiles [i][j]
@@ -533,6 +533,7 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
 #endif
   for (long r = blockIdx.x; r < n_rows; r += gridDim.x) {
     const long p0 = indptr[r], p1 = indptr[r + 1];
+    if (p1 - p0 <= min_pairs) continue;  // (solved by k_wrmf_solve_lowrank)
     if (p1 <= p0) {  // no observed pair: b = 0, so x = 0
       for (int c = t; c < dim; c += blockDim.x) X[r * dim + c] = 0.f;
       continue;
@@ -780,10 +781,198 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
 #endif
 }
 
+// ---- rows with few pairs: the Woodbury identity -------------------------------------------------
+// With M = (G + lambda I)^{-1} (the same for every row of the half-step, k_wrmf_ginv) and the row's
+// n pairs F_r (n x d), weights w_s = c_s - 1:
+//   A_r = M^{-1} + F_r^T W F_r,  A_r^{-1} = M - P^T (W^{-1} + P F_r^T)^{-1} P,  P = F_r M,
+//   x_r = A_r^{-1} F_r^T c = P^T (c - u),  S u = P b,  S = W^{-1} + P F_r^T,  b = F_r^T c,
+// an n x n system instead of d x d: its serial chain is n pivots, not d. Pairs with w_s = 0 (c_s = 1)
+// add nothing to A_r: their rows of S become the identity and their u_s = 0. fp64 throughout.
+// k_wrmf_ginv: M by Gauss-Jordan on [G + lambda I | I] (SPD: no pivoting), one workgroup, the
+// working matrix in global memory (L2-resident on the workgroup's XCD).
+__global__ __launch_bounds__(1024) void k_wrmf_ginv(const wacc_t* __restrict__ G, int dim, float lambda,
+                                                    wacc_t* __restrict__ W, wacc_t* __restrict__ M) {
+  const int D = (dim + 15) & ~15, D2 = 2 * D, t = threadIdx.x;
+  __shared__ double fcol[kWrmfMaxDim], prow[2 * kWrmfMaxDim];
+  for (int e = t; e < D * D2; e += blockDim.x) {
+    const int i = e / D2, j = e - i * D2;
+    W[e] = j < D ? G[(size_t)i * D + j] + (i == j ? (i < dim ? (double)lambda : 1.0) : 0.0) : (j - D == i ? 1.0 : 0.0);
+  }
+  for (int k = 0; k < D; ++k) {
+    __syncthreads();
+    const double piv = W[(size_t)k * D2 + k];
+    if (t < D2) prow[t] = W[(size_t)k * D2 + t] / piv;
+    if (t < D) fcol[t] = W[(size_t)t * D2 + k];
+    __syncthreads();
+    for (int e = t; e < D * D2; e += blockDim.x) {
+      const int i = e / D2, j = e - i * D2;
+      W[e] = i == k ? prow[j] : fma(-fcol[i], prow[j], W[e]);
+    }
+  }
+  __syncthreads();
+  for (int e = t; e < D * D; e += blockDim.x) {
+    const int i = e / D, j = e - i * D;
+    M[e] = W[(size_t)i * D2 + D + j];
+  }
+}
+
+// One workgroup per row with 1 <= n <= 16 NR pairs (rows with none: x = 0; the rest are left to
+// k_wrmf_solve_mfma). LDS: P [16 NR][D16 + 2] fp64 (pitch: conflict-free column reads), F_r
+// [16 NR][D16] fp32 (S [16 NR][16 NR + 1] fp64 over it once P F_r^T is in registers), c, w, b, P b, u.
+template <int NB, int NR>
+constexpr size_t wl_lds_bytes() {
+  constexpr int D16 = 16 * NB, NP = 16 * NR;
+  constexpr size_t f = sizeof(float) * NP * D16, sb = sizeof(double) * NP * (NP + 1);
+  return sizeof(double) * ((size_t)NP * (D16 + 2) + 4 * NP + D16) + (f > sb ? f : sb);
+}
+template <int NB, int NR>
+__global__ __launch_bounds__(256) void k_wrmf_solve_lowrank(float* __restrict__ X, long n_rows,
+                                                           const float* __restrict__ F, int dim,
+                                                           const wacc_t* __restrict__ M,
+                                                           const int64_t* __restrict__ indptr,
+                                                           const int32_t* __restrict__ indices,
+                                                           const float* __restrict__ values, float alpha) {
+  constexpr int D16 = 16 * NB, NP = 16 * NR, PP = D16 + 2, SP = NP + 1;
+  extern __shared__ __attribute__((aligned(16))) double lsm[];
+  double* Ps = lsm;                 // [NP][PP]
+  double* cs = Ps + NP * PP;        // c_s
+  double* ws = cs + NP;             // w_s = c_s - 1
+  double* rh = ws + NP;             // (P b)_s
+  double* us = rh + NP;             // u_s
+  double* bs = us + NP;             // b = F_r^T c
+  float* Fs = reinterpret_cast<float*>(bs + D16);  // [NP][D16]
+  double* Ss = reinterpret_cast<double*>(Fs);      // [NP][SP], after P F_r^T
+  const int t = threadIdx.x, lane = t & 63, li = lane & 15, lk = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  for (long r = blockIdx.x; r < n_rows; r += gridDim.x) {
+    const long p0 = indptr[r], p1 = indptr[r + 1];
+    const int n = (int)(p1 - p0);
+    if (n > NP) continue;
+    if (n <= 0) {
+      for (int c = t; c < dim; c += blockDim.x) X[r * dim + c] = 0.f;
+      continue;
+    }
+    __syncthreads();  // (the previous row's reads)
+    for (int e = t; e < NP * D16; e += blockDim.x) {
+      const int sf = e / D16, c = e - sf * D16;
+      Fs[e] = sf < n && c < dim ? F[(long)indices[p0 + sf] * dim + c] : 0.f;
+    }
+    if (t < NP) {
+      const double w = t < n ? (double)(alpha * (values ? values[p0 + t] : 1.f)) : 0.0;
+      ws[t] = w;
+      cs[t] = t < n ? 1.0 + w : 0.0;
+    }
+    __syncthreads();
+    // P = F_r M: 16 x 16 tiles (RI, CJ), RI over the pairs' row tiles, K = D16, B straight from M
+    const int nr = (n + 15) >> 4;
+    for (int q = wave; q < nr * NB; q += 4) {
+      const int RI = q / NB, CJ = q - RI * NB;
+      wf64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < D16 / 4; ++kk) {
+        const double a = (double)Fs[(16 * RI + li) * D16 + 4 * kk + lk];
+        const double b = M[(size_t)(4 * kk + lk) * D16 + 16 * CJ + li];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Ps[(16 * RI + lk + 4 * e) * PP + 16 * CJ + li] = acc[e];
+    }
+    // b = F_r^T c
+    for (int c = t; c < D16; c += blockDim.x) {
+      double v = 0.0;
+      for (int sf = 0; sf < n; ++sf) v = fma(cs[sf], (double)Fs[sf * D16 + c], v);
+      bs[c] = v;
+    }
+    __syncthreads();
+    // S = P F_r^T: tiles (RI, RJ), one per wave (nr <= 2) or strided; in registers until every
+    // wave is done with F_r, then over it
+    wf64x4 sacc[(NR * NR + 3) / 4];
+#pragma unroll
+    for (int m = 0; m < (NR * NR + 3) / 4; ++m) {
+      sacc[m] = wf64x4{0.0, 0.0, 0.0, 0.0};
+      const int q = wave + 4 * m, RI = q / NR, RJ = q - RI * NR;
+      if (q < NR * NR && RI < nr && RJ < nr) {
+#pragma unroll
+        for (int kk = 0; kk < D16 / 4; ++kk) {
+          const double a = Ps[(16 * RI + li) * PP + 4 * kk + lk];
+          const double b = (double)Fs[(16 * RJ + li) * D16 + 4 * kk + lk];
+          sacc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, sacc[m], 0, 0, 0);
+        }
+      }
+    }
+    // (P b)_s: eight lanes per pair
+    {
+      const int sf = t >> 3, part = t & 7;
+      double v = 0.0;
+      if (sf < NP)
+        for (int c = part; c < D16; c += 8) v = fma(Ps[sf * PP + c], bs[c], v);
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      if (sf < NP && part == 0) rh[sf] = sf < n && ws[sf] != 0.0 ? v : 0.0;
+    }
+    __syncthreads();  // (F_r's last reads)
+#pragma unroll
+    for (int m = 0; m < (NR * NR + 3) / 4; ++m) {
+      const int q = wave + 4 * m, RI = q / NR, RJ = q - RI * NR;
+      if (q < NR * NR) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 16 * RI + lk + 4 * e, j = 16 * RJ + li;
+          // rows of pairs without weight and the padding: the identity (their u = 0)
+          const bool live = i < n && j < n && ws[i] != 0.0 && ws[j] != 0.0;
+          Ss[i * SP + j] = live ? sacc[m][e] + (i == j ? 1.0 / ws[i] : 0.0) : (i == j ? 1.0 : 0.0);
+        }
+      }
+    }
+    __syncthreads();
+    // S u = P b by Gauss-Jordan in wave 0: lane j holds row j of [S | P b]; step k broadcasts row
+    // k (v_readlane) after dividing it by its pivot and eliminates column k from every other row
+    if (wave == 0) {
+      const int j = lane < NP ? lane : NP - 1;
+      double R[NP + 1];
+#pragma unroll
+      for (int c = 0; c < NP; ++c) R[c] = Ss[j * SP + c];
+      R[NP] = rh[j];
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        const double inv = 1.0 / readlane_d(R[k], k);
+        const double g = lane == k ? 0.0 : R[k] * inv;  // this row's multiple of the (raw) pivot row
+#pragma unroll
+        for (int c = k + 1; c <= NP; ++c) {
+          const double pk = readlane_d(R[c], k);
+          R[c] = lane == k ? pk * inv : fma(-g, pk, R[c]);
+        }
+      }
+      if (lane < NP) us[lane] = R[NP];
+    }
+    __syncthreads();
+    // x = P^T (c - u)
+    for (int c = t; c < dim; c += blockDim.x) {
+      double v = 0.0;
+      for (int sf = 0; sf < n; ++sf) v = fma(Ps[sf * PP + c], cs[sf] - us[sf], v);
+      X[r * dim + c] = (float)v;
+    }
+  }
+}
+
 template <int NB>
 static int launch_wrmf_mfma(float* solve, long n_rows, const float* fixed, int dim, const wacc_t* G,
                             const int64_t* indptr, const int32_t* indices, const float* values, float alpha,
-                            float lambda, hipStream_t s) {
+                            float lambda, const wacc_t* M, hipStream_t s) {
+  // rows with at most 32 pairs by the Woodbury identity (M = (G + lambda I)^{-1}; DCUE_WRMF_LOWRANK=0:
+  // every row by the Cholesky)
+  constexpr int kLowNR = 2;
+  const int min_pairs = M ? 16 * kLowNR : 0;
+  if (M) {
+    const size_t llds = wl_lds_bytes<NB, kLowNR>();
+    auto lk = k_wrmf_solve_lowrank<NB, kLowNR>;
+    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)lk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)llds));
+    const long lgrid = n_rows < 8192 ? n_rows : 8192;
+    DCUE_LAUNCH(lk, dim3((unsigned)lgrid), dim3(256), llds, s, solve, n_rows, fixed, dim, M, indptr, indices,
+                values, alpha);
+    DCUE_LAUNCH_CHECK();
+  }
   static const int phases = [] {  // (DCUE_WRMF_PHASES: see dcue_wrmf_half_step; + 64: the inverse)
     const char* e = getenv("DCUE_WRMF_PHASES");
     return e ? atoi(e) : 127;
@@ -793,7 +982,7 @@ static int launch_wrmf_mfma(float* solve, long n_rows, const float* fixed, int d
   DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const long grid = n_rows < 4096 ? n_rows : 4096;
   DCUE_LAUNCH(kern, dim3((unsigned)grid), dim3(256), lds, s, solve, n_rows, fixed, dim, G, indptr, indices, values,
-              alpha, lambda, phases);
+              alpha, lambda, phases, min_pairs);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
@@ -812,7 +1001,8 @@ int dcue_wrmf_workspace_bytes(int32_t dim, int64_t n_fixed, size_t* bytes_host) 
   if (!bytes_host || dim <= 0 || dim > dcue::kWrmfMaxDim || n_fixed < 0) return DCUE_ERR_INVALID;
   const long nch = dcue::wrmf_gram_chunks(n_fixed < 1 ? 1 : n_fixed);
   const size_t d16 = (size_t)((dim + 15) & ~15);
-  *bytes_host = sizeof(dcue::wacc_t) * ((size_t)nch * dim * dim + d16 * d16) + 256;
+  // partials, G, and the Woodbury path's inverse M with its Gauss-Jordan scratch [d16][2 d16]
+  *bytes_host = sizeof(dcue::wacc_t) * ((size_t)nch * dim * dim + 4 * d16 * d16) + 256;
   return DCUE_OK;
 }
 
@@ -858,15 +1048,27 @@ int dcue_wrmf_half_step(float* solve, int64_t n_rows, const float* fixed, int64_
     return e && e[0] == 't';
   }();
   if (!tile_solve) {
+    static const bool lowrank = [] {
+      const char* e = getenv("DCUE_WRMF_LOWRANK");
+      return !(e && e[0] == '0');
+    }();
+    wacc_t* M = nullptr;
+    if (lowrank) {
+      const size_t d16 = (size_t)((dim + 15) & ~15);
+      wacc_t* Wg = G + d16 * d16;
+      M = Wg + 2 * d16 * d16;
+      DCUE_LAUNCH(k_wrmf_ginv, dim3(1), dim3(1024), 0, s, G, (int)dim, lambda, Wg, M);
+      DCUE_LAUNCH_CHECK();
+    }
     switch ((dim + 15) / 16) {
-      case 1: return launch_wrmf_mfma<1>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
-      case 2: return launch_wrmf_mfma<2>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
-      case 3: return launch_wrmf_mfma<3>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
-      case 4: return launch_wrmf_mfma<4>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
-      case 5: return launch_wrmf_mfma<5>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
-      case 6: return launch_wrmf_mfma<6>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
-      case 7: return launch_wrmf_mfma<7>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
-      default: return launch_wrmf_mfma<8>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, s);
+      case 1: return launch_wrmf_mfma<1>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, M, s);
+      case 2: return launch_wrmf_mfma<2>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, M, s);
+      case 3: return launch_wrmf_mfma<3>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, M, s);
+      case 4: return launch_wrmf_mfma<4>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, M, s);
+      case 5: return launch_wrmf_mfma<5>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, M, s);
+      case 6: return launch_wrmf_mfma<6>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, M, s);
+      case 7: return launch_wrmf_mfma<7>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, M, s);
+      default: return launch_wrmf_mfma<8>(solve, (long)n_rows, fixed, dim, G, indptr, indices, values, alpha, lambda, M, s);
     }
   }
   // DCUE_WRMF_PHASES (timing diagnostic, wrong results): bit 1 the accumulation, 2 the Cholesky,

@@ -124,11 +124,12 @@ def test_dcbr_training_reduces_loss():
 
 
 def test_wrmf_mfma_solve_matches_tile_solve(tmp_path):
-    """The fp64-MFMA block-Cholesky solve (k_wrmf_solve_mfma, the default) and the register-tile
-    one (DCUE_WRMF_SOLVE=tile), over the fp64-MFMA Gram matrix (k_wrmf_gram_mfma, the default) or
-    the scalar one (DCUE_WRMF_GRAM=scalar), solve the same systems in fp64: their fp32 factors
-    agree to a few fp32 ulps (1e-6 of the max), at every block count (dims 7, 40, 100, 128), rows
-    without pairs zero."""
+    """The default solve (rows with <= 32 pairs by the Woodbury identity, k_wrmf_solve_lowrank;
+    the rest by the fp64-MFMA block Cholesky, k_wrmf_solve_mfma), the Cholesky for every row
+    (DCUE_WRMF_LOWRANK=0) and the register-tile solve (DCUE_WRMF_SOLVE=tile), over the fp64-MFMA
+    Gram matrix (the default) or the scalar one (DCUE_WRMF_GRAM=scalar), solve the same systems in
+    fp64: their fp32 factors agree to a few fp32 ulps (1e-6 of the max), at every block count (dims
+    7, 40, 100, 128), with zero-weight pairs, rows without pairs zero."""
     import os
     import subprocess
     import sys
@@ -142,6 +143,8 @@ out = {}
 for dim in (7, 40, 100, 128):
     n_users, n_items = 300, 1301  # (three Gram chunks of 512 rows, the last ending mid-step)
     rows, cols, vals = _problem(dim + 1, n_users, n_items, 9000, dim %% 2 == 0)
+    if vals is not None:
+        vals[::7] = 0  # pairs with c = 1: no weight in A, still in b
     m = WRMF(factors=dim, regularization=0.05, alpha=3.0, device="cuda:0")
     Y = torch.as_tensor(np.random.RandomState(5).randn(n_items, dim).astype(np.float32) * 0.3, device="cuda:0")
     X = torch.zeros(n_users, dim, device="cuda:0")
@@ -152,10 +155,11 @@ for dim in (7, 40, 100, 128):
 torch.save(out, sys.argv[1])
 ''' % (os.path.join(root, "amplifai-deepcontentrecommenders_amd"), os.path.join(root, "tests"))
     res = []
-    for i, extra in enumerate(({"DCUE_WRMF_SOLVE": "tile"}, {}, {"DCUE_WRMF_GRAM": "scalar"})):
+    for i, extra in enumerate(({"DCUE_WRMF_SOLVE": "tile"}, {}, {"DCUE_WRMF_GRAM": "scalar"},
+                               {"DCUE_WRMF_LOWRANK": "0"})):
         out = str(tmp_path / ("w%d.pt" % i))
         env = dict(os.environ, **extra)
-        for k in ("DCUE_WRMF_SOLVE", "DCUE_WRMF_GRAM"):
+        for k in ("DCUE_WRMF_SOLVE", "DCUE_WRMF_GRAM", "DCUE_WRMF_LOWRANK"):
             if k not in extra:
                 env.pop(k, None)
         p = subprocess.run([sys.executable, "-c", code, out], env=env, stdout=subprocess.PIPE,
