@@ -259,7 +259,7 @@ def row_flops(args, items_per_row):
     return 3 * item_flops(args.hidden, d) * items_per_row + 3 * 2 * (E * E + E * d)
 
 
-F64_PEAK_TFLOPS = 78.6  # MI355X fp64 vector (half the guide's 157.3 TF f32 vector rate; AMD spec)
+F64_PEAK_TFLOPS = 78.6  # MI355X fp64 vector and matrix (AMD spec: the two are equal on MI355X)
 
 
 def wrmf_half_step_flops(indptr, d, n_fixed):
@@ -327,9 +327,12 @@ def dcbr_phase(args, tracks, pair_user, pair_track, n_users, dev, M, comm=None, 
               wrmf_half_step_flops(w.by_item[0], d, n_users))
     ach = f_iter / t_iter / 1e12
     tile = os.environ.get("DCUE_WRMF_SOLVE", "")[:1] == "t"
-    wroof = {"kernel": "dcue_wrmf_half_step x 2 (k_wrmf_gram + %s)" % (
+    # (algorithmic FLOPs: the Cholesky formulation; the Woodbury path for rows with <= 32 pairs
+    # executes fewer, so `frac` there is an effective rate)
+    wroof = {"kernel": "dcue_wrmf_half_step x 2 (k_wrmf_gram_mfma + %s)" % (
                  "k_wrmf_solve: fp64 register-tile Cholesky" if tile else
-                 "k_wrmf_solve_mfma: fp64-MFMA block Cholesky, v_mfma_f64_16x16x4_f64"),
+                 "k_wrmf_solve_lowrank: Woodbury identity for rows with <= 32 pairs, k_wrmf_solve_mfma: "
+                 "fp64-MFMA block Cholesky for the rest; v_mfma_f64_16x16x4_f64"),
              "bound": "valu (fp64)" if tile else "mfma (fp64; MI355X's fp64 matrix and vector peaks are equal)",
              "achieved": ach, "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s (fp64)",
              "frac": ach / F64_PEAK_TFLOPS, "algorithmic_flops": f_iter, "traffic": None}
