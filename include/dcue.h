@@ -235,7 +235,9 @@ int dcue_train_backward(const dcue_model* m, const dcue_batch* b, const dcue_tra
  *   c_rj = 1 + alpha * v_rj (v = values, or 1 when values == NULL),
  * with F = `fixed` [n_fixed][dim] and row r's observed columns indices[indptr[r] .. indptr[r+1]).
  * Rows without an observed column get x_r = 0. dim <= 128; lambda > 0. Alternate users and items
- * (the item-side CSR is the transpose) for the ALS iterations. fp32 in-LDS Cholesky per row. */
+ * (the item-side CSR is the transpose) for the ALS iterations. fp64 throughout: rows with at most
+ * 32 observed columns through the Woodbury identity over (F^T F + lambda I)^{-1}, the others by a
+ * block Cholesky (fp64 MFMA). The workspace holds the Gram partials, G, and that inverse. */
 int dcue_wrmf_workspace_bytes(int32_t dim, int64_t n_fixed, size_t* bytes_host);
 int dcue_wrmf_half_step(float* solve, int64_t n_rows, const float* fixed, int64_t n_fixed, int32_t dim,
                         const int64_t* indptr, const int32_t* indices, const float* values, float alpha,
