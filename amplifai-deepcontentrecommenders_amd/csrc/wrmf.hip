@@ -844,6 +844,11 @@ __global__ __launch_bounds__(256) void k_wrmf_solve_lowrank(float* __restrict__ 
   double* Ss = reinterpret_cast<double*>(Fs);      // [NP][SP], after P F_r^T
   const int t = threadIdx.x, lane = t & 63, li = lane & 15, lk = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+#ifdef DCUE_KTRACE
+  // per-phase cycles (threads 0 and 64): 0 staging, 1 P, 2 b + S + P b, 3 S store, 4 Gauss-Jordan,
+  // 5 x, 6 the skipped rows' checks, 7 rows
+  unsigned long long kt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, kt0 = clock64();
+#endif
   for (long r = blockIdx.x; r < n_rows; r += gridDim.x) {
     const long p0 = indptr[r], p1 = indptr[r + 1];
     const int n = (int)(p1 - p0);
@@ -852,6 +857,10 @@ __global__ __launch_bounds__(256) void k_wrmf_solve_lowrank(float* __restrict__ 
       for (int c = t; c < dim; c += blockDim.x) X[r * dim + c] = 0.f;
       continue;
     }
+    WM_T(6);
+#ifdef DCUE_KTRACE
+    ++kt[7];
+#endif
     __syncthreads();  // (the previous row's reads)
     for (int e = t; e < NP * D16; e += blockDim.x) {
       const int sf = e / D16, c = e - sf * D16;
@@ -863,6 +872,7 @@ __global__ __launch_bounds__(256) void k_wrmf_solve_lowrank(float* __restrict__ 
       cs[t] = t < n ? 1.0 + w : 0.0;
     }
     __syncthreads();
+    WM_T(0);
     // P = F_r M: 16 x 16 tiles (RI, CJ), RI over the pairs' row tiles, K = D16, B straight from M
     const int nr = (n + 15) >> 4;
     for (int q = wave; q < nr * NB; q += 4) {
@@ -877,6 +887,7 @@ __global__ __launch_bounds__(256) void k_wrmf_solve_lowrank(float* __restrict__ 
 #pragma unroll
       for (int e = 0; e < 4; ++e) Ps[(16 * RI + lk + 4 * e) * PP + 16 * CJ + li] = acc[e];
     }
+    WM_T(1);
     // b = F_r^T c
     for (int c = t; c < D16; c += blockDim.x) {
       double v = 0.0;
@@ -912,6 +923,7 @@ __global__ __launch_bounds__(256) void k_wrmf_solve_lowrank(float* __restrict__ 
       if (sf < NP && part == 0) rh[sf] = sf < n && ws[sf] != 0.0 ? v : 0.0;
     }
     __syncthreads();  // (F_r's last reads)
+    WM_T(2);
 #pragma unroll
     for (int m = 0; m < (NR * NR + 3) / 4; ++m) {
       const int q = wave + 4 * m, RI = q / NR, RJ = q - RI * NR;
@@ -926,6 +938,7 @@ __global__ __launch_bounds__(256) void k_wrmf_solve_lowrank(float* __restrict__ 
       }
     }
     __syncthreads();
+    WM_T(3);
     // S u = P b by Gauss-Jordan in wave 0: lane j holds row j of [S | P b]; step k broadcasts row
     // k (v_readlane) after dividing it by its pivot and eliminates column k from every other row
     if (wave == 0) {
@@ -947,13 +960,20 @@ __global__ __launch_bounds__(256) void k_wrmf_solve_lowrank(float* __restrict__ 
       if (lane < NP) us[lane] = R[NP];
     }
     __syncthreads();
+    WM_T(4);
     // x = P^T (c - u)
     for (int c = t; c < dim; c += blockDim.x) {
       double v = 0.0;
       for (int sf = 0; sf < n; ++sf) v = fma(Ps[sf * PP + c], cs[sf] - us[sf], v);
       X[r * dim + c] = (float)v;
     }
+    WM_T(5);
   }
+#ifdef DCUE_KTRACE
+  WM_T(6);
+  if ((t == 0 || t == 64) && blockIdx.x < kKtraceBlocks)
+    for (int q = 0; q < 8; ++q) dcue_ktrace_buf[2 + (t >> 6)][blockIdx.x][q] = kt[q];
+#endif
 }
 
 template <int NB>
