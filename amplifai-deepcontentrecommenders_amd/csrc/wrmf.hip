@@ -823,7 +823,7 @@ template <int NB, int NR>
 constexpr size_t wl_lds_bytes() {
   constexpr int D16 = 16 * NB, NP = 16 * NR;
   constexpr size_t f = sizeof(float) * NP * D16, sb = sizeof(double) * NP * (NP + 1);
-  return sizeof(double) * ((size_t)NP * (D16 + 2) + 4 * NP + D16) + (f > sb ? f : sb);
+  return sizeof(double) * ((size_t)NP * (D16 + 2) + 4 * NP + D16 + 2 * 64 + 2) + (f > sb ? f : sb);
 }
 template <int NB, int NR>
 __global__ __launch_bounds__(256) void k_wrmf_solve_lowrank(float* __restrict__ X, long n_rows,
@@ -840,7 +840,8 @@ __global__ __launch_bounds__(256) void k_wrmf_solve_lowrank(float* __restrict__ 
   double* rh = ws + NP;             // (P b)_s
   double* us = rh + NP;             // u_s
   double* bs = us + NP;             // b = F_r^T c
-  float* Fs = reinterpret_cast<float*>(bs + D16);  // [NP][D16]
+  double* gb = bs + D16;            // Gauss-Jordan: [2][64] row multiples, [2] pivot inverses
+  float* Fs = reinterpret_cast<float*>(gb + 2 * 64 + 2);  // [NP][D16]
   double* Ss = reinterpret_cast<double*>(Fs);      // [NP][SP], after P F_r^T
   const int t = threadIdx.x, lane = t & 63, li = lane & 15, lk = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -939,25 +940,38 @@ __global__ __launch_bounds__(256) void k_wrmf_solve_lowrank(float* __restrict__ 
     }
     __syncthreads();
     WM_T(3);
-    // S u = P b by Gauss-Jordan in wave 0: lane j holds row j of [S | P b]; step k broadcasts row
-    // k (v_readlane) after dividing it by its pivot and eliminates column k from every other row
-    if (wave == 0) {
+    // S u = P b by Gauss-Jordan over all four waves: lane j holds row j, wave w columns
+    // CW w .. CW w + CW - 1 of [S | P b]. Step k: the pivot column's wave sends every row's multiple
+    // S[j][k] / S[k][k] through LDS (double-buffered: one barrier per step); each wave then takes
+    // row k of its columns by v_readlane and updates R[c] -= g_j S[k][c] (row k: divided by the
+    // pivot). Columns already eliminated take the update unchanged (their row-k entry is 0).
+    {
+      constexpr int CW = (NP + 1 + 3) / 4;
       const int j = lane < NP ? lane : NP - 1;
-      double R[NP + 1];
+      double R[CW];
 #pragma unroll
-      for (int c = 0; c < NP; ++c) R[c] = Ss[j * SP + c];
-      R[NP] = rh[j];
+      for (int i = 0; i < CW; ++i) {
+        const int c = CW * wave + i;
+        R[i] = c < NP ? Ss[j * SP + c] : (c == NP ? rh[j] : 0.0);
+      }
 #pragma unroll
       for (int k = 0; k < NP; ++k) {
-        const double inv = 1.0 / readlane_d(R[k], k);
-        const double g = lane == k ? 0.0 : R[k] * inv;  // this row's multiple of the (raw) pivot row
+        double* g2 = gb + (k & 1) * 64;
+        if (wave == k / CW) {
+          const double piv = readlane_d(R[k % CW], k);
+          const double inv = 1.0 / piv;
+          g2[lane] = lane == k ? 0.0 : R[k % CW] * inv;
+          if (lane == 0) gb[128 + (k & 1)] = inv;
+        }
+        __syncthreads();
+        const double g = g2[lane], inv = gb[128 + (k & 1)];
 #pragma unroll
-        for (int c = k + 1; c <= NP; ++c) {
-          const double pk = readlane_d(R[c], k);
-          R[c] = lane == k ? pk * inv : fma(-g, pk, R[c]);
+        for (int i = 0; i < CW; ++i) {
+          const double pk = readlane_d(R[i], k);
+          R[i] = lane == k ? pk * inv : fma(-g, pk, R[i]);
         }
       }
-      if (lane < NP) us[lane] = R[NP];
+      if (wave == NP / CW && lane < NP) us[lane] = R[NP % CW];
     }
     __syncthreads();
     WM_T(4);
