@@ -788,32 +788,32 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
 //   x_r = A_r^{-1} F_r^T c = P^T (c - u),  S u = P b,  S = W^{-1} + P F_r^T,  b = F_r^T c,
 // an n x n system instead of d x d: its serial chain is n pivots, not d. Pairs with w_s = 0 (c_s = 1)
 // add nothing to A_r: their rows of S become the identity and their u_s = 0. fp64 throughout.
-// k_wrmf_ginv: M by Gauss-Jordan on [G + lambda I | I] (SPD: no pivoting), one workgroup, the
-// working matrix in global memory (L2-resident on the workgroup's XCD).
+// k_wrmf_ginv: M by in-place Gauss-Jordan inversion of G + lambda I (SPD: no pivoting) in one
+// workgroup's LDS (128 KB at d = 128).
 __global__ __launch_bounds__(1024) void k_wrmf_ginv(const wacc_t* __restrict__ G, int dim, float lambda,
-                                                    wacc_t* __restrict__ W, wacc_t* __restrict__ M) {
-  const int D = (dim + 15) & ~15, D2 = 2 * D, t = threadIdx.x;
-  __shared__ double fcol[kWrmfMaxDim], prow[2 * kWrmfMaxDim];
-  for (int e = t; e < D * D2; e += blockDim.x) {
-    const int i = e / D2, j = e - i * D2;
-    W[e] = j < D ? G[(size_t)i * D + j] + (i == j ? (i < dim ? (double)lambda : 1.0) : 0.0) : (j - D == i ? 1.0 : 0.0);
+                                                    wacc_t* __restrict__ M) {
+  const int D = (dim + 15) & ~15, t = threadIdx.x;
+  extern __shared__ __attribute__((aligned(16))) double ga[];  // [D][D]
+  __shared__ double fcol[kWrmfMaxDim], prow[kWrmfMaxDim];
+  for (int e = t; e < D * D; e += blockDim.x) {
+    const int i = e / D, j = e - i * D;
+    ga[e] = G[e] + (i == j ? (i < dim ? (double)lambda : 1.0) : 0.0);
   }
   for (int k = 0; k < D; ++k) {
     __syncthreads();
-    const double piv = W[(size_t)k * D2 + k];
-    if (t < D2) prow[t] = W[(size_t)k * D2 + t] / piv;
-    if (t < D) fcol[t] = W[(size_t)t * D2 + k];
+    const double p = 1.0 / ga[k * D + k];
+    if (t < D) {
+      fcol[t] = ga[t * D + k];
+      prow[t] = (t == k ? 1.0 : ga[k * D + t]) * p;  // row k / pivot, its pivot entry 1 / pivot
+    }
     __syncthreads();
-    for (int e = t; e < D * D2; e += blockDim.x) {
-      const int i = e / D2, j = e - i * D2;
-      W[e] = i == k ? prow[j] : fma(-fcol[i], prow[j], W[e]);
+    for (int e = t; e < D * D; e += blockDim.x) {
+      const int i = e / D, j = e - i * D;
+      ga[e] = i == k ? prow[j] : fma(-fcol[i], prow[j], j == k ? 0.0 : ga[e]);
     }
   }
   __syncthreads();
-  for (int e = t; e < D * D; e += blockDim.x) {
-    const int i = e / D, j = e - i * D;
-    M[e] = W[(size_t)i * D2 + D + j];
-  }
+  for (int e = t; e < D * D; e += blockDim.x) M[e] = ga[e];
 }
 
 // One workgroup per row with 1 <= n <= 16 NR pairs (rows with none: x = 0; the rest are left to
@@ -1035,8 +1035,8 @@ int dcue_wrmf_workspace_bytes(int32_t dim, int64_t n_fixed, size_t* bytes_host) 
   if (!bytes_host || dim <= 0 || dim > dcue::kWrmfMaxDim || n_fixed < 0) return DCUE_ERR_INVALID;
   const long nch = dcue::wrmf_gram_chunks(n_fixed < 1 ? 1 : n_fixed);
   const size_t d16 = (size_t)((dim + 15) & ~15);
-  // partials, G, and the Woodbury path's inverse M with its Gauss-Jordan scratch [d16][2 d16]
-  *bytes_host = sizeof(dcue::wacc_t) * ((size_t)nch * dim * dim + 4 * d16 * d16) + 256;
+  // partials, G, and the Woodbury path's inverse M
+  *bytes_host = sizeof(dcue::wacc_t) * ((size_t)nch * dim * dim + 2 * d16 * d16) + 256;
   return DCUE_OK;
 }
 
@@ -1089,9 +1089,11 @@ int dcue_wrmf_half_step(float* solve, int64_t n_rows, const float* fixed, int64_
     wacc_t* M = nullptr;
     if (lowrank) {
       const size_t d16 = (size_t)((dim + 15) & ~15);
-      wacc_t* Wg = G + d16 * d16;
-      M = Wg + 2 * d16 * d16;
-      DCUE_LAUNCH(k_wrmf_ginv, dim3(1), dim3(1024), 0, s, G, (int)dim, lambda, Wg, M);
+      M = G + d16 * d16;
+      const size_t glds = sizeof(wacc_t) * d16 * d16;
+      DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)k_wrmf_ginv, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)glds));
+      DCUE_LAUNCH(k_wrmf_ginv, dim3(1), dim3(1024), glds, s, G, (int)dim, lambda, M);
       DCUE_LAUNCH_CHECK();
     }
     switch ((dim + 15) / 16) {
