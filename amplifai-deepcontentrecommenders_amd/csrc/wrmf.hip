@@ -99,11 +99,7 @@ __device__ __forceinline__ void wrmf_gram_wave(const float* __restrict__ F, long
       v[X] = row < r1 && c < dim ? x : 0.f;
     }
   };
-  float cur[8], nxt[8];
-  load(r0, cur);
-#pragma unroll 1
-  for (long r = r0; r < r1; r += 4) {
-    if (r + 4 < r1) load(r + 4, nxt);  // (the next step's loads in flight during these MFMAs)
+  auto step = [&](const float (&cur)[8]) {
     if (IA < NB) {
 #pragma unroll
       for (int J = 0; J <= IA; ++J)
@@ -115,8 +111,23 @@ __device__ __forceinline__ void wrmf_gram_wave(const float* __restrict__ F, long
         acc[IA + 1 + J] =
             __builtin_amdgcn_mfma_f64_16x16x4f64((double)cur[IB], (double)cur[J], acc[IA + 1 + J], 0, 0, 0);
     }
+  };
+  // two steps (8 rows) per iteration, the next two steps' loads in flight during these MFMAs (rows
+  // past the chunk load as zeros, so the last pair may run half empty)
+  float c0[8], c1[8], n0[8], n1[8];
+  load(r0, c0);
+  load(r0 + 4, c1);
+#pragma unroll 1
+  for (long r = r0; r < r1; r += 8) {
+    load(r + 8, n0);
+    load(r + 12, n1);
+    step(c0);
+    step(c1);
 #pragma unroll
-    for (int X = 0; X < 8; ++X) cur[X] = nxt[X];
+    for (int X = 0; X < 8; ++X) {
+      c0[X] = n0[X];
+      c1[X] = n1[X];
+    }
   }
   // tile (I, J) and, off the diagonal, its transpose (C layout: lane l holds column l & 15, rows
   // (l >> 4) + 4 q)
@@ -162,9 +173,17 @@ __global__ __launch_bounds__(256) void k_wrmf_gram_reduce(const wacc_t* __restri
   if (e >= (long)D16 * D16) return;
   const int i = (int)(e / D16), j = (int)(e - (long)i * D16);
   wacc_t s = 0.0;
-  if (i < dim && j < dim) {
+  if (i < dim && j < dim) {  // (four partial sums over z mod 4, combined in a fixed order)
     const long dd = (long)dim * dim;
-    for (int z = 0; z < nchunk; ++z) s += part[(size_t)z * dd + (long)i * dim + j];
+    const wacc_t* src = part + (long)i * dim + j;
+    wacc_t q[4] = {0.0, 0.0, 0.0, 0.0};
+    int z = 0;
+#pragma unroll 2
+    for (; z + 4 <= nchunk; z += 4)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] += src[(size_t)(z + u) * dd];
+    for (; z < nchunk; ++z) q[z & 3] += src[(size_t)z * dd];
+    s = (q[0] + q[1]) + (q[2] + q[3]);
   }
   G[e] = s;
 }
@@ -807,9 +826,13 @@ __global__ __launch_bounds__(1024) void k_wrmf_ginv(const wacc_t* __restrict__ G
       prow[t] = (t == k ? 1.0 : ga[k * D + t]) * p;  // row k / pivot, its pivot entry 1 / pivot
     }
     __syncthreads();
-    for (int e = t; e < D * D; e += blockDim.x) {
-      const int i = e / D, j = e - i * D;
-      ga[e] = i == k ? prow[j] : fma(-fcol[i], prow[j], j == k ? 0.0 : ga[e]);
+    const int j = t & 127;  // (column t % 128, rows t / 128 + 8 q: no division in the step)
+    if (j < D) {
+      const double pj = prow[j];
+      for (int i = t >> 7; i < D; i += 8) {
+        double* e = ga + i * D + j;
+        *e = i == k ? pj : fma(-fcol[i], pj, j == k ? 0.0 : *e);
+      }
     }
   }
   __syncthreads();
