@@ -518,7 +518,7 @@ int launch_user_fwd(const dcue_model* md, const TGemmArgs& g1, const TGemmArgs& 
   a.p = md->emb; a.m = md->emb_exp_avg; a.v = md->emb_exp_avg_sq;
   a.hdr = md->emb_log; a.emb_step = md->emb_step;
   a.users = users; a.B = B; a.E = md->dims.user_embdim;
-  static unsigned* const fail = user_fwd_fail_flag();
+  unsigned* const fail = user_fwd_fail_flag();  // this device's word (cached per device)
   if (!fail) return DCUE_ERR_HIP;
   a.fail = fail;
   DCUE_LAUNCH(k_user_fwd, dim3((unsigned)((B + 15) / 16)), dim3(512), 0, s, a);

@@ -494,9 +494,12 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     p.C = bn_channels(&m->dims, l);
     return p;
   };
-  // the forward sums and value ranges start cleared (train: by the step prologue, or here)
+  // the forward sums and value ranges start cleared (train: by the step prologue, or here). The text
+  // branch's position-merge tickets sit at the end of that part; when the branch runs on a side
+  // stream (text_join) that stream clears them itself, in its own order (forward_impl), so this
+  // clear cannot land between its parts' arrivals
   if (!train || !acc_cleared)
-    DCUE_HIP_CHECK(hipMemsetAsync(w.bnacc, 0, sizeof(unsigned long long) * w.nfwd, s));
+    DCUE_HIP_CHECK(hipMemsetAsync(w.bnacc, 0, sizeof(unsigned long long) * (w.nfwd - (text_join ? w.ntick : 0)), s));
   if (!c.bn) {  // mean 0, invstd = a = 1, beta 0 for every layer: the BN-free towers
     TRY(launch_bn_identity(w.mean, w.invstd, w.a, w.ones, w.zeros, w.cmax, c.H, c.D, s));
     // (the epilogues still add their unused BN sums) the raw input's range, for conv 1's split
@@ -844,7 +847,13 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
       const char* e = getenv("DCUE_USER_FWD");
       return e && e[0] == 's';
     }();
-    {
+    TimerScope tsu;  // (the fused launch is timed live: DCUE_TIMED_USER_FWD)
+    TRY(timer_begin(&tsu, split_fwd ? -1 : DCUE_TIMED_USER_FWD, su));
+    if (tsu.b && !tsu.capturing) {  // a timed launch: the timer's stop event is its end
+      TRY(user_forward_fused(c, w, b->users, b->n_rows, su));
+      ev_uf = tsu.b;
+      TRY(timer_end(&tsu));
+    } else {  // (untimed, or a captured plan: its timer node follows the launch)
       ForkAfter fk(sp, su, &ev_uf);
       if (split_fwd) {
         if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
@@ -855,6 +864,7 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
       HPROF("capi:7");
       TRY(fk.done());
       HPROF("capi:8");
+      TRY(timer_end(&tsu));
     }
     TRY(probe(PR_H1, w.h1, (long)b->n_rows * c.E, su));
     TRY(probe(PR_UF, w.uf, (long)b->n_rows * c.D, su));
@@ -865,6 +875,11 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
       hipStream_t stx = sp->st[2];
       TRY(wait_point(stx, ev_in));
       if (o.wait_late) TRY(wait_point(stx, o.wait_late));
+      // the position-merge tickets: cleared by the step prologue (plans, before ev_in), else here --
+      // item_forward's clear on the caller's stream leaves them out
+      if (!(train && o.prologue_done) && w.ntick)
+        DCUE_HIP_CHECK(hipMemsetAsync(w.tticket, 0, sizeof(unsigned long long) * w.ntick, stx));
+      TRY(debug_delay(DCUE_SITE_TEXT_FWD, stx));
       TimerScope tsc;
       TRY(timer_begin(&tsc, DCUE_TIMED_TEXT_FWD, stx));
       if (tsc.b && !tsc.capturing) {  // a timed launch: the timer's stop event is its end

@@ -22,6 +22,7 @@
 namespace dcue {
 
 namespace {
+constexpr int kMaxDevices = 64;
 std::atomic<int> g_delay_us[DCUE_N_DEBUG_SITES];
 std::atomic<ProbeRec*> g_probes{nullptr};
 std::atomic<bool> g_poison{false};
@@ -64,9 +65,18 @@ __global__ __launch_bounds__(256) void k_probe(const float* __restrict__ x, long
 // the fused user-tower forward's "a bounded wait gave up" word (adam.hip)
 __device__ unsigned g_user_fwd_fail;
 
+// The symbol's address differs per device: looked up on the current device, cached per device id.
 unsigned* user_fwd_fail_flag() {
+  static std::atomic<unsigned*> cache[kMaxDevices];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
+  if (dev < kMaxDevices) {
+    unsigned* c = cache[dev].load(std::memory_order_acquire);
+    if (c) return c;
+  }
   void* p = nullptr;
   if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_user_fwd_fail)) != hipSuccess) return nullptr;
+  if (dev < kMaxDevices) cache[dev].store(static_cast<unsigned*>(p), std::memory_order_release);
   return static_cast<unsigned*>(p);
 }
 
@@ -133,6 +143,14 @@ int dcue_debug_fail_flags(uint32_t* flags_host) {
   const unsigned zero = 0;
   DCUE_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(dcue::g_user_fwd_fail), &zero, sizeof zero));
   *flags_host = v;
+  return DCUE_OK;
+}
+
+int dcue_debug_raise_fail_flags(uint32_t bits) {
+  unsigned v = 0;
+  DCUE_HIP_CHECK(hipMemcpyFromSymbol(&v, HIP_SYMBOL(dcue::g_user_fwd_fail), sizeof v));
+  v |= bits;
+  DCUE_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(dcue::g_user_fwd_fail), &v, sizeof v));
   return DCUE_OK;
 }
 

@@ -35,7 +35,11 @@ typedef double wacc_t;
 // rows 0..128 (128: the augmented row) of the tile-padded triangle, then an 8-double dummy row
 constexpr int kWrmfDummy = 32 * (kWrmfMaxDim / 8) * (kWrmfMaxDim / 8 + 1) + 8 * (kWrmfMaxDim / 8 + 1);
 constexpr int kWrmfTri = kWrmfDummy + 8;
-constexpr int kWrmfGramChunk = 512;          // fixed-side rows per gram workgroup (a multiple of 4)
+constexpr int kWrmfGramChunk = 512;          // fixed-side rows per gram step (a multiple of 8)
+// at most this many gram workgroups (2 per CU): past 512 x 512 fixed rows each workgroup strides over
+// several chunks, so the fp64 partials ([workgroups][d][d], 64 MB at d = 128) and the reduce's
+// traffic stay bounded however large the fixed side grows
+constexpr long kWrmfGramMaxBlocks = 512;
 constexpr int kWrmfStage = 16;               // observed factors staged in LDS per pass
 
 __global__ __launch_bounds__(256) void k_wrmf_gram(const float* __restrict__ F, long n, int dim,
@@ -46,9 +50,8 @@ __global__ __launch_bounds__(256) void k_wrmf_gram(const float* __restrict__ F, 
   wacc_t acc[64];
 #pragma unroll
   for (int q = 0; q < 64; ++q) acc[q] = 0.0;
-  const long r0 = (long)blockIdx.x * kWrmfGramChunk;
-  const long r1 = min(r0 + kWrmfGramChunk, n);
-  for (long rb = r0; rb < r1; rb += kWrmfStage) {
+  for (long r0 = (long)blockIdx.x * kWrmfGramChunk; r0 < n; r0 += (long)gridDim.x * kWrmfGramChunk)
+  for (long rb = r0, r1 = min(r0 + kWrmfGramChunk, n); rb < r1; rb += kWrmfStage) {
     const int nr = (int)min((long)kWrmfStage, r1 - rb);
     for (int e = t; e < kWrmfStage * kWrmfMaxDim; e += blockDim.x) {
       const int r = e / kWrmfMaxDim, c = e - r * kWrmfMaxDim;
@@ -78,7 +81,7 @@ __global__ __launch_bounds__(256) void k_wrmf_gram(const float* __restrict__ F, 
 // full [chunk][d][d] layout and k_wrmf_gram_reduce is shared.
 typedef double wgf64x4 __attribute__((ext_vector_type(4)));
 template <int W>  // the wave: block rows IA = W and IB = 7 - W, compile-time so every index is
-__device__ __forceinline__ void wrmf_gram_wave(const float* __restrict__ F, long r0, long r1, int dim,
+__device__ __forceinline__ void wrmf_gram_wave(const float* __restrict__ F, long n, int dim,
                                                wacc_t* __restrict__ out) {
   constexpr int IA = W, IB = 7 - W;
   const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
@@ -89,6 +92,7 @@ __device__ __forceinline__ void wrmf_gram_wave(const float* __restrict__ F, long
   for (int q = 0; q < 9; ++q) acc[q] = wgf64x4{0.0, 0.0, 0.0, 0.0};
   // the step's operands: v[X] = F[r + lk][16 X + li] (0 past the chunk or past dim); the loads are
   // unconditional (clamped), their values selected
+  long r1 = 0;  // the current chunk's end
   auto load = [&](const long r, float (&v)[8]) {
     const long row = r + lk;
     const float* src = F + (row < r1 ? row : r1 - 1) * dim;
@@ -115,18 +119,23 @@ __device__ __forceinline__ void wrmf_gram_wave(const float* __restrict__ F, long
   // two steps (8 rows) per iteration, the next two steps' loads in flight during these MFMAs (rows
   // past the chunk load as zeros, so the last pair may run half empty)
   float c0[8], c1[8], n0[8], n1[8];
-  load(r0, c0);
-  load(r0 + 4, c1);
+  // the workgroup's chunks: blockIdx.x, + gridDim.x, ... (one chunk each below 512 x 512 rows)
 #pragma unroll 1
-  for (long r = r0; r < r1; r += 8) {
-    load(r + 8, n0);
-    load(r + 12, n1);
-    step(c0);
-    step(c1);
+  for (long r0 = (long)blockIdx.x * kWrmfGramChunk; r0 < n; r0 += (long)gridDim.x * kWrmfGramChunk) {
+    r1 = min(r0 + kWrmfGramChunk, n);
+    load(r0, c0);
+    load(r0 + 4, c1);
+#pragma unroll 1
+    for (long r = r0; r < r1; r += 8) {
+      load(r + 8, n0);
+      load(r + 12, n1);
+      step(c0);
+      step(c1);
 #pragma unroll
-    for (int X = 0; X < 8; ++X) {
-      c0[X] = n0[X];
-      c1[X] = n1[X];
+      for (int X = 0; X < 8; ++X) {
+        c0[X] = n0[X];
+        c1[X] = n1[X];
+      }
     }
   }
   // tile (I, J) and, off the diagonal, its transpose (C layout: lane l holds column l & 15, rows
@@ -153,14 +162,12 @@ __device__ __forceinline__ void wrmf_gram_wave(const float* __restrict__ F, long
 
 __global__ __launch_bounds__(256, 2) void k_wrmf_gram_mfma(const float* __restrict__ F, long n, int dim,
                                                           wacc_t* __restrict__ part) {
-  const long r0 = (long)blockIdx.x * kWrmfGramChunk;
-  const long r1 = min(r0 + kWrmfGramChunk, n);
   wacc_t* out = part + (size_t)blockIdx.x * dim * dim;
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: wrmf_gram_wave<0>(F, r0, r1, dim, out); break;
-    case 1: wrmf_gram_wave<1>(F, r0, r1, dim, out); break;
-    case 2: wrmf_gram_wave<2>(F, r0, r1, dim, out); break;
-    default: wrmf_gram_wave<3>(F, r0, r1, dim, out); break;
+    case 0: wrmf_gram_wave<0>(F, n, dim, out); break;
+    case 1: wrmf_gram_wave<1>(F, n, dim, out); break;
+    case 2: wrmf_gram_wave<2>(F, n, dim, out); break;
+    default: wrmf_gram_wave<3>(F, n, dim, out); break;
   }
 }
 
@@ -186,6 +193,14 @@ __global__ __launch_bounds__(256) void k_wrmf_gram_reduce(const wacc_t* __restri
     s = (q[0] + q[1]) + (q[2] + q[3]);
   }
   G[e] = s;
+}
+
+// whether a row's pair weights alpha * v include a negative one (block-uniform; values NULL: all 1)
+__device__ inline bool wrmf_row_has_negative(const float* __restrict__ values, long p0, long p1, float alpha) {
+  if (!values || !(alpha > 0.f)) return false;
+  bool neg = false;
+  for (long p = p0 + threadIdx.x; p < p1; p += blockDim.x) neg |= alpha * values[p] < 0.f;
+  return __syncthreads_or(neg);
 }
 
 // uniform broadcast of lane `lane`'s value (v_readlane, no LDS round trip); `lane` is uniform
@@ -552,7 +567,11 @@ __global__ __launch_bounds__(256, 2) void k_wrmf_solve_mfma(float* __restrict__ 
 #endif
   for (long r = blockIdx.x; r < n_rows; r += gridDim.x) {
     const long p0 = indptr[r], p1 = indptr[r + 1];
-    if (p1 - p0 <= min_pairs) continue;  // (solved by k_wrmf_solve_lowrank)
+    // (rows with at most min_pairs pairs are solved by k_wrmf_solve_lowrank -- unless a weight is
+    // negative: its Woodbury system S = W^-1 + P F^T is then indefinite and unpivoted elimination
+    // could meet a near-zero pivot, while A = G + lambda I + F^T W F may still be SPD; those come here)
+    // (rows without pairs are zeroed below, also when k_wrmf_solve_lowrank is off: min_pairs 0)
+    if (p1 > p0 && p1 - p0 <= min_pairs && !wrmf_row_has_negative(values, p0, p1, alpha)) continue;
     if (p1 <= p0) {  // no observed pair: b = 0, so x = 0
       for (int c = t; c < dim; c += blockDim.x) X[r * dim + c] = 0.f;
       continue;
@@ -877,6 +896,7 @@ __global__ __launch_bounds__(256) void k_wrmf_solve_lowrank(float* __restrict__ 
     const long p0 = indptr[r], p1 = indptr[r + 1];
     const int n = (int)(p1 - p0);
     if (n > NP) continue;
+    if (wrmf_row_has_negative(values, p0, p1, alpha)) continue;  // (k_wrmf_solve_mfma's, see there)
     if (n <= 0) {
       for (int c = t; c < dim; c += blockDim.x) X[r * dim + c] = 0.f;
       continue;
@@ -1048,7 +1068,11 @@ size_t wrmf_solve_lds_bytes() {
   return sizeof(wacc_t) * ((size_t)kWrmfTri + kWrmfMaxDim) + sizeof(float) * ((size_t)kWrmfStage * kWrmfMaxDim + kWrmfStage);
 }
 
-long wrmf_gram_chunks(long n_fixed) { return (n_fixed + kWrmfGramChunk - 1) / kWrmfGramChunk; }
+// gram workgroups (= partial sets): one per 512-row chunk, at most kWrmfGramMaxBlocks
+long wrmf_gram_chunks(long n_fixed) {
+  const long c = (n_fixed + kWrmfGramChunk - 1) / kWrmfGramChunk;
+  return c < kWrmfGramMaxBlocks ? c : kWrmfGramMaxBlocks;
+}
 
 }  // namespace dcue
 

@@ -93,6 +93,8 @@ TIMED_ADAM_EMBED = 3
 TIMED_ALLREDUCE = 4
 TIMED_EMB_SLICE = 5
 TIMED_TEXT_FWD = 6
+TIMED_USER_FWD = 7
+TIMED_TEXT_WGRAD = 8
 COMM_ID_BYTES = 128
 
 
@@ -103,13 +105,13 @@ class PlanConfig(ctypes.Structure):
 
 MT_STATE_BYTES = 624 * 4 + 16
 MAX_LOG_CAP = 256
-ABI_VERSION = 15
+ABI_VERSION = 16
 COMM_F32, COMM_U64 = 0, 1  # dcue_host_allreduce_fn dtypes
 HOST_ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32)
 RANK_SPLIT, RANK_SINGLE = 0, 1
 # dcue_debug_delay sites (include/dcue.h)
 DEBUG_SITES = ("user_fwd", "user_bwd", "wgrad_hi", "wgrad_2", "fc_wgrad", "late_adam", "prologue", "lookahead",
-               "conv2", "dgrad_2", "wgrad_1")
+               "conv2", "dgrad_2", "wgrad_1", "text_fwd")
 
 _P = ctypes.c_void_p
 _SIGS = {
@@ -189,6 +191,7 @@ _SIGS = {
     "dcue_debug_probe_name": ([ctypes.c_int32], ctypes.c_char_p),
     "dcue_debug_poison": ([ctypes.c_int32], ctypes.c_int),
     "dcue_debug_fail_flags": ([_P], ctypes.c_int),
+    "dcue_debug_raise_fail_flags": ([ctypes.c_uint32], ctypes.c_int),
 }
 
 _lib = None

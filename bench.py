@@ -222,6 +222,18 @@ def synthetic_sentences(n, T, n_words, device, seed, pad=0, bos=1, eos=2):
 DGRAD_F16 = os.environ.get("DCUE_DGRAD_F16", "1")[:1] != "0"
 
 
+def fail_flag_failures(flags):
+    """The library's device fail word (dcue_debug_fail_flags) as checks.failed entries: bit 0 is a
+    bounded wait in the fused user-tower forward that gave up (adam.hip k_user_fwd) -- its rows may
+    then have been read before their Adam replay, so the run is failed, whatever its throughput."""
+    out = []
+    if flags & 1:
+        out.append("fail flags: the fused user-tower forward's bounded wait for a claimed row gave up (bit 0)")
+    if flags & ~1:
+        out.append("fail flags: unknown bits 0x%x" % (flags & ~1))
+    return out
+
+
 def executed_work(args, items_per_row, M):
     """The FLOPs one row's step actually executes and their time at the ceiling of the arithmetic
     that runs them: forwards on split-f16 MFMA (3 f16 products per f32 product: 2500/3
@@ -269,6 +281,23 @@ def wrmf_half_step_flops(indptr, d, n_fixed):
     nnz = (indptr[1:] - indptr[:-1]).double()
     rows = float((nnz > 0).sum())
     fma = float(nnz.sum()) * (d * (d + 1) / 2 + d) + rows * (d ** 3 / 6 + d * d) + n_fixed * d * (d + 1) / 2
+    return 2.0 * fma
+
+
+def wrmf_half_step_flops_executed(indptr, d, n_fixed, woodbury_max=32):
+    """fp64 FLOPs one default WRMF half-step executes, each row counted by the path
+    that solves it: the Gram matrix (n_fixed x d(d+1)/2 FMAs); M = (G + lambda I)^-1 by Gauss-Jordan
+    (d^3); a row with 1..32 pairs by the Woodbury identity (k_wrmf_solve_lowrank: P = F_r M n d^2,
+    S = P F_r^T n^2 d, b / P b / x 3 n d, the n x (n + 1) elimination n^2 (n + 1)); a row with more by
+    the block Cholesky (k_wrmf_solve_mfma: n (d(d+1)/2 + d) + d^3/6 + d^2)."""
+    nnz = (indptr[1:] - indptr[:-1]).double()
+    low = (nnz > 0) & (nnz <= woodbury_max)
+    high = nnz > woodbury_max
+    nl = nnz[low]
+    fma = float((nl * d * d + nl * nl * d + 3 * nl * d + nl * nl * (nl + 1)).sum())
+    nh = nnz[high]
+    fma += float(nh.sum()) * (d * (d + 1) / 2 + d) + float(high.sum()) * (d ** 3 / 6 + d * d)
+    fma += n_fixed * d * (d + 1) / 2 + float(d) ** 3
     return 2.0 * fma
 
 
@@ -323,19 +352,26 @@ def dcbr_phase(args, tracks, pair_user, pair_track, n_users, dev, M, comm=None, 
     # rooflines: the ALS iteration against the fp64 vector peak (its solve is fp64 VALU work); the
     # regression step against the ceiling of the arithmetic its kernels run (executed_work, per item,
     # the user tower left out)
-    f_iter = (wrmf_half_step_flops(w.by_user[0], d, args.tracks) +
+    f_chol = (wrmf_half_step_flops(w.by_user[0], d, args.tracks) +
               wrmf_half_step_flops(w.by_item[0], d, n_users))
-    ach = f_iter / t_iter / 1e12
     tile = os.environ.get("DCUE_WRMF_SOLVE", "")[:1] == "t"
-    # (algorithmic FLOPs: the Cholesky formulation; the Woodbury path for rows with <= 32 pairs
-    # executes fewer, so `frac` there is an effective rate)
+    woodbury = not tile and os.environ.get("DCUE_WRMF_LOWRANK", "1")[:1] != "0"
+    # `achieved` / `frac`: the FLOPs the kernels execute, each row by its own path (Woodbury rows
+    # never form or factor the d x d system); the Cholesky formulation's count for every row, divided
+    # by the same time, is kept beside it as an effective rate
+    f_iter = (wrmf_half_step_flops_executed(w.by_user[0], d, args.tracks) +
+              wrmf_half_step_flops_executed(w.by_item[0], d, n_users)) if woodbury else f_chol
+    ach = f_iter / t_iter / 1e12
     wroof = {"kernel": "dcue_wrmf_half_step x 2 (k_wrmf_gram_mfma + %s)" % (
                  "k_wrmf_solve: fp64 register-tile Cholesky" if tile else
                  "k_wrmf_solve_lowrank: Woodbury identity for rows with <= 32 pairs, k_wrmf_solve_mfma: "
                  "fp64-MFMA block Cholesky for the rest; v_mfma_f64_16x16x4_f64"),
              "bound": "valu (fp64)" if tile else "mfma (fp64; MI355X's fp64 matrix and vector peaks are equal)",
              "achieved": ach, "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s (fp64)",
-             "frac": ach / F64_PEAK_TFLOPS, "algorithmic_flops": f_iter, "traffic": None}
+             "frac": ach / F64_PEAK_TFLOPS, "algorithmic_flops": f_iter,
+             "flops_counted": "executed per path (Woodbury rows: n d^2 + n^2 d + n^3; Cholesky rows)"
+                              if woodbury else "Cholesky formulation (every row)",
+             "effective_tflops_cholesky_formulation": f_chol / t_iter / 1e12, "traffic": None}
     pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_wrmf_solve.json")
     if os.path.exists(pmc):
         with open(pmc) as fh:
@@ -587,7 +623,7 @@ def main():
             comm_error = str(e)
 
     timed = [nat.TIMED_CONV1_WGRAD, nat.TIMED_CONV1_FWD, nat.TIMED_EMB_SLICE, nat.TIMED_EMB_FLUSH,
-             nat.TIMED_ALLREDUCE, nat.TIMED_TEXT_FWD]
+             nat.TIMED_ALLREDUCE, nat.TIMED_TEXT_FWD, nat.TIMED_USER_FWD, nat.TIMED_TEXT_WGRAD]
     # every stride-th launch of each class is timed live (a timed launch costs its stream a few us)
     stride = max(1, min(args.timer_stride, args.steps // 4))
 
@@ -692,10 +728,12 @@ def main():
             act = 4 * int((((em.view(torch.int32) | ev.view(torch.int32)) != 0).view(-1, 4).any(1)).sum())
         return 8.0 * n + 12.0 * act + 4.0 * em.shape[0], act / max(n, 1)
 
-    def kernel_rooflines(kern, M, steps, optim=None):
+    def kernel_rooflines(kern, M, steps, optim=None, d=None):
         """Live HIP-event timing of the candidate kernels: per launch and per step, with each
         one's algorithmic work against its roofline."""
         H, E = args.hidden, args.user_embdim
+        d = args.feature_dim if d is None else d
+        Tt, Ew, Ct = args.text_len, args.word_dim, args.text_dim
         conv1 = 2.0 * H * 128 * 4 * (M * 132)
         rows_slice = n_users_local / args.flush_every
         table_bytes, active = replay_bytes(opt if optim is None else optim)
@@ -722,7 +760,18 @@ def main():
                                  "per f32 product; peak = f16 dense peak / 3)"
                                  % (args.word_dim, args.text_dim, args.text_len), "mfma",
                                  M * text_conv_flops(args.text_len, args.word_dim, args.text_dim)),
+            # user stream, beside the item tower (the score kernel waits for it): B rows x (E x E + E x d)
+            # MACs on f32 MFMA (k_tgemm's 16x16x4 blocks), plus the batch rows' deferred Adam replay
+            nat.TIMED_USER_FWD: ("k_user_fwd (fused user-tower forward: the batch rows' deferred Adam replay, "
+                                 "then Linear(%d,%d)+ReLU+Linear(%d,%d) on f32 MFMA; user stream)" % (E, E, E, d),
+                                 "mfma", B * 2.0 * (E * E + E * d)),
+            # wgrad stream 1: dW[o][c][k] = sum_i g[i][o] e[i][t*(i,o)+k-1][c], exact f32 FMAs (VALU);
+            # bytes: the batch's sentences' word rows, tokens, g and argmax codes read once, dW + db written
+            nat.TIMED_TEXT_WGRAD: ("k_text_wgrad (config 4 text conv weight gradient: max-routed gather of "
+                                   "word rows x dL/ds, f32 FMAs; wgrad stream 1)", "valu",
+                                   M * (Tt * Ew * 4.0 + Tt * 4.0 + Ct * 5.0) + Ct * Ew * 3 * 4.0 + Ct * 4.0),
         }
+        side_stream = (nat.TIMED_EMB_SLICE, nat.TIMED_EMB_FLUSH, nat.TIMED_USER_FWD, nat.TIMED_TEXT_WGRAD)
         out = []
         for k, samples in kern.items():
             n = len(samples)
@@ -745,7 +794,7 @@ def main():
                    "median_ms": med, "min_ms": srt[0], "max_ms": srt[-1],
                    "samples_ms": [round(v, 5) for v in samples[:64]],
                    "ms_per_step": med * per_step,
-                   "critical_path": k not in (nat.TIMED_EMB_SLICE, nat.TIMED_EMB_FLUSH)}
+                   "critical_path": k not in side_stream}
             if bound == "mfma":
                 # split-f16 kernels: f32-equivalent FLOPs against the f16 peak over their products per
                 # f32 product (forward: 3; conv-1 weight gradient on the fp16 table: 2)
@@ -764,6 +813,10 @@ def main():
                 if k in (nat.TIMED_EMB_SLICE, nat.TIMED_EMB_FLUSH):
                     ent["active_fraction"] = active  # of the table's elements with live moments
                 ent["frac" if bound == "hbm" else "hbm_frac"] = ent["achieved"] / HBM_PEAK_GBS
+                if k == nat.TIMED_TEXT_WGRAD:  # its f32 FMAs against the f32 vector peak, for information
+                    fl = 2.0 * M * Ct * Ew * 3
+                    ent.update(algorithmic_flops=fl, achieved_tflops=fl / (med * 1e-3) / 1e12,
+                               valu_frac=fl / (med * 1e-3) / 1e12 / F32_PEAK_TFLOPS)
             out.append(ent)
         byk = {e["kernel"]: e for e in out}
         sl = byk.get(spec[nat.TIMED_EMB_SLICE][0])
@@ -779,7 +832,8 @@ def main():
 
     def traffic_for(kernel_name, mode):
         tag = {"k_conv1_wgrad": "conv1_wgrad", "k_conv_wgrad16": "conv1_wgrad16", "k_emb_flush_rows": "emb_flush_rows",
-               "k_conv_rows<0,0>": "conv1_fwd", "k_text_fwd": "text_fwd"}.get(kernel_name.split(" ")[0])
+               "k_conv_rows<0,0>": "conv1_fwd", "k_text_fwd": "text_fwd", "k_user_fwd": "user_fwd",
+               "k_text_wgrad": "text_wgrad"}.get(kernel_name.split(" ")[0])
         path = os.path.join(ROOT, "profiles", "pmc_%s_%s.json" % (tag, mode)) if tag else None
         if path and os.path.exists(path):
             try:
@@ -791,6 +845,8 @@ def main():
     def summary(dt, t_enq, kern, M, items_per_row, mode, phase):
         rows = world * B * args.steps / dt
         ks = kernel_rooflines(kern, M, args.steps)
+        for k in ks:  # the committed PMC summary's HBM bytes per launch, where one exists
+            k["traffic"] = traffic_for(k["kernel"], mode)
         # the roofline line names the largest kernel on the step's critical path (the caller's stream);
         # side-stream kernels that the step does not wait for are listed in "kernels" only
         mf = [k for k in ks if k["bound"] in ("mfma", "hbm") and k["critical_path"]]
@@ -855,8 +911,12 @@ def main():
             ck.finite(st[k], "user table Adam " + k)
         checks["after"].append(phase)
         checks["failed"] += [phase + ": " + f for f in ck.failed()]
+        checks["failed"] += [phase + ": " + f for f in fail_flag_failures(nat.debug_fail_flags())]
         checks["last_loss_" + phase] = float(p.loss)
 
+    if os.environ.get("DCUE_BENCH_FORCE_FAIL_FLAG") == "1":
+        # test hook (tests/test_gpu_bench_checks.py): raise the device's fail word as a gave-up wait would
+        nat.check(nat.lib().dcue_debug_raise_fail_flags(1), "dcue_debug_raise_fail_flags")
     check_state(plan, "inbatch")
     plan.close()
     # ---- phase 3: catalogue negatives (the reference's live sampler)
@@ -969,7 +1029,9 @@ def main():
         ub, ib = batches(args.warmup + args.steps)
         dt, t_enq, _, kern = timed_phase("text", tplan, text_step(ub, ib), optim=topt)
         rows = world * B * args.steps / dt
-        ks = kernel_rooflines(kern, B, args.steps, optim=topt)
+        ks = kernel_rooflines(kern, B, args.steps, optim=topt, d=Dt)
+        for k in ks:
+            k["traffic"] = traffic_for(k["kernel"], "text")
         tk = [k for k in ks if k["kernel"].startswith("k_text_fwd")]
         troof = dict(tk[0]) if tk else {}
         if troof:
@@ -995,6 +1057,7 @@ def main():
                       "datasets/dcuelmitemset.py:8); pinned against oracle/text_oracle.py (tests/test_gpu_text.py)"}
         if not out["text"]["finite"]:
             checks["failed"].append("text: non-finite dense parameters or loss")
+        checks["failed"] += ["text: " + f for f in fail_flag_failures(nat.debug_fail_flags())]
         tplan.close()
         del tplan, topt, tnet, tokens
     # ---- phase 5 (N = 1): the DCBR path (BASELINE config 5): WRMF target factors of

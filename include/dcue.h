@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DCUE_ABI_VERSION 15
+#define DCUE_ABI_VERSION 16
 #define DCUE_N_MELS 128
 #define DCUE_N_FRAMES 131
 #define DCUE_N_BN 6
@@ -417,7 +417,8 @@ int dcue_plan_destroy(dcue_plan* plan);
 #define DCUE_SITE_CONV2 8      /* caller's stream: conv 2 forward */
 #define DCUE_SITE_DGRAD_2 9    /* caller's stream: conv-2 input gradient (g1) */
 #define DCUE_SITE_WGRAD_1 10   /* caller's stream: conv-1 weight gradient */
-#define DCUE_N_DEBUG_SITES 11
+#define DCUE_SITE_TEXT_FWD 11  /* text tower: the text branch's forward on its side stream (ABI 16) */
+#define DCUE_N_DEBUG_SITES 12
 int dcue_debug_delay(int32_t site, int32_t microseconds);
 /* Probes: buf = NULL (off) or a device array of dcue_debug_probe_count() records
  * { uint32 nonfinite; uint32 nonzero; uint64 first_bad } (the caller sets first_bad to UINT64_MAX
@@ -430,9 +431,12 @@ int dcue_debug_probe_count(void);
 const char* dcue_debug_probe_name(int32_t i);
 /* on != 0: plans created afterwards fill the scratch they allocate with 0xFF bytes (float NaN). */
 int dcue_debug_poison(int32_t on);
-/* Reads and clears the device word the fused user-tower forward (DCUE_USER_FWD=fused) sets when a
- * bounded wait for another workgroup's row gave up (bit 0; never expected). */
+/* Reads and clears the current device's word that the fused user-tower forward sets when a bounded
+ * wait for another workgroup's row gave up (bit 0; never expected). bench.py fails its line on a
+ * non-zero value. */
 int dcue_debug_fail_flags(uint32_t* flags_host);
+/* ORs `bits` into the current device's fail word (tests: a forced flag must fail the bench line; ABI 16). */
+int dcue_debug_raise_fail_flags(uint32_t bits);
 
 /* ------------------------------------------------- data-parallel gradient exchange (RCCL) */
 /* One process per GPU; users are sharded over the ranks, so the only exchange of a step is the
@@ -497,7 +501,9 @@ int dcue_plan_set_sync_bn(dcue_plan* plan, int32_t on);
 #define DCUE_TIMED_ALLREDUCE 4    /* a plan's RCCL gradient exchange (each bucket's all-reduce) */
 #define DCUE_TIMED_EMB_SLICE 5    /* deferred user-table Adam: one step's rolling-flush slice */
 #define DCUE_TIMED_TEXT_FWD 6     /* text tower: the text conv forward (k_text_fwd, config 4) */
-#define DCUE_N_TIMED 7
+#define DCUE_TIMED_USER_FWD 7     /* the fused user-tower forward (k_user_fwd; ABI 16) */
+#define DCUE_TIMED_TEXT_WGRAD 8   /* text tower: the text conv's weight gradient (k_text_wgrad; ABI 16) */
+#define DCUE_N_TIMED 9
 int dcue_timer_enable(int32_t kernel, int32_t enable);
 int dcue_timer_read(int32_t kernel, double* total_ms_host, int64_t* launches_host);
 /* The same recorded launches one by one: each duration in ms into ms_host[0 .. min(n, cap)), the

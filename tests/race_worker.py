@@ -23,6 +23,10 @@ TOWERS = {
     "res": {"feature_dim": 64, "conv_hidden": 64, "model_type": "truedcuemel1dresbn"},
     "text": {"feature_dim": 64, "conv_hidden": 64, "model_type": "truedcuemel1dbntext", "text_dim": 64,
              "word_dim": 32, "text_len": 16, "n_words": 50, "pad_idx": 0},
+    # 32 positions: two 16-position tiles, so DCUE_TEXT_PARTS=2 splits each item over two workgroups
+    # that merge through the accumulator block's tickets (text.hip k_text_fwd_full)
+    "text32": {"feature_dim": 64, "conv_hidden": 64, "model_type": "truedcuemel1dbntext", "text_dim": 64,
+               "word_dim": 32, "text_len": 32, "n_words": 50, "pad_idx": 0},
 }
 
 
@@ -41,7 +45,7 @@ def run(tower="bn", delays=None, steps=5, inbatch=True, check=None, B=16, N=5):
     X = torch.randn(n_tracks, 128, 131, generator=gen).half()
     table = X.transpose(1, 2).contiguous().to(DEV)
     tokens = None
-    if tower == "text":
+    if tower.startswith("text"):
         from oracle import text_oracle as TO
         tokens = TO.sentences(gen, n_tracks, args["text_len"], args["n_words"], args["pad_idx"]).to(DEV)
     M = B if inbatch else B * (1 + N)

@@ -221,3 +221,20 @@ def test_plan_launch_with_comm_feeds_other_optimizers_world1(kind):
         comm.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_bench_forced_fail_flag_fails_the_line():
+    """a non-zero device fail word (dcue_debug_fail_flags: the fused user-tower
+    forward's bounded wait gave up) fails the bench line -- checks.failed names it and the exit status
+    is 1 -- instead of being visible to the tests only. DCUE_BENCH_FORCE_FAIL_FLAG raises the word
+    through dcue_debug_raise_fail_flags after the in-batch phase."""
+    import json
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--modes", "inbatch", "--no-f32-probe"]
+                         + SMALL, capture_output=True, text=True, timeout=240,
+                         env=dict(os.environ, DCUE_BENCH_FORCE_FAIL_FLAG="1"))
+    assert out.returncode == 1, out.stdout[-2000:] + out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    r = json.loads(lines[0])
+    assert any("fail flags" in f for f in r["checks"]["failed"]), r["checks"]
+    assert "fail flags" in out.stderr

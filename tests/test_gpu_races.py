@@ -46,7 +46,7 @@ def test_delays_bit_identical(tower):
     from dcrecommend import _native as nat
     base = W.run(tower)
     assert W.finite(base)
-    sites = SITES + (["fc_wgrad"] if tower in ("text", "res") else [])
+    sites = SITES + (["fc_wgrad"] if tower in ("text", "res") else []) + (["text_fwd"] if tower == "text" else [])
     for site in sites:
         _check(base, W.run(tower, {site: DELAY_US}), "%s tower, delay at %s" % (tower, site))
     # every side stream late at once
@@ -95,3 +95,21 @@ def test_legacy_orders_fail():
     assert res["legacy_orders"] == "1" and res["base_finite"]
     assert not res["wgrad_2"]["identical"], res
     assert not res["dgrad_2"]["identical"], res
+
+
+def test_text_position_parts_delays():
+    """the text branch runs on a side stream; with position parts (DCUE_TEXT_PARTS=2) its
+    two workgroups per item merge through tickets in the accumulator block's forward part. The
+    tickets are cleared in the text stream's own order (the plan's prologue, or the branch's own clear
+    in eager launches), never by the caller stream's accumulator clear. Delays at the text forward, the
+    user tower and conv 2 must leave the run bit-identical."""
+    env = dict(os.environ, DCUE_TEXT_PARTS="2")
+    p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "race_worker.py"), "text32",
+                        "text_fwd,user_fwd,conv2", str(DELAY_US)], env=env, stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=100)
+    assert p.returncode == 0, p.stdout[-3000:]
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    print(res)
+    assert res["base_finite"]
+    for site in ("text_fwd", "user_fwd", "conv2"):
+        assert res[site]["identical"] and res[site]["finite"], (site, res[site])
