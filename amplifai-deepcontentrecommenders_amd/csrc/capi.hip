@@ -475,7 +475,8 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
                  double copies, bool train, const float* counts, float* f_out, hipStream_t s,
                  bool acc_cleared = false, bool stats_done = false, bool clear_bn0 = false,
                  hipEvent_t before_l2 = nullptr, const std::function<int()>* after_l1 = nullptr,
-                 dcue_comm* sync_bn = nullptr, const std::function<int()>* text_join = nullptr) {
+                 dcue_comm* sync_bn = nullptr, const std::function<int()>* text_join = nullptr,
+                 const DevWait* l2_wait = nullptr) {
   const dcue_model* m = c.m;
   if (c.text && !t->tokens) return DCUE_ERR_INVALID;
   const int src = t->dtype == 0 ? SRC_TRACK_F16 : SRC_TRACK_F32;
@@ -540,6 +541,7 @@ int item_forward(const Ctx& c, const Ws& w, const dcue_tracks* t, const int32_t*
     a.out_range = rng_at(w, l);
     a.M = M;
     a.nout = l == 5 ? c.D : c.H;
+    if (l == 2 && l2_wait) a.wait = *l2_wait;  // (plans: the previous step's late Adam, on the device)
     if (l == 2 && train) {  // conv 2's input-gradient operands, left by the split plans' late Adam
       a.rp = pack_seg(m, c.poff, 2);
       a.rp.fwd = a.rp.f16 = -1;
@@ -833,6 +835,10 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   HPROF("capi:4");
   hipEvent_t ev_uf = nullptr, ev_tx = nullptr;
   const bool text_side = c.text && text_side_on();
+  // plans: the score kernel waits for the user tower on the device (DevWait), not by a stream wait
+  const bool uf_sig = o.sig != nullptr && !capturing_step();
+  DevWait uf_wait{};
+  if (uf_sig) uf_wait = DevWait{o.sig + kSigUf, ++o.sig_issued[kSigUf], user_fwd_fail_flag()};
   // the user tower on su: emb rows brought up to date, then the two GEMMs (+ the text branch, the
   // rolling flush slice)
   const std::function<int()> user_part = [&]() -> int {
@@ -866,6 +872,7 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
       HPROF("capi:8");
       TRY(timer_end(&tsu));
     }
+    if (uf_sig) TRY(launch_signal(o.sig + kSigUf, uf_wait.val, su));
     TRY(probe(PR_H1, w.h1, (long)b->n_rows * c.E, su));
     TRY(probe(PR_UF, w.uf, (long)b->n_rows * c.D, su));
     if (text_side) {  // the text branch: the item tower's fc input columns [0, C_s), beside its convs
@@ -916,14 +923,16 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   };
   bool user_done = false;
   if (text_side) user_done = !early || side.threaded();  // (text_join issues the user part)
+  // conv 2's wait for the previous step's late Adam: on the device when the plan signals it
+  const bool l2_dev = o.late_wait.flag != nullptr && !late_first && !capturing_step();
   TRY(item_forward(c, w, t, b->item_track, b->n_items, copies, train != 0, w.counts, nullptr, s,
                    o.prologue_done, o.input_stats_done && o.prologue_done, o.clear_bn0,
-                   late_first ? nullptr : o.wait_late,
+                   late_first || l2_dev ? nullptr : o.wait_late,
                    early && !side.threaded() ? &user_part : nullptr, o.sync_bn,
-                   text_side ? &text_join : nullptr));
+                   text_side ? &text_join : nullptr, l2_dev ? &o.late_wait : nullptr));
   if (!early && !side.threaded() && !user_done) TRY(user_part());
   TRY(side.wait(useq));
-  TRY(wait_point(s, ev_uf));
+  if (!uf_sig) TRY(wait_point(s, ev_uf));
   HPROF("capi:9");
   if (o.fuse_score) {
     // a fork point after the score kernel only for a caller that asks for one: a launch-bound event
@@ -937,18 +946,19 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
     };
     if (!o.score_done) {
       TRY(launch_score_fused(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.rowsum, w.du,
-                             w.dfcopy, s));
+                             w.dfcopy, s, uf_wait));
       return probes();
     }
     hipEvent_t ev = nullptr;
     ForkAfter fk(sp, s, &ev);
     TRY(launch_score_fused(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.rowsum, w.du,
-                           w.dfcopy, s));
+                           w.dfcopy, s, uf_wait));
     TRY(fk.done());
     HPROF("capi:10");
     *o.score_done = ev;
     return probes();
   }
+  if (uf_sig) return DCUE_ERR_INVALID;  // (device waits: plans, which fuse the score backward)
   return launch_score_fwd(w.uf, w.f, b, c.D, margin, w.scores, w.cosv, w.norms, w.hinge, w.loss,
                           w.dhinge, s);
 }
@@ -1264,6 +1274,12 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   // and the next launch waits for it before conv 1 (late_wait_at_conv1)
   const bool inputs_via_late = o.dense_split && !o.comm && o.late_done && late_wait_at_conv1();
   hipEvent_t joined = nullptr;
+  // plans (split, no exchange): the late Adam also signals the next step's conv 2 (DevWait)
+  DevWait late_sig{};
+  if (o.dense_split && !o.comm && o.late_sig && o.sig && !capturing_step()) {
+    late_sig = DevWait{o.sig + kSigLate, ++o.sig_issued[kSigLate], user_fwd_fail_flag()};
+    *o.late_sig = late_sig;
+  }
   dcue_adam_args dense = {};
   if (o.dense_split) {
     dense = *o.dense_split;
@@ -1294,6 +1310,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
         TRY(launch_adam(m, &dense, c.poff, su, true, late, -1, !legacy_orders()));
         TRY(fk.done());
       }
+      if (late_sig.flag) TRY(launch_signal(o.sig + kSigLate, late_sig.val, su));
       TRY(probe(PR_P_LATE, m->params + late, c.poff[kSeg] - late, su));
     }
     return DCUE_OK;
@@ -1418,6 +1435,9 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     TRY(probe(PR_G4 + (5 - l), w.g[l - 1], (long)M * layer_geom(l - 1).lp * H, s));
     HPROF("capi:16");
   }
+  // plans: the next step's prepared inputs ordered by the conv-1 weight gradient's device-side wait
+  // (k_conv_wgrad16t, DevWait) instead of a stream wait before it
+  const bool inputs_dev = o.inputs_wait.flag != nullptr && f16w && !inputs_via_late && !capturing_step();
   // conv weight gradient of layer l on stream `so` (its own split-K partial set `ps`); `tail`:
   // a fork point after its last kernel
   auto issue_wgrad = [&](int l, hipStream_t so, int ps, hipEvent_t* tail) -> int {
@@ -1445,6 +1465,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       wa.x_range = rng_at(w, l - 1); wa.y_range = rng_at(w, l); wa.g_range = grng_at(w, l);
       wa.kd_max = kd_max * wa.invN;
     }
+    if (l == 1 && inputs_dev) wa.wait = o.inputs_wait;
     const int nch = wgrad_nchunk(l, M, C, cin);
     if (l == 1 && !f16w) {  // the GEMM reads the pooled BN1 backward, expanded to rows at MFMA time
       TRY(launch_conv1_dx(wa, w.dx1, so));
@@ -1486,7 +1507,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   };
   // layer 1 (the step's tail) follows the chain on the caller's stream, issued right away
   if (ev_x0) TRY(wait_point(s, ev_x0));
-  if (o.wait_inputs && !inputs_via_late) {
+  if (o.wait_inputs && !inputs_via_late && !inputs_dev) {
     TRY(side.wait(o.ahead ? ahead_seq : o.wait_inputs_seq));
     TRY(wait_point(s, o.wait_inputs));
   }

@@ -300,6 +300,9 @@ __device__ __forceinline__ void conv_rows_body(const RowsArgs& a, const int bx, 
   DCUE_KTW(KID, 6);
   DCUE_KT(KID, 0);
   const ChanPre cpre = chan_preload<SRC, F16>(a, KC);
+  // (plans, conv 2: the previous step's late Adam on the user stream wrote its weights -- read below,
+  // after the loads above, which read only this stream's data)
+  if (MODE == 0) dev_wait(a.wait);
   if (MODE == 0 && a.rp_src) {  // conv 2's deferred input-gradient operands (RowsArgs::rp)
     const long n = (long)a.rp.cout * a.rp.cin * a.rp.ks;
     const long nt = (long)gridDim.x * gridDim.y * blockDim.x;

@@ -704,6 +704,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_wgrad16(WgradArgs a) {
   const int gx = gridDim.x, gy = gridDim.y;
   const int L = xcd_swizzle(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
   wgrad16_body<SRCX, KS, PAD, LIN, R, POOL, LP, EDGES>(a, L % gx, (L / gx) % gy, L / (gx * gy), lds16);
+  if constexpr (SRCX != SRC_ACT) dev_wait_order(a.wait);  // (as k_conv_wgrad16t, layer 1)
 }
 
 template <int L>
@@ -1078,6 +1079,8 @@ __global__ __launch_bounds__(kW16tThreads, 1) void k_conv_wgrad16t(WgradArgs a) 
   const int ot = (a.cout + kW16tO - 1) / kW16tO;
   const int L = xcd_swizzle(blockIdx.x, gridDim.x);
   wgrad16t_body<SRCX, KS, PAD, LIN, R, POOL, LP>(a, L % ot, L / ot, lds16t);
+  // (plans, layer 1: the next step's prepared inputs -- only an order for the kernels after this one)
+  if constexpr (SRCX != SRC_ACT) dev_wait_order(a.wait);
 }
 
 // whether the weight gradients run on split-f16 MFMA (DCUE_WGRAD_F16=0: the f32-MFMA kernels)

@@ -190,6 +190,52 @@ __device__ __forceinline__ float ord_value(unsigned k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
+// A cross-stream order kept on the device. A plan's producer on a side
+// stream is followed there by k_signal, which stores a value into one of the plan's signal words
+// (agent-scope atomic; the producer kernel's end released its data); the consumer kernel on the
+// caller's stream, issued with no stream wait, polls the word at its start until it reaches the value
+// (relaxed agent-scope loads, one lane), then takes an agent-scope acquire (this CU's L1 invalidated)
+// before any load of the produced data. A HIP cross-queue event wait costs the waiting queue a
+// barrier packet of 5-10 us even when its event completed long before; this costs one L2 round trip
+// when the producer is done. Values grow by one per issue (wrap-safe compare). A wait that gives up
+// (never expected: the producer is issued right after) sets bit 1 of the device fail word.
+struct DevWait {
+  const unsigned* flag;  // null: no wait
+  unsigned val;
+  unsigned* fail;
+};
+__device__ __forceinline__ void dev_wait(const DevWait& w) {
+  if (!w.flag) return;
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while ((int)(__hip_atomic_load(w.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - w.val) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 21)) {
+        if (w.fail) atomicOr(w.fail, 2u);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+// An order only: the kernel reads nothing the producer wrote, but later kernels on its stream must
+// start after the producer (their own start-of-kernel acquire then sees its data). One lane polls at
+// the end of the kernel's work; no barrier, no acquire.
+__device__ __forceinline__ void dev_wait_order(const DevWait& w) {
+  if (!w.flag || threadIdx.x != 0) return;
+  unsigned spins = 0;
+  while ((int)(__hip_atomic_load(w.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - w.val) < 0) {
+    __builtin_amdgcn_s_sleep(2);
+    if (++spins > (1u << 21)) {
+      if (w.fail) atomicOr(w.fail, 2u);
+      break;
+    }
+  }
+}
+
 // bump allocator over a caller-owned workspace (host side)
 struct Arena {
   char* base;

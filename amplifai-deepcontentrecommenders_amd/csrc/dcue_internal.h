@@ -125,9 +125,11 @@ struct RowsArgs {
   const float* rp_src;
   float* rp_wpack;  // the model's wpack
   PackSeg rp;
+  DevWait wait;  // plans: a side stream's signal to wait for at the kernel's start (conv 2: the late Adam)
 };
 
 struct WgradArgs {
+  DevWait wait;               // plans, layer 1 (k_conv_wgrad16t): the next step's prepared inputs
   int bn_world;               // SyncBN (> 1): dz sums are over the ranks; BN_l's dgamma/dbeta get 1/world
   const void* xsrc;           // layer input: tracks (l=1) or y_{l-1} [M][Lin][cin]
   const int32_t* item_track;
@@ -354,7 +356,11 @@ int launch_score_fwd(const float* uf, const float* f, const dcue_batch* b, int d
 // du / dfcopy and the per-row hinge sums; k_item_grad (given the row sums) takes the loss mean
 int launch_score_fused(const float* uf, const float* f, const dcue_batch* b, int d, float margin,
                        float* scores, float* cosv, float* norms, float* rowsum, float* du,
-                       float* dfcopy, hipStream_t s);
+                       float* dfcopy, hipStream_t s, DevWait uf_wait = DevWait{});
+// k_signal: store `val` into the signal word `flag` once the stream's earlier work is done (DevWait)
+int launch_signal(unsigned* flag, unsigned val, hipStream_t s);
+// a plan's signal words (StepOpts::sig): the user tower's output, the late Adam, the prepared inputs
+enum SigSlot { kSigUf = 0, kSigLate = 1, kSigInputs = 2, kSigText = 3, kSigSlots = 16 };
 int launch_score_bwd(const float* uf, const float* f, const dcue_batch* b, int d,
                      const float* dscores, const float* cosv, const float* norms, float* du,
                      float* dfcopy, hipStream_t s);
@@ -603,6 +609,16 @@ struct StepOpts {
   const dcue_adam_args* dense_split = nullptr;
   hipEvent_t* late_done = nullptr;
   hipEvent_t wait_late = nullptr;  // forward: the previous split step's late_done
+  // plans (round 6): device-side waits (DevWait) in place of the caller stream's event waits -- the
+  // plan's signal words [kSigSlots] and its host counters of the values issued into them (null:
+  // event waits); late_wait: the previous step's late Adam (conv 2 waits for it instead of wait_late),
+  // *late_sig receives this step's; inputs_wait: the next step's prepared inputs (the conv-1 weight
+  // gradient waits for it instead of wait_inputs)
+  unsigned* sig = nullptr;
+  unsigned* sig_issued = nullptr;
+  DevWait late_wait{};
+  DevWait* late_sig = nullptr;
+  DevWait inputs_wait{};
   // the step's per-item copy lists (gather layout, built by the plan's prologue; StepPrologue)
   const int32_t* copy_ptr = nullptr;
   const int32_t* copy_idx = nullptr;

@@ -56,7 +56,21 @@ struct dcue_plan {
   bool sync_bn = false;           // SyncBN over `comm` (dcue_plan_set_sync_bn)
   long late = 0, n_dense = 0;     // flat-gradient floats: end of bn0/conv1/bn1, total
   int comm_world = 1;
+  // device-side waits (StepOpts::sig, DevWait): the plan's signal words, the values issued into
+  // them, and the last split step's late-Adam signal (what the next step's conv 2 waits for)
+  unsigned* sig = nullptr;
+  unsigned sig_issued[dcue::kSigSlots] = {};
+  dcue::DevWait late_sig{};
 };
+
+// DCUE_XQ_WAIT=event: the plan's caller-stream waits as HIP event waits (rounds 1-5; A/B)
+static bool dev_waits_on() {
+  static const bool on = [] {
+    const char* e = getenv("DCUE_XQ_WAIT");
+    return !(e && e[0] == 'e');
+  }();
+  return on;
+}
 
 namespace {
 
@@ -156,7 +170,11 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   p->next_items = nullptr;
   p->inputs_ready = ring_event(sp);  // slot nxt's inputs, for the next launch (recorded below)
   // the lookahead, then the inputs_ready record, on wgrad stream 0 after `after`
-  const std::function<int(hipEvent_t)> lookahead = [p, sa, nxt, look, ir = p->inputs_ready](hipEvent_t after) -> int {
+  // device-side waits (no communicator: its exchange keeps the event orders)
+  const bool dev = p->sig && !p->comm && dev_waits_on();
+  DevWait in_sig{};
+  if (dev && inputs_wait == 1) in_sig = DevWait{p->sig + kSigInputs, ++p->sig_issued[kSigInputs], user_fwd_fail_flag()};
+  const std::function<int(hipEvent_t)> lookahead = [p, sa, nxt, look, ir = p->inputs_ready, in_sig](hipEvent_t after) -> int {
     if (look) {
       if (after) TRY(wait_point(sa, after));
       TRY(debug_delay(DCUE_SITE_LOOKAHEAD, sa));
@@ -164,6 +182,7 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
                             p->xh[nxt], sa));
     }
     DCUE_HIP_CHECK(hipEventRecord(ir, sa));
+    if (in_sig.flag) TRY(launch_signal(const_cast<unsigned*>(in_sig.flag), in_sig.val, sa));
     return DCUE_OK;
   };
   SideQueue side;
@@ -189,6 +208,14 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   o.comm = dense_split ? p->comm : nullptr;  // the exchange inside the backward (comm_exchange_split)
   hipEvent_t late_done = nullptr;
   o.late_done = &late_done;
+  DevWait late_sig{};
+  if (dev) {
+    o.sig = p->sig;
+    o.sig_issued = p->sig_issued;
+    o.late_wait = p->late_sig;
+    o.late_sig = &late_sig;
+    o.inputs_wait = in_sig;
+  }
   // the previous step's rolling-flush slice runs after this step's user tower (StepOpts)
   const bool deferred = p->model.emb_step != nullptr;
   o.flush_slice_step = deferred ? p->pending_flush : -1;
@@ -252,6 +279,7 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   HPROF("plan:5");
   p->pending_flush = o.defer_flush_slice ? emb_adam->step : -1;
   p->late_done = dense_split ? late_done : nullptr;
+  p->late_sig = dense_split ? late_sig : DevWait{};
   p->last_stream = s;
   ++p->launches;
   return DCUE_OK;
@@ -318,12 +346,17 @@ extern "C" int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const 
     // conv 1's output per slot (StepOpts::y1): [M][33][H_s] floats
     const size_t by1 = al(sizeof(float) * (size_t)M * dcue::layer_geom(1).lp * dcue::st_hidden(&m->dims));
     void* mem = nullptr;
-    const size_t mem_bytes = 2 * (bneg + bcnt + bacc + bxh + bptr + bidx + by1) + bmt;
+    const size_t bsig = al(sizeof(unsigned) * dcue::kSigSlots);
+    const size_t mem_bytes = 2 * (bneg + bcnt + bacc + bxh + bptr + bidx + by1) + bmt + bsig;
     DCUE_HIP_CHECK(hipMalloc(&mem, mem_bytes));
     if (dcue::poison_on()) {  // debug: a read of a word no kernel wrote shows as NaN
       DCUE_HIP_CHECK(hipMemset(mem, 0xFF, mem_bytes));
       DCUE_HIP_CHECK(hipDeviceSynchronize());
     }
+    // the signal words start at 0, as the host's issue counters (after the poison fill)
+    unsigned* sig = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(mem) + mem_bytes - bsig);
+    DCUE_HIP_CHECK(hipMemset(sig, 0, bsig));
+    DCUE_HIP_CHECK(hipDeviceSynchronize());
     dcue_plan* p = new dcue_plan;
     p->model = *m;
     p->batch = *b;
@@ -345,6 +378,7 @@ extern "C" int dcue_plan_create(const dcue_model* m, const dcue_batch* b, const 
       p->y1[i] = (float*)q; q += by1;
     }
     p->mt_ahead = (dcue_mt_state*)q;
+    p->sig = sig;
     p->nacc = nacc;
     *plan_host = p;
     return DCUE_OK;

@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ u
                                                      const float* __restrict__ f, dcue_batch b, int d,
                                                      float margin, float* scores, float* cosv,
                                                      float* norms, float* rowsum, float* dU,
-                                                     float* dfcopy) {
+                                                     float* dfcopy, DevWait uf_wait) {
   critical_path_priority();
   DCUE_KTW(0, 6);
   DCUE_KT(0, 0);
@@ -234,6 +234,8 @@ __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ u
         v[q][e] = (wave + 4 * q <= N && e < per && k < d) ? f[(long)item[q] * d + k] : 0.f;
       }
   }
+  // (plans: uf comes from the user stream; the copies' features above are this stream's)
+  dev_wait(uf_wait);
   float u[4];
   float su = 0.f;
 #pragma unroll
@@ -395,19 +397,30 @@ __global__ __launch_bounds__(256) void k_score_fused(const float* __restrict__ u
   DCUE_KTW(0, 7);
 }
 
+// DevWait's producer side: stream-ordered after the producer kernel (whose end released its data)
+__global__ void k_signal(unsigned* flag, unsigned val) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+int launch_signal(unsigned* flag, unsigned val, hipStream_t s) {
+  DCUE_LAUNCH(k_signal, dim3(1), dim3(64), 0, s, flag, val);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
 int launch_score_fused(const float* uf, const float* f, const dcue_batch* b, int d, float margin,
                        float* scores, float* cosv, float* norms, float* rowsum, float* du,
-                       float* dfcopy, hipStream_t s) {
+                       float* dfcopy, hipStream_t s, DevWait uf_wait) {
   if (d > 256 || b->n_neg > 1024 || b->n_rows > 1024) return DCUE_ERR_UNSUPPORTED;
   if (b->n_neg + 1 <= 16)
     DCUE_LAUNCH(k_score_fused<4>, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, margin, scores, cosv,
-                norms, rowsum, du, dfcopy);
+                norms, rowsum, du, dfcopy, uf_wait);
   else if (b->n_neg + 1 <= 32)
     DCUE_LAUNCH(k_score_fused<8>, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, margin, scores, cosv,
-                norms, rowsum, du, dfcopy);
+                norms, rowsum, du, dfcopy, uf_wait);
   else
     DCUE_LAUNCH(k_score_fused<0>, dim3(b->n_rows), dim3(256), 0, s, uf, f, *b, d, margin, scores, cosv,
-                norms, rowsum, du, dfcopy);
+                norms, rowsum, du, dfcopy, uf_wait);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }

@@ -26,10 +26,10 @@
 //   k_text_wgrad   dW[o][c][k] = sum_i g[i][o] e[i][t*(i,o) + k - 1][c] -- the max routes each (item,
 //                  channel) gradient to one position, so the weight gradient is a gathered sum, not a
 //                  dense GEMM over positions (3 x C x E FMAs per item instead of 3 x C x E x T). A
-//                  workgroup owns 32 word channels x all C output channels over a chunk of items: the
-//                  chunk's word-vector slices staged in LDS once, 3 x C/8 fp32 accumulators per thread,
-//                  exact fp32 FMAs in item order (deterministic).
-//   k_text_wreduce the chunk partials in chunk order, and db[o] = sum_i g[i][o] in item order.
+//                  workgroup owns 8 output channels x 32 word channels over all of its chunk's items,
+//                  3 fp32 accumulators per thread, exact fp32 FMAs in item order (deterministic);
+//                  db[o] = sum_i g[i][o] in item order.
+//   k_text_wreduce the chunk partials in chunk order (only when M needs more than one chunk).
 #include <cstring>
 
 #include "dcue_internal.h"
@@ -471,78 +471,88 @@ struct TextWgradArgs {
   const uint8_t* tidx;   // [M][C]
   int M, T, E, C;
   int items_per_chunk;
-  float* wpart;          // [nchunk][C * E * 3 + C]: the chunk's dW ([C][E][3]) and db partials
+  float* dW;             // one chunk: [C][E][3] and db [C] written directly
+  float* db;
+  float* wpart;          // several: [nchunk][C * E * 3 + C], the chunk's dW and db partials
 };
 
-constexpr int kTextWIB = 4;  // items staged per pass
+constexpr int kTwO = 8;        // output channels per workgroup (32 word channels each: 256 threads)
+constexpr int kTwItems = 64;   // items whose tokens / routing are staged in LDS per pass
+constexpr int kTwG = 8;        // items per load group (3 word loads each in flight per thread)
 
-// thread t: word channel c = 32 * blockIdx.x + (t & 31), output channels o = (t >> 5) + 8 j, j < C/8
-template <int OPT>
+// Round 6: a workgroup owns 8 output channels x 32 word channels over ALL of its
+// chunk's items (one chunk at the in-batch shape: no partials, no reduce launch), so the grid is
+// (C / 8) x (E / 32) workgroups -- 320 at config 4 -- with 3 accumulators per thread. Per item a
+// thread reads its channel of the three word rows around the item's argmax position for its output
+// channel straight from L2 (the tokens and the routing staged in LDS once); a group of 8 items' 24
+// loads is issued before their FMAs. Exact fp32 FMAs in item order (deterministic); the chunk
+// partials, where M needs several chunks, are summed in chunk order by k_text_wreduce.
 __global__ __launch_bounds__(256) void k_text_wgrad(TextWgradArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float tw_lds[];
-  const int RS = a.T + 2;  // staged rows: positions -1 .. T
-  float* xsl = tw_lds;                                  // [kTextWIB][RS][33]
-  float* gs = xsl + kTextWIB * RS * 33;                 // [kTextWIB][C]
-  int* ts = reinterpret_cast<int*>(gs + kTextWIB * a.C);  // [kTextWIB][C]
-  const int tid = threadIdx.x, cl = tid & 31, og = tid >> 5;
-  const int c = blockIdx.x * 32 + cl;
-  const int ib = blockIdx.y * a.items_per_chunk;
-  const int ie = min(a.M, ib + a.items_per_chunk);
-  float acc[OPT][3], bacc[OPT];
-#pragma unroll
-  for (int j = 0; j < OPT; ++j) acc[j][0] = acc[j][1] = acc[j][2] = bacc[j] = 0.f;
-  for (int i0 = ib; i0 < ie; i0 += kTextWIB) {
-    const int ni = min(kTextWIB, ie - i0);
-    __syncthreads();  // the previous pass's readers are done
-    for (int e = tid; e < ni * RS * 32; e += 256) {
-      const int s = e / (RS * 32), rem = e - s * RS * 32;
-      const int r = rem >> 5, cc = rem & 31;
-      const int t = r - 1, ch = blockIdx.x * 32 + cc;
-      float v = 0.f;
-      if (t >= 0 && t < a.T && ch < a.E) {
-        const int tk = a.tokens[(long)a.item_track[i0 + s] * a.T + t];
-        v = a.words[(long)tk * a.E + ch];
-      }
-      xsl[(s * RS + r) * 33 + cc] = v;
+  __shared__ int32_t tok_s[kTwItems * 128];  // [item][T], T <= 128
+  __shared__ float g_s[kTwItems][kTwO];
+  __shared__ int32_t ti_s[kTwItems][kTwO];
+  const int tid = threadIdx.x, cl = tid & 31, ol = tid >> 5;
+  const int ob = blockIdx.x * kTwO;
+  const int c = blockIdx.y * 32 + cl;
+  const int cc = c < a.E ? c : a.E - 1;  // (loads unconditional: clamped column, value dropped past E)
+  const int T = a.T;
+  const int ib = blockIdx.z * a.items_per_chunk, ie = min(a.M, ib + a.items_per_chunk);
+  float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, bacc = 0.f;
+  for (int i0 = ib; i0 < ie; i0 += kTwItems) {
+    const int ni = min(kTwItems, ie - i0);
+    __syncthreads();  // (the previous pass's readers)
+    for (int e = tid; e < ni * T; e += 256) {
+      const int sl = e / T, t = e - sl * T;
+      tok_s[e] = a.tokens[(long)a.item_track[i0 + sl] * T + t];
     }
-    for (int e = tid; e < ni * a.C; e += 256) {
-      const int s = e / a.C, o = e - s * a.C;
-      const int ti = a.tidx[(long)(i0 + s) * a.C + o];
-      ts[e] = ti;
-      gs[e] = ti == kTextNoGrad ? 0.f : a.dt[(long)(i0 + s) * a.C + o];
+    for (int e = tid; e < ni * kTwO; e += 256) {
+      const int sl = e / kTwO, oo = e - sl * kTwO;
+      const long off = (long)(i0 + sl) * a.C + ob + oo;
+      const int ti = a.tidx[off];
+      ti_s[sl][oo] = ti;
+      g_s[sl][oo] = ti == kTextNoGrad ? 0.f : a.dt[off];
     }
     __syncthreads();
-    for (int s = 0; s < ni; ++s)
+    for (int s0 = 0; s0 < ni; s0 += kTwG) {
+      float x[kTwG][3], gv[kTwG];
+      unsigned ok = 0, live = 0;
 #pragma unroll
-      for (int j = 0; j < OPT; ++j) {
-        const int o = og + 8 * j;
-        const int ti = ts[s * a.C + o];
-        if (ti != kTextNoGrad) {  // uniform over the 32 lanes of one o
-          const float gv = gs[s * a.C + o];
-          bacc[j] += gv;  // db's partial, in item order
-          const float* xr = xsl + (s * RS + ti) * 33 + cl;  // staged row ti + k = position ti + k - 1
-          acc[j][0] = fmaf(gv, xr[0], acc[j][0]);
-          acc[j][1] = fmaf(gv, xr[33], acc[j][1]);
-          acc[j][2] = fmaf(gv, xr[66], acc[j][2]);
+      for (int j = 0; j < kTwG; ++j) {
+        const int sl = min(s0 + j, ni - 1);
+        const int ti = ti_s[sl][ol];
+        const bool lv = s0 + j < ni && ti != kTextNoGrad;
+        live |= (unsigned)lv << j;
+        gv[j] = g_s[sl][ol];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int t = ti + k - 1;  // staged position ti + k - 1 (outside the sentence: a zero row)
+          const bool in = lv && t >= 0 && t < T;
+          ok |= (unsigned)in << (3 * j + k);
+          const int tk = tok_s[sl * T + (in ? t : 0)];
+          x[j][k] = a.words[(long)(in ? tk : 0) * a.E + cc];
         }
       }
-  }
-  const long n = (long)a.C * a.E * 3;
-  float* wp = a.wpart + (long)blockIdx.y * (n + a.C);  // chunk block: dW partial, then db partial
-  if (c < a.E) {
 #pragma unroll
-    for (int j = 0; j < OPT; ++j) {
-      const int o = og + 8 * j;
-      float* d = wp + ((long)o * a.E + c) * 3;
-      d[0] = acc[j][0];
-      d[1] = acc[j][1];
-      d[2] = acc[j][2];
+      for (int j = 0; j < kTwG; ++j) {
+        if (!((live >> j) & 1u)) continue;  // (uniform over the 32 lanes of one output channel)
+        bacc += gv[j];  // db's partial, in item order
+        acc0 = fmaf(gv[j], (ok >> (3 * j)) & 1u ? x[j][0] : 0.f, acc0);
+        acc1 = fmaf(gv[j], (ok >> (3 * j + 1)) & 1u ? x[j][1] : 0.f, acc1);
+        acc2 = fmaf(gv[j], (ok >> (3 * j + 2)) & 1u ? x[j][2] : 0.f, acc2);
+      }
     }
   }
-  if (blockIdx.x == 0 && cl == 0) {
-#pragma unroll
-    for (int j = 0; j < OPT; ++j) wp[n + og + 8 * j] = bacc[j];
+  const int o = ob + ol;
+  const long n = (long)a.C * a.E * 3;
+  float* dw = gridDim.z == 1 ? a.dW : a.wpart + (long)blockIdx.z * (n + a.C);
+  float* dbp = gridDim.z == 1 ? a.db : dw + n;
+  if (c < a.E) {
+    float* d = dw + ((long)o * a.E + c) * 3;
+    d[0] = acc0;
+    d[1] = acc1;
+    d[2] = acc2;
   }
+  if (blockIdx.y == 0 && cl == 0) dbp[o] = bacc;
 }
 
 // the chunk partials [nchunk][n + C] (dW then db per chunk) summed in chunk order
@@ -667,38 +677,30 @@ int launch_text_fwd(const TextBranch& tb, const int32_t* item_track, int M, floa
   return launch_text_fwd_t<8, 1>(a, s);
 }
 
+// item chunks of the text weight gradient: one up to 128 items (the in-batch shapes: no partials),
+// else about 128 items per chunk, at most 16 chunks
 int text_wgrad_nchunk(int M) {
-  const int n = M / 8;
-  return n < 1 ? 1 : (n > 32 ? 32 : n);
-}
-
-template <int OPT>
-static int launch_text_wgrad_t(const TextWgradArgs& a, int nchunk, hipStream_t s) {
-  const size_t lds = sizeof(float) * ((size_t)kTextWIB * (a.T + 2) * 33 + (size_t)kTextWIB * a.C) +
-                     sizeof(int) * (size_t)kTextWIB * a.C;
-  dim3 grid((unsigned)((a.E + 31) / 32), (unsigned)nchunk);
-  DCUE_LAUNCH((k_text_wgrad<OPT>), grid, dim3(256), lds, s, a);
-  DCUE_LAUNCH_CHECK();
-  return DCUE_OK;
+  const int n = (M + 127) / 128;
+  return n < 1 ? 1 : (n > 16 ? 16 : n);
 }
 
 int launch_text_wgrad(const TextBranch& tb, const int32_t* item_track, int M, const float* dt, const uint8_t* tidx,
                       float* wpart, float* dW, float* db, hipStream_t s) {
+  if (tb.C % kTwO || tb.T < 1 || tb.T > 128 || M < 1) return DCUE_ERR_INVALID;
   TextWgradArgs a;
   a.tokens = tb.tokens; a.item_track = item_track; a.words = tb.words;
   a.dt = dt; a.tidx = tidx;
   a.M = M; a.T = tb.T; a.E = tb.E; a.C = tb.C;
   const int nchunk = text_wgrad_nchunk(M);
   a.items_per_chunk = (M + nchunk - 1) / nchunk;
-  a.wpart = wpart;
-  int st;
-  switch (tb.C) {
-    case 64: st = launch_text_wgrad_t<8>(a, nchunk, s); break;
-    case 128: st = launch_text_wgrad_t<16>(a, nchunk, s); break;
-    case 256: st = launch_text_wgrad_t<32>(a, nchunk, s); break;
-    default: return DCUE_ERR_INVALID;
-  }
-  if (st) return st;
+  a.dW = dW; a.db = db; a.wpart = wpart;
+  const dim3 grid((unsigned)(tb.C / kTwO), (unsigned)((tb.E + 31) / 32), (unsigned)nchunk);
+  TimerScope tsc;  // (live timing: DCUE_TIMED_TEXT_WGRAD)
+  TRY(timer_begin(&tsc, DCUE_TIMED_TEXT_WGRAD, s));
+  DCUE_LAUNCH(k_text_wgrad, grid, dim3(256), 0, s, a);
+  DCUE_LAUNCH_CHECK();
+  TRY(timer_end(&tsc));
+  if (nchunk == 1) return DCUE_OK;
   const long n = (long)tb.C * tb.E * 3;
   DCUE_LAUNCH(k_text_wreduce, dim3((unsigned)((n + tb.C + 255) / 256)), dim3(256), 0, s, wpart, nchunk, n, tb.C,
               dW, db);

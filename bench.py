@@ -225,12 +225,16 @@ DGRAD_F16 = os.environ.get("DCUE_DGRAD_F16", "1")[:1] != "0"
 def fail_flag_failures(flags):
     """The library's device fail word (dcue_debug_fail_flags) as checks.failed entries: bit 0 is a
     bounded wait in the fused user-tower forward that gave up (adam.hip k_user_fwd) -- its rows may
-    then have been read before their Adam replay, so the run is failed, whatever its throughput."""
+    then have been read before their Adam replay; bit 1 a plan's device-side cross-stream wait that
+    gave up (dcue_common.h DevWait) -- its kernel then read a producer's data early. Either fails the
+    run, whatever its throughput."""
     out = []
     if flags & 1:
         out.append("fail flags: the fused user-tower forward's bounded wait for a claimed row gave up (bit 0)")
-    if flags & ~1:
-        out.append("fail flags: unknown bits 0x%x" % (flags & ~1))
+    if flags & 2:
+        out.append("fail flags: a plan's device-side cross-stream wait (DevWait) gave up (bit 1)")
+    if flags & ~3:
+        out.append("fail flags: unknown bits 0x%x" % (flags & ~3))
     return out
 
 
