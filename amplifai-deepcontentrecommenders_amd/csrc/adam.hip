@@ -250,6 +250,11 @@ __global__ void k_emb_flush_done(dcue_emb_log* hdr) { hdr->flush_step = hdr->ste
 // current, so every row is replayed at least once per `cap` steps -- the replay work spread evenly
 // over the steps (it runs on the user-tower stream, beside the item tower) instead of a full-table
 // sweep every cap steps. A workgroup owns whole rows: it reads their clocks, replays, then sets them.
+// Round 6: a bounded grid (DCUE_SLICE_WGS, default 64) striding over groups of rows_per_block rows --
+// the slice is off the critical path with a whole step to finish in, and one workgroup per three rows
+// (2,778 at config 2) filled the dispatcher and the CUs the critical-path kernels need at once (the
+// steady-state tax); the window's history and replay bound are staged once per
+// workgroup instead of once per three rows.
 __global__ __launch_bounds__(256) void k_emb_flush_rows(float* __restrict__ p, float* __restrict__ m,
                                                         float* __restrict__ v, const dcue_emb_log* hdr,
                                                         int32_t* emb_step, long r0, long r1, int E,
@@ -258,46 +263,48 @@ __global__ __launch_bounds__(256) void k_emb_flush_rows(float* __restrict__ p, f
   __shared__ ReplayBound sb;
   __shared__ int from_s[256];
   const int T = hdr->step_done, F = hdr->flush_step, cap = hdr->cap;
-  const long rb = r0 + (long)blockIdx.x * rows_per_block;
-  const int nr = (int)min((long)rows_per_block, r1 - rb);
-  if (nr <= 0) return;
+  if (r0 + (long)blockIdx.x * rows_per_block >= r1) return;
   const AdamScalars* hist = reinterpret_cast<const AdamScalars*>(hdr + 1);
   const int lo = max(F + 1, T - cap + 1);
   for (int j = lo + (int)threadIdx.x; j <= T; j += blockDim.x) hs[j % cap] = hist[j % cap];
-  for (int i = threadIdx.x; i < nr; i += blockDim.x) from_s[i] = max(emb_step[rb + i], F);
   __syncthreads();
   window_bound(hs, lo, T, cap, gz, &sb);
   __syncthreads();
   const ReplayBound b = sb;
-  if ((E & 3) == 0) {
-    const int E4 = E >> 2;
-    for (int e = threadIdx.x; e < nr * E4; e += blockDim.x) {
-      const int i = e / E4;
-      const long off = (rb + i) * E + 4 * (e - i * E4);
-      const float4 m4 = ld4(m + off), v4 = ld4(v + off);
-      if (b.nd && idle_moments4(m4, v4)) continue;  // fixed point (idle_moments)
-      const float4 p4 = ld4(p + off);
-      float pp[4] = {p4.x, p4.y, p4.z, p4.w}, mm[4] = {m4.x, m4.y, m4.z, m4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
-      replay_run<4>(pp, mm, vv, hs, from_s[i] + 1, T, cap, b, gz);
-      if ((__float_as_uint(pp[0]) ^ __float_as_uint(p4.x)) | (__float_as_uint(pp[1]) ^ __float_as_uint(p4.y)) |
-          (__float_as_uint(pp[2]) ^ __float_as_uint(p4.z)) | (__float_as_uint(pp[3]) ^ __float_as_uint(p4.w)))
-        st4(p + off, make_float4(pp[0], pp[1], pp[2], pp[3]));  // long-idle: p unchanged, no store
-      st4(m + off, make_float4(mm[0], mm[1], mm[2], mm[3]));
-      st4(v + off, make_float4(vv[0], vv[1], vv[2], vv[3]));
+  for (long rb = r0 + (long)blockIdx.x * rows_per_block; rb < r1; rb += (long)gridDim.x * rows_per_block) {
+    const int nr = (int)min((long)rows_per_block, r1 - rb);
+    for (int i = threadIdx.x; i < nr; i += blockDim.x) from_s[i] = max(emb_step[rb + i], F);
+    __syncthreads();
+    if ((E & 3) == 0) {
+      const int E4 = E >> 2;
+      for (int e = threadIdx.x; e < nr * E4; e += blockDim.x) {
+        const int i = e / E4;
+        const long off = (rb + i) * E + 4 * (e - i * E4);
+        const float4 m4 = ld4(m + off), v4 = ld4(v + off);
+        if (b.nd && idle_moments4(m4, v4)) continue;  // fixed point (idle_moments)
+        const float4 p4 = ld4(p + off);
+        float pp[4] = {p4.x, p4.y, p4.z, p4.w}, mm[4] = {m4.x, m4.y, m4.z, m4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
+        replay_run<4>(pp, mm, vv, hs, from_s[i] + 1, T, cap, b, gz);
+        if ((__float_as_uint(pp[0]) ^ __float_as_uint(p4.x)) | (__float_as_uint(pp[1]) ^ __float_as_uint(p4.y)) |
+            (__float_as_uint(pp[2]) ^ __float_as_uint(p4.z)) | (__float_as_uint(pp[3]) ^ __float_as_uint(p4.w)))
+          st4(p + off, make_float4(pp[0], pp[1], pp[2], pp[3]));  // long-idle: p unchanged, no store
+        st4(m + off, make_float4(mm[0], mm[1], mm[2], mm[3]));
+        st4(v + off, make_float4(vv[0], vv[1], vv[2], vv[3]));
+      }
+    } else {
+      for (int e = threadIdx.x; e < nr * E; e += blockDim.x) {
+        const int i = e / E;
+        const long off = (rb + i) * E + (e - i * E);
+        float mm[1] = {m[off]}, vv[1] = {v[off]};
+        if (b.nd && idle_moments(mm[0], vv[0])) continue;
+        float pp[1] = {p[off]};
+        replay_run<1>(pp, mm, vv, hs, from_s[i] + 1, T, cap, b, gz);
+        p[off] = pp[0]; m[off] = mm[0]; v[off] = vv[0];
+      }
     }
-  } else {
-    for (int e = threadIdx.x; e < nr * E; e += blockDim.x) {
-      const int i = e / E;
-      const long off = (rb + i) * E + (e - i * E);
-      float mm[1] = {m[off]}, vv[1] = {v[off]};
-      if (b.nd && idle_moments(mm[0], vv[0])) continue;
-      float pp[1] = {p[off]};
-      replay_run<1>(pp, mm, vv, hs, from_s[i] + 1, T, cap, b, gz);
-      p[off] = pp[0]; m[off] = mm[0]; v[off] = vv[0];
-    }
+    __syncthreads();  // (every replay read from_s; the rows' values before their clocks)
+    for (int i = threadIdx.x; i < nr; i += blockDim.x) emb_step[rb + i] = T;
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < nr; i += blockDim.x) emb_step[rb + i] = T;
 }
 
 int launch_emb_flush_rows(const dcue_model* md, int step, hipStream_t s) {
@@ -306,10 +313,16 @@ int launch_emb_flush_rows(const dcue_model* md, int step, hipStream_t s) {
   const int k = step % cap;
   const long r0 = n * k / cap, r1 = n * (k + 1) / cap;
   if (r1 <= r0) return DCUE_OK;
-  int rpb = 1024 / E;
+  int rpb = 4096 / E;  // rows per group: ~4 K elements (1 K float4) per pass of 256 threads
   if (rpb < 1) rpb = 1;
   if (rpb > 256) rpb = 256;
-  const long blocks = (r1 - r0 + rpb - 1) / rpb;
+  static const long max_wgs = [] {
+    const char* e = getenv("DCUE_SLICE_WGS");
+    const long v = e ? atol(e) : 1L << 30;
+    return v < 1 ? 1L : v;
+  }();
+  long blocks = (r1 - r0 + rpb - 1) / rpb;
+  if (blocks > max_wgs) blocks = max_wgs;
   TimerScope tsc;
   int st = timer_begin(&tsc, DCUE_TIMED_EMB_SLICE, s);
   if (st) return st;

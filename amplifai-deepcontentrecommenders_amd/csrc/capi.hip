@@ -459,6 +459,16 @@ TextBranch text_branch_ws(const Ctx& c, const dcue_tracks* t, const Ws& w) {
   return tb;
 }
 
+// DCUE_SLICE_STREAM: the side stream of the rolling flush slice (0: the user stream; w0 / w1: the
+// weight-gradient streams st[1] / st[2])
+int slice_stream() {
+  static const int v = [] {
+    const char* e = getenv("DCUE_SLICE_STREAM");
+    return !e ? 0 : (e[0] == 'w' && e[1] == '0') ? 1 : (e[0] == 'w' && e[1] == '1') ? 2 : 0;
+  }();
+  return v;
+}
+
 // DCUE_TEXT_SIDE=0: the training forward's text branch on the caller's stream after conv 5 instead
 // of on the user stream beside the audio convs (A/B)
 bool text_side_on() {
@@ -899,7 +909,26 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
       }
       TRY(timer_end(&tsc));
     }
-    if (o.flush_slice_step >= 0 && m->emb_step) TRY(launch_emb_flush_rows(m, o.flush_slice_step, su));
+    static const bool skip_slice = [] {  // DCUE_SLICE_SKIP=1: timing diagnostic only (wrong table)
+      const char* e = getenv("DCUE_SLICE_SKIP");
+      return e && e[0] == '1';
+    }();
+    if (o.flush_slice_step >= 0 && m->emb_step && !skip_slice) {
+      // DCUE_SLICE_STREAM=w1 / w0: the slice on a weight-gradient stream, after this user tower (its
+      // rows' claims) and before the step's user-table Adam (which waits for *slice_done): a long
+      // slice then holds no user-stream work behind it (A/B)
+      const int ss = slice_stream();
+      if (ss > 0 && o.slice_done) {
+        hipEvent_t e_u = nullptr;
+        TRY(fork_point(sp, su, &e_u));
+        TRY(wait_point(sp->st[ss], e_u));
+        ForkAfter fk(sp, sp->st[ss], o.slice_done);
+        TRY(launch_emb_flush_rows(m, o.flush_slice_step, sp->st[ss]));
+        TRY(fk.done());
+      } else {
+        TRY(launch_emb_flush_rows(m, o.flush_slice_step, su));
+      }
+    }
     return DCUE_OK;
   };
   // DCUE_USER_EARLY=1: the user tower is issued right after conv 1 instead of after the whole item
@@ -1155,6 +1184,7 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
     // deferred user-table Adam with the step (plans): the compact rows and their Adam step in one
     // launch (k_emb_grad_adam: each distinct user's workgroup sums its rows, then steps them)
     const bool emb_fused = o.emb_adam && m->emb_step && o.defer_flush_slice;
+    if (o.slice_done && *o.slice_done) TRY(wait_point(su, *o.slice_done));  // (a slice off this stream)
     {
       ForkAfter fk(sp, su, &tail[1]);
       if (emb_fused)

@@ -596,6 +596,9 @@ struct StepOpts {
   // tower -- same stream order relative to every Adam step, but off the next step's user-tower path
   bool defer_flush_slice = false;
   int flush_slice_step = -1;
+  // the slice issued off the user stream (DCUE_SLICE_STREAM): its end, which the backward's
+  // user-table Adam waits for (written by the forward's user part, read by the backward's)
+  hipEvent_t* slice_done = nullptr;
   // prepared one step ahead from the announced next batch (plans, dcue_plan_set_next): bn0's batch
   // sums already in `acc`, and the conv-1 weight gradient's X operand (k_xhat0) already built
   bool input_stats_done = false;

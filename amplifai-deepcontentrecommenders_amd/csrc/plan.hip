@@ -220,6 +220,8 @@ int issue_eager(dcue_plan* p, const int64_t* users_src, const int32_t* items_src
   const bool deferred = p->model.emb_step != nullptr;
   o.flush_slice_step = deferred ? p->pending_flush : -1;
   o.defer_flush_slice = deferred && emb_adam != nullptr;
+  hipEvent_t slice_done = nullptr;
+  o.slice_done = &slice_done;
   // DCUE_SCORE_FORK=1: the score kernel binds a fork point that the user tower's backward waits for
   // (A/B; default: it waits for the dgrad chain's first fork point, one bound event fewer)
   static const bool score_fork = [] {

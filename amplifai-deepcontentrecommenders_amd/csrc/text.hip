@@ -478,26 +478,70 @@ struct TextWgradArgs {
 
 constexpr int kTwO = 8;        // output channels per workgroup (32 word channels each: 256 threads)
 constexpr int kTwItems = 64;   // items whose tokens / routing are staged in LDS per pass
-constexpr int kTwG = 8;        // items per load group (3 word loads each in flight per thread)
+// items per load group: their 3 word loads each are in flight per thread together, and the next
+// group's are issued before this group's FMAs (two register sets)
+constexpr int kTwG = 16;
 
 // Round 6: a workgroup owns 8 output channels x 32 word channels over ALL of its
 // chunk's items (one chunk at the in-batch shape: no partials, no reduce launch), so the grid is
 // (C / 8) x (E / 32) workgroups -- 320 at config 4 -- with 3 accumulators per thread. Per item a
 // thread reads its channel of the three word rows around the item's argmax position for its output
-// channel straight from L2 (the tokens and the routing staged in LDS once); a group of 8 items' 24
-// loads is issued before their FMAs. Exact fp32 FMAs in item order (deterministic); the chunk
-// partials, where M needs several chunks, are summed in chunk order by k_text_wreduce.
+// channel straight from L2 (the tokens and the routing staged in LDS once). Exact fp32 FMAs in item
+// order (deterministic); the chunk partials, where M needs several chunks, are summed in chunk order
+// by k_text_wreduce.
+struct TwGroup {
+  float x[kTwG][3];
+  float gv[kTwG];
+  uint64_t ok;  // bit 3 j + k: position ti + k - 1 inside the sentence (kTwG <= 21)
+  unsigned live;
+};
+static_assert(3 * kTwG <= 64, "TwGroup::ok bits");
 __global__ __launch_bounds__(256) void k_text_wgrad(TextWgradArgs a) {
   __shared__ int32_t tok_s[kTwItems * 128];  // [item][T], T <= 128
   __shared__ float g_s[kTwItems][kTwO];
   __shared__ int32_t ti_s[kTwItems][kTwO];
   const int tid = threadIdx.x, cl = tid & 31, ol = tid >> 5;
-  const int ob = blockIdx.x * kTwO;
-  const int c = blockIdx.y * 32 + cl;
+  // XCD-aware (o block, word-channel block): consecutive logical blocks -- the o blocks of one
+  // word-channel block, which read the same 128-B slices of the batch's word rows -- on one XCD, so
+  // each XCD's L2 fetches about 1/8 of the rows' bytes instead of all of them
+  const int nob = gridDim.x, nbl = gridDim.x * gridDim.y;
+  const int Lg = xcd_swizzle(blockIdx.x + nob * blockIdx.y, nbl);
+  const int ob = (Lg % nob) * kTwO;
+  const int c = (Lg / nob) * 32 + cl;
   const int cc = c < a.E ? c : a.E - 1;  // (loads unconditional: clamped column, value dropped past E)
   const int T = a.T;
   const int ib = blockIdx.z * a.items_per_chunk, ie = min(a.M, ib + a.items_per_chunk);
   float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, bacc = 0.f;
+  // group [s0, s0 + kTwG) of the staged items: routing from LDS, the word loads issued
+  auto issue = [&](int s0, int ni, TwGroup& G) {
+    G.ok = G.live = 0;
+#pragma unroll
+    for (int j = 0; j < kTwG; ++j) {
+      const int sl = min(s0 + j, ni - 1);
+      const int ti = ti_s[sl][ol];
+      const bool lv = s0 + j < ni && ti != kTextNoGrad;
+      G.live |= (unsigned)lv << j;
+      G.gv[j] = g_s[sl][ol];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int t = ti + k - 1;  // staged position ti + k - 1 (outside the sentence: a zero row)
+        const bool in = lv && t >= 0 && t < T;
+        G.ok |= (uint64_t)in << (3 * j + k);
+        const int tk = tok_s[sl * T + (in ? t : 0)];
+        G.x[j][k] = a.words[(long)(in ? tk : 0) * a.E + cc];
+      }
+    }
+  };
+  auto consume = [&](const TwGroup& G) {
+#pragma unroll
+    for (int j = 0; j < kTwG; ++j) {
+      if (!((G.live >> j) & 1u)) continue;  // (uniform over the 32 lanes of one output channel)
+      bacc += G.gv[j];  // db's partial, in item order
+      acc0 = fmaf(G.gv[j], (G.ok >> (3 * j)) & 1u ? G.x[j][0] : 0.f, acc0);
+      acc1 = fmaf(G.gv[j], (G.ok >> (3 * j + 1)) & 1u ? G.x[j][1] : 0.f, acc1);
+      acc2 = fmaf(G.gv[j], (G.ok >> (3 * j + 2)) & 1u ? G.x[j][2] : 0.f, acc2);  // (64-bit mask)
+    }
+  };
   for (int i0 = ib; i0 < ie; i0 += kTwItems) {
     const int ni = min(kTwItems, ie - i0);
     __syncthreads();  // (the previous pass's readers)
@@ -513,33 +557,14 @@ __global__ __launch_bounds__(256) void k_text_wgrad(TextWgradArgs a) {
       g_s[sl][oo] = ti == kTextNoGrad ? 0.f : a.dt[off];
     }
     __syncthreads();
-    for (int s0 = 0; s0 < ni; s0 += kTwG) {
-      float x[kTwG][3], gv[kTwG];
-      unsigned ok = 0, live = 0;
-#pragma unroll
-      for (int j = 0; j < kTwG; ++j) {
-        const int sl = min(s0 + j, ni - 1);
-        const int ti = ti_s[sl][ol];
-        const bool lv = s0 + j < ni && ti != kTextNoGrad;
-        live |= (unsigned)lv << j;
-        gv[j] = g_s[sl][ol];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const int t = ti + k - 1;  // staged position ti + k - 1 (outside the sentence: a zero row)
-          const bool in = lv && t >= 0 && t < T;
-          ok |= (unsigned)in << (3 * j + k);
-          const int tk = tok_s[sl * T + (in ? t : 0)];
-          x[j][k] = a.words[(long)(in ? tk : 0) * a.E + cc];
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < kTwG; ++j) {
-        if (!((live >> j) & 1u)) continue;  // (uniform over the 32 lanes of one output channel)
-        bacc += gv[j];  // db's partial, in item order
-        acc0 = fmaf(gv[j], (ok >> (3 * j)) & 1u ? x[j][0] : 0.f, acc0);
-        acc1 = fmaf(gv[j], (ok >> (3 * j + 1)) & 1u ? x[j][1] : 0.f, acc1);
-        acc2 = fmaf(gv[j], (ok >> (3 * j + 2)) & 1u ? x[j][2] : 0.f, acc2);
-      }
+    TwGroup G0, G1;
+    issue(0, ni, G0);
+    for (int s0 = 0; s0 < ni; s0 += 2 * kTwG) {
+      if (s0 + kTwG < ni) issue(s0 + kTwG, ni, G1);  // in flight under G0's FMAs
+      consume(G0);
+      if (s0 + kTwG >= ni) break;
+      if (s0 + 2 * kTwG < ni) issue(s0 + 2 * kTwG, ni, G0);
+      consume(G1);
     }
   }
   const int o = ob + ol;
@@ -552,7 +577,7 @@ __global__ __launch_bounds__(256) void k_text_wgrad(TextWgradArgs a) {
     d[1] = acc1;
     d[2] = acc2;
   }
-  if (blockIdx.y == 0 && cl == 0) dbp[o] = bacc;
+  if (c == cl && cl == 0) dbp[o] = bacc;  // (the first word-channel block)
 }
 
 // the chunk partials [nchunk][n + C] (dW then db per chunk) summed in chunk order

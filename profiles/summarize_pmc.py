@@ -25,7 +25,8 @@ import sys
 # tap-fused weight gradient runs beside the dgrad chain on a side stream
 KERNELS = {"conv1_wgrad": "k_conv1_wgrad", "conv1_wgrad16": "k_conv_wgrad16t<0,",
            "wgrad16t_layer2": "k_conv_wgrad16t<2,", "wgrad16_multi": "k_conv_wgrad16_multi", "emb_flush_rows": "k_emb_flush_rows",
-           "conv1_fwd": "k_conv_rows<0, 0,", "text_fwd": "k_text_fwd"}
+           "conv1_fwd": "k_conv_rows<0, 0,", "text_fwd": "k_text_fwd", "user_fwd": "k_user_fwd",
+           "text_wgrad": "k_text_wgrad"}
 MARK = "spin_kernel"
 
 
