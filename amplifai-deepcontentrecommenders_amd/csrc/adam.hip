@@ -1,5 +1,8 @@
 // torch.optim.Adam over the flat dense buffer and the user table, plus the weight repack -- gfx950.
 // Reference: optim.Adam as built at nn/dcue.py:143-147 and stepped at :209 (CPU single-tensor path).
+#include <mutex>
+#include <unordered_map>
+
 #include "dcue_internal.h"
 #include "tgemm.h"
 #include "bn0adam.h"
@@ -50,6 +53,10 @@ __device__ __forceinline__ void window_bound(const AdamScalars* hs, int j0, int 
     *out = b;
   }
 }
+
+// frozen rows (adam_replay.h): a frozen row is brought current (m / v only) by the rolling slice once
+// it is this many flush periods behind, so a later reader's recurrence stays short
+constexpr int kFrzRefreshCaps = 8;
 
 struct PackArgs;
 PackArgs pack_args(const dcue_model* md, const int64_t* poff);
@@ -158,11 +165,14 @@ __global__ __launch_bounds__(1024) void k_emb_sync(float* __restrict__ p, float*
   __shared__ int s_from;
   const int T = hdr->step_done, F = hdr->flush_step, cap = hdr->cap;
   const int64_t u = users[blockIdx.x];
+  __shared__ int s_frz;
   if (threadIdx.x == 0) {
     int from = T;  // nothing to do
     const int old = emb_step[u];
-    if (old != INT_MIN && max(old, F) < T && atomicCAS(&emb_step[u], old, INT_MIN) == old) from = max(old, F);
+    if (old != INT_MIN && max(clock_of(old), F) < T && atomicCAS(&emb_step[u], old, INT_MIN) == old)
+      from = max(clock_of(old), F);
     s_from = from;
+    s_frz = is_frozen(old);
   }
   __syncthreads();
   const int from = s_from;
@@ -180,7 +190,12 @@ __global__ __launch_bounds__(1024) void k_emb_sync(float* __restrict__ p, float*
   // row is spread over as many lanes as it has elements (launch: blockDim >= E)
   for (int k = threadIdx.x; k < E; k += blockDim.x) {
     float mm[1] = {mr[k]}, vv[1] = {vr[k]};
-    if (b.nd && idle_moments(mm[0], vv[0])) continue;  // fixed point (idle_moments)
+    if (idle_moments(mm[0], vv[0]) && (b.nd || s_frz)) continue;  // fixed point (idle_moments)
+    if (s_frz) {  // frozen: the m / v recurrence, p unchanged (adam_replay.h)
+      frz_replay(mm[0], vv[0], hs[T % cap].lerp_c, hs[T % cap].b2, T - from);
+      mr[k] = mm[0]; vr[k] = vv[0];
+      continue;
+    }
     float pp[1] = {pr[k]};
     replay_run<1>(pp, mm, vv, hs, from + 1, T, cap, b, gz);
     pr[k] = pp[0]; mr[k] = mm[0]; vr[k] = vv[0];
@@ -217,9 +232,17 @@ __global__ __launch_bounds__(256) void k_emb_flush(float* __restrict__ p, float*
     const int E4 = E >> 2;
     const long n4 = n_rows * E4;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-      const int from = max(emb_step[i / E4], F);
+      const int e = emb_step[i / E4];
+      const int from = max(clock_of(e), F);
       const float4 m4 = ld4(m + 4 * i), v4 = ld4(v + 4 * i);
-      if (b.nd && idle_moments4(m4, v4)) continue;  // fixed point (idle_moments)
+      if (idle_moments4(m4, v4) && (b.nd || is_frozen(e))) continue;  // fixed point (idle_moments)
+      if (is_frozen(e)) {  // the recurrence from the row's own clock, however old (no history needed)
+        float mm[4] = {m4.x, m4.y, m4.z, m4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
+        frz_replay_n<4>(mm, vv, hs[T % cap].lerp_c, hs[T % cap].b2, T - from);
+        st4(m + 4 * i, make_float4(mm[0], mm[1], mm[2], mm[3]));
+        st4(v + 4 * i, make_float4(vv[0], vv[1], vv[2], vv[3]));
+        continue;
+      }
       const float4 p4 = ld4(p + 4 * i);
       float pp[4] = {p4.x, p4.y, p4.z, p4.w}, mm[4] = {m4.x, m4.y, m4.z, m4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
       replay_run<4>(pp, mm, vv, hs, max(from + 1, lo), T, cap, b, gz);
@@ -234,9 +257,15 @@ __global__ __launch_bounds__(256) void k_emb_flush(float* __restrict__ p, float*
   } else {
     const long n = n_rows * E;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-      const int from = max(emb_step[i / E], F);
+      const int e = emb_step[i / E];
+      const int from = max(clock_of(e), F);
       float mm[1] = {m[i]}, vv[1] = {v[i]};
-      if (b.nd && idle_moments(mm[0], vv[0])) continue;
+      if (idle_moments(mm[0], vv[0]) && (b.nd || is_frozen(e))) continue;
+      if (is_frozen(e)) {
+        frz_replay(mm[0], vv[0], hs[T % cap].lerp_c, hs[T % cap].b2, T - from);
+        m[i] = mm[0]; v[i] = vv[0];
+        continue;
+      }
       float pp[1] = {p[i]};
       replay_run<1>(pp, mm, vv, hs, max(from + 1, lo), T, cap, b, gz);
       p[i] = pp[0]; m[i] = mm[0]; v[i] = vv[0];
@@ -245,6 +274,106 @@ __global__ __launch_bounds__(256) void k_emb_flush(float* __restrict__ p, float*
 }
 
 __global__ void k_emb_flush_done(dcue_emb_log* hdr) { hdr->flush_step = hdr->step_done; }
+
+// ------------------------------------------------------------------- frozen-row epochs
+// Thaw: every frozen row brought current to step_done by the recurrence (valid: every step up to it
+// was inside the epoch) and its bit cleared -- before the first step outside the epoch is recorded.
+__global__ __launch_bounds__(256) void k_emb_thaw(float* __restrict__ m, float* __restrict__ v,
+                                                  const dcue_emb_log* hdr, int32_t* emb_step, long n_rows, int E,
+                                                  int rows_per_block) {
+  __shared__ int from_s[256], frz_s[256];
+  const int T = hdr->step_done, F = hdr->flush_step, cap = hdr->cap;
+  const AdamScalars last = log_hist(const_cast<dcue_emb_log*>(hdr))[T % cap];
+  for (long rb = (long)blockIdx.x * rows_per_block; rb < n_rows; rb += (long)gridDim.x * rows_per_block) {
+    const int nr = (int)min((long)rows_per_block, n_rows - rb);
+    for (int i = threadIdx.x; i < nr; i += blockDim.x) {
+      const int e = emb_step[rb + i];
+      from_s[i] = max(clock_of(e), F);
+      frz_s[i] = is_frozen(e);
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < nr * E; e += blockDim.x) {
+      const int i = e / E;
+      if (!frz_s[i] || from_s[i] >= T) continue;
+      const long off = (rb + i) * E + (e - i * E);
+      float mm = m[off], vv = v[off];
+      if (idle_moments(mm, vv)) continue;
+      frz_replay(mm, vv, last.lerp_c, last.b2, T - from_s[i]);
+      m[off] = mm; v[off] = vv;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nr; i += blockDim.x)
+      if (frz_s[i]) emb_step[rb + i] = max(from_s[i], T);
+    __syncthreads();
+  }
+}
+
+__global__ void k_frz_set(dcue_emb_log* hdr, int start, float S, float eps) {
+  hdr->frz_start = start;
+  hdr->frz_S = S;
+  hdr->frz_eps = eps;
+}
+
+namespace {
+struct FrzHost {
+  bool on = false;
+  float S = 0.f, eps = 0.f, lc = 0.f, b2 = 0.f;
+};
+std::mutex& frz_mu() {
+  static std::mutex m;
+  return m;
+}
+std::unordered_map<const void*, FrzHost>& frz_map() {
+  static std::unordered_map<const void*, FrzHost> m;
+  return m;
+}
+// DCUE_FROZEN_ROWS=0: no epochs, no frozen rows (A/B; the replay is then rounds 1-5's)
+bool frozen_rows_on() {
+  static const bool on = [] {
+    const char* e = getenv("DCUE_FROZEN_ROWS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+}  // namespace
+
+void frz_forget(const dcue_emb_log* hdr) {
+  std::lock_guard<std::mutex> lk(frz_mu());
+  frz_map().erase(hdr);
+}
+
+// Before step t's scalars are recorded into the log (on the recording kernel's stream): a step
+// outside the current epoch thaws every frozen row first; a step that admits frozen rows opens an
+// epoch bounded by its own |neg_step| and eps (the first Adam step's lr / (1 - beta1) bounds every
+// later step of a schedule that never raises lr above its start).
+int frz_before_record(const dcue_model* md, const AdamScalars& sc, int t, hipStream_t s) {
+  if (!frozen_rows_on() || !md->emb_step || !md->emb_log) return DCUE_OK;
+  std::lock_guard<std::mutex> lk(frz_mu());
+  FrzHost& f = frz_map()[md->emb_log];
+  const float a = fabsf(sc.neg_step);
+  const bool q = sc.wd == 0.f && !std::signbit(sc.lerp_c) && sc.lerp_c >= 0.f && sc.lerp_c < 0.5f && sc.eps > 0.f &&
+                 sc.b2 >= 0.f && sc.b2 < 1.f && sc.bc2_sqrt > 0.f && sc.bc2_sqrt <= 1.f && a <= 0x1p60f;
+  if (f.on && (!q || sc.lerp_c != f.lc || sc.b2 != f.b2 || a > f.S || sc.eps < f.eps)) {
+    const int E = md->dims.user_embdim;
+    int rpb = 4096 / E;
+    rpb = rpb < 1 ? 1 : (rpb > 256 ? 256 : rpb);
+    long blocks = (md->dims.n_users + rpb - 1) / rpb;
+    blocks = blocks < 1 ? 1 : (blocks > 4096 ? 4096 : blocks);
+    DCUE_LAUNCH(k_emb_thaw, dim3((unsigned)blocks), dim3(256), 0, s, md->emb_exp_avg, md->emb_exp_avg_sq,
+                md->emb_log, md->emb_step, (long)md->dims.n_users, E, rpb);
+    DCUE_LAUNCH_CHECK();
+    DCUE_LAUNCH(k_frz_set, dim3(1), dim3(1), 0, s, md->emb_log, 0, 0.f, 0.f);
+    DCUE_LAUNCH_CHECK();
+    f.on = false;
+  }
+  if (!f.on && q) {
+    f.on = true;
+    f.S = a; f.eps = sc.eps; f.lc = sc.lerp_c; f.b2 = sc.b2;
+    DCUE_LAUNCH(k_frz_set, dim3(1), dim3(1), 0, s, md->emb_log, t, a, sc.eps);
+    DCUE_LAUNCH_CHECK();
+  }
+  return DCUE_OK;
+}
 
 // Rolling flush: at step t the rows of chunk t mod cap (a contiguous 1/cap of the table) are brought
 // current, so every row is replayed at least once per `cap` steps -- the replay work spread evenly
@@ -261,9 +390,16 @@ __global__ __launch_bounds__(256) void k_emb_flush_rows(float* __restrict__ p, f
                                                         int rows_per_block, float gz) {
   __shared__ AdamScalars hs[DCUE_MAX_LOG_CAP];
   __shared__ ReplayBound sb;
-  __shared__ int from_s[256];
+  __shared__ int from_s[256], mode_s[256], frz_s[256];
   const int T = hdr->step_done, F = hdr->flush_step, cap = hdr->cap;
   if (r0 + (long)blockIdx.x * rows_per_block >= r1) return;
+  // frozen rows (adam_replay.h): under an epoch, a replayed row whose every element is long idle for
+  // any future step gets the frozen bit; frozen rows are skipped, or -- once kFrzRefresh steps behind
+  // -- only their m / v are brought current (the recurrence; no p traffic), so a later reader's replay
+  // stays short
+  const bool epoch = hdr->frz_start > 0 && T >= hdr->frz_start - 1;
+  const float fS = hdr->frz_S, feps = hdr->frz_eps;
+  const int refresh = kFrzRefreshCaps * cap;
   const AdamScalars* hist = reinterpret_cast<const AdamScalars*>(hdr + 1);
   const int lo = max(F + 1, T - cap + 1);
   for (int j = lo + (int)threadIdx.x; j <= T; j += blockDim.x) hs[j % cap] = hist[j % cap];
@@ -273,37 +409,70 @@ __global__ __launch_bounds__(256) void k_emb_flush_rows(float* __restrict__ p, f
   const ReplayBound b = sb;
   for (long rb = r0 + (long)blockIdx.x * rows_per_block; rb < r1; rb += (long)gridDim.x * rows_per_block) {
     const int nr = (int)min((long)rows_per_block, r1 - rb);
-    for (int i = threadIdx.x; i < nr; i += blockDim.x) from_s[i] = max(emb_step[rb + i], F);
+    for (int i = threadIdx.x; i < nr; i += blockDim.x) {
+      const int e = emb_step[rb + i];
+      const int from = max(clock_of(e), F);
+      from_s[i] = from;
+      // 0: replay (history), 1: frozen, refresh m / v, 2: frozen, skip
+      mode_s[i] = !is_frozen(e) ? 0 : (T - from >= refresh ? 1 : 2);
+      frz_s[i] = epoch ? 1 : 0;
+    }
     __syncthreads();
+    const float lc = hs[T % cap].lerp_c, b2 = hs[T % cap].b2;  // (the epoch's constants)
     if ((E & 3) == 0) {
       const int E4 = E >> 2;
       for (int e = threadIdx.x; e < nr * E4; e += blockDim.x) {
         const int i = e / E4;
+        const int md = mode_s[i];
+        if (md == 2) continue;
         const long off = (rb + i) * E + 4 * (e - i * E4);
         const float4 m4 = ld4(m + off), v4 = ld4(v + off);
-        if (b.nd && idle_moments4(m4, v4)) continue;  // fixed point (idle_moments)
-        const float4 p4 = ld4(p + off);
-        float pp[4] = {p4.x, p4.y, p4.z, p4.w}, mm[4] = {m4.x, m4.y, m4.z, m4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
-        replay_run<4>(pp, mm, vv, hs, from_s[i] + 1, T, cap, b, gz);
-        if ((__float_as_uint(pp[0]) ^ __float_as_uint(p4.x)) | (__float_as_uint(pp[1]) ^ __float_as_uint(p4.y)) |
-            (__float_as_uint(pp[2]) ^ __float_as_uint(p4.z)) | (__float_as_uint(pp[3]) ^ __float_as_uint(p4.w)))
-          st4(p + off, make_float4(pp[0], pp[1], pp[2], pp[3]));  // long-idle: p unchanged, no store
+        if (idle_moments4(m4, v4) && (b.nd || md == 1)) continue;  // fixed point (idle_moments)
+        float mm[4] = {m4.x, m4.y, m4.z, m4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
+        if (md == 1) {
+          frz_replay_n<4>(mm, vv, lc, b2, T - from_s[i]);
+        } else {
+          const float4 p4 = ld4(p + off);
+          float pp[4] = {p4.x, p4.y, p4.z, p4.w};
+          replay_run<4>(pp, mm, vv, hs, from_s[i] + 1, T, cap, b, gz);
+          if ((__float_as_uint(pp[0]) ^ __float_as_uint(p4.x)) | (__float_as_uint(pp[1]) ^ __float_as_uint(p4.y)) |
+              (__float_as_uint(pp[2]) ^ __float_as_uint(p4.z)) | (__float_as_uint(pp[3]) ^ __float_as_uint(p4.w)))
+            st4(p + off, make_float4(pp[0], pp[1], pp[2], pp[3]));  // long-idle: p unchanged, no store
+          if (epoch) {
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ok &= frz_elem_ok(pp[q], mm[q], vv[q], fS, feps);
+            if (!ok) frz_s[i] = 0;
+          }
+        }
         st4(m + off, make_float4(mm[0], mm[1], mm[2], mm[3]));
         st4(v + off, make_float4(vv[0], vv[1], vv[2], vv[3]));
       }
     } else {
       for (int e = threadIdx.x; e < nr * E; e += blockDim.x) {
         const int i = e / E;
+        const int md = mode_s[i];
+        if (md == 2) continue;
         const long off = (rb + i) * E + (e - i * E);
         float mm[1] = {m[off]}, vv[1] = {v[off]};
-        if (b.nd && idle_moments(mm[0], vv[0])) continue;
-        float pp[1] = {p[off]};
-        replay_run<1>(pp, mm, vv, hs, from_s[i] + 1, T, cap, b, gz);
-        p[off] = pp[0]; m[off] = mm[0]; v[off] = vv[0];
+        if (idle_moments(mm[0], vv[0]) && (b.nd || md == 1)) continue;
+        if (md == 1) {
+          frz_replay(mm[0], vv[0], lc, b2, T - from_s[i]);
+        } else {
+          float pp[1] = {p[off]};
+          replay_run<1>(pp, mm, vv, hs, from_s[i] + 1, T, cap, b, gz);
+          p[off] = pp[0];
+          if (epoch && !frz_elem_ok(pp[0], mm[0], vv[0], fS, feps)) frz_s[i] = 0;
+        }
+        m[off] = mm[0]; v[off] = vv[0];
       }
     }
     __syncthreads();  // (every replay read from_s; the rows' values before their clocks)
-    for (int i = threadIdx.x; i < nr; i += blockDim.x) emb_step[rb + i] = T;
+    for (int i = threadIdx.x; i < nr; i += blockDim.x) {
+      const int md = mode_s[i];
+      if (md == 2) continue;  // (frozen, left behind)
+      emb_step[rb + i] = T | (md == 1 || frz_s[i] ? kFrozenBit : 0);
+    }
   }
 }
 
@@ -349,21 +518,29 @@ __global__ __launch_bounds__(256) void k_adam_touched(float* __restrict__ p, flo
   for (int b = blockIdx.x; b < n; b += gridDim.x) {
     const int64_t u = emb_rows[b];
     if (u < 0) continue;
-    if (threadIdx.x == 0) s_from = max(emb_step[u], F);
+    if (threadIdx.x == 0) {
+      const int e = emb_step[u];
+      s_from = max(clock_of(e), F) | (is_frozen(e) ? kFrozenBit : 0);
+    }
     __syncthreads();
-    const int from = s_from;
+    const int from = clock_of(s_from);
+    const bool frz = is_frozen(s_from);
     float* pr = p + u * E;
     float* mr = m + u * E;
     float* vr = v + u * E;
     const float* gr = gcompact + (long)b * E;
     for (int k = threadIdx.x; k < E; k += blockDim.x) {
       float pp = pr[k], mm = mr[k], vv = vr[k];
-      for (int j = from + 1; j < t; ++j) adam_replay(pp, mm, vv, hist[j % cap], gz);  // normally none
+      if (frz && from + 1 < t)  // (frozen: the recurrence with the epoch's constants, step t-1's)
+        frz_replay(mm, vv, hist[(t - 1) % cap].lerp_c, hist[(t - 1) % cap].b2, t - 1 - from);
+      else
+        for (int j = from + 1; j < t; ++j) adam_replay(pp, mm, vv, hist[j % cap], gz);  // normally none
       adam_elem(pp, gr[k], mm, vv, s);
       pr[k] = pp; mr[k] = mm; vr[k] = vv;
     }
     __syncthreads();
     if (threadIdx.x == 0) emb_step[u] = t;
+    __syncthreads();  // (s_from's next write)
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     log_hist(hdr)[t % cap] = s;
@@ -393,7 +570,9 @@ __global__ __launch_bounds__(256) void k_emb_grad_adam(const float* __restrict__
   if (!first) {
     if (threadIdx.x == 0) emb_rows[b] = -1;
   } else {
-    const int from = max(emb_step[u], F);
+    const int e0 = emb_step[u];
+    const int from = max(clock_of(e0), F);
+    const bool frz = is_frozen(e0);
     const AdamScalars* hist = log_hist(hdr);
     float* pr = p + u * E;
     float* mr = m + u * E;
@@ -405,7 +584,10 @@ __global__ __launch_bounds__(256) void k_emb_grad_adam(const float* __restrict__
       const float g = gsum * scale;
       emb_grad[(long)b * E + k] = g;
       float pp = pr[k], mm = mr[k], vv = vr[k];
-      for (int j = from + 1; j < t; ++j) adam_replay(pp, mm, vv, hist[j % cap], gz);  // normally none
+      if (frz && from + 1 < t)  // (frozen: the recurrence with the epoch's constants, step t-1's)
+        frz_replay(mm, vv, hist[(t - 1) % cap].lerp_c, hist[(t - 1) % cap].b2, t - 1 - from);
+      else
+        for (int j = from + 1; j < t; ++j) adam_replay(pp, mm, vv, hist[j % cap], gz);  // normally none
       adam_elem(pp, g, mm, vv, s);
       pr[k] = pp; mr[k] = mm; vr[k] = vv;
     }
@@ -426,6 +608,7 @@ int launch_emb_grad_adam(const dcue_model* md, const dcue_adam_args* a, const fl
                          float scale, hipStream_t s) {
   if (!md->emb_step || !md->emb_rows || !md->emb_log) return DCUE_ERR_INVALID;
   const AdamScalars sc = form_scalars(a);
+  TRY(frz_before_record(md, sc, a->step, s));
   DCUE_LAUNCH(k_emb_grad_adam, dim3((unsigned)B), dim3(256), 0, s, de, users, B, md->dims.user_embdim, scale,
               md->emb_grad, md->emb_slot, md->emb_rows, md->emb, md->emb_exp_avg, md->emb_exp_avg_sq, md->emb_step,
               md->emb_log, a->step, sc, 0.f);
@@ -467,9 +650,9 @@ __global__ __launch_bounds__(512) void k_user_fwd(UserFwdArgs a) {
       const int64_t u = a.users[r0 + t];
       const int old = a.emb_step[u];
       int from = T, claimed = 0;
-      if (old != INT_MIN && max(old, F) < T && atomicCAS(&a.emb_step[u], old, INT_MIN) == old) {
-        from = max(old, F);
-        claimed = 1;
+      if (old != INT_MIN && max(clock_of(old), F) < T && atomicCAS(&a.emb_step[u], old, INT_MIN) == old) {
+        from = max(clock_of(old), F);
+        claimed = is_frozen(old) ? 2 : 1;  // (2: frozen, the m / v recurrence)
       }
       from_s[t] = from;
       claim_s[t] = claimed;
@@ -488,7 +671,12 @@ __global__ __launch_bounds__(512) void k_user_fwd(UserFwdArgs a) {
       if (!claim_s[i]) continue;
       const long off = a.users[r0 + i] * a.E + k;
       float mm[1] = {a.m[off]}, vv[1] = {a.v[off]};
-      if (b.nd && idle_moments(mm[0], vv[0])) continue;  // fixed point (idle_moments)
+      if (idle_moments(mm[0], vv[0]) && (b.nd || claim_s[i] == 2)) continue;  // fixed point (idle_moments)
+      if (claim_s[i] == 2) {  // frozen (adam_replay.h): p unchanged
+        frz_replay(mm[0], vv[0], hs[T % cap].lerp_c, hs[T % cap].b2, T - from_s[i]);
+        a.m[off] = mm[0]; a.v[off] = vv[0];
+        continue;
+      }
       float pp[1] = {a.p[off]};
       replay_run<1>(pp, mm, vv, hs, from_s[i] + 1, T, cap, b, 0.f);
       a.p[off] = pp[0]; a.m[off] = mm[0]; a.v[off] = vv[0];
@@ -545,9 +733,13 @@ __global__ void k_emb_log_init(dcue_emb_log* hdr, int cap, int step) {
   hdr->n_touched = 0;
   hdr->grad_step = -1;
   hdr->cap = cap;
+  hdr->frz_start = 0;
+  hdr->frz_S = 0.f;
+  hdr->frz_eps = 0.f;
 }
 
 int launch_emb_log_init(const dcue_model* md, int cap, int step, hipStream_t s) {
+  frz_forget(md->emb_log);
   DCUE_HIP_CHECK(hipMemsetAsync(md->emb_step, 0, sizeof(int32_t) * md->dims.n_users, s));
   DCUE_LAUNCH(k_emb_log_init, dim3(1), dim3(1), 0, s, md->emb_log, cap, step);
   DCUE_LAUNCH_CHECK();
@@ -658,6 +850,7 @@ int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* po
     DCUE_LAUNCH_CHECK();
   }
   if ((parts & DCUE_ADAM_EMBEDDING) && md->emb_step) {
+    TRY(frz_before_record(md, sc, a->step, s));
     DCUE_LAUNCH(k_adam_touched, dim3(256), dim3(256), 0, s, md->emb, md->emb_exp_avg,
                        md->emb_exp_avg_sq, md->emb_grad, md->emb_rows, md->emb_step, md->emb_log,
                        md->dims.user_embdim, a->step, sc, 0.f);

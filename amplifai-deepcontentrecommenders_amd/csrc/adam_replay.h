@@ -174,4 +174,47 @@ DCUE_RHD void replay_run(float (&p)[W], float (&m)[W], float (&v)[W], const Adam
   }
 }
 
+// ------------------------------------------------------------------ frozen rows (round 6)
+// A row whose every element is long idle for EVERY future step, not only over the current history
+// window, needs no history at all: its remaining zero-gradient steps are the m / v recurrence with
+// the optimizer's constant (lerp_c, b2), p bit-identical. Such a row is "frozen": bit 30 of its clock
+// (emb_step) is set, the rolling slices skip it (no p / m / v traffic) or only refresh its m / v
+// with the recurrence now and then, and whoever next reads it replays the recurrence from its clock.
+// The future is bounded by an epoch the host keeps (adam.hip frz_before_record): every step of the
+// epoch has wd = 0, lerp base m with the epoch's lerp_c < 0.5, the epoch's b2, |neg_step| <= S and
+// eps >= eps_min; a step outside it first thaws every frozen row (k_emb_thaw: replayed to the last
+// step, the bit cleared). Then the long-idle bound of above holds for any later step k with
+// LB = eps_min (d_k >= eps_k >= eps_min): S |m| <= eps_min |p| 2^-27 at freezing time suffices.
+constexpr int kFrozenBit = 0x40000000;
+DCUE_RHD int clock_of(int e) { return e < 0 ? e : (e & ~kFrozenBit); }
+DCUE_RHD bool is_frozen(int e) { return e >= 0 && (e & kFrozenBit) != 0; }
+
+// (m, v) = (+0, +0) (idle: a fixed point), or long idle under every step of the epoch
+DCUE_RHD bool frz_elem_ok(float p, float m, float v, float S, float eps_min) {
+  if ((__builtin_bit_cast(unsigned, m) | __builtin_bit_cast(unsigned, v)) == 0u) return true;
+  const float ap = p < 0.f ? -p : p, am = m < 0.f ? -m : m;
+  return (ap >= 0x1p-60f) & (ap <= 0x1p100f) & (am <= 0x1p100f) & (v >= 0.f) & (v <= 0x1p126f) &
+         (S * am <= eps_min * ap * 0x1p-27f);
+}
+
+// n zero-gradient steps of a frozen element: m = fma(c, -m, m), v = v b2 (replay_run's long-idle
+// loop with the epoch's constants)
+DCUE_RHD void frz_replay(float& m, float& v, float lc, float b2, int n) {
+  for (int k = 0; k < n; ++k) {
+    m = rn_fma(lc, rn_sub(0.f, m), m);
+    v = rn_mul(v, b2);
+  }
+}
+// the same for W elements in lockstep (independent chains interleaved)
+template <int W>
+DCUE_RHD void frz_replay_n(float (&m)[W], float (&v)[W], float lc, float b2, int n) {
+  for (int k = 0; k < n; ++k) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      m[w] = rn_fma(lc, rn_sub(0.f, m[w]), m[w]);
+      v[w] = rn_mul(v[w], b2);
+    }
+  }
+}
+
 }  // namespace dcue

@@ -562,6 +562,8 @@ bool probes_on();
 int probe(int id, const float* x, long n, hipStream_t s);
 bool poison_on();
 unsigned* user_fwd_fail_flag();
+// frozen-row epochs of a user-table Adam log (adam.hip): forget the host's epoch (the log re-initialised)
+void frz_forget(const dcue_emb_log* hdr);
 // DCUE_LEGACY_ORDERS=1: the round-4 cross-stream orders, without the waits that closed its races
 //  -- only to show tests/test_gpu_races.py failing on them
 bool legacy_orders();

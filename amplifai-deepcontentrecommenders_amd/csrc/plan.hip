@@ -63,11 +63,16 @@ struct dcue_plan {
   dcue::DevWait late_sig{};
 };
 
-// DCUE_XQ_WAIT=event: the plan's caller-stream waits as HIP event waits (rounds 1-5; A/B)
+// DCUE_XQ_WAIT=event: the plan's caller-stream waits as HIP event waits (rounds 1-5; A/B). Also off
+// under rocprofv3 counter collection (ROCPROF_COUNTER_COLLECTION): it runs one dispatch at a time, so
+// a consumer kernel polling for a producer on another queue would hold the GPU until its wait gave up
+// (DevWait's bound; measured: the fail word's bit 1 set, 1.4 ms steps)
 static bool dev_waits_on() {
   static const bool on = [] {
     const char* e = getenv("DCUE_XQ_WAIT");
-    return !(e && e[0] == 'e');
+    const char* pmc = getenv("ROCPROF_COUNTER_COLLECTION");
+    const bool counters = pmc && pmc[0] && pmc[0] != '0' && pmc[0] != 'f' && pmc[0] != 'F';
+    return !(e && e[0] == 'e') && !counters;
   }();
   return on;
 }

@@ -717,6 +717,8 @@ def main():
             nat.timer_enable(k, False)
         return dt, t_enq, (ev0.elapsed_time(ev1) / args.steps if gpu_only else None), kern
 
+    frozen_frac = [None]
+
     def replay_bytes(optim):
         """Bytes the user-table replay moves over the whole table (k_emb_flush; adam.hip): m and v
         read for every element, p read and m, v written for the float4 groups whose moments are not
@@ -725,6 +727,8 @@ def main():
         physical. Counted after the phase's final flush (an idle group stays idle)."""
         st = optim._adam_state()
         em, ev = st["em"], st["ev"]
+        if st.get("emb_step") is not None:  # frozen rows (csrc/adam_replay.h): clock bit 30
+            frozen_frac[0] = float(((st["emb_step"] & 0x40000000) != 0).float().mean())
         n = em.numel()
         if n % 4:
             act = int(((em.view(torch.int32) | ev.view(torch.int32)) != 0).sum())
@@ -816,6 +820,7 @@ def main():
                            algorithmic_bytes=work)
                 if k in (nat.TIMED_EMB_SLICE, nat.TIMED_EMB_FLUSH):
                     ent["active_fraction"] = active  # of the table's elements with live moments
+                    ent["frozen_row_fraction"] = frozen_frac[0]  # rows the slices skip (adam_replay.h)
                 ent["frac" if bound == "hbm" else "hbm_frac"] = ent["achieved"] / HBM_PEAK_GBS
                 if k == nat.TIMED_TEXT_WGRAD:  # its f32 FMAs against the f32 vector peak, for information
                     fl = 2.0 * M * Ct * Ew * 3
@@ -885,14 +890,19 @@ def main():
     # ---- phase 1: in-batch, cold user table
     plan = make_plan(False)
     ub, ib = batches(args.warmup + args.steps)
-    dt, t_enq, _, kern = timed_phase("inbatch_cold", plan, inbatch_step(ub, ib))
+    # (--gpu-only applies to the cold phase when that is the profiled one: its GPU-only timeline)
+    cold_gpu_only = args.gpu_only and args.profile_phase == "inbatch_cold"
+    dt, t_enq, gpu_ms_c, kern = timed_phase("inbatch_cold", plan, inbatch_step(ub, ib), gpu_only=cold_gpu_only)
     out["inbatch_cold"] = summary(dt, t_enq, kern, B, 1, "inbatch", "inbatch_cold")
+    if gpu_ms_c is not None:
+        out["inbatch_cold"]["gpu_only_ms_per_step"] = gpu_ms_c
     # ---- phase 2: every local user once (outside any timed region), then in-batch steady state
     warm = inbatch_step(warm_users, warm_items)
     run(plan, warm, warm_users.shape[0])
     if "inbatch" in modes:
         ub, ib = batches(args.warmup + args.steps)
-        dt, t_enq, gpu_ms, kern = timed_phase("inbatch", plan, inbatch_step(ub, ib), gpu_only=args.gpu_only)
+        dt, t_enq, gpu_ms, kern = timed_phase("inbatch", plan, inbatch_step(ub, ib),
+                                              gpu_only=args.gpu_only and not cold_gpu_only)
         out["inbatch"] = summary(dt, t_enq, kern, B, 1, "inbatch", "inbatch")
         if gpu_ms is not None:
             out["inbatch"]["gpu_only_ms_per_step"] = gpu_ms

@@ -94,7 +94,12 @@ typedef struct dcue_emb_log {
   int32_t n_touched;   /* emb_rows entries written by the last backward */
   int32_t grad_step;   /* the Adam step the last backward's compact gradient belongs to */
   int32_t cap;         /* history ring capacity in steps (= flush period) */
-  int32_t pad[3];
+  /* frozen rows (ABI 16): the epoch whose steps all keep long-idle rows long idle -- its first step
+   * (0: none), the largest |lr / bias_correction1| and the smallest eps it admits; a row's clock
+   * (emb_step) with bit 30 set is frozen under it. Written by the library only. */
+  int32_t frz_start;
+  float frz_S;
+  float frz_eps;
 } dcue_emb_log;
 
 /* Model state. Replaces DCUENet's parameters/buffers (dcue/dcue.py:21-68) + torch.optim.Adam state. */

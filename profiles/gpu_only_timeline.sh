@@ -9,7 +9,8 @@ OUT=$ROOT/gpurun_out/gpuonly_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace -f csv -d "$OUT/trace" -o run -- python3 $ROOT/bench.py \
-  --no-cpu-baseline --no-eval --steps ${STEPS:-8} --warmup 3 --modes inbatch --gpu-only --profile-phase inbatch \
+  --no-cpu-baseline --no-eval --no-f32-probe --steps ${STEPS:-8} --warmup 3 --modes inbatch --gpu-only \
+  --profile-phase ${PHASE:-inbatch} \
   > "$OUT/prof.log" 2>&1 || exit 1
 python3 $ROOT/profiles/timeline.py "$OUT/trace" "k_conv_rows<0, 0," > "$OUT/timeline.txt" 2>&1
 python3 $ROOT/profiles/phase_kernels.py "$OUT/trace" 40 > "$OUT/kernels.txt"

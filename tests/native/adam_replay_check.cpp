@@ -177,8 +177,57 @@ int main(int argc, char** argv) {
       }
     }
   }
+  // Frozen rows (adam_replay.h, round 6): an element that passes frz_elem_ok under an epoch (S bounds
+  // every later |neg_step|, eps_min every later eps, lerp_c / b2 fixed) takes any number of later
+  // zero-gradient steps of that epoch -- lr, eps and bc2 varying within it -- with p unchanged and
+  // m / v exactly frz_replay's recurrence. Reference: adam_elem step by step.
+  long frz_elems = 0, frz_steps = 0, frz_mism = 0;
+  for (long c = 0; c < cases; ++c) {
+    const double b1 = pick(4) ? 0.9 : 0.5 + 0.49 * U(rng);
+    const double b2 = pick(3) ? (pick(2) ? 0.99 : 0.999) : 0.9 + 0.0999 * U(rng);
+    const double eps_min = pick(4) ? 1e-8 : logu(-12, -4);
+    const double lr_hi = logu(-5, -1);
+    const AdamScalars s1 = scalars(lr_hi, b1, b2, eps_min, 1);
+    const float S = std::fabs(s1.neg_step), lc = s1.lerp_c, fb2 = s1.b2;
+    float p = (float)(sgn() * logu(-3, 1)), m, v;
+    const double g = logu(-9, 1);
+    v = (float)(g * g * (1.0 - b2) * logu(-3, 2));
+    switch (pick(4)) {
+      case 0:  // just inside the freeze threshold
+        m = (float)(sgn() * (double)eps_min * std::fabs((double)p) * std::ldexp(1.0, -27) / S * (0.5 + 0.5 * U(rng)));
+        break;
+      case 1:  // far below it
+        m = (float)(sgn() * (double)eps_min * std::fabs((double)p) * std::ldexp(1.0, -27) / S * logu(-6, -1));
+        break;
+      case 2:  // binade-edge p, at the threshold
+        p = (float)(sgn() * std::ldexp(1.0, -20 + pick(24)));
+        m = (float)(sgn() * (double)eps_min * std::fabs((double)p) * std::ldexp(1.0, -27) / S);
+        break;
+      default:  // subnormal moments
+        m = (float)(sgn() * std::ldexp(1.0, -130 - pick(19)));
+        v = pick(2) ? 0.f : (float)std::ldexp(1.0, -128 - pick(20));
+        break;
+    }
+    if (!frz_elem_ok(p, m, v, S, (float)eps_min)) continue;
+    ++frz_elems;
+    const int t0 = 1 + pick(5000), n = 1 + pick(pick(8) ? 300 : 4000);
+    float rp = p, rm = m, rv = v;
+    for (int k = 0; k < n; ++k) {  // the epoch's steps: lr <= lr_hi, eps >= eps_min, the same betas
+      const double lr = lr_hi * U(rng) + 1e-12;
+      const double eps = eps_min * (pick(3) ? 1.0 : 1.0 + 9.0 * U(rng));
+      adam_elem(rp, 0.f, rm, rv, scalars(lr, b1, b2, eps, t0 + k));
+    }
+    float fm = m, fv = v;
+    frz_replay(fm, fv, lc, fb2, n);
+    frz_steps += n;
+    if (bits(rp) != bits(p) || bits(rm) != bits(fm) || bits(rv) != bits(fv)) {
+      if (frz_mism < 10)
+        std::printf("FROZEN MISMATCH case %ld: p %a -> %a, m %a vs %a, v %a vs %a\n", c, p, rp, rm, fm, rv, fv);
+      ++frz_mism;
+    }
+  }
   std::printf("cases %ld elements %ld element-steps %ld shortcut-elements %ld shortcut-steps %ld "
-              "worst-margin %.6f mismatches %ld\n",
-              cases, elems, steps_total, deep_elems, steps_short, worst, mismatches);
-  return mismatches == 0 && worst < 1.0 ? 0 : 1;
+              "worst-margin %.6f mismatches %ld frozen-elements %ld frozen-steps %ld frozen-mismatches %ld\n",
+              cases, elems, steps_total, deep_elems, steps_short, worst, mismatches, frz_elems, frz_steps, frz_mism);
+  return mismatches == 0 && frz_mism == 0 && worst < 1.0 ? 0 : 1;
 }

@@ -38,3 +38,6 @@ def test_replay_shortcut_bit_exact(checker, seed):
     assert int(stats["mismatches"]) == 0
     assert int(stats["shortcut-steps"]) > 0.1 * int(stats["element-steps"])  # the shortcut is exercised
     assert float(stats["worst-margin"]) < 1.0
+    # frozen rows (round 6): the epoch-bounded freeze test and the history-free recurrence
+    assert int(stats["frozen-mismatches"]) == 0
+    assert int(stats["frozen-elements"]) > 1000
