@@ -78,7 +78,7 @@ struct PackArgs {
 __global__ __launch_bounds__(256) void k_adam_dense_pack(float* __restrict__ p, float* __restrict__ g,
                                                          float* __restrict__ m, float* __restrict__ v,
                                                          long lo, long n, AdamScalars s, PackArgs pa,
-                                                         float* __restrict__ wpack, float gdiv) {
+                                                         float* __restrict__ wpack, float gdiv, unsigned* sig) {
   const long n4 = n / 4;
   for (long i = lo / 4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     float4 pp = ld4(p + 4 * i), gg = ld4(g + 4 * i), mm = ld4(m + 4 * i), vv = ld4(v + 4 * i);
@@ -112,6 +112,7 @@ __global__ __launch_bounds__(256) void k_adam_dense_pack(float* __restrict__ p, 
     if (gdiv > 0.f) g[i] = gi = __fdiv_rn(gi, gdiv);
     adam_elem(p[i], gi, m[i], v[i], s);
   }
+  dev_signal_wg(sig);  // (plans: the late segments' Adam, for the next step's conv 2)
 }
 
 // User table: one wave per row; rows without a gradient this step get g = 0 (the reference's dense
@@ -635,6 +636,7 @@ struct UserFwdArgs {
   const int64_t* users;
   int B, E;
   unsigned* fail;          // set when a wait for another workgroup's claim gave up (never expected)
+  unsigned* sig;           // plans: +1 per workgroup once its uf rows are stored (dev_signal_wg)
 };
 
 __global__ __launch_bounds__(512) void k_user_fwd(UserFwdArgs a) {
@@ -709,10 +711,13 @@ __global__ __launch_bounds__(512) void k_user_fwd(UserFwdArgs a) {
   for (int by = half; by < gy1 + (gy1 & 1); by += 2) tgemm_block<1, 0, 1, 0>(a.g1, blockIdx.x, by, L[half], th);
   __syncthreads();
   for (int by = half; by < gy2 + (gy2 & 1); by += 2) tgemm_block<1, 0, 1, 0>(a.g2, blockIdx.x, by, L[half], th);
+  dev_signal_wg(a.sig);
 }
 
+int user_fwd_blocks(int B) { return (B + 15) / 16; }
+
 int launch_user_fwd(const dcue_model* md, const TGemmArgs& g1, const TGemmArgs& g2, const int64_t* users, int B,
-                    hipStream_t s) {
+                    hipStream_t s, unsigned* sig) {
   if (g1.sak != 1 || g1.sbn == 1 || g2.sak != 1 || g2.sbn == 1 || !g1.arow || g2.arow) return DCUE_ERR_INVALID;
   UserFwdArgs a;
   a.g1 = g1; a.g2 = g2;
@@ -722,7 +727,8 @@ int launch_user_fwd(const dcue_model* md, const TGemmArgs& g1, const TGemmArgs& 
   unsigned* const fail = user_fwd_fail_flag();  // this device's word (cached per device)
   if (!fail) return DCUE_ERR_HIP;
   a.fail = fail;
-  DCUE_LAUNCH(k_user_fwd, dim3((unsigned)((B + 15) / 16)), dim3(512), 0, s, a);
+  a.sig = sig;
+  DCUE_LAUNCH(k_user_fwd, dim3((unsigned)user_fwd_blocks(B)), dim3(512), 0, s, a);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
@@ -834,19 +840,21 @@ int launch_bn0_grads_adam(const float* G, const float* E, const float* gamma0, c
   return DCUE_OK;
 }
 
+long adam_dense_blocks(long len) { return len >= 512L * 1024 ? 512 : (len / 4 + 255) / 256 + 1; }
+
 int launch_adam(const dcue_model* md, const dcue_adam_args* a, const int64_t* poff, hipStream_t s,
-                bool flush_slice, long dense_lo, long dense_hi, bool defer_dgrad2) {
+                bool flush_slice, long dense_lo, long dense_hi, bool defer_dgrad2, unsigned* sig) {
   const AdamScalars sc = form_scalars(a);
   const float gdiv = a->grad_div > 1.0 ? (float)a->grad_div : 0.f;
   const int parts = a->parts ? a->parts : (DCUE_ADAM_DENSE | DCUE_ADAM_EMBEDDING);
   const long n = dense_hi >= 0 ? dense_hi : poff[DCUE_N_DENSE_SEGMENTS];
   if (parts & DCUE_ADAM_DENSE) {  // Adam + the conv-weight repack in one sweep
     const long len = n - dense_lo;
-    const long blocks = len >= 512L * 1024 ? 512 : (len / 4 + 255) / 256 + 1;
+    const long blocks = adam_dense_blocks(len);
     PackArgs pa = pack_args(md, poff);
     if (defer_dgrad2) pa.seg[1].bwd = pa.seg[1].f16b = -1;  // (the next forward of conv 2 writes them)
     DCUE_LAUNCH(k_adam_dense_pack, dim3((unsigned)blocks), dim3(256), 0, s, md->params, md->grads, md->exp_avg,
-                       md->exp_avg_sq, dense_lo, n, sc, pa, md->wpack, gdiv);
+                       md->exp_avg_sq, dense_lo, n, sc, pa, md->wpack, gdiv, sig);
     DCUE_LAUNCH_CHECK();
   }
   if ((parts & DCUE_ADAM_EMBEDDING) && md->emb_step) {

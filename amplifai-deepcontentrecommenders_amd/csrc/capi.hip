@@ -633,8 +633,10 @@ int user_forward(const Ctx& c, const Ws& w, const int64_t* users, int B, float* 
   return launch_tgemm(1, 0, g, s);
 }
 
-// the same, with the deferred rows' sync in one launch (k_user_fwd): the train forward's user tower
-int user_forward_fused(const Ctx& c, const Ws& w, const int64_t* users, int B, hipStream_t s) {
+// the same, with the deferred rows' sync in one launch (k_user_fwd): the train forward's user tower;
+// sig: the plan's signal word its workgroups add to once uf is stored (DevWait)
+int user_forward_fused(const Ctx& c, const Ws& w, const int64_t* users, int B, hipStream_t s,
+                       unsigned* sig = nullptr) {
   const dcue_model* m = c.m;
   TGemmArgs g1 = {}, g2 = {};
   g1.M = B; g1.N = c.E; g1.K = c.E;
@@ -647,7 +649,7 @@ int user_forward_fused(const Ctx& c, const Ws& w, const int64_t* users, int B, h
   g2.B = c.P(SEG_L2_W); g2.sbk = 1; g2.sbn = c.E;
   g2.bias = c.P(SEG_L2_B);
   g2.C = w.uf; g2.scm = c.D; g2.scn = 1;
-  return launch_user_fwd(m, g1, g2, users, B, s);
+  return launch_user_fwd(m, g1, g2, users, B, s, sig);
 }
 
 // whether a gather batch gets per-item copy lists (the prologue's histogram path)
@@ -847,8 +849,15 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
   const bool text_side = c.text && text_side_on();
   // plans: the score kernel waits for the user tower on the device (DevWait), not by a stream wait
   const bool uf_sig = o.sig != nullptr && !capturing_step();
+  static const bool split_fwd = [] {  // DCUE_USER_FWD=split: k_emb_sync + two k_tgemm (A/B)
+    const char* e = getenv("DCUE_USER_FWD");
+    return e && e[0] == 's';
+  }();
   DevWait uf_wait{};
-  if (uf_sig) uf_wait = DevWait{o.sig + kSigUf, ++o.sig_issued[kSigUf], user_fwd_fail_flag()};
+  // the fused launch signals from its own workgroups; the three-launch form through k_signal
+  if (uf_sig)
+    uf_wait = DevWait{o.sig + kSigUf, o.sig_issued[kSigUf] += split_fwd ? 1u : (unsigned)user_fwd_blocks(b->n_rows),
+                      user_fwd_fail_flag()};
   // the user tower on su: emb rows brought up to date, then the two GEMMs (+ the text branch, the
   // rolling flush slice)
   const std::function<int()> user_part = [&]() -> int {
@@ -859,14 +868,11 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
     // as three (k_emb_sync, one workgroup per row, then two k_tgemm) -- A/B and the schedule test.
     // (Round 4 made the fused form opt-in after non-finite runs; their cause was the plan's
     // cross-stream races, DESIGN.md §4.7 round 5, tests/test_gpu_races.py.)
-    static const bool split_fwd = [] {
-      const char* e = getenv("DCUE_USER_FWD");
-      return e && e[0] == 's';
-    }();
+    unsigned* const ufs = uf_sig && !split_fwd ? o.sig + kSigUf : nullptr;
     TimerScope tsu;  // (the fused launch is timed live: DCUE_TIMED_USER_FWD)
     TRY(timer_begin(&tsu, split_fwd ? -1 : DCUE_TIMED_USER_FWD, su));
     if (tsu.b && !tsu.capturing) {  // a timed launch: the timer's stop event is its end
-      TRY(user_forward_fused(c, w, b->users, b->n_rows, su));
+      TRY(user_forward_fused(c, w, b->users, b->n_rows, su, ufs));
       ev_uf = tsu.b;
       TRY(timer_end(&tsu));
     } else {  // (untimed, or a captured plan: its timer node follows the launch)
@@ -875,14 +881,14 @@ int forward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t,
         if (m->emb_step) TRY(launch_emb_sync(m, b->users, b->n_rows, su));
         TRY(user_forward(c, w, b->users, b->n_rows, nullptr, su));
       } else {
-        TRY(user_forward_fused(c, w, b->users, b->n_rows, su));
+        TRY(user_forward_fused(c, w, b->users, b->n_rows, su, ufs));
       }
       HPROF("capi:7");
       TRY(fk.done());
       HPROF("capi:8");
       TRY(timer_end(&tsu));
     }
-    if (uf_sig) TRY(launch_signal(o.sig + kSigUf, uf_wait.val, su));
+    if (uf_sig && split_fwd) TRY(launch_signal(o.sig + kSigUf, uf_wait.val, su));
     TRY(probe(PR_H1, w.h1, (long)b->n_rows * c.E, su));
     TRY(probe(PR_UF, w.uf, (long)b->n_rows * c.D, su));
     if (text_side) {  // the text branch: the item tower's fc input columns [0, C_s), beside its convs
@@ -1307,7 +1313,9 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   // plans (split, no exchange): the late Adam also signals the next step's conv 2 (DevWait)
   DevWait late_sig{};
   if (o.dense_split && !o.comm && o.late_sig && o.sig && !capturing_step()) {
-    late_sig = DevWait{o.sig + kSigLate, ++o.sig_issued[kSigLate], user_fwd_fail_flag()};
+    // its dense sweep's workgroups signal themselves (k_adam_dense_pack, dev_signal_wg)
+    const unsigned nwg = (unsigned)adam_dense_blocks(c.poff[kSeg] - c.poff[DCUE_SEG_LATE]);
+    late_sig = DevWait{o.sig + kSigLate, o.sig_issued[kSigLate] += nwg, user_fwd_fail_flag()};
     *o.late_sig = late_sig;
   }
   dcue_adam_args dense = {};
@@ -1337,10 +1345,10 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       TRY(debug_delay(DCUE_SITE_LATE_ADAM, su));
       {
         ForkAfter fk(sp, su, o.late_done);
-        TRY(launch_adam(m, &dense, c.poff, su, true, late, -1, !legacy_orders()));
+        TRY(launch_adam(m, &dense, c.poff, su, true, late, -1, !legacy_orders(),
+                        late_sig.flag ? o.sig + kSigLate : nullptr));
         TRY(fk.done());
       }
-      if (late_sig.flag) TRY(launch_signal(o.sig + kSigLate, late_sig.val, su));
       TRY(probe(PR_P_LATE, m->params + late, c.poff[kSeg] - late, su));
     }
     return DCUE_OK;

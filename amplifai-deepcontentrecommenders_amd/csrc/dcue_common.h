@@ -221,6 +221,21 @@ __device__ __forceinline__ void dev_wait(const DevWait& w) {
   __syncthreads();
 }
 
+// The producer side inside the producer kernel itself (no k_signal launch): every workgroup, once
+// all its stores are done, releases them at agent scope and adds 1 to the signal word; the consumer
+// waits for the word to reach the count of workgroups issued so far (the host adds each launch's grid
+// size to its issue counter). All threads of the workgroup must call it (a barrier inside).
+__device__ __forceinline__ void dev_signal_wg(unsigned* sig) {
+  if (!sig) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // An order only: the kernel reads nothing the producer wrote, but later kernels on its stream must
 // start after the producer (their own start-of-kernel acquire then sees its data). One lane polls at
 // the end of the kernel's work; no barrier, no acquire.

@@ -344,7 +344,8 @@ int launch_tgemm(int ta, int tb, const TGemmArgs& g, hipStream_t s);
 // the user tower's forward in one launch (adam.hip k_user_fwd): deferred mode's row sync, then g1
 // (h1 = relu(E[users]) W1^T + b1) and g2 (uf = relu(h1) W2^T + b2) as launch_tgemm(1, 0, .) computes them
 int launch_user_fwd(const dcue_model* md, const TGemmArgs& g1, const TGemmArgs& g2, const int64_t* users, int B,
-                    hipStream_t s);
+                    hipStream_t s, unsigned* sig = nullptr);
+int user_fwd_blocks(int B);  // k_user_fwd's workgroups (each adds 1 to sig)
 // two independent GEMMs in one launch: g1 as launch_tgemm(0, 1, .) with a k-strided A, g2 as
 // launch_tgemm(0, 0, .) with a k-contiguous A; both with n-contiguous B (the user tower's backward)
 int launch_tgemm_pair(const TGemmArgs& g1, const TGemmArgs& g2, hipStream_t s);
@@ -381,7 +382,10 @@ int launch_emb_grad(const float* de, const int64_t* users, int B, int E, float s
 // the next training forward of conv 2 (RowsArgs::rp): the split plans' late Adam, which may run
 // beside the caller stream's dgrad of conv 2 that reads them
 int launch_adam(const dcue_model* m, const dcue_adam_args* a, const int64_t* poff, hipStream_t s,
-                bool flush_slice = true, long dense_lo = 0, long dense_hi = -1, bool defer_dgrad2 = false);
+                bool flush_slice = true, long dense_lo = 0, long dense_hi = -1, bool defer_dgrad2 = false,
+                unsigned* sig = nullptr);
+// workgroups of the dense Adam sweep over len floats (each adds 1 to launch_adam's sig)
+long adam_dense_blocks(long len);
 // conv layer l's packed copies (adam.hip pack_args)
 PackSeg pack_seg(const dcue_model* m, const int64_t* poff, int l);
 int launch_emb_flush_rows(const dcue_model* m, int step, hipStream_t s);

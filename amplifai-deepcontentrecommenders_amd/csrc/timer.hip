@@ -63,13 +63,14 @@ bool timer_take_turn(int cls) {
 }
 
 int timer_begin(TimerScope* sc, int cls, hipStream_t s) {
-  std::lock_guard<std::recursive_mutex> lk(tmu());
   sc->cls = cls;
   sc->s = s;
   sc->a = sc->b = nullptr;
   sc->capturing = false;
   sc->preds.clear();
-  if (cls < 0 || cls >= DCUE_N_TIMED || !ts().stride[cls]) return DCUE_OK;
+  if (cls < 0 || cls >= DCUE_N_TIMED) return DCUE_OK;  // (no lock for untimed launches: most of them)
+  std::lock_guard<std::recursive_mutex> lk(tmu());
+  if (!ts().stride[cls]) return DCUE_OK;
   if (ts().seen[cls]++ % ts().stride[cls]) return DCUE_OK;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   const hipGraphNode_t* deps = nullptr;
@@ -90,6 +91,7 @@ int timer_begin(TimerScope* sc, int cls, hipStream_t s) {
 }
 
 int timer_end(TimerScope* sc) {
+  if (!sc->capturing && !sc->a) return DCUE_OK;  // (an untimed launch: no lock)
   std::lock_guard<std::recursive_mutex> lk(tmu());
   if (sc->capturing) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
@@ -134,9 +136,11 @@ struct HostProfile {
   std::chrono::steady_clock::time_point last;
   std::map<std::string, std::pair<double, long>> acc;
   std::vector<std::string> order;
+  bool slow = false;  // DCUE_HOST_PROFILE=2: also every single interval above 100 us, as it happens
   HostProfile() {
     const char* e = getenv("DCUE_HOST_PROFILE");
-    on = e && e[0] == '1';
+    on = e && (e[0] == '1' || e[0] == '2');
+    slow = e && e[0] == '2';
     last = std::chrono::steady_clock::now();
   }
   ~HostProfile() {
@@ -168,6 +172,7 @@ void host_profile_mark(const char* label) {
   }
   it->second.first += us;
   it->second.second += 1;
+  if (p.slow && us > 100.0) fprintf(stderr, "[dcue host slow] %s %.1f us (call %ld)\n", label, us, it->second.second);
 }
 
 void set_last_error(const char* expr, hipError_t e, const char* file, int line) {
@@ -187,7 +192,9 @@ extern "C" int dcue_timer_enable(int32_t kernel, int32_t enable) {
   if (enable < 0) return DCUE_ERR_INVALID;
   std::lock_guard<std::recursive_mutex> lk(dcue::tmu());
   dcue::ts().stride[kernel] = enable;
-  dcue::ts().seen[kernel] = 0;
+  // the first timed launch is the enable-th (ABI 16; was the first): a timed launch costs the host
+  // tens of microseconds, and the first launches after enabling are the ones a measurement starts with
+  dcue::ts().seen[kernel] = 1;
   return DCUE_OK;
 }
 

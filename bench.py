@@ -20,6 +20,7 @@ N>1 runs one process per GPU: under torch.distributed.run (RANK/WORLD_SIZE set) 
 directly, bench.py launches the N ranks itself before touching any GPU.
 """
 import argparse
+import gc
 import json
 import math
 import os
@@ -82,6 +83,10 @@ def parse():
     ap.add_argument("--eval-pct", type=float, default=0.025, help="users sampled for AUC@val (eval_pct)")
     ap.add_argument("--timer-stride", type=int, default=8,
                     help="time every n-th launch of the roofline kernels live (HIP events)")
+    ap.add_argument("--gc-mode", choices=["on", "off"], default="on",
+                    help="diagnostic: off = gc.collect() then gc.disable() around each phase's timed steps")
+    ap.add_argument("--host-trace", action="store_true",
+                    help="diagnostic: report each timed step's host issue time (host_issue_us per phase)")
     ap.add_argument("--gpu-only", action="store_true",
                     help="diagnostic: hold the stream behind a sleep kernel while the warm in-batch "
                          "steps are enqueued, then report the GPU's own time for them")
@@ -630,6 +635,8 @@ def main():
              nat.TIMED_ALLREDUCE, nat.TIMED_TEXT_FWD, nat.TIMED_USER_FWD, nat.TIMED_TEXT_WGRAD]
     # every stride-th launch of each class is timed live (a timed launch costs its stream a few us)
     stride = max(1, min(args.timer_stride, args.steps // 4))
+    if args.timer_stride <= 0:  # (diagnostic: no live kernel timing at all)
+        timed = []
 
     def make_plan(catalogue):
         plan = TrainPlan(net, tracks, B, N, mt_state=None if catalogue else mt, emb_grad_scale=1.0 / world,
@@ -640,13 +647,16 @@ def main():
                 plan.set_sync_bn(True)
         return plan
 
-    def run(plan, step_fn, n, phase="warm-up"):
+    def run(plan, step_fn, n, phase="warm-up", stamps=None):
         for s in range(n):
             # a step's exchange is issued inside plan.step; a rank stuck in it stops here or in the
             # synchronize after the loop, with that step's two buckets (bn0/conv1/bn1 and the rest)
             # pending on the communicator's stream
-            mark("%s step %d/%d issued (its RCCL buckets: late segments then bn0/conv-1/bn1)" % (phase, s + 1, n))
+            if wd is not None:
+                mark("%s step %d/%d issued (its RCCL buckets: late segments then bn0/conv-1/bn1)" % (phase, s + 1, n))
             step_fn(plan, s)
+            if stamps is not None:
+                stamps.append(time.perf_counter())
 
     def inbatch_step(users_b, items_b):
         # per-step batch views made once, outside the timed region (the batch composition is prepared
@@ -675,6 +685,7 @@ def main():
         torch.cuda.synchronize()
 
     launches = {}  # kernel launches per timed step, per phase (libdcue_hip's own count)
+    host_trace = {}  # --host-trace: per-step host issue times, per phase
 
     def timed_phase(name, plan, step_fn, gpu_only=False, optim=None):
         """W warm-up steps, then EXACTLY K timed steps between barrier + synchronize on both
@@ -682,6 +693,9 @@ def main():
         optim = opt if optim is None else optim
         run(plan, step_fn, args.warmup, name + " warm-up")
         optim.flush()
+        if args.gc_mode == "off":  # (A/B: Python's cyclic collector held off over the timed steps)
+            gc.collect()
+            gc.disable()
         mark(name + ": barrier before the timed steps")
         if world > 1:
             dist.barrier()
@@ -698,9 +712,14 @@ def main():
             ev0.record()
         l0 = nat.lib().dcue_launch_count()
         t0 = time.perf_counter()
-        run(plan, lambda p, s: step_fn(p, args.warmup + s), args.steps, name + " timed")
+        stamps = [] if args.host_trace else None
+        run(plan, lambda p, s: step_fn(p, args.warmup + s), args.steps, name + " timed", stamps)
+        if stamps is not None:  # --host-trace: each timed step's host issue time (us)
+            host_trace[name] = [round((b - a) * 1e6, 1) for a, b in zip([t0] + stamps[:-1], stamps)]
         optim.flush()  # deferred user-table steps still pending are part of the timed work
         t_enq = time.perf_counter() - t0
+        if args.gc_mode == "off":
+            gc.enable()
         launches[name] = (nat.lib().dcue_launch_count() - l0) / args.steps
         if gpu_only:
             ev1.record()
@@ -1127,6 +1146,8 @@ def main():
         "inbatch_cold": {k: out["inbatch_cold"][k] for k in ("ms_per_step", "rows_per_s", "triplets_per_s",
                                                              "host_enqueue_ms_per_step", "launches_per_step")},
     }
+    if host_trace:
+        result["host_issue_us"] = host_trace
     if "allreduce_ms_per_step" in head:
         result["allreduce_ms_per_step"] = head["allreduce_ms_per_step"]
     if "gpu_only_ms_per_step" in head:

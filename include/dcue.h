@@ -495,8 +495,9 @@ int dcue_plan_set_comm(dcue_plan* plan, dcue_comm* comm);
 int dcue_plan_set_sync_bn(dcue_plan* plan, int32_t on);
 
 /* ------------------------------------------------------------------- live kernel timing */
-/* enable = n > 0: every n-th launch of the kernel class (also inside plans created afterwards)
- * gets a HIP event pair bound to the launch itself (its dispatch's start and end); 0 disables.
+/* enable = n > 0: every n-th launch of the kernel class (also inside plans created afterwards),
+ * starting with the n-th after this call (ABI 16), gets a HIP event pair bound to the launch itself
+ * (its dispatch's start and end); 0 disables.
  * dcue_timer_read waits for the recorded pairs, returns their summed time and count, and resets.
  * For bench rooflines: a timed launch costs the stream a few microseconds, so time a sample. */
 #define DCUE_TIMED_CONV1_WGRAD 0 /* conv layer-1 weight gradient (the step's largest MFMA kernel) */
