@@ -380,11 +380,10 @@ int frz_before_record(const dcue_model* md, const AdamScalars& sc, int t, hipStr
 // current, so every row is replayed at least once per `cap` steps -- the replay work spread evenly
 // over the steps (it runs on the user-tower stream, beside the item tower) instead of a full-table
 // sweep every cap steps. A workgroup owns whole rows: it reads their clocks, replays, then sets them.
-// Round 6: a bounded grid (DCUE_SLICE_WGS, default 64) striding over groups of rows_per_block rows --
-// the slice is off the critical path with a whole step to finish in, and one workgroup per three rows
-// (2,778 at config 2) filled the dispatcher and the CUs the critical-path kernels need at once (the
-// steady-state tax); the window's history and replay bound are staged once per
-// workgroup instead of once per three rows.
+// Round 6: the grid strides over groups of rows_per_block rows, so DCUE_SLICE_WGS can bound it (A/B
+// diagnostic for the steady-state tax). Bounds of 64-512 workgroups made the slice
+// slower without shortening the critical path, so the default stays one workgroup
+// per group; a workgroup stages the window's history and replay bound once for all its groups.
 __global__ __launch_bounds__(256) void k_emb_flush_rows(float* __restrict__ p, float* __restrict__ m,
                                                         float* __restrict__ v, const dcue_emb_log* hdr,
                                                         int32_t* emb_step, long r0, long r1, int E,

@@ -745,8 +745,11 @@ template <int R, int KS>
 constexpr int w16t_img_rows() { return kW16Rows + (KS - 1) * (R >= kW16Rows ? 2 : kW16Rows / R + 2); }
 template <int R, int KS>
 constexpr size_t w16t_lds_bytes(bool xraw) {
-  return (size_t)2 * kW16Rows * 128 + (size_t)(xraw ? 1 : 2) * w16t_img_rows<R, KS>() * 256 +
-         (size_t)(kW16tO + 128) * sizeof(int);
+  // the stage images, or (epilogue) the partial tile: 64 o rows of KS * 128 + 4 floats
+  const size_t st = (size_t)2 * kW16Rows * 128 + (size_t)(xraw ? 1 : 2) * w16t_img_rows<R, KS>() * 256 +
+                    (size_t)(kW16tO + 128) * sizeof(int);
+  const size_t ep = (size_t)kW16tO * (KS * 128 + 4) * sizeof(float);
+  return st > ep ? st : ep;
 }
 // 16-byte chunk ch (of 8) of 128-byte dz row r: a transposed read's 32-lane half touches rows
 // r0 + {0..3} + {0, 8}, two chunks each -- row bits 1 and 3 spread them over all 64 banks
@@ -779,7 +782,7 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, l16 = lane & 15;
   const int kx = wave & 3, oh = wave >> 2;  // this wave's tap and o half
-  const int cout = a.cout, cin = a.cin, kcn = KS * cin;
+  const int cout = a.cout, cin = a.cin;
   const int obase = by * kW16tO;
   const int total = a.M * R;  // rows (the host keeps M * R below 2^30)
   const int r_begin = bz * a.rows_per_chunk;  // a multiple of RCH
@@ -803,83 +806,30 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
   const int oc = o_ok ? o : 0;
   const int cq = tid & 31, xs = tid >> 5;
   const int cx = 4 * cq;
-  float mu[4] = {}, iv[4] = {}, av[4] = {}, sd[4] = {}, sdx[4] = {};
-  {
-    const float4 m4 = ld4(a.mean_l + oc), i4 = ld4(a.invstd_l + oc), a4 = ld4(a.a_l + oc);
-    mu[0] = m4.x; mu[1] = m4.y; mu[2] = m4.z; mu[3] = m4.w;
-    iv[0] = i4.x; iv[1] = i4.y; iv[2] = i4.z; iv[3] = i4.w;
-    av[0] = a4.x; av[1] = a4.y; av[2] = a4.z; av[3] = a4.w;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      sd[s] = (float)acc_sum(a.dz_acc, cout, 0, oc + s);
-      sdx[s] = (float)acc_sum(a.dz_acc, cout, 1, oc + s);
-    }
-  }
-  if (by == 0 && bz == 0 && tid < cout) {  // BN_l = gamma * xhat + beta: dbeta = sum g, dgamma = sum g * xhat
-    a.dbeta[tid] = (float)(acc_sum(a.dz_acc, cout, 0, tid) * bn_grad_scale(a));
-    a.dgamma[tid] = (float)(acc_sum(a.dz_acc, cout, 1, tid) * bn_grad_scale(a));
-  }
-  const float4 xmu = ld4(a.x_mean + cx), xsc = ld4(a.x_a + cx);
-  const float4 xbe = a.x_beta ? ld4(a.x_beta + cx) : make_float4(0.f, 0.f, 0.f, 0.f);
-  const float xm[4] = {xmu.x, xmu.y, xmu.z, xmu.w}, xs_[4] = {xsc.x, xsc.y, xsc.z, xsc.w};
-  const float xb[4] = {xbe.x, xbe.y, xbe.z, xbe.w};
-  // column scales as wgrad16_body: scaled dz = cas g - count (cA + xhat cB), scaled x = (src - xm) xas + xbs
-  float cas[4], cA[4], cB[4], xas[4], xbs[4];
-  {
-    int eo[4], ec[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const float gmax = w16_key(a.g_range, oc + s);
-      const float ym = fmaxf(w16_key(a.y_range, oc + s), 0.f);
-      const float xhm = fmaxf(fabsf(mu[s]), fabsf(ym - mu[s])) * iv[s];
-      const float bo = fabsf(av[s]) * (gmax + a.kd_max * (fabsf(sd[s]) + xhm * fabsf(sdx[s])));
-      eo[s] = o_ok ? w16_exp(bo) : 0;
-      float lo, hi;
-      if constexpr (TRACK) {
-        lo = -w16_key(a.x_range + kRngC, cx + s);
-        hi = w16_key(a.x_range, cx + s);
-      } else {  // a ReLU output
-        lo = 0.f;
-        hi = fmaxf(w16_key(a.x_range, cx + s), 0.f);
-      }
-      const float bx_ = fmaxf(fabsf((lo - xm[s]) * xs_[s] + xb[s]), fabsf((hi - xm[s]) * xs_[s] + xb[s]));
-      ec[s] = XRAW ? 0 : w16_exp(bx_);
-      const float so = ldexpf(1.f, eo[s]), sx = ldexpf(1.f, ec[s]);
-      cas[s] = av[s] * so;
-      cA[s] = av[s] * a.invN * sd[s] * so;
-      cB[s] = av[s] * a.invN * sdx[s] * so;
-      xas[s] = xs_[s] * sx;
-      xbs[s] = xb[s] * sx;
-    }
-    if (tid < 16)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) exp_o[4 * q + s] = eo[s];
-    if (xs == 0)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) exp_c[4 * cq + s] = ec[s];
-  }
-  __syncthreads();
-  DCUE_KT(KID, 1);
-
   // raw operands of one stage, loaded branch-free: the thread's dz window (g, y, argmax bytes, the
   // item's count) and its x image rows xs, xs + 16, ...
-  float4 wg = make_float4(0.f, 0.f, 0.f, 0.f), wy = wg;
-  uint32_t wid = 0;
-  float wcnt = 1.f;
-  float4 xr[XRAW ? 1 : FX];
-  uint2 xr16[XRAW ? FX : 1];
-  uint32_t xvalid = 0;
-  auto issue = [&](int rb) {
+  // (a register set per stage in flight: one -- a second, two stages ahead, measured no faster: the
+  // stages are MFMA + LDS bound, not load-latency bound; profiles/r06_ktrace_wgrad.txt)
+  struct StageRegs {
+    float4 wg, wy;
+    uint32_t wid;
+    float wcnt;
+    float4 xr[XRAW ? 1 : FX];
+    uint2 xr16[XRAW ? FX : 1];
+    uint32_t xvalid;
+  };
+  StageRegs s0 = {};
+  auto issue = [&](StageRegs& S, int rb) {
     const int i0 = rb / R, D = rb - i0 * R;  // the stage starts D rows into item i0
     if (dzt) {
       int rw = rb + ws * POOL;
       rw = rw < r_end ? rw : rb;
       const int ii = rw / R, t0 = rw - ii * R;
       const int base = (ii * LP + t0 / POOL) * cout + oc;
-      wg = ld4(a.g_l + base);
-      wy = ld4(a.y_l + base);
-      wid = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
-      wcnt = a.counts ? a.counts[ii] : 1.f;
+      S.wg = ld4(a.g_l + base);
+      S.wy = ld4(a.y_l + base);
+      S.wid = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
+      S.wcnt = a.counts ? a.counts[ii] : 1.f;
     }
     long t_a = 0, t_b = 0;
     if constexpr (TRACK && TWO) {
@@ -907,30 +857,95 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
           trk = a.item_track[ok ? i : i0];
         const long e = (trk * kFrames + (ok ? p : 0)) * kMels + cx;
         if constexpr (XRAW)
-          xr16[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.xsrc) + e);
+          S.xr16[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.xsrc) + e);
         else
-          xr[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + e);
+          S.xr[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + e);
       } else {
-        xr[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + (((long)(ok ? i : i0) * LIN + (ok ? p : 0)) * cin + cx));
+        S.xr[j] = ld4(reinterpret_cast<const float*>(a.xsrc) + (((long)(ok ? i : i0) * LIN + (ok ? p : 0)) * cin + cx));
       }
     }
-    xvalid = vm;
+    S.xvalid = vm;
   };
+  // The column constants' loads (independent of each other) go out first, then the first stage's:
+  // loads return in issue order, so the constants' math overlaps the stage's flight. (Round 6, per-WG
+  // phase trace: prologue + first fill 4.5 us either way -- the kernel's first loads after its
+  // producer cost ~3 us however they are ordered; profiles/r06_ktrace_wgrad.txt)
+  float mu[4] = {}, iv[4] = {}, av[4] = {}, sd[4] = {}, sdx[4] = {};
+  float gmx[4], ymx[4], xlo[4], xhi[4];
+  {
+    const float4 m4 = ld4(a.mean_l + oc), i4 = ld4(a.invstd_l + oc), a4 = ld4(a.a_l + oc);
+    mu[0] = m4.x; mu[1] = m4.y; mu[2] = m4.z; mu[3] = m4.w;
+    iv[0] = i4.x; iv[1] = i4.y; iv[2] = i4.z; iv[3] = i4.w;
+    av[0] = a4.x; av[1] = a4.y; av[2] = a4.z; av[3] = a4.w;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sd[s] = (float)acc_sum(a.dz_acc, cout, 0, oc + s);
+      sdx[s] = (float)acc_sum(a.dz_acc, cout, 1, oc + s);
+      gmx[s] = w16_key(a.g_range, oc + s);
+      ymx[s] = w16_key(a.y_range, oc + s);
+      if constexpr (TRACK) {
+        xlo[s] = -w16_key(a.x_range + kRngC, cx + s);
+        xhi[s] = w16_key(a.x_range, cx + s);
+      } else {  // a ReLU output
+        xlo[s] = 0.f;
+        xhi[s] = fmaxf(w16_key(a.x_range, cx + s), 0.f);
+      }
+    }
+  }
+  const float4 xmu = ld4(a.x_mean + cx), xsc = ld4(a.x_a + cx);
+  const float4 xbe = a.x_beta ? ld4(a.x_beta + cx) : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (r_begin < r_end) issue(s0, r_begin);
+  if (by == 0 && bz == 0 && tid < cout) {  // BN_l = gamma * xhat + beta: dbeta = sum g, dgamma = sum g * xhat
+    a.dbeta[tid] = (float)(acc_sum(a.dz_acc, cout, 0, tid) * bn_grad_scale(a));
+    a.dgamma[tid] = (float)(acc_sum(a.dz_acc, cout, 1, tid) * bn_grad_scale(a));
+  }
+  const float xm[4] = {xmu.x, xmu.y, xmu.z, xmu.w}, xs_[4] = {xsc.x, xsc.y, xsc.z, xsc.w};
+  const float xb[4] = {xbe.x, xbe.y, xbe.z, xbe.w};
+  // column scales as wgrad16_body: scaled dz = cas g - count (cA + xhat cB), scaled x = (src - xm) xas + xbs
+  float cas[4], cA[4], cB[4], xas[4], xbs[4];
+  {
+    int eo[4], ec[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float gmax = gmx[s];
+      const float ym = fmaxf(ymx[s], 0.f);
+      const float xhm = fmaxf(fabsf(mu[s]), fabsf(ym - mu[s])) * iv[s];
+      const float bo = fabsf(av[s]) * (gmax + a.kd_max * (fabsf(sd[s]) + xhm * fabsf(sdx[s])));
+      eo[s] = o_ok ? w16_exp(bo) : 0;
+      const float lo = xlo[s], hi = xhi[s];
+      const float bx_ = fmaxf(fabsf((lo - xm[s]) * xs_[s] + xb[s]), fabsf((hi - xm[s]) * xs_[s] + xb[s]));
+      ec[s] = XRAW ? 0 : w16_exp(bx_);
+      const float so = ldexpf(1.f, eo[s]), sx = ldexpf(1.f, ec[s]);
+      cas[s] = av[s] * so;
+      cA[s] = av[s] * a.invN * sd[s] * so;
+      cB[s] = av[s] * a.invN * sdx[s] * so;
+      xas[s] = xs_[s] * sx;
+      xbs[s] = xb[s] * sx;
+    }
+    if (tid < 16)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) exp_o[4 * q + s] = eo[s];
+    if (xs == 0)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) exp_c[4 * cq + s] = ec[s];
+  }
+  __syncthreads();
+  DCUE_KT(KID, 1);
+
 
   // fragment read offsets: lane 4q'+p of its 16-lane group g supplies row (8g + 4h + q') of the
   // k-step, columns 4p..4p+3 of the 16-column tile
   const int fq = l16 >> 2, fp = l16 & 3;
-  if (r_begin < r_end) issue(r_begin);
-  for (int rb = r_begin; rb < r_end; rb += RCH) {
+  auto stage = [&](StageRegs& S, int rb) {
     if (dzt) {  // dz: BN_1's backward for the thread's window, scaled, split, written to its rows
       const int rw = rb + ws * POOL;
       const bool wv = rw < r_end && o_ok;
-      const float gv[4] = {wg.x, wg.y, wg.z, wg.w}, yv[4] = {wy.x, wy.y, wy.z, wy.w};
+      const float gv[4] = {S.wg.x, S.wg.y, S.wg.z, S.wg.w}, yv[4] = {S.wy.x, S.wy.y, S.wy.z, S.wy.w};
       float d[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const float xh_ = (yv[s] - mu[s]) * iv[s];
-        const float v = cas[s] * gv[s] - wcnt * (cA[s] + xh_ * cB[s]);
+        const float v = cas[s] * gv[s] - S.wcnt * (cA[s] + xh_ * cB[s]);
         d[s] = (wv && yv[s] > 0.f) ? v : 0.f;
       }
       bacc[0].x += d[0]; bacc[0].y += d[1]; bacc[0].z += d[2]; bacc[0].w += d[3];
@@ -940,7 +955,7 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
         float e1[4], e2[4], e3[4], e4[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const uint32_t r = (wid >> (8 * s)) & 0xffu;
+          const uint32_t r = (S.wid >> (8 * s)) & 0xffu;
           e1[s] = (first && r == 0u) ? d[s] : 0.f;
           e2[s] = (first && r == 1u) ? d[s] : 0.f;
           e3[s] = (last && r == (uint32_t)(POOL - 2)) ? d[s] : 0.f;
@@ -957,10 +972,10 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
       const uint2 hb = __builtin_bit_cast(uint2, h), lb = __builtin_bit_cast(uint2, l);
 #pragma unroll
       for (int jp = 0; jp < POOL; ++jp) {
-        const uint32_t m0 = ((wid & 0xffu) == (uint32_t)jp ? 0x0000ffffu : 0u) |
-                            (((wid >> 8) & 0xffu) == (uint32_t)jp ? 0xffff0000u : 0u);
-        const uint32_t m1 = (((wid >> 16) & 0xffu) == (uint32_t)jp ? 0x0000ffffu : 0u) |
-                            ((wid >> 24) == (uint32_t)jp ? 0xffff0000u : 0u);
+        const uint32_t m0 = ((S.wid & 0xffu) == (uint32_t)jp ? 0x0000ffffu : 0u) |
+                            (((S.wid >> 8) & 0xffu) == (uint32_t)jp ? 0xffff0000u : 0u);
+        const uint32_t m1 = (((S.wid >> 16) & 0xffu) == (uint32_t)jp ? 0x0000ffffu : 0u) |
+                            ((S.wid >> 24) == (uint32_t)jp ? 0xffff0000u : 0u);
         const int off = w16_off128(ws * POOL + jp, q >> 1) + 8 * (q & 1);
         *reinterpret_cast<uint2*>(dzh + off) = make_uint2(hb.x & m0, hb.y & m1);
         *reinterpret_cast<uint2*>(dzl + off) = make_uint2(lb.x & m0, lb.y & m1);
@@ -970,12 +985,12 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
     for (int j = 0; j < FX; ++j) {  // x image (zero padding and past-the-batch rows are zeros)
       const int jr = xs + 16 * j;
       if (jr < IMG) {
-        const bool ok = (xvalid >> j) & 1u;
+        const bool ok = (S.xvalid >> j) & 1u;
         const int off = w16_off(jr, cq >> 1) + 8 * (cq & 1);
         if constexpr (XRAW) {
-          *reinterpret_cast<uint2*>(xh + off) = ok ? xr16[j] : make_uint2(0u, 0u);
+          *reinterpret_cast<uint2*>(xh + off) = ok ? S.xr16[j] : make_uint2(0u, 0u);
         } else {
-          const float x[4] = {xr[j].x, xr[j].y, xr[j].z, xr[j].w};
+          const float x[4] = {S.xr[j].x, S.xr[j].y, S.xr[j].z, S.xr[j].w};
           float v[4];
 #pragma unroll
           for (int s = 0; s < 4; ++s) v[s] = ok ? (x[s] - xm[s]) * xas[s] + xbs[s] : 0.f;
@@ -987,7 +1002,7 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
     if (rb == r_begin) DCUE_KT(KID, 2);
     const int i0 = rb / R;
     const int lb = (i0 + 1) * R - rb;  // the stage row where item i0 + 1 starts (TWO)
-    if (rb + RCH < r_end) issue(rb + RCH);  // next stage's loads fly while the MFMAs run
+    if (rb + RCH < r_end) issue(S, rb + RCH);  // next stage's loads fly while the MFMAs run
 #pragma unroll
     for (int ks = 0; ks < RCH / 32; ++ks) {
       const int r0 = 32 * ks + 8 * g + fq;  // this lane's conv rows: r0 (first read), r0 + 4 (second)
@@ -1033,22 +1048,44 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
       }
     }
     __syncthreads();
-  }
+  };
+  for (int rb = r_begin; rb < r_end; rb += RCH) stage(s0, rb);
 
   DCUE_KT(KID, 3);
-  // partial block -> wpart[z][o][kx * cin + c], unscaled; D lane map: o = 4g + reg, c = l16
-  float* wp = a.wpart + (size_t)bz * cout * kcn;
-#pragma unroll
-  for (int n = 0; n < 8; ++n) {
-    const int cl = 16 * n + l16;
-    const int ecn = exp_c[cl];
+  int eo_bias;  // (the bias partials' exponent, read before the tile staging overwrites exp_o)
+  // partial block -> wpart[z][o][kx * cin + c], unscaled; D lane map: o = 4g + reg, c = l16. The
+  // workgroup's 64 o x KS*128 kc block is contiguous in wpart: it is staged through LDS (row pitch
+  // KC + 4 floats: the four g rows of a store land on disjoint banks) and written with linear float4
+  // stores -- the accumulators' per-lane dword stores took 3.7 of the workgroup's 16 us (round 6)
+  {
+    constexpr int KC = KS * 128, PITCH = KC + 4;  // (cin == 128: the launch checks it)
+    int eo_r[2][4], ec_r[8];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int ol = 32 * oh + 16 * m + 4 * g + j;
-        if (obase + ol < cout) wp[(size_t)(obase + ol) * kcn + kx * cin + cl] = ldexpf(acc[m][n][j], -(exp_o[ol] + ecn));
-      }
+      for (int j = 0; j < 4; ++j) eo_r[m][j] = exp_o[32 * oh + 16 * m + 4 * g + j];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) ec_r[n] = exp_c[16 * n + l16];
+    eo_bias = tid < kW16tO ? exp_o[tid] : 0;
+    __syncthreads();  // (the exponents are read: the tile overwrites them)
+    float* tl = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int n = 0; n < 8; ++n)
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          tl[(32 * oh + 16 * m + 4 * g + j) * PITCH + kx * 128 + 16 * n + l16] =
+              ldexpf(acc[m][n][j], -(eo_r[m][j] + ec_r[n]));
+    __syncthreads();
+    const int nrow = min(kW16tO, cout - obase);
+    float* wp = a.wpart + ((size_t)bz * cout + obase) * KC;
+    constexpr int Q = KC / 4;  // float4 per row
+    for (int i = tid; i < nrow * Q; i += kW16tThreads) {
+      const int r = i / Q, k4 = i - r * Q;
+      st4(wp + (size_t)r * KC + 4 * k4, *reinterpret_cast<const float4*>(tl + r * PITCH + 4 * k4));
+    }
+    __syncthreads();  // (bsum below reuses the tile's LDS)
   }
   // bias (+ edge) partials of the tile's 64 channels: the 16 window slots, summed in order (the
   // operand images are free: the last stage ended with a barrier)
@@ -1057,13 +1094,12 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
     for (int e = 0; e < NB; ++e) st4(&bsum[ws][e][4 * q], bacc[e]);
   __syncthreads();
   if (tid < kW16tO && obase + tid < cout) {
-    const int eo = exp_o[tid];
 #pragma unroll
     for (int e = 0; e < NB; ++e) {
       float v = 0.f;
 #pragma unroll
       for (int sl = 0; sl < 16; ++sl) v += bsum[sl][e][tid];
-      a.bpart[((size_t)bz * NB + e) * cout + obase + tid] = ldexpf(v, -eo);
+      a.bpart[((size_t)bz * NB + e) * cout + obase + tid] = ldexpf(v, -eo_bias);
     }
   }
   DCUE_KT(KID, 4);

@@ -64,6 +64,7 @@ class SideIssuer {
     if (hipSetDevice(dev_) != hipSuccess) err_.store(DCUE_ERR_HIP);
     auto idle_since = std::chrono::steady_clock::now();
     unsigned spins = 0;
+    bool worked = false;  // a closure ran since the idle clock was last started
     while (!stop_.load(std::memory_order_acquire)) {
       const uint64_t d = done_.load(std::memory_order_relaxed);
       if (d < head_.load(std::memory_order_acquire)) {
@@ -75,12 +76,17 @@ class SideIssuer {
         }
         done_.store(d + 1, std::memory_order_release);
         spins = 0;
+        worked = true;
         continue;
       }
       __builtin_ia32_pause();
       if (++spins < 4096) continue;
       spins = 0;
       const auto now = std::chrono::steady_clock::now();
+      if (worked) {  // idle time counts from the last closure, not from the last wake-up (round 6:
+        worked = false;  // a stale clock parked the worker ~100 us into every idle stretch of a
+        idle_since = now;  // running step loop, and each post then paid a futex wake-up)
+      }
       if (now - idle_since < std::chrono::milliseconds(50)) {
         std::this_thread::yield();
         continue;
