@@ -741,13 +741,16 @@ __global__ __launch_bounds__(256, OCC) void k_conv_wgrad16_multi(WgradMulti w) {
 // x rows 256 B (cin = 128: the mels, or layer 2's input at H = 128).
 constexpr int kW16tO = 64;   // o per workgroup
 constexpr int kW16tThreads = 512;
+// conv 1 (the track table): a chunk's items' track ids (+ the next item's, for the halo) are staged in
+// LDS, at most this many -- wgrad_nchunk keeps rows_per_chunk <= (kWgItems - 3) R
+constexpr int kWgItems = 128;
 template <int R, int KS>
 constexpr int w16t_img_rows() { return kW16Rows + (KS - 1) * (R >= kW16Rows ? 2 : kW16Rows / R + 2); }
 template <int R, int KS>
 constexpr size_t w16t_lds_bytes(bool xraw) {
   // the stage images, or (epilogue) the partial tile: 64 o rows of KS * 128 + 4 floats
   const size_t st = (size_t)2 * kW16Rows * 128 + (size_t)(xraw ? 1 : 2) * w16t_img_rows<R, KS>() * 256 +
-                    (size_t)(kW16tO + 128) * sizeof(int);
+                    (size_t)(kW16tO + 128 + 2 * kWgItems) * sizeof(int);
   const size_t ep = (size_t)kW16tO * (KS * 128 + 4) * sizeof(float);
   return st > ep ? st : ep;
 }
@@ -774,6 +777,8 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
   char* xl = xh + IMG * 256;
   int* exp_o = reinterpret_cast<int*>(xh + (XRAW ? 1 : 2) * IMG * 256);
   int* exp_c = exp_o + kW16tO;
+  [[maybe_unused]] int* trk_s = exp_c + 128;  // (conv 1) the chunk's items' track ids and counts
+  [[maybe_unused]] float* cnt_s = reinterpret_cast<float*>(trk_s + kWgItems);
   float (*bsum)[NB][kW16tO] = reinterpret_cast<float (*)[NB][kW16tO]>(lds);  // after the last stage
 
   [[maybe_unused]] constexpr int KID = TRACK ? 0 : 1;
@@ -787,6 +792,7 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
   const int total = a.M * R;  // rows (the host keeps M * R below 2^30)
   const int r_begin = bz * a.rows_per_chunk;  // a multiple of RCH
   const int r_end = min(r_begin + a.rows_per_chunk, total);
+  [[maybe_unused]] const int item0 = r_begin / R;
 
   f32x4 acc[2][8];
 #pragma unroll
@@ -819,9 +825,12 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
     uint32_t xvalid;
   };
   StageRegs s0 = {};
+  // (every thread issues the same loads on every path -- threads 256..511 a copy of 0..255's dz
+  // window, counts through LDS or a select: the compiler's wait counts merge paths conservatively,
+  // and a load skipped on one path made a stage wait for every load in flight)
   auto issue = [&](StageRegs& S, int rb) {
     const int i0 = rb / R, D = rb - i0 * R;  // the stage starts D rows into item i0
-    if (dzt) {
+    {
       int rw = rb + ws * POOL;
       rw = rw < r_end ? rw : rb;
       const int ii = rw / R, t0 = rw - ii * R;
@@ -829,12 +838,17 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
       S.wg = ld4(a.g_l + base);
       S.wy = ld4(a.y_l + base);
       S.wid = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
-      S.wcnt = a.counts ? a.counts[ii] : 1.f;
+      if constexpr (TRACK && TWO) {
+        S.wcnt = cnt_s[ii - item0];
+      } else {
+        const float c = *(a.counts ? a.counts + ii : a.mean_l);
+        S.wcnt = a.counts ? c : 1.f;
+      }
     }
     long t_a = 0, t_b = 0;
-    if constexpr (TRACK && TWO) {
-      t_a = a.item_track[i0];
-      t_b = a.item_track[min(i0 + 1, a.M - 1)];
+    if constexpr (TRACK && TWO) {  // (from LDS: a global load here would hold the x loads -- and so
+      t_a = trk_s[i0 - item0];      // the stage's MFMAs behind them -- for an L2 round trip a stage)
+      t_b = trk_s[min(i0 + 1, a.M - 1) - item0];
     }
     uint32_t vm = 0;
 #pragma unroll
@@ -894,6 +908,14 @@ __device__ __forceinline__ void wgrad16t_body(const WgradArgs& a, int by, int bz
   }
   const float4 xmu = ld4(a.x_mean + cx), xsc = ld4(a.x_a + cx);
   const float4 xbe = a.x_beta ? ld4(a.x_beta + cx) : make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (TRACK && TWO) {
+    const int nitem = min(a.M - item0, (r_end - 1) / R - item0 + 2);
+    for (int k = tid; k < nitem; k += kW16tThreads) {
+      trk_s[k] = a.item_track[item0 + k];
+      cnt_s[k] = a.counts ? a.counts[item0 + k] : 1.f;
+    }
+    __syncthreads();
+  }
   if (r_begin < r_end) issue(s0, r_begin);
   if (by == 0 && bz == 0 && tid < cout) {  // BN_l = gamma * xhat + beta: dbeta = sum g, dgamma = sum g * xhat
     a.dbeta[tid] = (float)(acc_sum(a.dz_acc, cout, 0, tid) * bn_grad_scale(a));
@@ -1117,6 +1139,310 @@ __global__ __launch_bounds__(kW16tThreads, 1) void k_conv_wgrad16t(WgradArgs a) 
   wgrad16t_body<SRCX, KS, PAD, LIN, R, POOL, LP>(a, L % ot, L / ot, lds16t);
   // (plans, layer 1: the next step's prepared inputs -- only an order for the kernels after this one)
   if constexpr (SRCX != SRC_ACT) dev_wait_order(a.wait);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Conv-1 weight gradient, one tap per workgroup (round 6). wgrad16t_body gives
+// a workgroup a 64 o x 512 kc tile, so the chip fills only through split-K: 33 chunks x 2 tiles at
+// the in-batch shape, 8.7 MB of partial blocks for a 0.26 MB dW, and a workgroup's 4 stages run at
+// one per CU. Here the dW is cut into 32 o x 128 c tiles (4 o tiles x 4 taps = 16 per chunk) of 256
+// threads, so ~16 chunks fill the chip: half the partial bytes, and the x and dz operands a chunk's
+// 16 tiles share are re-read from L2 (the tiles of a chunk are consecutive logical blocks: one XCD).
+// Operands, column scaling and the hi + lo split of dz are wgrad16t_body's (XRAW: x is the raw fp16
+// table, exact in f16); the partial layout is the same, so launch_wgrad_reduce and bn0's gradient
+// kernels read it unchanged. Two stages' loads are in flight (the stage work is a quarter of
+// wgrad16t's, so the L2 round trip is what a stage would otherwise wait on).
+constexpr int kW1kO = 32;         // o per workgroup
+constexpr int kW1kThreads = 256;  // 4 waves: o block (16) x c half (64)
+template <int R, int KS>
+constexpr size_t w1k_lds_bytes() {
+  // dz hi / lo images (64 rows x 128 B; the tile's 32 o use the first 64 B of a row), the x image
+  // (IMG rows x 256 B) and the o exponents; after the stages the same bytes hold the tile (32 rows
+  // of 128 + 4 floats), then the bias partials (16 x 5 x 32 floats)
+  const size_t st = (size_t)2 * kW16Rows * 128 + (size_t)w16t_img_rows<R, KS>() * 256 + kW1kO * sizeof(int) +
+                    (size_t)kWgItems * (sizeof(int) + sizeof(float));
+  const size_t ep = (size_t)kW1kO * (128 + 4) * sizeof(float);
+  const size_t bs = (size_t)16 * 5 * kW1kO * sizeof(float);
+  const size_t m = st > ep ? st : ep;
+  return m > bs ? m : bs;
+}
+
+template <int KS, int PAD, int LIN, int R, int POOL, int LP>
+__device__ __forceinline__ void wgrad1k_body(const WgradArgs& a, int ot, int kx, int bz, char* lds) {
+  constexpr int RCH = kW16Rows;
+  constexpr int NB = 5;  // bias + the four edge sums (conv 1's zero padding)
+  constexpr int HALO = KS - 1;
+  constexpr int IMG = w16t_img_rows<R, KS>();
+  constexpr int FX = (IMG + 7) / 8;  // x image rows per thread (8 row slots x 32 channel quads)
+  static_assert(KS == 4 && POOL == 4 && R % POOL == 0 && R >= RCH, "conv 1: 16 windows a stage, at most two items");
+  char* dzh = lds;
+  char* dzl = dzh + RCH * 128;
+  char* xh = dzl + RCH * 128;
+  int* exp_o = reinterpret_cast<int*>(xh + IMG * 256);
+  int* trk_s = exp_o + kW1kO;  // the chunk's items' track ids and counts (the host bounds their number)
+  float* cnt_s = reinterpret_cast<float*>(trk_s + kWgItems);
+  float (*bsum)[NB][kW1kO] = reinterpret_cast<float (*)[NB][kW1kO]>(lds);  // after the tile's stores
+
+  DCUE_KTW(0, 6);
+  DCUE_KT(0, 0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int ob = wave & 1, chh = wave >> 1;  // this wave's o block (16 o) and c half (64 c)
+  const int cout = a.cout;
+  const int obase = ot * kW1kO;
+  const int total = a.M * R;  // rows (the host keeps M * R below 2^30)
+  const int r_begin = bz * a.rows_per_chunk;  // a multiple of RCH
+  const int r_end = min(r_begin + a.rows_per_chunk, total);
+  const int item0 = r_begin / R;
+
+  f32x4 acc[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 bacc[NB];
+#pragma unroll
+  for (int e = 0; e < NB; ++e) bacc[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  // dz: threads 0..127, window slot ws (16 a stage) x o quad q (8); x: every thread, row slot xs (8)
+  // x channel quad cq (32)
+  const bool dzt = tid < 128;
+  const int q = tid & 7, ws = (tid >> 3) & 15;
+  const int o = obase + 4 * q;
+  const bool o_ok = o < cout;
+  const int oc = o_ok ? o : 0;
+  const int cq = tid & 31, xs = tid >> 5;
+  const int cx = 4 * cq;
+  struct StageRegs {
+    float4 wg, wy;
+    uint32_t wid;
+    float wcnt;
+    uint2 xr[FX];
+    uint32_t xvalid;
+  };
+  StageRegs s0 = {}, s1 = {};
+  // One stage's raw operands. Every thread issues the same loads on every path (threads 128..255 load
+  // a copy of threads 0..127's windows; a stage past the chunk reloads its first): the compiler's
+  // wait counts merge paths conservatively, so a load skipped on one path made every stage wait for
+  // all loads in flight -- the other stage's too -- which undid the two-stage pipeline
+  auto issue = [&](StageRegs& S, int rb_) {
+    const int rb = rb_ < r_end ? rb_ : r_begin;
+    const int i0 = rb / R, D = rb - i0 * R;  // the stage starts D rows into item i0
+    {
+      int rw = rb + ws * POOL;
+      rw = rw < r_end ? rw : rb;
+      const int ii = rw / R, t0 = rw - ii * R;
+      const int base = (ii * LP + t0 / POOL) * cout + oc;
+      S.wg = ld4(a.g_l + base);
+      S.wy = ld4(a.y_l + base);
+      S.wid = *reinterpret_cast<const uint32_t*>(a.idx_l + base);
+      S.wcnt = cnt_s[ii - item0];
+    }
+    // (track ids from LDS: a dependent global load here would make the stage's x loads wait for it,
+    // and loads retire in order, so for every load in flight before it -- the other stage's)
+    const long t_a = trk_s[i0 - item0], t_b = trk_s[min(i0 + 1, a.M - 1) - item0];
+    uint32_t vm = 0;
+#pragma unroll
+    for (int j = 0; j < FX; ++j) {
+      const int jr = xs + 8 * j;                       // image row
+      const int k = jr + D >= R + HALO ? 1 : 0;        // items after i0
+      const int i = i0 + k;
+      const int p = jr + D - k * (R + HALO) - PAD;     // input position in item i
+      const bool ok = jr < IMG && i < a.M && p >= 0 && p < LIN;
+      vm |= ok ? (1u << j) : 0u;
+      const long e = ((k ? t_b : t_a) * kFrames + (ok ? p : 0)) * kMels + cx;
+      S.xr[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half*>(a.xsrc) + e);
+    }
+    S.xvalid = vm;
+  };
+
+  // the column constants' loads first, then the first two stages' (loads return in issue order)
+  float mu[4], iv[4], av[4], sd[4], sdx[4], gmx[4], ymx[4];
+  {
+    const float4 m4 = ld4(a.mean_l + oc), i4 = ld4(a.invstd_l + oc), a4 = ld4(a.a_l + oc);
+    mu[0] = m4.x; mu[1] = m4.y; mu[2] = m4.z; mu[3] = m4.w;
+    iv[0] = i4.x; iv[1] = i4.y; iv[2] = i4.z; iv[3] = i4.w;
+    av[0] = a4.x; av[1] = a4.y; av[2] = a4.z; av[3] = a4.w;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sd[s] = (float)acc_sum(a.dz_acc, cout, 0, oc + s);
+      sdx[s] = (float)acc_sum(a.dz_acc, cout, 1, oc + s);
+      gmx[s] = w16_key(a.g_range, oc + s);
+      ymx[s] = w16_key(a.y_range, oc + s);
+    }
+  }
+  {
+    const int nitem = min(a.M - item0, (r_end - 1) / R - item0 + 2);
+    for (int k = tid; k < nitem; k += kW1kThreads) {
+      trk_s[k] = a.item_track[item0 + k];
+      cnt_s[k] = a.counts ? a.counts[item0 + k] : 1.f;
+    }
+  }
+  __syncthreads();
+  issue(s0, r_begin);
+  issue(s1, r_begin + RCH);
+  if (ot == 0 && kx == 0 && bz == 0 && tid < cout) {  // BN_1 = gamma * xhat + beta: dbeta = sum g, dgamma = sum g * xhat
+    a.dbeta[tid] = (float)(acc_sum(a.dz_acc, cout, 0, tid) * bn_grad_scale(a));
+    a.dgamma[tid] = (float)(acc_sum(a.dz_acc, cout, 1, tid) * bn_grad_scale(a));
+  }
+  // scaled dz = cas g - count (cA + xhat cB), as wgrad16t_body (x: raw fp16, exponent 0)
+  float cas[4], cA[4], cB[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const float ym = fmaxf(ymx[s], 0.f);
+    const float xhm = fmaxf(fabsf(mu[s]), fabsf(ym - mu[s])) * iv[s];
+    const float bo = fabsf(av[s]) * (gmx[s] + a.kd_max * (fabsf(sd[s]) + xhm * fabsf(sdx[s])));
+    const int eo = o_ok ? w16_exp(bo) : 0;
+    const float so = ldexpf(1.f, eo);
+    cas[s] = av[s] * so;
+    cA[s] = av[s] * a.invN * sd[s] * so;
+    cB[s] = av[s] * a.invN * sdx[s] * so;
+    if (tid < 8) exp_o[4 * q + s] = eo;
+  }
+  __syncthreads();
+  DCUE_KT(0, 1);
+
+  // fragment read offsets: lane 4q'+p of its 16-lane group g supplies row (8g + 4h + q') of the
+  // k-step, columns 4p..4p+3 of the 16-column tile
+  const int fq = l16 >> 2, fp = l16 & 3;
+  auto stage = [&](StageRegs& S, int rb) {
+    if (dzt) {  // dz: BN_1's backward for the thread's window, scaled, split, written to its rows
+      const int rw = rb + ws * POOL;
+      const bool wv = rw < r_end && o_ok;
+      const float gv[4] = {S.wg.x, S.wg.y, S.wg.z, S.wg.w}, yv[4] = {S.wy.x, S.wy.y, S.wy.z, S.wy.w};
+      float d[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const float xh_ = (yv[s] - mu[s]) * iv[s];
+        const float v = cas[s] * gv[s] - S.wcnt * (cA[s] + xh_ * cB[s]);
+        d[s] = (wv && yv[s] > 0.f) ? v : 0.f;
+      }
+      bacc[0].x += d[0]; bacc[0].y += d[1]; bacc[0].z += d[2]; bacc[0].w += d[3];
+      {  // t = 0, 1 (first window), R-2, R-1 (last window)
+        const int t0 = rw - (rw / R) * R;
+        const bool first = t0 == 0, last = t0 == R - POOL;
+        float e1[4], e2[4], e3[4], e4[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const uint32_t r = (S.wid >> (8 * s)) & 0xffu;
+          e1[s] = (first && r == 0u) ? d[s] : 0.f;
+          e2[s] = (first && r == 1u) ? d[s] : 0.f;
+          e3[s] = (last && r == (uint32_t)(POOL - 2)) ? d[s] : 0.f;
+          e4[s] = (last && r == (uint32_t)(POOL - 1)) ? d[s] : 0.f;
+        }
+        bacc[1].x += e1[0]; bacc[1].y += e1[1]; bacc[1].z += e1[2]; bacc[1].w += e1[3];
+        bacc[2].x += e2[0]; bacc[2].y += e2[1]; bacc[2].z += e2[2]; bacc[2].w += e2[3];
+        bacc[3].x += e3[0]; bacc[3].y += e3[1]; bacc[3].z += e3[2]; bacc[3].w += e3[3];
+        bacc[4].x += e4[0]; bacc[4].y += e4[1]; bacc[4].z += e4[2]; bacc[4].w += e4[3];
+      }
+      const w16_h4 h = {(_Float16)d[0], (_Float16)d[1], (_Float16)d[2], (_Float16)d[3]};
+      const w16_h4 l = {(_Float16)(d[0] - (float)h[0]), (_Float16)(d[1] - (float)h[1]),
+                        (_Float16)(d[2] - (float)h[2]), (_Float16)(d[3] - (float)h[3])};
+      const uint2 hb = __builtin_bit_cast(uint2, h), lb = __builtin_bit_cast(uint2, l);
+#pragma unroll
+      for (int jp = 0; jp < POOL; ++jp) {  // the window's argmax row carries it, the others zeros
+        const uint32_t m0 = ((S.wid & 0xffu) == (uint32_t)jp ? 0x0000ffffu : 0u) |
+                            (((S.wid >> 8) & 0xffu) == (uint32_t)jp ? 0xffff0000u : 0u);
+        const uint32_t m1 = (((S.wid >> 16) & 0xffu) == (uint32_t)jp ? 0x0000ffffu : 0u) |
+                            ((S.wid >> 24) == (uint32_t)jp ? 0xffff0000u : 0u);
+        const int off = w16_off128(ws * POOL + jp, q >> 1) + 8 * (q & 1);
+        *reinterpret_cast<uint2*>(dzh + off) = make_uint2(hb.x & m0, hb.y & m1);
+        *reinterpret_cast<uint2*>(dzl + off) = make_uint2(lb.x & m0, lb.y & m1);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < FX; ++j) {  // x image (zero padding and past-the-batch rows are zeros)
+      const int jr = xs + 8 * j;
+      if (jr < IMG) {
+        const bool ok = (S.xvalid >> j) & 1u;
+        *reinterpret_cast<uint2*>(xh + w16_off(jr, cq >> 1) + 8 * (cq & 1)) = ok ? S.xr[j] : make_uint2(0u, 0u);
+      }
+    }
+    __syncthreads();
+    if (rb == r_begin) DCUE_KT(0, 2);
+    const int lb = (rb / R + 1) * R - rb;  // the stage row where the next item starts
+    issue(S, rb + 2 * RCH);  // (S is in LDS: its registers take stage + 2)
+#pragma unroll
+    for (int ks = 0; ks < RCH / 32; ++ks) {
+      const int r0 = 32 * ks + 8 * g + fq;  // this lane's conv rows: r0 (first read), r0 + 4 (second)
+      const int ch = 2 * ob + (fp >> 1);
+      const int o0 = w16_off128(r0, ch) + 8 * (fp & 1), o1 = w16_off128(r0 + 4, ch) + 8 * (fp & 1);
+      const w16_h4 h0 = w16_tr(dzh, o0), h1 = w16_tr(dzh, o1), l0 = w16_tr(dzl, o0), l1 = w16_tr(dzl, o1);
+      const w16_h8 ah = w16_h8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+      const w16_h8 al = w16_h8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+      const int img0 = r0 + kx + (r0 >= lb ? HALO : 0), img1 = r0 + 4 + kx + (r0 + 4 >= lb ? HALO : 0);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int cc = 2 * (4 * chh + n) + (fp >> 1);
+        const int ob0 = w16_off(img0, cc) + 8 * (fp & 1), ob1 = w16_off(img1, cc) + 8 * (fp & 1);
+        const w16_h4 x0 = w16_tr(xh, ob0), x1 = w16_tr(xh, ob1);
+        const w16_h8 bh = w16_h8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+        acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[n], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  };
+  // stages in pairs: a chunk's odd last stage is paired with an empty one (every dz masked: it adds
+  // zeros), so the two register sets alternate on every path
+  for (int rb = r_begin; rb < r_end; rb += 2 * RCH) {
+    stage(s0, rb);
+    stage(s1, rb + RCH);
+  }
+
+  DCUE_KT(0, 3);
+  // partial block -> wpart[z][o][kx * 128 + c], unscaled; D lane map: o = 4g + reg, c = l16. The
+  // tile's 32 rows of 128 floats go through LDS (row pitch 132: the four g rows of a store land on
+  // disjoint banks) and out as linear float4 stores (512-byte row segments)
+  int eo_r[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) eo_r[j] = exp_o[16 * ob + 4 * g + j];
+  const int eo_bias = tid < kW1kO ? exp_o[tid] : 0;
+  __syncthreads();  // (the exponents are read: the tile overwrites them)
+  {
+    constexpr int PITCH = 128 + 4, KC = KS * 128;
+    float* tl = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        tl[(16 * ob + 4 * g + j) * PITCH + 16 * (4 * chh + n) + l16] = ldexpf(acc[n][j], -eo_r[j]);
+    __syncthreads();
+    const int nrow = min(kW1kO, cout - obase);
+    float* wp = a.wpart + ((size_t)bz * cout + obase) * KC + kx * 128;
+    for (int i = tid; i < nrow * 32; i += kW1kThreads) {
+      const int r = i >> 5, k4 = i & 31;
+      st4(wp + (size_t)r * KC + 4 * k4, *reinterpret_cast<const float4*>(tl + r * PITCH + 4 * k4));
+    }
+  }
+  if (kx == 0) {  // bias (+ edge) partials: the tap-0 workgroups (every tap sees the same dz)
+    __syncthreads();  // (bsum reuses the tile's LDS)
+    if (dzt)
+#pragma unroll
+      for (int e = 0; e < NB; ++e) st4(&bsum[ws][e][4 * q], bacc[e]);
+    __syncthreads();
+    if (tid < kW1kO && obase + tid < cout) {
+#pragma unroll
+      for (int e = 0; e < NB; ++e) {
+        float v = 0.f;
+#pragma unroll
+        for (int sl = 0; sl < 16; ++sl) v += bsum[sl][e][tid];  // the 16 window slots, in order
+        a.bpart[((size_t)bz * NB + e) * cout + obase + tid] = ldexpf(v, -eo_bias);
+      }
+    }
+  }
+  DCUE_KT(0, 4);
+  DCUE_KTW(0, 7);
+}
+
+template <int KS, int PAD, int LIN, int R, int POOL, int LP>
+__global__ __launch_bounds__(kW1kThreads, 2) void k_conv_wgrad1k(WgradArgs a) {
+  critical_path_priority();  // the step's tail on the caller's stream
+  extern __shared__ __attribute__((aligned(16))) char lds1k[];
+  // a chunk's 16 tiles (o tile fastest, then tap) are consecutive logical blocks: one XCD, one L2
+  const int ot = (a.cout + kW1kO - 1) / kW1kO;
+  const int L = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int tile = L % (ot * KS);
+  wgrad1k_body<KS, PAD, LIN, R, POOL, LP>(a, tile % ot, tile / ot, L / (ot * KS), lds1k);
+  dev_wait_order(a.wait);  // (plans: the next step's prepared inputs -- an order for later kernels only)
 }
 
 // whether the weight gradients run on split-f16 MFMA (DCUE_WGRAD_F16=0: the f32-MFMA kernels)
@@ -1490,6 +1816,18 @@ static long w16_rows_per_chunk(long rows, int nchunk) {
   return (rpc + kW16Rows - 1) / kW16Rows * kW16Rows;
 }
 
+// conv 1's split-f16 weight gradient on k_conv_wgrad1k (one tap per workgroup, round 6; needs
+// 128 input channels and cout <= 256) under DCUE_W1K=1. Off by default: at the in-batch shape it
+// measured 24.6-34.5 us (2-16 stages a chunk) against k_conv_wgrad16t's 19.9 us, although it writes
+// half the partial bytes (profiles/r06_w1k_sweep.txt).
+static bool w1k_layer1(int cin, int cout) {
+  static const bool on = [] {
+    const char* e = getenv("DCUE_W1K");
+    return e && e[0] == '1';
+  }();
+  return on && wgrad_f16_on() && cin == kMels && cout % 4 == 0 && cout <= kW1kThreads;
+}
+
 int wgrad_nchunk(int layer, int M, int cout, int cin) {
   // one workgroup per CU (LDS-bound): at most 256 / tiles chunks, each of >= 64 rows; partial
   // blocks cost a write + a read of cout*ks*cin floats per chunk (layer 6: the fc, geometry of 5)
@@ -1507,6 +1845,29 @@ int wgrad_nchunk(int layer, int M, int cout, int cin) {
     long n = forced ? forced : 512 / tiles1;
     const long wins = (long)M * gm.lp;
     if (n > (wins + 4 * kW1Win - 1) / (4 * kW1Win)) n = (wins + 4 * kW1Win - 1) / (4 * kW1Win);
+    return (int)(n < 1 ? 1 : n);
+  }
+  if (layer == 1 && w1k_layer1(cin, cout)) {
+    // k_conv_wgrad1k: 16 tiles a chunk (4 o tiles x 4 taps at H = 128), two workgroups per CU, and
+    // at least DCUE_W1K_MIN_STAGES (default 8) 64-row stages a chunk: each chunk writes a 0.26 MB
+    // partial block, so the split-K depth is held down (in-batch: 15 chunks, 3.9 MB of partials
+    // against rounds 3-5's 33 and 8.7 MB)
+    static const long min_st = [] {
+      const char* e = getenv("DCUE_W1K_MIN_STAGES");
+      const long v = e ? atol(e) : 0;
+      return v >= 1 && v <= 256 ? v : 8L;
+    }();
+    const long tiles1 = ((cout + kW1kO - 1) / kW1kO) * gm.ks;
+    long n = 512 / tiles1;
+    const long per = min_st * kW16Rows;
+    if (n > (rows + per - 1) / per) n = (rows + per - 1) / per;
+    const long cap = (8L << 20) / ((long)cout * gm.ks * cin);
+    if (n > cap) n = cap;
+    // a chunk's items fit the kernel's LDS table: rows_per_chunk <= (kWgItems - 3) R
+    const long rmax = ((long)(kWgItems - 3) * gm.lp * gm.pool) / kW16Rows * kW16Rows;
+    if (n < (rows + rmax - 1) / rmax) n = (rows + rmax - 1) / rmax;
+    if (n < 1) n = 1;
+    n = (rows + w16_rows_per_chunk(rows, (int)n) - 1) / w16_rows_per_chunk(rows, (int)n);
     return (int)(n < 1 ? 1 : n);
   }
   const long tiles = w16t_layer(layer, cin)
@@ -1542,6 +1903,10 @@ int wgrad_nchunk(int layer, int M, int cout, int cin) {
   }
   const long cap = (8L << 20) / ((long)cout * gm.ks * cin);
   if (n > cap) n = cap;
+  if (layer == 1 && wgrad_f16_on()) {  // the tap-fused kernel's LDS item table (kWgItems)
+    const long rmax = ((long)(kWgItems - 3) * gm.lp * gm.pool) / kW16Rows * kW16Rows;
+    if (n < (rows + rmax - 1) / rmax) n = (rows + rmax - 1) / rmax;
+  }
   if (n < 1) n = 1;
   if (wgrad_f16_on())  // whole stages per chunk: no chunk left empty by the rounding
     n = (rows + w16_rows_per_chunk(rows, (int)n) - 1) / w16_rows_per_chunk(rows, (int)n);
@@ -1587,8 +1952,31 @@ static int wgrad16t_launch(const WgradArgs& a0, int nchunk, hipStream_t s) {
   const long rows = (long)a.M * R;
   if (rows >= (1L << 30)) return DCUE_ERR_UNSUPPORTED;  // 32-bit row indices
   a.rows_per_chunk = (int)w16_rows_per_chunk(rows, nchunk);
+  if (SRCX != SRC_ACT && R >= kW16Rows && a.rows_per_chunk / R + 3 > kWgItems) return DCUE_ERR_INVALID;
   const unsigned ot = (unsigned)((a.cout + kW16tO - 1) / kW16tO);
   DCUE_LAUNCH(kern, dim3(ot * (unsigned)nchunk), dim3(kW16tThreads), LDS, s, a);
+  DCUE_LAUNCH_CHECK();
+  return DCUE_OK;
+}
+
+static int wgrad1k_launch(const WgradArgs& a0, int nchunk, hipStream_t s) {
+  constexpr LayerGeom gm = layer_geom(1);
+  constexpr int R = gm.lp * gm.pool;
+  constexpr size_t LDS = w1k_lds_bytes<R, gm.ks>();
+  auto kern = k_conv_wgrad1k<gm.ks, gm.pad, gm.lin, R, gm.pool, gm.lp>;
+  if (a0.cin != kMels || a0.cout % 4 || a0.cout > kW1kThreads) return DCUE_ERR_INVALID;
+  static bool attr = false;
+  if (!attr) {
+    DCUE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS));
+    attr = true;
+  }
+  WgradArgs a = a0;
+  const long rows = (long)a.M * R;
+  if (rows >= (1L << 30)) return DCUE_ERR_UNSUPPORTED;  // 32-bit row indices
+  a.rows_per_chunk = (int)w16_rows_per_chunk(rows, nchunk);
+  if (a.rows_per_chunk / R + 3 > kWgItems) return DCUE_ERR_INVALID;  // (wgrad_nchunk keeps it in range)
+  const unsigned tiles = (unsigned)(((a.cout + kW1kO - 1) / kW1kO) * gm.ks);
+  DCUE_LAUNCH(kern, dim3(tiles * (unsigned)nchunk), dim3(kW1kThreads), LDS, s, a);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }
@@ -1597,6 +1985,8 @@ template <int L, int SRCX>
 static int wgrad16_layer(const WgradArgs& a0, int nchunk, hipStream_t s) {
   constexpr LayerGeom gm = layer_geom(L);
   constexpr int R = gm.lp * gm.pool;
+  if constexpr (L == 1 && SRCX == SRC_TRACK_F16)
+    if (w1k_layer1(a0.cin, a0.cout)) return wgrad1k_launch(a0, nchunk, s);
   if constexpr (L == 1)
     if (w16t_layer(1, a0.cin)) return wgrad16t_launch<1, SRCX>(a0, nchunk, s);
   auto kern = k_conv_wgrad16<SRCX, gm.ks, gm.pad, gm.lin, R, gm.pool, gm.lp, L == 1>;

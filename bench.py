@@ -42,6 +42,7 @@ F16_PEAK_TFLOPS = 2500.0  # MI355X dense FP16/BF16 MFMA (no sparsity), MI355X_MI
 # conv forwards run on split-f16 MFMA (three f16 products per f32 product) unless DCUE_CONV_F16=0
 CONV_F16 = os.environ.get("DCUE_CONV_F16", "1")[:1] != "0"
 WGRAD_F16 = os.environ.get("DCUE_WGRAD_F16", "1")[:1] != "0"
+W1K = WGRAD_F16 and os.environ.get("DCUE_W1K", "0")[:1] == "1"  # conv 1: k_conv_wgrad1k (round 6, A/B)
 
 
 
@@ -765,7 +766,11 @@ def main():
         rows_slice = n_users_local / args.flush_every
         table_bytes, active = replay_bytes(opt if optim is None else optim)
         spec = {
-            nat.TIMED_CONV1_WGRAD: (("k_conv_wgrad16 layer 1 (conv-1 weight gradient, split-f16 MFMA 16x16x32 on "
+            nat.TIMED_CONV1_WGRAD: (("k_conv_wgrad1k (conv-1 weight gradient, one tap per workgroup: 32 o x 128 c "
+                                     "tiles, split-K over 64-row stages, split-f16 MFMA 16x16x32 on the raw fp16 "
+                                     "table: two f16 products per f32 product, dz hi+lo x exact x; peak = f16 dense "
+                                     "peak / 2)") if W1K else
+                                    ("k_conv_wgrad16 layer 1 (conv-1 weight gradient, split-f16 MFMA 16x16x32 on "
                                      "the raw fp16 table: two f16 products per f32 product, dz hi+lo x exact x; "
                                      "peak = f16 dense peak / 2)") if WGRAD_F16 else
                                     "k_conv1_wgrad (conv-1 weight gradient, f32 MFMA 32x32x2)", "mfma", conv1),
@@ -859,7 +864,8 @@ def main():
         return out
 
     def traffic_for(kernel_name, mode):
-        tag = {"k_conv1_wgrad": "conv1_wgrad", "k_conv_wgrad16": "conv1_wgrad16", "k_emb_flush_rows": "emb_flush_rows",
+        tag = {"k_conv1_wgrad": "conv1_wgrad", "k_conv_wgrad16": "conv1_wgrad16", "k_conv_wgrad1k": "conv1_wgrad1k",
+               "k_emb_flush_rows": "emb_flush_rows",
                "k_conv_rows<0,0>": "conv1_fwd", "k_text_fwd": "text_fwd", "k_user_fwd": "user_fwd",
                "k_text_wgrad": "text_wgrad"}.get(kernel_name.split(" ")[0])
         path = os.path.join(ROOT, "profiles", "pmc_%s_%s.json" % (tag, mode)) if tag else None

@@ -21,9 +21,10 @@ import json
 import os
 import sys
 
-# conv-1 weight gradient: the tap-fused kernel (k_conv_wgrad16t, round 3) is the default; layer 2's
-# tap-fused weight gradient runs beside the dgrad chain on a side stream
-KERNELS = {"conv1_wgrad": "k_conv1_wgrad", "conv1_wgrad16": "k_conv_wgrad16t<0,",
+# conv-1 weight gradient: the tap-fused kernel (k_conv_wgrad16t, round 3) is the default, the one-tap
+# k_conv_wgrad1k (round 6) an A/B under DCUE_W1K=1; layer 2's tap-fused weight gradient runs beside
+# the dgrad chain on a side stream
+KERNELS = {"conv1_wgrad": "k_conv1_wgrad", "conv1_wgrad16": "k_conv_wgrad16t<0,", "conv1_wgrad1k": "k_conv_wgrad1k<",
            "wgrad16t_layer2": "k_conv_wgrad16t<2,", "wgrad16_multi": "k_conv_wgrad16_multi", "emb_flush_rows": "k_emb_flush_rows",
            "conv1_fwd": "k_conv_rows<0, 0,", "text_fwd": "k_text_fwd", "user_fwd": "k_user_fwd",
            "text_wgrad": "k_text_wgrad"}

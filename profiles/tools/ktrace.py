@@ -42,7 +42,7 @@ for kid, nm in zip(range(2, 7), ["fwd L1", "fwd L2", "fwd L3", "fwd L4", "fwd L5
     KERNELS.append(("fwd", kid, "k_conv_rows " + nm, ["chan+range setup", "slab stores", "barrier", "MFMA", "epilogue"], [0, 5, 1, 2, 3, 4]))
 for kid, nm in zip(range(7, 12), ["dgrad in L1?", "dgrad l=2 (in 32)", "dgrad l=3 (in 8)", "dgrad l=4 (in 2)", "dgrad l=5 (in 1)"]):
     KERNELS.append(("dgrad", kid, "k_conv_rows " + nm, ["chan+range setup", "slab stores", "barrier", "MFMA", "epilogue"], [0, 5, 1, 2, 3, 4]))
-KERNELS.append(("wgrad", 0, "k_conv_wgrad16t conv 1", ["prologue consts", "first stage fill", "stages (MFMA)", "partial stores"], [0, 1, 2, 3, 4]))
+KERNELS.append(("wgrad", 0, "k_conv_wgrad1k conv 1" if os.environ.get("DCUE_W1K", "0") == "1" else "k_conv_wgrad16t conv 1", ["prologue consts", "first stage fill", "stages (MFMA)", "partial stores"], [0, 1, 2, 3, 4]))
 KERNELS.append(("wgrad", 1, "k_conv_wgrad16t layer 2", ["prologue consts", "first stage fill", "stages (MFMA)", "partial stores"], [0, 1, 2, 3, 4]))
 for s_ in range(40):
     plan.set_next(items[(s_ + 1) % 40])
