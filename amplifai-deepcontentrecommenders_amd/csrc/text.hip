@@ -476,19 +476,22 @@ struct TextWgradArgs {
   float* wpart;          // several: [nchunk][C * E * 3 + C], the chunk's dW and db partials
 };
 
-constexpr int kTwO = 8;        // output channels per workgroup (32 word channels each: 256 threads)
+constexpr int kTwW = 64;       // word channels per workgroup: one wave, so a word load is one 256-B row slice
+constexpr int kTwO = 256 / kTwW;  // output channels per workgroup (256 threads)
 constexpr int kTwItems = 64;   // items whose tokens / routing are staged in LDS per pass
 // items per load group: their 3 word loads each are in flight per thread together, and the next
 // group's are issued before this group's FMAs (two register sets)
 constexpr int kTwG = 16;
 
-// Round 6: a workgroup owns 8 output channels x 32 word channels over ALL of its
-// chunk's items (one chunk at the in-batch shape: no partials, no reduce launch), so the grid is
-// (C / 8) x (E / 32) workgroups -- 320 at config 4 -- with 3 accumulators per thread. Per item a
-// thread reads its channel of the three word rows around the item's argmax position for its output
+// Round 6: a workgroup owns 4 output channels x 64 word channels (a wave per
+// output channel, so an item's routing is wave-uniform and a word load is one 256-B row slice) over
+// ALL of its chunk's items (one chunk at the in-batch shape: no partials, no reduce launch), so the
+// grid is (C / 4) x (E / 64) workgroups -- 320 at config 4 -- with 3 accumulators per thread. Per item
+// a thread reads its channel of the three word rows around the item's argmax position for its output
 // channel straight from L2 (the tokens and the routing staged in LDS once). Exact fp32 FMAs in item
 // order (deterministic); the chunk partials, where M needs several chunks, are summed in chunk order
-// by k_text_wreduce.
+// by k_text_wreduce. (8 x 32 workgroups, 16-64 items per chunk: each 22-24 us as well; per-workgroup
+// trace: staging 5 us, the 64 items 16.5 us -- profiles/r06_text_wgrad_ab.txt.)
 struct TwGroup {
   float x[kTwG][3];
   float gv[kTwG];
@@ -500,14 +503,16 @@ __global__ __launch_bounds__(256) void k_text_wgrad(TextWgradArgs a) {
   __shared__ int32_t tok_s[kTwItems * 128];  // [item][T], T <= 128
   __shared__ float g_s[kTwItems][kTwO];
   __shared__ int32_t ti_s[kTwItems][kTwO];
-  const int tid = threadIdx.x, cl = tid & 31, ol = tid >> 5;
+  DCUE_KTW(1, 6);
+  DCUE_KT(1, 0);
+  const int tid = threadIdx.x, cl = tid & (kTwW - 1), ol = tid / kTwW;
   // XCD-aware (o block, word-channel block): consecutive logical blocks -- the o blocks of one
   // word-channel block, which read the same 128-B slices of the batch's word rows -- on one XCD, so
   // each XCD's L2 fetches about 1/8 of the rows' bytes instead of all of them
   const int nob = gridDim.x, nbl = gridDim.x * gridDim.y;
   const int Lg = xcd_swizzle(blockIdx.x + nob * blockIdx.y, nbl);
   const int ob = (Lg % nob) * kTwO;
-  const int c = (Lg / nob) * 32 + cl;
+  const int c = (Lg / nob) * kTwW + cl;
   const int cc = c < a.E ? c : a.E - 1;  // (loads unconditional: clamped column, value dropped past E)
   const int T = a.T;
   const int ib = blockIdx.z * a.items_per_chunk, ie = min(a.M, ib + a.items_per_chunk);
@@ -535,7 +540,7 @@ __global__ __launch_bounds__(256) void k_text_wgrad(TextWgradArgs a) {
   auto consume = [&](const TwGroup& G) {
 #pragma unroll
     for (int j = 0; j < kTwG; ++j) {
-      if (!((G.live >> j) & 1u)) continue;  // (uniform over the 32 lanes of one output channel)
+      if (!((G.live >> j) & 1u)) continue;  // (uniform over the wave: one output channel)
       bacc += G.gv[j];  // db's partial, in item order
       acc0 = fmaf(G.gv[j], (G.ok >> (3 * j)) & 1u ? G.x[j][0] : 0.f, acc0);
       acc1 = fmaf(G.gv[j], (G.ok >> (3 * j + 1)) & 1u ? G.x[j][1] : 0.f, acc1);
@@ -557,6 +562,7 @@ __global__ __launch_bounds__(256) void k_text_wgrad(TextWgradArgs a) {
       g_s[sl][oo] = ti == kTextNoGrad ? 0.f : a.dt[off];
     }
     __syncthreads();
+    if (i0 == ib) DCUE_KT(1, 1);
     TwGroup G0, G1;
     issue(0, ni, G0);
     for (int s0 = 0; s0 < ni; s0 += 2 * kTwG) {
@@ -567,6 +573,7 @@ __global__ __launch_bounds__(256) void k_text_wgrad(TextWgradArgs a) {
       consume(G1);
     }
   }
+  DCUE_KT(1, 2);
   const int o = ob + ol;
   const long n = (long)a.C * a.E * 3;
   float* dw = gridDim.z == 1 ? a.dW : a.wpart + (long)blockIdx.z * (n + a.C);
@@ -578,6 +585,8 @@ __global__ __launch_bounds__(256) void k_text_wgrad(TextWgradArgs a) {
     d[2] = acc2;
   }
   if (c == cl && cl == 0) dbp[o] = bacc;  // (the first word-channel block)
+  DCUE_KT(1, 3);
+  DCUE_KTW(1, 7);
 }
 
 // the chunk partials [nchunk][n + C] (dW then db per chunk) summed in chunk order
@@ -705,7 +714,13 @@ int launch_text_fwd(const TextBranch& tb, const int32_t* item_track, int M, floa
 // item chunks of the text weight gradient: one up to 128 items (the in-batch shapes: no partials),
 // else about 128 items per chunk, at most 16 chunks
 int text_wgrad_nchunk(int M) {
-  const int n = (M + 127) / 128;
+  // DCUE_TEXT_WGRAD_ITEMS: items per chunk (A/B diagnostic; default 128)
+  static const int per = [] {
+    const char* e = getenv("DCUE_TEXT_WGRAD_ITEMS");
+    const int v = e ? atoi(e) : 0;
+    return v >= 8 && v <= 4096 ? v : 128;
+  }();
+  const int n = (M + per - 1) / per;
   return n < 1 ? 1 : (n > 16 ? 16 : n);
 }
 
@@ -719,7 +734,7 @@ int launch_text_wgrad(const TextBranch& tb, const int32_t* item_track, int M, co
   const int nchunk = text_wgrad_nchunk(M);
   a.items_per_chunk = (M + nchunk - 1) / nchunk;
   a.dW = dW; a.db = db; a.wpart = wpart;
-  const dim3 grid((unsigned)(tb.C / kTwO), (unsigned)((tb.E + 31) / 32), (unsigned)nchunk);
+  const dim3 grid((unsigned)(tb.C / kTwO), (unsigned)((tb.E + kTwW - 1) / kTwW), (unsigned)nchunk);
   TimerScope tsc;  // (live timing: DCUE_TIMED_TEXT_WGRAD)
   TRY(timer_begin(&tsc, DCUE_TIMED_TEXT_WGRAD, s));
   DCUE_LAUNCH(k_text_wgrad, grid, dim3(256), 0, s, a);

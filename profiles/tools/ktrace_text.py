@@ -58,4 +58,18 @@ for s_ in range(40):
               % (s_, len(t), span, np.median(wall), wall.max(), spread,
                  ", ".join("%s %.2f/%.2f" % (l, np.median(ph[:, i]) / cyc, ph[:, i].max() / cyc)
                            for i, l in enumerate(labels))), flush=True)
+        # kernel 1: k_text_wgrad (slots by blockIdx.x only: one sample per o block)
+        t = buf[1].astype(np.int64)
+        t = t[t[:, 6] > 0]
+        if len(t):
+            t = t[t[:, 6] >= t[:, 6].max() - 100000]
+            w = t[:, 7] - t[:, 6]
+            ok = w > 0
+            wall = w[ok] * 10 / 1000.0
+            ph = np.diff(t[ok, :4], axis=1)
+            cyc = np.median((t[ok, 3] - t[ok, 0]) / np.maximum(wall, 1e-3))
+            print("step %d k_text_wgrad WGs(sampled) %4d WG wall med %5.1f max %5.1f; %s" % (
+                s_, len(t), np.median(wall), wall.max(),
+                ", ".join("%s %.2f/%.2f" % (l, np.median(ph[:, i]) / cyc, ph[:, i].max() / cyc) for i, l in
+                          enumerate(["stage tokens + routing", "items (word loads + FMAs)", "stores"]))), flush=True)
 plan.close()
