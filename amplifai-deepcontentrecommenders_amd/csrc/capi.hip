@@ -1312,9 +1312,16 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
   hipEvent_t joined = nullptr;
   // plans (split, no exchange): the late Adam also signals the next step's conv 2 (DevWait)
   DevWait late_sig{};
+  // The late Adam's signal is a one-lane k_signal after the sweep: every workgroup of the sweep
+  // releasing its stores itself (dev_signal_wg, DCUE_LATE_SIG=kernel) costs an L2 writeback each on
+  // gfx950 -- 440 of them -- and measured 2-4 us slower per step (profiles/r06_ab_late_signal.txt)
+  static const bool late_sig_launch = [] {
+    const char* e = getenv("DCUE_LATE_SIG");
+    return !(e && e[0] == 'k');
+  }();
   if (o.dense_split && !o.comm && o.late_sig && o.sig && !capturing_step()) {
-    // its dense sweep's workgroups signal themselves (k_adam_dense_pack, dev_signal_wg)
-    const unsigned nwg = (unsigned)adam_dense_blocks(c.poff[kSeg] - c.poff[DCUE_SEG_LATE]);
+    // (DCUE_LATE_SIG=kernel: the sweep's workgroups signal themselves, k_adam_dense_pack)
+    const unsigned nwg = late_sig_launch ? 1u : (unsigned)adam_dense_blocks(c.poff[kSeg] - c.poff[DCUE_SEG_LATE]);
     late_sig = DevWait{o.sig + kSigLate, o.sig_issued[kSigLate] += nwg, user_fwd_fail_flag()};
     *o.late_sig = late_sig;
   }
@@ -1346,9 +1353,10 @@ int backward_impl(const dcue_model* m, const dcue_batch* b, const dcue_tracks* t
       {
         ForkAfter fk(sp, su, o.late_done);
         TRY(launch_adam(m, &dense, c.poff, su, true, late, -1, !legacy_orders(),
-                        late_sig.flag ? o.sig + kSigLate : nullptr));
+                        late_sig.flag && !late_sig_launch ? o.sig + kSigLate : nullptr));
         TRY(fk.done());
       }
+      if (late_sig.flag && late_sig_launch) TRY(launch_signal(o.sig + kSigLate, late_sig.val, su));
       TRY(probe(PR_P_LATE, m->params + late, c.poff[kSeg] - late, su));
     }
     return DCUE_OK;

@@ -476,22 +476,22 @@ struct TextWgradArgs {
   float* wpart;          // several: [nchunk][C * E * 3 + C], the chunk's dW and db partials
 };
 
-constexpr int kTwW = 64;       // word channels per workgroup: one wave, so a word load is one 256-B row slice
+constexpr int kTwW = 32;       // word channels per workgroup (64: a wave per output channel -- as fast, 9.1 MB)
 constexpr int kTwO = 256 / kTwW;  // output channels per workgroup (256 threads)
 constexpr int kTwItems = 64;   // items whose tokens / routing are staged in LDS per pass
 // items per load group: their 3 word loads each are in flight per thread together, and the next
 // group's are issued before this group's FMAs (two register sets)
 constexpr int kTwG = 16;
 
-// Round 6: a workgroup owns 4 output channels x 64 word channels (a wave per
-// output channel, so an item's routing is wave-uniform and a word load is one 256-B row slice) over
-// ALL of its chunk's items (one chunk at the in-batch shape: no partials, no reduce launch), so the
-// grid is (C / 4) x (E / 64) workgroups -- 320 at config 4 -- with 3 accumulators per thread. Per item
-// a thread reads its channel of the three word rows around the item's argmax position for its output
+// Round 6: a workgroup owns 8 output channels x 32 word channels over ALL of its
+// chunk's items (one chunk at the in-batch shape: no partials, no reduce launch), so the grid is
+// (C / 8) x (E / 32) workgroups -- 320 at config 4 -- with 3 accumulators per thread. Per item a
+// thread reads its channel of the three word rows around the item's argmax position for its output
 // channel straight from L2 (the tokens and the routing staged in LDS once). Exact fp32 FMAs in item
 // order (deterministic); the chunk partials, where M needs several chunks, are summed in chunk order
-// by k_text_wreduce. (8 x 32 workgroups, 16-64 items per chunk: each 22-24 us as well; per-workgroup
-// trace: staging 5 us, the 64 items 16.5 us -- profiles/r06_text_wgrad_ab.txt.)
+// by k_text_wreduce. (4 x 64 workgroups -- a wave per output channel -- and 16-64 items per chunk:
+// each 22-24 us as well, the 4 x 64 form at 9.1 MB against 7.6; per-workgroup trace: staging 5 us,
+// the 64 items 16.5 us -- profiles/r06_text_wgrad_ab.txt.)
 struct TwGroup {
   float x[kTwG][3];
   float gv[kTwG];
@@ -540,7 +540,7 @@ __global__ __launch_bounds__(256) void k_text_wgrad(TextWgradArgs a) {
   auto consume = [&](const TwGroup& G) {
 #pragma unroll
     for (int j = 0; j < kTwG; ++j) {
-      if (!((G.live >> j) & 1u)) continue;  // (uniform over the wave: one output channel)
+      if (!((G.live >> j) & 1u)) continue;  // (uniform over the kTwW lanes of one output channel)
       bacc += G.gv[j];  // db's partial, in item order
       acc0 = fmaf(G.gv[j], (G.ok >> (3 * j)) & 1u ? G.x[j][0] : 0.f, acc0);
       acc1 = fmaf(G.gv[j], (G.ok >> (3 * j + 1)) & 1u ? G.x[j][1] : 0.f, acc1);
