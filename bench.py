@@ -58,6 +58,11 @@ def parse():
     ap.add_argument("--text-feature-dim", type=int, default=256, help="config 4: d = 256")
     ap.add_argument("--word-dim", type=int, default=300)
     ap.add_argument("--text-len", type=int, default=64)
+    ap.add_argument("--spin-sync", type=int, default=1,
+                    help="1 (default): poll for the GPU's idle before the pre-timing synchronize, so the "
+                         "issuing thread is not asleep in the driver when the timed steps start (its "
+                         "wake-up cost the first timed step 0.5-0.9 ms of host time; DESIGN.md §7); "
+                         "0: synchronize directly")
     ap.add_argument("--n-words", type=int, default=20000)
     ap.add_argument("--users", type=int, default=100_000)
     ap.add_argument("--tracks", type=int, default=200_000)
@@ -700,6 +705,14 @@ def main():
         mark(name + ": barrier before the timed steps")
         if world > 1:
             dist.barrier()
+        # (outside the timed region) wait for the GPU by polling, so the host thread stays awake on its
+        # core, then synchronize: a thread put to sleep in the driver's wait issued the first timed step
+        # 2-4x slower (profiles/r06_ab_spin_sync.txt)
+        if args.spin_sync:
+            done = torch.cuda.Event()
+            done.record()
+            while not done.query():
+                pass
         torch.cuda.synchronize()
         for k in timed:
             nat.timer_enable(k, stride)  # from the first timed step on (restarts the stride count)
