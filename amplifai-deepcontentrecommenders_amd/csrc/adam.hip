@@ -8,6 +8,8 @@
 #include "bn0adam.h"
 
 
+DCUE_KTRACE_READER(adam)  // diagnostic builds only (dcue_common.h): kernel 0 = k_user_fwd
+
 namespace dcue {
 
 // (m, v) = (+0, +0) is a fixed point of the zero-gradient step without weight decay (adam_zero_elem:
@@ -638,17 +640,24 @@ struct UserFwdArgs {
   unsigned* sig;           // plans: +1 per workgroup once its uf rows are stored (dev_signal_wg)
 };
 
-__global__ __launch_bounds__(512) void k_user_fwd(UserFwdArgs a) {
-  __shared__ TgLds L[2];
+// 256-thread GEMM parts per workgroup. (3 -- 768 threads, 2 GEMM-1 rounds instead of 3 -- fits the
+// LDS, 159 KB, but not the registers at 3 waves per SIMD: 93 VGPRs spilled; not kept, round 6)
+constexpr int kUfParts = 2;
+__global__ __launch_bounds__(256 * kUfParts) void k_user_fwd(UserFwdArgs a) {
+  __shared__ TgLds L[kUfParts];
   __shared__ AdamScalars hs[DCUE_MAX_LOG_CAP];
   __shared__ ReplayBound sb;
   __shared__ int from_s[16], claim_s[16];
+  __shared__ int64_t user_s[16];
+  DCUE_KTW(0, 6);
+  DCUE_KT(0, 0);
   const int t = threadIdx.x, half = t >> 8, th = t & 255;
   const int r0 = blockIdx.x * 16, nr = min(16, a.B - r0);
   if (a.emb_step) {
     const int T = a.hdr->step_done, F = a.hdr->flush_step, cap = a.hdr->cap;
     if (t < nr) {
       const int64_t u = a.users[r0 + t];
+      user_s[t] = u;
       const int old = a.emb_step[u];
       int from = T, claimed = 0;
       if (old != INT_MIN && max(clock_of(old), F) < T && atomicCAS(&a.emb_step[u], old, INT_MIN) == old) {
@@ -662,37 +671,61 @@ __global__ __launch_bounds__(512) void k_user_fwd(UserFwdArgs a) {
     const AdamScalars* hist = log_hist(a.hdr);
     for (int j = lo + t; j <= T; j += blockDim.x) hs[j % cap] = hist[j % cap];
     __syncthreads();
+    DCUE_KT(0, 1);
     // (lo > T: nothing to replay -- no row is claimed -- but sb is still read below: give it a value)
     if (lo <= T) window_bound(hs, lo, T, cap, 0.f, &sb);
     else if (t == 0) sb = ReplayBound{};
     __syncthreads();
     const ReplayBound b = sb;
-    for (int e = t; e < nr * a.E; e += blockDim.x) {
-      const int i = e / a.E, k = e - i * a.E;
-      if (!claim_s[i]) continue;
-      const long off = a.users[r0 + i] * a.E + k;
-      float mm[1] = {a.m[off]}, vv[1] = {a.v[off]};
-      if (idle_moments(mm[0], vv[0]) && (b.nd || claim_s[i] == 2)) continue;  // fixed point (idle_moments)
-      if (claim_s[i] == 2) {  // frozen (adam_replay.h): p unchanged
-        frz_replay(mm[0], vv[0], hs[T % cap].lerp_c, hs[T % cap].b2, T - from_s[i]);
-        a.m[off] = mm[0]; a.v[off] = vv[0];
-        continue;
+    // A thread's elements in groups of kUfG: the group's p / m / v loads go out together (clamped,
+    // unconditional), then the replays run -- one load latency a group instead of one an element
+    // (round 6: the replay phase was 30 us of the workgroup's 80, per-workgroup trace)
+    constexpr int kUfG = 8;
+    const int tot = nr * a.E;
+    for (int e0 = t; e0 < tot; e0 += kUfG * (int)blockDim.x) {
+      float pg[kUfG], mg[kUfG], vg[kUfG];
+      long og[kUfG];
+      int cg[kUfG], fg[kUfG];
+#pragma unroll
+      for (int j = 0; j < kUfG; ++j) {
+        const int e = e0 + j * (int)blockDim.x;
+        const int ec = e < tot ? e : e0;
+        const int i = ec / a.E, k = ec - i * a.E;
+        cg[j] = e < tot ? claim_s[i] : 0;
+        fg[j] = from_s[i];
+        og[j] = user_s[i] * a.E + k;
+        mg[j] = a.m[og[j]];
+        vg[j] = a.v[og[j]];
+        pg[j] = a.p[og[j]];
       }
-      float pp[1] = {a.p[off]};
-      replay_run<1>(pp, mm, vv, hs, from_s[i] + 1, T, cap, b, 0.f);
-      a.p[off] = pp[0]; a.m[off] = mm[0]; a.v[off] = vv[0];
+#pragma unroll
+      for (int j = 0; j < kUfG; ++j) {
+        if (!cg[j]) continue;
+        const long off = og[j];
+        float mm[1] = {mg[j]}, vv[1] = {vg[j]};
+        if (idle_moments(mm[0], vv[0]) && (b.nd || cg[j] == 2)) continue;  // fixed point (idle_moments)
+        if (cg[j] == 2) {  // frozen (adam_replay.h): p unchanged
+          frz_replay(mm[0], vv[0], hs[T % cap].lerp_c, hs[T % cap].b2, T - fg[j]);
+          a.m[off] = mm[0]; a.v[off] = vv[0];
+          continue;
+        }
+        float pp[1] = {pg[j]};
+        replay_run<1>(pp, mm, vv, hs, fg[j] + 1, T, cap, b, 0.f);
+        a.p[off] = pp[0]; a.m[off] = mm[0]; a.v[off] = vv[0];
+      }
     }
     __syncthreads();
+    DCUE_KT(0, 2);
     // Every claimed clock is released before any lane waits: claimers and waiters are lanes of one
     // wave, and a wave spinning with its claimer lanes masked off would never release them (two
     // workgroups each waiting for a row the other holds would then both spin to the bound).
     if (t < nr && claim_s[t]) {
       __threadfence();  // the row's replayed values before its clock (other workgroups wait on it)
-      __hip_atomic_store(a.emb_step + a.users[r0 + t], T, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.emb_step + user_s[t], T, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (t < nr && !claim_s[t]) {
-      int32_t* clk = a.emb_step + a.users[r0 + t];
+      int32_t* clk = a.emb_step + user_s[t];
       unsigned spins = 0;
       while (__hip_atomic_load(clk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == INT_MIN) {
         __builtin_amdgcn_s_sleep(2);
@@ -705,12 +738,19 @@ __global__ __launch_bounds__(512) void k_user_fwd(UserFwdArgs a) {
     }
     __syncthreads();
   }
-  // GEMM 1: the N / 64 column blocks two at a time (an out-of-range block stores nothing)
+  DCUE_KT(0, 3);
+  // GEMM 1: the N / 64 column blocks kUfParts at a time (every part runs the same number of rounds: an
+  // out-of-range block stores nothing). Per-workgroup trace (round 6, profiles/r06_ktrace_user_fwd.txt):
+  // claims 2.4 us, replay 30, GEMM 1 34 (three rounds of two 16 x 64 blocks at E = 300), GEMM 2 12
   const int gy1 = (a.g1.N + 63) / 64, gy2 = (a.g2.N + 63) / 64;
-  for (int by = half; by < gy1 + (gy1 & 1); by += 2) tgemm_block<1, 0, 1, 0>(a.g1, blockIdx.x, by, L[half], th);
+  const int ry1 = (gy1 + kUfParts - 1) / kUfParts * kUfParts, ry2 = (gy2 + kUfParts - 1) / kUfParts * kUfParts;
+  for (int by = half; by < ry1; by += kUfParts) tgemm_block<1, 0, 1, 0>(a.g1, blockIdx.x, by, L[half], th);
   __syncthreads();
-  for (int by = half; by < gy2 + (gy2 & 1); by += 2) tgemm_block<1, 0, 1, 0>(a.g2, blockIdx.x, by, L[half], th);
+  DCUE_KT(0, 4);
+  for (int by = half; by < ry2; by += kUfParts) tgemm_block<1, 0, 1, 0>(a.g2, blockIdx.x, by, L[half], th);
   dev_signal_wg(a.sig);
+  DCUE_KT(0, 5);
+  DCUE_KTW(0, 7);
 }
 
 int user_fwd_blocks(int B) { return (B + 15) / 16; }
@@ -727,7 +767,7 @@ int launch_user_fwd(const dcue_model* md, const TGemmArgs& g1, const TGemmArgs& 
   if (!fail) return DCUE_ERR_HIP;
   a.fail = fail;
   a.sig = sig;
-  DCUE_LAUNCH(k_user_fwd, dim3((unsigned)user_fwd_blocks(B)), dim3(512), 0, s, a);
+  DCUE_LAUNCH(k_user_fwd, dim3((unsigned)user_fwd_blocks(B)), dim3(256 * kUfParts), 0, s, a);
   DCUE_LAUNCH_CHECK();
   return DCUE_OK;
 }

@@ -16,7 +16,9 @@ from dcrecommend.dcue.plan import TrainPlan  # noqa: E402
 from dcrecommend.optim import NativeAdam  # noqa: E402
 
 dev = "cuda:0"
-B, N, n_users, n_tracks = 64, 20, 5000, 8000
+B, N, n_tracks = 64, 20, 8000
+n_users = int(os.environ.get("KT_USERS", "5000"))
+n_steps = int(os.environ.get("KT_STEPS", "40"))  # (more steps: the user table's replays reach steady state)
 torch.manual_seed(0)
 net = DCUENet({"feature_dim": 128, "conv_hidden": 128, "user_embdim": 300, "user_count": n_users,
                "model_type": "truedcuemel1dbn"}).to(dev).train()
@@ -26,12 +28,12 @@ table = torch.randn(n_tracks, 131, 128, generator=gen, device=dev).half()
 mt = torch.empty(nat.MT_STATE_BYTES, dtype=torch.uint8, device=dev)
 nat.check(nat.lib().dcue_mt_seed(nat.ptr(mt), 7, nat.stream_handle()), "mt_seed")
 plan = TrainPlan(net, table, B, N, mt_state=mt, optimizer=opt)
-users = torch.randint(0, n_users, (40, B), generator=gen, device=dev)
-items = torch.randint(0, n_tracks, (40, B), generator=gen, device=dev).to(torch.int32)
+users = torch.randint(0, n_users, (n_steps, B), generator=gen, device=dev)
+items = torch.randint(0, n_tracks, (n_steps, B), generator=gen, device=dev).to(torch.int32)
 lib = nat.lib()
 KK, KB = 16, 512
 readers = {}
-for n in ("tail", "fwd", "dgrad", "wgrad"):
+for n in ("tail", "fwd", "dgrad", "wgrad", "adam"):
     fn = getattr(lib, "dcue_ktrace_read_" + n)
     fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     readers[n] = fn
@@ -43,11 +45,12 @@ for kid, nm in zip(range(2, 7), ["fwd L1", "fwd L2", "fwd L3", "fwd L4", "fwd L5
 for kid, nm in zip(range(7, 12), ["dgrad in L1?", "dgrad l=2 (in 32)", "dgrad l=3 (in 8)", "dgrad l=4 (in 2)", "dgrad l=5 (in 1)"]):
     KERNELS.append(("dgrad", kid, "k_conv_rows " + nm, ["chan+range setup", "slab stores", "barrier", "MFMA", "epilogue"], [0, 5, 1, 2, 3, 4]))
 KERNELS.append(("wgrad", 0, "k_conv_wgrad1k conv 1" if os.environ.get("DCUE_W1K", "0") == "1" else "k_conv_wgrad16t conv 1", ["prologue consts", "first stage fill", "stages (MFMA)", "partial stores"], [0, 1, 2, 3, 4]))
+KERNELS.append(("adam", 0, "k_user_fwd", ["claims + history", "replay", "release + waits", "GEMM 1", "GEMM 2 + signal"], [0, 1, 2, 3, 4, 5]))
 KERNELS.append(("wgrad", 1, "k_conv_wgrad16t layer 2", ["prologue consts", "first stage fill", "stages (MFMA)", "partial stores"], [0, 1, 2, 3, 4]))
-for s_ in range(40):
-    plan.set_next(items[(s_ + 1) % 40])
+for s_ in range(n_steps):
+    plan.set_next(items[(s_ + 1) % n_steps])
     plan.step(users[s_], items[s_])
-    if s_ >= 37:
+    if s_ >= n_steps - 3:
         torch.cuda.synchronize()
         for n, fn in readers.items():
             assert fn(bufs[n].ctypes.data, bufs[n].nbytes) == 0
